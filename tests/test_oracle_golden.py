@@ -1,0 +1,102 @@
+"""Pin the CPU oracle against golden vectors captured from the real reference (CPU only)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import transmvs_ref as oracle
+from transmvsnet_amd import synthetic
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load(name):
+    return dict(np.load(os.path.join(GOLD, name)))
+
+
+@pytest.fixture(scope="module")
+def sd():
+    with open(os.path.join(GOLD, "state_dict_keys.json")) as f:
+        keys = json.load(f)
+    shapes = {k: (tuple(v[0]), v[1]) for k, v in keys.items()}
+    return synthetic.synthetic_state_dict(shapes, seed=0, sharpen=100.0)
+
+
+def test_state_dict_contract(sd):
+    assert len(sd) == 465
+    nparam = sum(v.numel() for k, v in sd.items()
+                 if not k.endswith(("running_mean", "running_var", "num_batches_tracked")))
+    assert nparam == 1148924
+
+
+def _check_stage_dump(out, vw, g, full=True):
+    for s in (1, 2, 3):
+        o = out[f"stage{s}"]
+        np.testing.assert_array_equal(o["depth"].numpy(), g[f"stage{s}_depth"])
+        np.testing.assert_array_equal(o["photo_confidence"].numpy(), g[f"stage{s}_conf"])
+        if f"stage{s}_prob" in g:
+            np.testing.assert_array_equal(o["prob_volume"].numpy(), g[f"stage{s}_prob"])
+            np.testing.assert_array_equal(o["depth_values"].numpy(), g[f"stage{s}_hyp"])
+    np.testing.assert_array_equal(vw.numpy(), g["view_weights"])
+
+
+def test_oracle_e2e_c1_features_bitexact(sd):
+    g = _load("e2e_c1_features.npz")
+    H, W, N = 128, 160, 3
+    feats = synthetic.synthetic_features(N, H, W, seed=2)
+    out, vw = oracle.forward_from_features(sd, feats, synthetic.synthetic_cameras(N, H, W, seed=1),
+                                           synthetic.synthetic_depth_values(1), (H, W), ndepths=(8, 8, 8),
+                                           with_view_weights=True)
+    _check_stage_dump(out, vw, g)
+    assert set(out) == {"stage1", "stage2", "stage3", "depth", "photo_confidence", "prob_volume", "depth_values"}
+
+
+def test_oracle_e2e_cascade_bitexact(sd):
+    g = _load("e2e_cascade_256x320.npz")
+    H, W, N = 256, 320, 3
+    feats = synthetic.synthetic_features(N, H, W, seed=2)
+    out, vw = oracle.forward_from_features(sd, feats, synthetic.synthetic_cameras(N, H, W, seed=1),
+                                           synthetic.synthetic_depth_values(1), (H, W), with_view_weights=True)
+    _check_stage_dump(out, vw, g)
+
+
+def test_oracle_e2e_images(sd):
+    g = _load("e2e_c1_imgs.npz")
+    H, W, N = 128, 160, 3
+    out, vw = oracle.forward(sd, synthetic.synthetic_images(N, H, W, seed=0),
+                             synthetic.synthetic_cameras(N, H, W, seed=1), synthetic.synthetic_depth_values(1),
+                             ndepths=(8, 8, 8), with_view_weights=True)
+    _check_stage_dump(out, vw, g)
+
+
+def test_oracle_ops(sd):
+    g = _load("ops.npz")
+    t = {k: torch.from_numpy(v) for k, v in g.items()}
+    p = t["warp_proj"]
+    warped = oracle.homo_warping(t["warp_src"], oracle.compose_proj(p[:, 1]), oracle.compose_proj(p[:, 0]), t["warp_hyp"])
+    np.testing.assert_array_equal(warped.numpy(), g["warp_out"])
+    sim = (warped * t["warp_ref"].unsqueeze(2)).mean(1, keepdim=True)
+    np.testing.assert_array_equal(sim.numpy(), g["warp_sim"])
+    np.testing.assert_array_equal(oracle.pixelwise_net(sd, sim).numpy(), g["pixelwise_out"])
+    np.testing.assert_array_equal(oracle.cost_reg_net(sd, "cost_regularization.0.", t["costreg_in"]).numpy(),
+                                  g["costreg_out"])
+    prob, depth, conf = oracle.softmax_regression(t["wta_logits"].unsqueeze(1), t["wta_hyp"])
+    np.testing.assert_array_equal(prob.numpy(), g["wta_prob"])
+    np.testing.assert_array_equal(depth.numpy(), g["wta_depth"])
+    np.testing.assert_array_equal(conf.numpy(), g["wta_conf"])
+    assert g["wta_depth"][0, 0, 0] == g["wta_hyp"][0, 2, 0, 0]      # first-max tie rule
+    assert g["wta_depth"][0, 1, 0] == g["wta_hyp"][0, 0, 1, 0]
+    np.testing.assert_array_equal(oracle.linear_attention(t["la_q"], t["la_k"], t["la_v"]).numpy(), g["la_out"])
+    np.testing.assert_array_equal(oracle.encoder_layer(sd, "FMT_with_pathway.FMT.layers.1.", t["enc_x"], t["enc_src"]).numpy(),
+                                  g["enc_out"])
+
+
+def test_oracle_stage_glue():
+    g = _load("ops.npz")
+    dv = synthetic.synthetic_depth_values(1)
+    for s, (nd, hh, ww) in ((2, (32, 64, 80)), (3, (8, 64, 80))):
+        prev = torch.from_numpy(g[f"glue{s}_prev"])
+        hyp = oracle.stage_hypotheses(prev, dv, s - 1, (hh, ww), ndepths=(48, 32, 8))
+        np.testing.assert_array_equal(hyp.numpy(), g[f"glue{s}_hyp"])
