@@ -1,0 +1,259 @@
+"""Benchmark: depth maps/sec of the TransMVSNet hot path at DTU 864x1152, N=5, 48/32/8.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode replica|views] [--no-cpu-baseline]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step is one hot-path forward (TransMVSNet.forward_features: FMT + pathway + 3-stage
+stage glue / fused cost volume / CostRegNet / softmax-WTA) of one depth map from synthetic
+FeatureNet-shaped features already resident in HBM; random-init weights of the reference
+architecture (key-seeded, transmvsnet_amd.synthetic). FeatureNet (the next row)
+is outside the timed step. Multi-GPU:
+  replica (default) -- every rank computes its own depth maps, no collective ("weak");
+  views             -- the 4 source views are sharded over ranks, one RCCL all-reduce of
+                       (sum w*sim, sum w) per stage (transmvsnet_amd.distributed).
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+H, W, NVIEWS = 864, 1152, 5
+NDEPTHS = (48, 32, 8)
+C_STAGE = (32, 16, 8)
+SCALES = (4, 2, 1)
+PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+PEAK_F32_MFMA_TFS = 157.3  # MI355X_MICROARCH.md: fp32 MFMA dense peak
+
+
+def _args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--mode", choices=("replica", "views"), default="replica")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--profile-steps", type=int, default=3)
+    return ap.parse_args()
+
+
+class EventTimer:
+    """HIP events around every C-ABI launch, on the stream the kernels are launched on."""
+
+    def __init__(self):
+        self.spans = []
+
+    def begin(self, name):
+        if name == "tmvs_bn_fold":
+            return None
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream())
+        return (name, e0)
+
+    def end(self, tok):
+        if tok is None:
+            return
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(torch.cuda.current_stream())
+        self.spans.append((tok[0], tok[1], e1))
+
+    def durations(self):
+        torch.cuda.synchronize()
+        return [(n, a.elapsed_time(b)) for n, a, b in self.spans]
+
+
+def algorithmic():
+    """Per-depth-map work units (SURVEY.md 8d / BASELINE.md 3)."""
+    v = NVIEWS - 1
+    warp_bytes, cr_flop = [], []
+    for s in range(3):
+        p = (H // SCALES[s]) * (W // SCALES[s])
+        warp_bytes.append(4 * p * (C_STAGE[s] * (1 + v) + 2 * NDEPTHS[s] + v))
+        cr_flop.append(6912 * NDEPTHS[s] * p)
+    return warp_bytes, cr_flop
+
+
+def make_inputs(device, seed_feat=2):
+    from transmvsnet_amd import synthetic
+    proj = synthetic.synthetic_cameras(NVIEWS, H, W, seed=1)
+    dv = synthetic.synthetic_depth_values(1)
+    g = torch.Generator(device="cpu").manual_seed(seed_feat)
+    feats = {}
+    for name, c, s in (("stage1", 32, 4), ("stage2", 16, 2), ("stage3", 8, 1)):
+        feats[name] = torch.randn(1, NVIEWS, c, H // s, W // s, generator=g)
+    return feats, proj, dv
+
+
+def main():
+    args = _args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from transmvsnet_amd import TransMVSNet, ops, synthetic
+    model = TransMVSNet().eval()
+    model.load_state_dict(synthetic.synthetic_state_dict(synthetic.state_dict_shapes(model), seed=0, sharpen=100.0))
+    model = model.to(dev)
+    feats_cpu, proj, dv = make_inputs(dev)
+    feats = {k: v.to(dev) for k, v in feats_cpu.items()}
+    dv_dev = dv.to(dev)
+    shard = None
+    if args.mode == "views" and world > 1:
+        from transmvsnet_amd.distributed import ViewShard
+        shard = ViewShard(rank, world, NVIEWS - 1)
+
+    def step():
+        return model.forward_features(feats, proj, dv_dev, (H, W), view_shard=shard)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            out = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        elapsed = t1 - t0
+        if world > 1:
+            t = torch.tensor([elapsed], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+
+        # instrumented steps (outside the timed region): per-launch HIP-event durations
+        timer = EventTimer()
+        ops.set_timer(timer)
+        for _ in range(args.profile_steps):
+            step()
+        ops.set_timer(None)
+        spans = timer.durations()
+
+    maps_per_step = 1 if args.mode == "views" else world
+    value = maps_per_step * args.steps / elapsed
+    per_kernel = {}
+    for n, ms in spans:
+        per_kernel.setdefault(n, []).append(ms)
+    steps_p = max(1, args.profile_steps)
+    breakdown = {n: round(sum(v) / steps_p, 4) for n, v in per_kernel.items()}
+
+    warp_bytes, cr_flop = algorithmic()
+    warp_ms = per_kernel.get("tmvs_warp_corr", [])
+    cr_ms = per_kernel.get("tmvs_costregnet", [])
+    kern = []
+    if warp_ms:
+        per_launch = np.array(warp_ms).reshape(steps_p, -1).mean(0)  # stage order
+        ach = sum(warp_bytes) / (per_launch.sum() * 1e-3) / 1e9
+        kern.append({"kernel": "tmvs_warp_corr", "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
+                     "ms_per_depth_map": round(float(per_launch.sum()), 4),
+                     "algorithmic_bytes": int(sum(warp_bytes)),
+                     "per_stage_ms": [round(float(x), 4) for x in per_launch]})
+    if cr_ms:
+        per_launch = np.array(cr_ms).reshape(steps_p, -1).mean(0)
+        ach = sum(cr_flop) / (per_launch.sum() * 1e-3) / 1e12
+        kern.append({"kernel": "tmvs_costregnet", "bound": "mfma", "achieved": round(ach, 2),
+                     "peak": PEAK_F32_MFMA_TFS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_MFMA_TFS, 4),
+                     "traffic": None, "ms_per_depth_map": round(float(per_launch.sum()), 4),
+                     "algorithmic_flop": int(sum(cr_flop)),
+                     "per_stage_ms": [round(float(x), 4) for x in per_launch]})
+    dominant = max(kern, key=lambda k: k["ms_per_depth_map"]) if kern else None
+    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc))
+            for k in kern:
+                k["traffic"] = traffic.get(k["kernel"])
+        except Exception:
+            pass
+
+    cpu = None
+    l1 = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, l1 = cpu_baseline(args.cpu_threads, feats_cpu, proj, dv, out)
+
+    if rank == 0:
+        line = {
+            "metric": "depth maps/sec @ DTU 864x1152 N=5 (48/32/8 hyp); Abs depth L1 vs ref",
+            "value": round(value, 3),
+            "unit": "depth_maps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak" if args.mode == "replica" else "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded FeatureNet-shaped features, DTU-like cameras, key-seeded random weights)",
+            "config": {"workload": "DTU 864x1152, N=5 views, cascade 48/32/8, B=1, hot path from FeatureNet "
+                                   "outputs (FMT+pathway+stage glue+cost volume+CostRegNet+softmax/WTA)",
+                       "global_batch": maps_per_step, "parallelism": f"{args.mode}{world}"},
+            "roofline": dominant,
+            "roofline_kernels": kern,
+            "kernel_ms_per_depth_map": breakdown,
+            "cpu_baseline": cpu,
+            "abs_depth_l1_vs_ref": l1,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(threads, feats_cpu, proj, dv, gpu_out):
+    """The oracle (torch-CPU restatement of the reference forward) on the host cores.
+
+    Bounded sample: one full DTU depth map (same inputs/weights) after one untimed
+    repetition; also returns the mean |depth_gpu - depth_cpu| (the 'Abs depth L1 vs ref').
+    """
+    import platform
+
+    from oracle import transmvs_ref as oracle
+    from transmvsnet_amd import synthetic
+    torch.set_num_threads(threads)
+    from transmvsnet_amd import TransMVSNet
+    shapes = synthetic.state_dict_shapes(TransMVSNet())
+    sd = synthetic.synthetic_state_dict(shapes, seed=0, sharpen=100.0)
+    feats = [{k: v[:, i] for k, v in feats_cpu.items()} for i in range(NVIEWS)]
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        ref = oracle.forward_from_features(sd, feats, proj, dv, (H, W))
+        t1 = time.perf_counter()
+    d_gpu = gpu_out["depth"].float().cpu().numpy().astype(np.float64)
+    d_ref = ref["depth"].numpy().astype(np.float64)
+    l1 = float(np.abs(d_gpu - d_ref).mean())
+    cpu_model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return ({"value": round(1.0 / (t1 - t0), 5), "unit": "depth_maps/s", "cores": threads, "kind": "port",
+             "sample": f"1 DTU depth map (864x1152, N=5, 48/32/8) through the oracle's hot path, "
+                       f"{t1 - t0:.2f} s, torch-CPU fp32, {threads} threads, {cpu_model}"},
+            {"stage3_mean_abs_mm": l1,
+             "stage3_max_abs_mm": float(np.abs(d_gpu - d_ref).max()),
+             "stage3_frac_pixels_differing": float((np.abs(d_gpu - d_ref) > 1e-3).mean())})
+
+
+if __name__ == "__main__":
+    main()

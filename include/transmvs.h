@@ -1,0 +1,189 @@
+/*
+ * transmvs.h -- C-ABI of the MI355X-native TransMVSNet depth-inference hot path.
+ *
+ * The reference (delldu/TransMVSNet) is pure PyTorch; its "operator API" for this path is
+ * the set of Python callables the north star names. Each entry point below replaces one of
+ * them (reference file:line cited) and is what a ctypes / cffi / pybind binding binds
+ * (see INTEGRATION.md). Conventions, identical for every entry point:
+ *
+ *   - extern "C", stateless, re-entrant; no allocation and no host synchronisation inside
+ *     a call (graph-capturable); scratch memory is passed in by the caller.
+ *   - every tensor argument is a DEVICE pointer to fp32 data unless marked HOST; sizes and
+ *     strides are explicit ints; layouts are stated per argument. "NHWC" = channels-last.
+ *   - `stream` is a hipStream_t passed as void* (NULL = legacy default stream).
+ *   - return value: TMVS_OK (0) or a negative status (bad argument, unsupported shape,
+ *     HIP launch error); tmvs_status_string() names it. A failing call launches nothing
+ *     on bad arguments/shapes.
+ */
+#ifndef TRANSMVS_H_
+#define TRANSMVS_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TMVS_ABI_VERSION 1
+
+#define TMVS_OK 0
+#define TMVS_ERR_ARG (-1)    /* null pointer / non-positive size / bad enum        */
+#define TMVS_ERR_SHAPE (-2)  /* shape the kernels do not support (e.g. D % 8 != 0) */
+#define TMVS_ERR_HIP (-3)    /* hipGetLastError() reported a launch failure       */
+
+#define TMVS_MAX_VIEWS 16    /* source views per warp_corr launch                  */
+
+int tmvs_abi_version(void);
+const char* tmvs_status_string(int status);
+
+/* ------------------------------------------------------------------ host helpers
+ * Eval-mode BatchNorm as the reference's PyTorch-CPU kernel evaluates it
+ * (nn.BatchNorm{2,3}d, models/module.py:132,173,218):
+ *   alpha = (1 / sqrtf(var + eps)) * gamma;   shift = fmaf(-mean, alpha, beta);
+ *   y     = fmaf(x, alpha, shift).
+ * All pointers HOST. */
+int tmvs_bn_fold(const float* gamma, const float* beta, const float* mean, const float* var, int n, float eps,
+                 float* alpha, float* shift);
+
+/* ------------------------------------------------------------------ stage glue
+ * Depth hypotheses of one cascade stage: get_depth_samples (models/module.py:606-634) plus
+ * the bilinear up-sampling of the previous stage's depth and the trilinear resampling to
+ * the stage resolution (models/TransMVSNet.py:147-149,174-204), fused, without the
+ * full-resolution [B,D,H,W] intermediate.
+ *   depth_values : [B][n_values]     (the forward's depth_values input; [0,0] and [0,-1] of
+ *                                     batch 0 give depth_interval, as at TransMVSNet.py:147-149)
+ *   prev_depth   : [B][prev_h][prev_w] previous stage's UNCLAMPED WTA depth, or NULL (stage 1)
+ *   ndepth, ratio: this stage's hypothesis count and interval ratio (TransMVSNet.py:113-114)
+ *   full_h/full_w: image size; stage_scale: 4, 2 or 1 (TransMVSNet.py:128-132)
+ *   hyp_out      : [B][ndepth][full_h/stage_scale][full_w/stage_scale]                      */
+int tmvs_stage_hypotheses(const float* depth_values, int n_values, const float* prev_depth, int prev_h, int prev_w,
+                          int batch, int ndepth, float ratio, int full_h, int full_w, int stage_scale,
+                          float* hyp_out, void* stream);
+
+/* ------------------------------------------------------------------ cost volume
+ * Fused DepthNet steps 1-2 (models/TransMVSNet.py:58-93): for every source view the
+ * homography warp + bilinear grid_sample of homo_warping (models/module.py:284-322), the
+ * single-group correlation (warped*ref).mean(C) (TransMVSNet.py:80), the stage-1 view
+ * weight PixelwiseNet (TransMVSNet.py:10-30) or the given up-sampled weights (:86), and the
+ * weighted view aggregation Σ w·sim / (1e-5 + Σ w) (:71-72,88-93). The [C,D,H,W] warped
+ * volume is never materialised.
+ *   ref_fea      : [B][H][W][C] (NHWC)      src_fea : [B][V][H][W][C] (NHWC)
+ *   proj         : HOST [B][V][12] = rows of (P_src · P_ref^-1)[:3,:4]  (module.py:295-297)
+ *   hyp          : [B][D][H][W]
+ *   view_w_in    : NULL (stage 1: compute with PixelwiseNet) or [B][vw_total][H>>vw_shift][W>>vw_shift]
+ *                  (stages 2/3: nearest x2^vw_shift up-sampling, TransMVSNet.py:194);
+ *                  this call's views are vw_offset .. vw_offset+V-1 of it
+ *   pw_params    : HOST, TMVS_PW_NPARAMS floats (layout below), used when view_w_in == NULL
+ *   flags        : TMVS_WARP_PARTIAL -> write sim_out = Σ_v w_v·sim_v and wsum_out = Σ_v w_v
+ *                  undivided (view-sharded mode; finish with tmvs_aggregate_finalize after the
+ *                  all-reduce); 0 -> sim_out = the reference's normalised similarity.
+ *   sim_out      : [B][D][H][W]       wsum_out : [B][H][W] (PARTIAL only, else may be NULL)
+ *   view_w_out   : [B][vw_total][H][W] written at vw_offset.. when view_w_in == NULL
+ * Supported: C in {8,16,32}; D % 4 == 0 (D <= 64 per pass); 1 <= V <= TMVS_MAX_VIEWS.     */
+#define TMVS_WARP_PARTIAL 1
+#define TMVS_PW_NPARAMS 201 /* w0[16] a0[16] s0[16] w1[8][16] a1[8] s1[8] w2[8] b2 */
+int tmvs_warp_corr(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,
+                   const float* view_w_in, int vw_shift, int vw_offset, int vw_total, const float* pw_params,
+                   int batch, int n_src, int channels, int ndepth, int height, int width, int flags,
+                   float* sim_out, float* wsum_out, float* view_w_out, void* stream);
+
+/* sim = sim_sum / (1e-5 + w_sum) after a cross-rank all-reduce of both (TransMVSNet.py:72,93). */
+int tmvs_aggregate_finalize(float* sim_sum, const float* w_sum, int batch, int ndepth, int height, int width,
+                            void* stream);
+
+/* Materialising homo_warping (models/module.py:284-322) for the reference seam / tests:
+ *   src_fea [B][C][H][W] (NCHW), proj HOST [B][12], hyp [B][D][H][W] -> out [B][C][D][H][W]. */
+int tmvs_homo_warping(const float* src_fea, const float* proj, const float* hyp, int batch, int channels,
+                      int ndepth, int height, int width, float* out, void* stream);
+
+/* ------------------------------------------------------------------ CostRegNet
+ * 3-D U-Net of models/module.py:425-456 on an NDHWC volume, eval-mode BN folded into a
+ * per-channel (alpha, shift) epilogue (tmvs_bn_fold). Weight packing ("packed" below):
+ *   Conv3d weight [Co][Ci][3][3][3]          -> [27][Co][Ci]  (tap = kd*9+kh*3+kw)
+ *   ConvTranspose3d weight [Ci][Co][3][3][3] -> [27][Co][Ci]
+ * conv0 (Ci=1) and prob (Co=1) keep their natural [Co][Ci][27] order.                     */
+typedef struct {
+  const float* w[11];      /* conv0..conv6, conv7, conv9, conv11 (packed), prob [1][8][27]  */
+  const float* alpha[10];  /* BN alpha of the first 10 layers                              */
+  const float* shift[10];  /* BN shift                                                     */
+  int base_ch;             /* cr_base_chs (models/TransMVSNet.py:115), 8                   */
+} TmvsCostRegWeights;
+
+/* bytes of scratch tmvs_costregnet needs for a [B][D][H][W] volume */
+size_t tmvs_costregnet_workspace(int batch, int depth, int height, int width, int base_ch);
+/* x: [B][D][H][W] (=NDHWC with C=1), logits: [B][D][H][W]. Needs D,H,W % 8 == 0. */
+int tmvs_costregnet(const float* x, int batch, int depth, int height, int width, const TmvsCostRegWeights* w,
+                    void* workspace, size_t workspace_bytes, float* logits, void* stream);
+
+/* Single layers (Conv3d / Deconv3d blocks, models/module.py:108-191), NDHWC in and out.
+ * conv: stride 1 or 2, padding 1;  y = relu(fmaf(conv, alpha, shift)).
+ * deconv: ConvTranspose3d k3 s2 p1 op1 (output 2x input);  y = skip + relu(fmaf(...)).    */
+int tmvs_conv3d_bn_relu(const float* x, int batch, int cin, int d, int h, int w, const float* wpk, const float* alpha,
+                        const float* shift, int cout, int stride, float* y, void* stream);
+int tmvs_deconv3d_bn_relu_add(const float* x, int batch, int cin, int d, int h, int w, const float* wpk,
+                              const float* alpha, const float* shift, int cout, const float* skip, float* y,
+                              void* stream);
+
+/* ------------------------------------------------------------------ regression
+ * prob = exp(log_softmax(logits, D)) (TransMVSNet.py:99); winner-take-all
+ * argmax (first maximum) + gather (module.py:474-482, TransMVSNet.py:217-218);
+ * photo_confidence = max_D prob (:103); depth clamped to [clamp_lo, clamp_hi] (:221).
+ *   logits, hyp, prob: [B][D][H][W];  depth (clamped), depth_raw (unclamped), conf: [B][H][W] */
+int tmvs_softmax_wta(const float* logits, const float* hyp, int batch, int ndepth, int height, int width,
+                     float clamp_lo, float clamp_hi, float* prob, float* depth, float* depth_raw, float* conf,
+                     void* stream);
+
+/* ------------------------------------------------------------------ FMT
+ * Feature Matching Transformer (models/FMT.py), d_model 32, 8 heads x 4, linear attention.
+ * Tokens are [nv][L][32] (= NHWC of the stage-1 map). Packed EncoderLayer weights
+ * (TMVS_ENC_NPARAMS floats, offsets TMVS_ENC_*):
+ *   Wq[32][32] bq[32] Wk[32][32] bk[32] Wv[32][32] bv[32] Wo[32][32] bo[32]
+ *   W1[64][32] b1[64] W2[32][64] b2[32] ln1_g[32] ln1_b[32] ln2_g[32] ln2_b[32]            */
+#define TMVS_ENC_WQ 0
+#define TMVS_ENC_BQ 1024
+#define TMVS_ENC_WK 1056
+#define TMVS_ENC_BK 2080
+#define TMVS_ENC_WV 2112
+#define TMVS_ENC_BV 3136
+#define TMVS_ENC_WO 3168
+#define TMVS_ENC_BO 4192
+#define TMVS_ENC_W1 4224
+#define TMVS_ENC_B1 6272
+#define TMVS_ENC_W2 6336
+#define TMVS_ENC_B2 8384
+#define TMVS_ENC_LN1G 8416
+#define TMVS_ENC_LN1B 8448
+#define TMVS_ENC_LN2G 8480
+#define TMVS_ENC_LN2B 8512
+#define TMVS_ENC_NPARAMS 8544
+#define TMVS_KV_NFLOATS 160 /* per view: KV[8 heads][4 m][4 d] then Ksum[8][4] */
+
+/* x + PositionEncodingSine (models/position_encoding.py:55-60) and 'n c h w -> n (h w) c'
+ * (FMT.py:152,168):  feat [nv][C][H][W] (NCHW, per-view stride feat_view_stride floats),
+ * pe [C][pe_h][pe_w] -> tokens [nv][H*W][C]. */
+int tmvs_fmt_embed(const float* feat, long feat_view_stride, const float* pe, int pe_h, int pe_w, int nv,
+                   int channels, int height, int width, float* tokens, void* stream);
+/* bytes of scratch for tmvs_fmt_kv over nv views of S tokens */
+size_t tmvs_fmt_kv_workspace(int nv, int s_tokens);
+/* K = elu(Wk x + bk) + 1, V = Wv x + bv over the source tokens; KV = Σ_s K⊗V, Ksum = Σ_s K
+ * (FMT.py:23-32). source [nv][S][32] -> kv [nv][TMVS_KV_NFLOATS]. */
+int tmvs_fmt_kv(const float* source, int nv, int s_tokens, const float* enc_w, void* workspace,
+                size_t workspace_bytes, float* kv, void* stream);
+/* The rest of EncoderLayer.forward (FMT.py:96-111, AttentionLayer :56-75, LinearAttention
+ * :22-37) per query token, in place on x [nv][L][32]. kv_view_stride = 0 shares one kv
+ * (cross layers: the ref view's K/V serve every source view). */
+int tmvs_fmt_apply(float* x, int nv, int l_tokens, const float* kv, long kv_view_stride, const float* enc_w,
+                   void* stream);
+
+/* FMT_with_pathway lateral step (models/FMT.py:221-228): out = smooth(up2(reduce(coarse)) + lateral)
+ *   coarse [nv][h][w][cc] (NHWC), lateral [nv][cf][2h][2w] (NCHW, per-view stride lat_view_stride),
+ *   w_reduce [cf][cc] (1x1 conv, no bias), w_smooth [cf][cf][3][3] (3x3, pad 1, no bias)
+ *   -> out [nv][2h][2w][cf] (NHWC).  Supported (cc,cf): (32,16), (16,8).                  */
+int tmvs_fmt_pathway(const float* coarse, const float* lateral, long lat_view_stride, const float* w_reduce,
+                     const float* w_smooth, int nv, int cc, int cf, int h, int w, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TRANSMVS_H_ */

@@ -1,0 +1,241 @@
+"""HIP path vs the CPU oracle / golden vectors (needs an MI355X; run with -m gpu).
+
+Tolerances (fp32 throughout; stated per check):
+  * cost volume similarity, PixelwiseNet view weights, pathway features: 2e-5 abs
+    (same op order as the reference except the channel-sum order of the correlation mean)
+  * CostRegNet logits: 2e-5 relative to the volume's max |logit| (MFMA k-order vs mkldnn order)
+  * probabilities: 1e-5 abs;  FMT tokens: 1e-4 abs (LayerNorm'd, O(1) values)
+  * hypotheses of the stage glue: bit-exact (same fp32 op sequence)
+  * depth: identical argmax except at near-ties (top-2 log-prob margin < 1e-4),
+    and mean |Δdepth| <= 1e-4 mm (the north-star bar)
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import transmvs_ref as oracle
+from transmvsnet_amd import TransMVSNet, ops, synthetic
+from tests._util import depth_parity, golden, golden_state_dict, to_np
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def sd():
+    return golden_state_dict()
+
+
+@pytest.fixture(scope="module")
+def model(sd):
+    m = TransMVSNet(ndepths=[8, 8, 8]).eval()
+    m.load_state_dict(sd, strict=True)
+    return m.to(DEV)
+
+
+def _nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def test_library_loads_on_gpu():
+    from transmvsnet_amd import _lib
+    assert _lib.load().tmvs_abi_version() == _lib.ABI_VERSION
+    assert torch.cuda.is_available()
+
+
+def test_homo_warping_seam():
+    g = golden("ops.npz")
+    p = torch.from_numpy(g["warp_proj"])
+    out = ops.homo_warping(torch.from_numpy(g["warp_src"]).to(DEV), oracle.compose_proj(p[:, 1]),
+                           oracle.compose_proj(p[:, 0]), torch.from_numpy(g["warp_hyp"]).to(DEV))
+    np.testing.assert_allclose(to_np(out), g["warp_out"], rtol=0, atol=2e-5)
+
+
+@pytest.mark.parametrize("c,d", [(8, 8), (16, 32), (32, 48)])
+def test_warp_corr_stage1_mode(sd, c, d):
+    """Fused warp+corr+PixelwiseNet+aggregation vs oracle build_cost_volume (3 src views)."""
+    torch.manual_seed(c + d)
+    n, h, w = 4, 24, 40
+    feats = [torch.randn(1, c, h, w) for _ in range(n)]
+    proj = synthetic.synthetic_cameras(n, h * 4, w * 4, seed=5)["stage1"]
+    hyp = (torch.rand(1, d, h, w) * 500 + 425)
+    hyp[0, 0, :3] = -20.0  # behind camera
+    sim_ref, vw_ref = oracle.build_cost_volume(sd, feats, proj, hyp)
+    nh = [_nhwc(f).to(DEV) for f in feats]
+    src = torch.stack([x[0] for x in nh[1:]], 0).unsqueeze(0).contiguous()
+    sim, _, vw = ops.warp_corr(nh[0], src, ops.proj_rows(proj), hyp.to(DEV), pw_params=_pw_params(sd))
+    np.testing.assert_allclose(to_np(sim)[:, None], to_np(sim_ref), rtol=0, atol=2e-5)
+    np.testing.assert_allclose(to_np(vw), to_np(vw_ref), rtol=0, atol=2e-5)
+
+
+def _pw_params(sd):
+    m = TransMVSNet()
+    m.load_state_dict(sd, strict=True)
+    return m.DepthNet.pixel_wise_net.packed()
+
+
+@pytest.mark.parametrize("shift", [1, 2])
+def test_warp_corr_given_weights_and_partial(shift):
+    torch.manual_seed(shift)
+    n, h, w, c, d = 5, 32, 48, 8, 8
+    feats = [torch.randn(1, c, h, w) for _ in range(n)]
+    proj = synthetic.synthetic_cameras(n, h, w, seed=6)["stage3"]
+    hyp = torch.rand(1, d, h, w) * 500 + 425
+    vw = torch.rand(1, n - 1, h >> shift, w >> shift)
+    vw_up = vw
+    for _ in range(shift):
+        vw_up = F.interpolate(vw_up, scale_factor=2, mode="nearest")
+    sim_ref, _ = oracle.build_cost_volume({}, feats, proj, hyp, view_weights=vw_up)
+    nh = [_nhwc(f).to(DEV) for f in feats]
+    src = torch.stack([x[0] for x in nh[1:]], 0).unsqueeze(0).contiguous()
+    rows = ops.proj_rows(proj)
+    sim, _, _ = ops.warp_corr(nh[0], src, rows, hyp.to(DEV), view_w_in=vw.to(DEV), vw_shift=shift)
+    np.testing.assert_allclose(to_np(sim)[:, None], to_np(sim_ref), rtol=0, atol=2e-5)
+    # view-sharded form: two partial sums (views 0-1 and 2-3) + finalize == unsharded
+    s_a, w_a, _ = ops.warp_corr(nh[0], src[:, :2].contiguous(), rows[:, :2], hyp.to(DEV), view_w_in=vw.to(DEV),
+                                vw_shift=shift, vw_offset=0, vw_total=4, partial=True)
+    s_b, w_b, _ = ops.warp_corr(nh[0], src[:, 2:].contiguous(), rows[:, 2:], hyp.to(DEV), view_w_in=vw.to(DEV),
+                                vw_shift=shift, vw_offset=2, vw_total=4, partial=True)
+    fin = ops.aggregate_finalize(s_a + s_b, w_a + w_b)
+    np.testing.assert_allclose(to_np(fin), to_np(sim), rtol=0, atol=2e-6)
+
+
+def test_costregnet_matches_golden(model):
+    g = golden("ops.npz")
+    x = torch.from_numpy(g["costreg_in"])[:, 0].to(DEV).contiguous()
+    st, _keep = model.cost_regularization[0].packed(DEV)
+    out = to_np(ops.costregnet(x, st))
+    ref = g["costreg_out"][:, 0]
+    scale = np.abs(ref).max()
+    assert np.abs(out - ref).max() <= 2e-5 * scale, (np.abs(out - ref).max(), scale)
+
+
+@pytest.mark.parametrize("layer,stride", [("conv1", 2), ("conv2", 1), ("conv3", 2), ("conv4", 1), ("conv5", 2),
+                                          ("conv6", 1)])
+def test_conv3d_layers(sd, model, layer, stride):
+    blk = getattr(model.cost_regularization[1], layer)
+    w = blk.conv.weight.detach().cpu()
+    co, ci = w.shape[:2]
+    x = torch.randn(1, ci, 8, 12, 20)
+    p = f"cost_regularization.1.{layer}."
+    ref = F.relu(F.batch_norm(F.conv3d(x, w, stride=stride, padding=1), sd[p + "bn.running_mean"],
+                              sd[p + "bn.running_var"], sd[p + "bn.weight"], sd[p + "bn.bias"], False, 0.1, 1e-5))
+    st, keep = model.cost_regularization[1].packed(DEV)
+    idx = int(layer[4:])
+    xin = x.permute(0, 2, 3, 4, 1).contiguous().to(DEV)
+    y = ops.conv3d_bn_relu(xin, keep[idx], keep[11 + idx], keep[21 + idx], co, stride)
+    np.testing.assert_allclose(to_np(y), ref.permute(0, 2, 3, 4, 1).numpy(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("layer,idx", [("conv7", 7), ("conv9", 8), ("conv11", 9)])
+def test_deconv3d_layers(sd, model, layer, idx):
+    blk = getattr(model.cost_regularization[1], layer)
+    w = blk.conv.weight.detach().cpu()
+    ci, co = w.shape[:2]
+    x = torch.randn(1, ci, 4, 6, 10)
+    skip = torch.randn(1, co, 8, 12, 20)
+    p = f"cost_regularization.1.{layer}."
+    y_ref = skip + F.relu(F.batch_norm(F.conv_transpose3d(x, w, stride=2, padding=1, output_padding=1),
+                                       sd[p + "bn.running_mean"], sd[p + "bn.running_var"], sd[p + "bn.weight"],
+                                       sd[p + "bn.bias"], False, 0.1, 1e-5))
+    st, keep = model.cost_regularization[1].packed(DEV)
+    y = ops.deconv3d_bn_relu_add(x.permute(0, 2, 3, 4, 1).contiguous().to(DEV), keep[idx], keep[11 + idx],
+                                 keep[21 + idx], co, skip.permute(0, 2, 3, 4, 1).contiguous().to(DEV))
+    np.testing.assert_allclose(to_np(y), y_ref.permute(0, 2, 3, 4, 1).numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_softmax_wta_ties():
+    g = golden("ops.npz")
+    prob, depth, raw, conf = ops.softmax_wta(torch.from_numpy(g["wta_logits"]).to(DEV),
+                                             torch.from_numpy(g["wta_hyp"]).to(DEV), clamp=(-1e30, 1e30))
+    np.testing.assert_allclose(to_np(prob), g["wta_prob"], rtol=0, atol=1e-6)
+    np.testing.assert_array_equal(to_np(depth), g["wta_depth"])
+    np.testing.assert_allclose(to_np(conf), g["wta_conf"], rtol=0, atol=1e-6)
+
+
+def test_stage_hypotheses_bitexact():
+    g = golden("ops.npz")
+    dv = synthetic.synthetic_depth_values(1).to(DEV)
+    h2 = ops.stage_hypotheses(dv, torch.from_numpy(g["glue2_prev"]).to(DEV), 32, 1.0, (64, 80), 2)
+    np.testing.assert_array_equal(to_np(h2), g["glue2_hyp"])
+    h3 = ops.stage_hypotheses(dv, torch.from_numpy(g["glue3_prev"]).to(DEV), 8, 0.5, (64, 80), 1)
+    np.testing.assert_array_equal(to_np(h3), g["glue3_hyp"])
+    h1 = ops.stage_hypotheses(dv, None, 48, 4.0, (64, 80), 4)
+    ref = oracle.stage_hypotheses(None, synthetic.synthetic_depth_values(1), 0, (64, 80))
+    np.testing.assert_array_equal(to_np(h1), ref.numpy())
+
+
+def test_fmt_encoder_layer(model):
+    g = golden("ops.npz")
+    enc = model.FMT_with_pathway.FMT.layers[1].packed().to(DEV)
+    x = torch.from_numpy(g["enc_x"]).to(DEV).contiguous()
+    src = torch.from_numpy(g["enc_src"]).to(DEV).contiguous()
+    kv = ops.fmt_kv(src, enc)
+    ops.fmt_apply(x, kv, enc)
+    np.testing.assert_allclose(to_np(x), g["enc_out"], rtol=0, atol=1e-4)
+
+
+def test_fmt_pathway(sd, model):
+    torch.manual_seed(3)
+    coarse = torch.randn(2, 32, 12, 20)
+    lat = torch.randn(2, 16, 24, 40)
+    ref = F.conv2d(F.interpolate(F.conv2d(coarse, sd["FMT_with_pathway.dim_reduction_1.weight"]), size=(24, 40),
+                                 mode="bilinear") + lat, sd["FMT_with_pathway.smooth_1.weight"], padding=1)
+    prep = model._prepared(torch.device(DEV))
+    out = ops.fmt_pathway(coarse.permute(0, 2, 3, 1).contiguous().to(DEV), lat.to(DEV), prep["red1"], prep["sm1"])
+    np.testing.assert_allclose(to_np(out), ref.permute(0, 2, 3, 1).numpy(), rtol=0, atol=2e-5)
+
+
+def _e2e_check(out, vw, g, stages=(1, 2, 3)):
+    report = {}
+    for s in stages:
+        o = out[f"stage{s}"]
+        pref = g.get(f"stage{s}_prob")
+        if pref is not None:
+            mean_l1, near, flips = depth_parity(to_np(o["depth"]), g[f"stage{s}_depth"], pref)
+            if s == 1:
+                np.testing.assert_array_equal(to_np(o["depth_values"]), g[f"stage{s}_hyp"])
+            report[s] = (mean_l1, near, flips)
+            assert flips == 0, (s, report[s])
+        mean_l1 = float(np.abs(to_np(o["depth"]).astype(np.float64) - g[f"stage{s}_depth"]).mean())
+        report[f"l1_{s}"] = mean_l1
+    assert report["l1_3"] <= 1e-4, report
+    if vw is not None:
+        np.testing.assert_allclose(to_np(vw), g["view_weights"], rtol=0, atol=1e-4)
+    return report
+
+
+def test_e2e_c1_features(model):
+    g = golden("e2e_c1_features.npz")
+    H, W, N = 128, 160, 3
+    feats = [{k: v.to(DEV) for k, v in f.items()} for f in synthetic.synthetic_features(N, H, W, seed=2)]
+    out, vw = model.forward_features(feats, synthetic.synthetic_cameras(N, H, W, seed=1),
+                                     synthetic.synthetic_depth_values(1).to(DEV), (H, W), return_view_weights=True)
+    rep = _e2e_check(out, vw, g)
+    for s in (1, 2, 3):
+        np.testing.assert_allclose(to_np(out[f"stage{s}"]["prob_volume"]), g[f"stage{s}_prob"], rtol=0, atol=1e-3)
+    print("e2e c1", rep)
+
+
+def test_e2e_cascade_48_32_8(sd):
+    g = golden("e2e_cascade_256x320.npz")
+    m = TransMVSNet().eval()
+    m.load_state_dict(sd, strict=True)
+    m = m.to(DEV)
+    H, W, N = 256, 320, 3
+    feats = [{k: v.to(DEV) for k, v in f.items()} for f in synthetic.synthetic_features(N, H, W, seed=2)]
+    out, vw = m.forward_features(feats, synthetic.synthetic_cameras(N, H, W, seed=1),
+                                 synthetic.synthetic_depth_values(1).to(DEV), (H, W), return_view_weights=True)
+    print("e2e cascade", _e2e_check(out, vw, g))
+
+
+def test_e2e_images_full_forward(model):
+    g = golden("e2e_c1_imgs.npz")
+    H, W, N = 128, 160, 3
+    with torch.no_grad():
+        out = model(synthetic.synthetic_images(N, H, W, seed=0).to(DEV), synthetic.synthetic_cameras(N, H, W, seed=1),
+                    synthetic.synthetic_depth_values(1).to(DEV))
+    l1 = float(np.abs(to_np(out["depth"]).astype(np.float64) - g["stage3_depth"]).mean())
+    assert l1 <= 1e-4, l1
+    assert set(out) == {"stage1", "stage2", "stage3", "depth", "photo_confidence", "prob_volume", "depth_values"}

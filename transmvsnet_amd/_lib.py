@@ -1,0 +1,77 @@
+"""ctypes binding of the C-ABI in include/transmvs.h (libtransmvs_hip.so, built in-tree).
+
+There is no fallback: if the library is missing or fails to load, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtransmvs_hip.so")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_long
+F = ctypes.c_float
+S = ctypes.c_size_t
+
+# name -> (restype, argtypes); every symbol include/transmvs.h declares
+SIGNATURES = {
+    "tmvs_abi_version": (I, []),
+    "tmvs_status_string": (ctypes.c_char_p, [I]),
+    "tmvs_bn_fold": (I, [P, P, P, P, I, F, P, P]),
+    "tmvs_stage_hypotheses": (I, [P, I, P, I, I, I, I, F, I, I, I, P, P]),
+    "tmvs_warp_corr": (I, [P, P, P, P, P, I, I, I, P, I, I, I, I, I, I, I, P, P, P, P]),
+    "tmvs_aggregate_finalize": (I, [P, P, I, I, I, I, P]),
+    "tmvs_homo_warping": (I, [P, P, P, I, I, I, I, I, P, P]),
+    "tmvs_costregnet_workspace": (S, [I, I, I, I, I]),
+    "tmvs_costregnet": (I, [P, I, I, I, I, P, P, S, P, P]),
+    "tmvs_conv3d_bn_relu": (I, [P, I, I, I, I, I, P, P, P, I, I, P, P]),
+    "tmvs_deconv3d_bn_relu_add": (I, [P, I, I, I, I, I, P, P, P, I, P, P, P]),
+    "tmvs_softmax_wta": (I, [P, P, I, I, I, I, F, F, P, P, P, P, P]),
+    "tmvs_fmt_embed": (I, [P, L, P, I, I, I, I, I, I, P, P]),
+    "tmvs_fmt_kv_workspace": (S, [I, I]),
+    "tmvs_fmt_kv": (I, [P, I, I, P, P, S, P, P]),
+    "tmvs_fmt_apply": (I, [P, I, I, P, L, P, P]),
+    "tmvs_fmt_pathway": (I, [P, P, L, P, P, I, I, I, I, I, P, P]),
+}
+
+ABI_VERSION = 1
+PW_NPARAMS = 201
+ENC_NPARAMS = 8544
+KV_NFLOATS = 160
+WARP_PARTIAL = 1
+
+
+class CostRegWeights(ctypes.Structure):
+    """TmvsCostRegWeights (include/transmvs.h)."""
+    _fields_ = [("w", P * 11), ("alpha", P * 10), ("shift", P * 10), ("base_ch", I)]
+
+
+_lib = None
+
+
+def load():
+    """Load and type the library; raises RuntimeError when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"transmvsnet_amd HIP extension not built ({LIB_PATH} missing): "
+                           "run `python -m transmvsnet_amd.build`")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.tmvs_abi_version() != ABI_VERSION:
+        raise RuntimeError("libtransmvs_hip.so ABI version mismatch; rebuild it")
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str):
+    if status != 0:
+        msg = load().tmvs_status_string(status).decode()
+        raise RuntimeError(f"{what} failed: {msg} ({status})")

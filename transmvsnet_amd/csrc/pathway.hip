@@ -1,0 +1,134 @@
+// FMT_with_pathway lateral step (models/FMT.py:195-228), fused:
+//   out = smooth(bilinear_up2(reduce(coarse)) + lateral)
+// reduce = 1x1 conv (no bias), bilinear align_corners=False (F.interpolate default, :209),
+// smooth = 3x3 conv pad 1 (no bias). A workgroup owns a 16x16 output tile: it reduces the
+// 10x10 coarse pixels the tile's 18x18 halo interpolates from into LDS, builds the up-sampled
+// + lateral halo in LDS, then each thread convolves one output pixel for all channels and
+// writes it channels-last -- the layout the cost-volume kernel gathers from.
+#include "common.h"
+
+namespace tmvs {
+
+constexpr int kTile = 16;
+constexpr int kHalo = kTile + 2;
+constexpr int kCoarse = kTile / 2 + 2;
+
+struct Axis {
+  int i0, i1;
+  float l0, l1;
+};
+
+__device__ __forceinline__ Axis up_axis(int dst, int in_size, int out_size) {
+  const float scale = (float)in_size / (float)out_size;
+  float src = scale * ((float)dst + 0.5f) - 0.5f;
+  src = src < 0.f ? 0.f : src;
+  Axis a;
+  a.i0 = min((int)floorf(src), in_size - 1);
+  a.i1 = a.i0 + (a.i0 < in_size - 1 ? 1 : 0);
+  const float l = fminf(fmaxf(src - (float)a.i0, 0.f), 1.f);
+  a.l1 = l;
+  a.l0 = 1.f - l;
+  return a;
+}
+
+template <int CC, int CF>
+__global__ __launch_bounds__(256) void pathway_kernel(const float* __restrict__ coarse,
+                                                      const float* __restrict__ lateral, long lat_stride,
+                                                      const float* __restrict__ wred,
+                                                      const float* __restrict__ wsm, int h, int w,
+                                                      float* __restrict__ out) {
+  __shared__ float red[CF][kCoarse][kCoarse + 1];
+  __shared__ float inb[CF][kHalo][kHalo + 1];
+  const int H = 2 * h, W = 2 * w;
+  const int v = blockIdx.z;
+  const int y0 = blockIdx.y * kTile, x0 = blockIdx.x * kTile;
+  const int cy0 = y0 / 2 - 1, cx0 = x0 / 2 - 1;
+  const float* cv = coarse + (size_t)v * h * w * CC;
+  // 1) 1x1 reduction of the coarse patch
+  for (int idx = threadIdx.x; idx < kCoarse * kCoarse; idx += blockDim.x) {
+    const int r = idx / kCoarse, c = idx - r * kCoarse;
+    const int cy = cy0 + r, cx = cx0 + c;
+    if (cy < 0 || cy >= h || cx < 0 || cx >= w) continue;
+    float xin[CC];
+    const float* p = cv + ((size_t)cy * w + cx) * CC;
+#pragma unroll
+    for (int i4 = 0; i4 < CC / 4; ++i4) {
+      const float4 t = *reinterpret_cast<const float4*>(p + 4 * i4);
+      xin[4 * i4] = t.x;
+      xin[4 * i4 + 1] = t.y;
+      xin[4 * i4 + 2] = t.z;
+      xin[4 * i4 + 3] = t.w;
+    }
+#pragma unroll
+    for (int o = 0; o < CF; ++o) {
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < CC; ++i) acc = fmaf(wred[o * CC + i], xin[i], acc);
+      red[o][r][c] = acc;
+    }
+  }
+  __syncthreads();
+  // 2) bilinear x2 up-sampling + lateral over the 18x18 halo (zero outside the image)
+  const float* lv = lateral + (size_t)v * lat_stride;
+  for (int idx = threadIdx.x; idx < kHalo * kHalo; idx += blockDim.x) {
+    const int r = idx / kHalo, c = idx - r * kHalo;
+    const int y = y0 - 1 + r, x = x0 - 1 + c;
+    if (y < 0 || y >= H || x < 0 || x >= W) {
+#pragma unroll
+      for (int o = 0; o < CF; ++o) inb[o][r][c] = 0.f;
+      continue;
+    }
+    const Axis ay = up_axis(y, h, H), ax = up_axis(x, w, W);
+    const int r0 = ay.i0 - cy0, r1 = ay.i1 - cy0, c0 = ax.i0 - cx0, c1 = ax.i1 - cx0;
+#pragma unroll
+    for (int o = 0; o < CF; ++o) {
+      const float t0 = fmaf(red[o][r0][c0], ax.l0, red[o][r0][c1] * ax.l1);
+      const float t1 = fmaf(red[o][r1][c0], ax.l0, red[o][r1][c1] * ax.l1);
+      const float up = fmaf(t0, ay.l0, t1 * ay.l1);
+      inb[o][r][c] = up + lv[((size_t)o * H + y) * W + x];
+    }
+  }
+  __syncthreads();
+  // 3) 3x3 smoothing conv, one output pixel per thread
+  const int ty = threadIdx.x / kTile, tx = threadIdx.x - ty * kTile;
+  const int y = y0 + ty, x = x0 + tx;
+  if (y >= H || x >= W) return;
+  float acc[CF];
+#pragma unroll
+  for (int o = 0; o < CF; ++o) acc[o] = 0.f;
+#pragma unroll
+  for (int i = 0; i < CF; ++i) {
+    float win[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) win[k] = inb[i][ty + k / 3][tx + k % 3];
+#pragma unroll
+    for (int o = 0; o < CF; ++o)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc[o] = fmaf(wsm[(o * CF + i) * 9 + k], win[k], acc[o]);
+  }
+  float4* op = reinterpret_cast<float4*>(out + (((size_t)v * H + y) * W + x) * CF);
+#pragma unroll
+  for (int o4 = 0; o4 < CF / 4; ++o4) op[o4] = make_float4(acc[4 * o4], acc[4 * o4 + 1], acc[4 * o4 + 2], acc[4 * o4 + 3]);
+}
+
+}  // namespace tmvs
+
+using namespace tmvs;
+
+extern "C" int tmvs_fmt_pathway(const float* coarse, const float* lateral, long lat_view_stride,
+                                const float* w_reduce, const float* w_smooth, int nv, int cc, int cf, int h, int w,
+                                float* out, void* stream) {
+  if (!coarse || !lateral || !w_reduce || !w_smooth || !out || nv <= 0 || h <= 0 || w <= 0) return TMVS_ERR_ARG;
+  const dim3 grid((2 * w + kTile - 1) / kTile, (2 * h + kTile - 1) / kTile, nv);
+  hipStream_t st = (hipStream_t)stream;
+  if (cc == 32 && cf == 16)
+    hipLaunchKernelGGL((pathway_kernel<32, 16>), grid, dim3(256), 0, st, coarse, lateral, lat_view_stride, w_reduce,
+                       w_smooth, h, w, out);
+  else if (cc == 16 && cf == 8)
+    hipLaunchKernelGGL((pathway_kernel<16, 8>), grid, dim3(256), 0, st, coarse, lateral, lat_view_stride, w_reduce,
+                       w_smooth, h, w, out);
+  else
+    return TMVS_ERR_SHAPE;
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}

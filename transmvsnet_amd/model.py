@@ -1,0 +1,346 @@
+"""TransMVSNet drop-in (models/TransMVSNet.py:112-226) over the MI355X HIP hot path.
+
+``TransMVSNet`` has the reference's constructor, ``forward(imgs, proj_matrix, depth_values)``
+signature, output dict and state_dict key layout (465 keys; checkpoints load strict=True).
+Its submodules are parameter containers with the reference names; the depth-inference hot
+path -- FMT linear attention, the FMT pathway, stage glue, the fused warp + correlation +
+view-aggregation cost volume, CostRegNet and softmax/WTA -- runs as hand-written HIP kernels
+through the C-ABI (include/transmvs.h). Weights are re-laid-out once per load_state_dict into
+the kernels' packed formats (BN folded exactly as the reference CPU kernel folds it).
+FeatureNet stays on PyTorch-ROCm for now (featurenet.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib, ops
+from .featurenet import FeatureNet
+
+NDEPTHS = (48, 32, 8)
+RATIOS = (4.0, 1.0, 0.5)
+STAGE_SCALES = (4, 2, 1)
+DEPTH_CLAMP = (425.0, 935.0)
+FMT_LAYERS = ("self", "cross") * 4
+
+
+# ----------------------------------------------------------------- parameter containers
+class _AttentionLayer(nn.Module):
+    """AttentionLayer (models/FMT.py:40-54) parameters."""
+
+    def __init__(self, d=32):
+        super().__init__()
+        self.query_projection = nn.Linear(d, d)
+        self.key_projection = nn.Linear(d, d)
+        self.value_projection = nn.Linear(d, d)
+        self.out_projection = nn.Linear(d, d)
+
+
+class EncoderLayer(nn.Module):
+    """EncoderLayer (models/FMT.py:78-94) parameters; forward runs in fmt.hip."""
+
+    def __init__(self, d=32):
+        super().__init__()
+        self.attention = _AttentionLayer(d)
+        self.linear1 = nn.Linear(d, 2 * d)
+        self.linear2 = nn.Linear(2 * d, d)
+        self.norm1 = nn.LayerNorm(d)
+        self.norm2 = nn.LayerNorm(d)
+
+    def packed(self):
+        a = self.attention
+        parts = [a.query_projection.weight, a.query_projection.bias, a.key_projection.weight, a.key_projection.bias,
+                 a.value_projection.weight, a.value_projection.bias, a.out_projection.weight, a.out_projection.bias,
+                 self.linear1.weight, self.linear1.bias, self.linear2.weight, self.linear2.bias,
+                 self.norm1.weight, self.norm1.bias, self.norm2.weight, self.norm2.bias]
+        flat = torch.cat([p.detach().float().reshape(-1) for p in parts])
+        assert flat.numel() == _lib.ENC_NPARAMS
+        return flat
+
+
+class FMT(nn.Module):
+    """FMT (models/FMT.py:114-129): 8 layers, self/cross alternating; sine PE (not persistent)."""
+
+    def __init__(self, d_model=32, nhead=8):
+        super().__init__()
+        self.d_model = d_model
+        self.nhead = nhead
+        self.layer_names = list(FMT_LAYERS)
+        self.layers = nn.ModuleList([EncoderLayer(d_model) for _ in FMT_LAYERS])
+
+
+class FMTWithPathway(nn.Module):
+    """FMT_with_pathway (models/FMT.py:183-199) parameters."""
+
+    def __init__(self, base_channels=8):
+        super().__init__()
+        b = base_channels
+        self.FMT = FMT(4 * b, 8)
+        self.dim_reduction_1 = nn.Conv2d(4 * b, 2 * b, 1, bias=False)
+        self.dim_reduction_2 = nn.Conv2d(2 * b, b, 1, bias=False)
+        self.smooth_1 = nn.Conv2d(2 * b, 2 * b, 3, padding=1, bias=False)
+        self.smooth_2 = nn.Conv2d(b, b, 3, padding=1, bias=False)
+
+
+class _ConvBn3d(nn.Module):
+    def __init__(self, cin, cout, k=3, stride=1, padding=1, transposed=False):
+        super().__init__()
+        if transposed:
+            self.conv = nn.ConvTranspose3d(cin, cout, k, stride=2, padding=1, output_padding=1, bias=False)
+        else:
+            self.conv = nn.Conv3d(cin, cout, k, stride=stride, padding=padding, bias=False)
+        self.bn = nn.BatchNorm3d(cout, momentum=0.1)
+
+
+class CostRegNet(nn.Module):
+    """CostRegNet (models/module.py:425-445) parameters; forward runs in costreg.hip."""
+
+    def __init__(self, in_channels=1, base_channels=8):
+        super().__init__()
+        b = base_channels
+        self.base_channels = b
+        self.conv0 = _ConvBn3d(in_channels, b)
+        self.conv1 = _ConvBn3d(b, 2 * b, stride=2)
+        self.conv2 = _ConvBn3d(2 * b, 2 * b)
+        self.conv3 = _ConvBn3d(2 * b, 4 * b, stride=2)
+        self.conv4 = _ConvBn3d(4 * b, 4 * b)
+        self.conv5 = _ConvBn3d(4 * b, 8 * b, stride=2)
+        self.conv6 = _ConvBn3d(8 * b, 8 * b)
+        self.conv7 = _ConvBn3d(8 * b, 4 * b, transposed=True)
+        self.conv9 = _ConvBn3d(4 * b, 2 * b, transposed=True)
+        self.conv11 = _ConvBn3d(2 * b, b, transposed=True)
+        self.prob = nn.Conv3d(b, 1, 3, stride=1, padding=1, bias=False)
+
+    def packed(self, device):
+        """Device tensors in TmvsCostRegWeights order (include/transmvs.h)."""
+        ws, als, shs = [], [], []
+
+        def conv_w(w):  # [Co][Ci][3,3,3] -> [27][Co][Ci]
+            co, ci = w.shape[:2]
+            return w.detach().float().reshape(co, ci, 27).permute(2, 0, 1).contiguous()
+
+        def deconv_w(w):  # [Ci][Co][3,3,3] -> [27][Co][Ci]
+            ci, co = w.shape[:2]
+            return w.detach().float().reshape(ci, co, 27).permute(2, 1, 0).contiguous()
+
+        names = ["conv0", "conv1", "conv2", "conv3", "conv4", "conv5", "conv6", "conv7", "conv9", "conv11"]
+        for i, n in enumerate(names):
+            blk = getattr(self, n)
+            w = blk.conv.weight
+            if i == 0:
+                ws.append(w.detach().float().reshape(w.shape[0], 27).contiguous())
+            elif i < 7:
+                ws.append(conv_w(w))
+            else:
+                ws.append(deconv_w(w))
+            a, s = ops.bn_fold(blk.bn.weight, blk.bn.bias, blk.bn.running_mean, blk.bn.running_var, blk.bn.eps)
+            als.append(torch.from_numpy(a))
+            shs.append(torch.from_numpy(s))
+        ws.append(self.prob.weight.detach().float().reshape(self.base_channels, 27).contiguous())
+        ws = [t.to(device) for t in ws]
+        als = [t.to(device) for t in als]
+        shs = [t.to(device) for t in shs]
+        st = _lib.CostRegWeights()
+        for i, t in enumerate(ws):
+            st.w[i] = t.data_ptr()
+        for i in range(10):
+            st.alpha[i] = als[i].data_ptr()
+            st.shift[i] = shs[i].data_ptr()
+        st.base_ch = self.base_channels
+        return st, ws + als + shs
+
+
+class _ConvBnReLU3D(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.conv = nn.Conv3d(cin, cout, 1, stride=1, padding=0, bias=False)
+        self.bn = nn.BatchNorm3d(cout)
+
+
+class PixelwiseNet(nn.Module):
+    """PixelwiseNet (models/TransMVSNet.py:10-18) parameters."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv0 = _ConvBnReLU3D(1, 16)
+        self.conv1 = _ConvBnReLU3D(16, 8)
+        self.conv2 = nn.Conv3d(8, 1, 1, stride=1, padding=0)
+
+    def packed(self):
+        a0, s0 = ops.bn_fold(self.conv0.bn.weight, self.conv0.bn.bias, self.conv0.bn.running_mean,
+                             self.conv0.bn.running_var, self.conv0.bn.eps)
+        a1, s1 = ops.bn_fold(self.conv1.bn.weight, self.conv1.bn.bias, self.conv1.bn.running_mean,
+                             self.conv1.bn.running_var, self.conv1.bn.eps)
+        f = lambda t: t.detach().float().cpu().reshape(-1).numpy()  # noqa: E731
+        out = np.concatenate([f(self.conv0.conv.weight), a0, s0, f(self.conv1.conv.weight), a1, s1,
+                              f(self.conv2.weight), f(self.conv2.bias)]).astype(np.float32)
+        assert out.size == _lib.PW_NPARAMS
+        return out
+
+
+class DepthNet(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.pixel_wise_net = PixelwiseNet()
+
+
+def position_encoding_sine(d_model, h, w, max_shape=(600, 600)):
+    """PositionEncodingSine buffer slice (models/position_encoding.py:28-60), same fp32 ops."""
+    pe = torch.zeros((d_model, *max_shape))
+    y_pos = torch.ones(max_shape).cumsum(0).float().unsqueeze(0)
+    x_pos = torch.ones(max_shape).cumsum(1).float().unsqueeze(0)
+    div = torch.exp(torch.arange(0, d_model // 2, 2).float() * (-math.log(10000.0) / (d_model // 2)))[:, None, None]
+    pe[0::4] = torch.sin(x_pos * div)
+    pe[1::4] = torch.cos(x_pos * div)
+    pe[2::4] = torch.sin(y_pos * div)
+    pe[3::4] = torch.cos(y_pos * div)
+    return pe[:, :h, :w].contiguous()
+
+
+# ----------------------------------------------------------------- the model
+class TransMVSNet(nn.Module):
+    def __init__(self, ndepths=(48, 32, 8), depth_interals_ratio=(4.0, 1.0, 0.5), cr_base_chs=(8, 8, 8)):
+        super().__init__()
+        assert len(ndepths) == len(depth_interals_ratio)
+        self.ndepths = list(ndepths)
+        self.depth_interals_ratio = list(depth_interals_ratio)
+        self.cr_base_chs = list(cr_base_chs)
+        self.num_stage = len(ndepths)
+        self.stage_scales = {"stage1": 4.0, "stage2": 2.0, "stage3": 1.0}
+        self.feature = FeatureNet(base_channels=8)
+        self.FMT_with_pathway = FMTWithPathway()
+        self.cost_regularization = nn.ModuleList([CostRegNet(1, self.cr_base_chs[i]) for i in range(self.num_stage)])
+        self.DepthNet = DepthNet()
+        self._prep = None
+        self._pe = {}
+        self.register_load_state_dict_post_hook(lambda m, k: m.invalidate())
+
+    def invalidate(self):
+        """Drop packed kernel weights (after any in-place parameter change)."""
+        self._prep = None
+
+    # --------------------------------------------------------- weight preparation
+    def _prepared(self, device):
+        if self._prep is not None and self._prep["device"] == device:
+            return self._prep
+        fp = self.FMT_with_pathway
+        enc = [layer.packed().to(device) for layer in fp.FMT.layers]
+        cr = [c.packed(device) for c in self.cost_regularization]
+        self._prep = {
+            "device": device,
+            "enc": enc,
+            "red1": fp.dim_reduction_1.weight.detach().float().reshape(16, 32).contiguous().to(device),
+            "red2": fp.dim_reduction_2.weight.detach().float().reshape(8, 16).contiguous().to(device),
+            "sm1": fp.smooth_1.weight.detach().float().contiguous().to(device),
+            "sm2": fp.smooth_2.weight.detach().float().contiguous().to(device),
+            "cr": cr,
+            "pw": self.DepthNet.pixel_wise_net.packed(),
+        }
+        return self._prep
+
+    def _pe_slice(self, h, w, device):
+        key = (h, w, str(device))
+        if key not in self._pe:
+            self._pe[key] = position_encoding_sine(32, h, w).to(device)
+        return self._pe[key]
+
+    # --------------------------------------------------------- forward
+    def forward(self, imgs, proj_matrix, depth_values):
+        """models/TransMVSNet.py:141-226."""
+        feats = [self.feature(imgs[:, v]) for v in range(imgs.size(1))]
+        return self.forward_features(feats, proj_matrix, depth_values, (imgs.shape[3], imgs.shape[4]))
+
+    @staticmethod
+    def stack_features(features):
+        """list of per-view {stage: [B,C,h,w]} -> {stage: [B,N,C,h,w]} contiguous."""
+        if isinstance(features, dict):
+            return {k: v.contiguous() for k, v in features.items()}
+        return {k: torch.stack([f[k] for f in features], 1).contiguous() for k in ("stage1", "stage2", "stage3")}
+
+    def forward_features(self, features, proj_matrix, depth_values, img_hw, return_view_weights=False,
+                         view_shard=None):
+        """Hot path after feature extraction (models/TransMVSNet.py:162-226).
+
+        features: per-view list of FeatureNet dicts, or {stage: [B,N,C,h,w]} stacked.
+        view_shard: optional transmvsnet_amd.distributed.ViewShard (source views split over ranks).
+        """
+        feats = self.stack_features(features)
+        dev = feats["stage1"].device
+        if not feats["stage1"].is_cuda:
+            raise RuntimeError("TransMVSNet (HIP) needs GPU features; the HIP path has no CPU fallback")
+        prep = self._prepared(dev)
+        dv = depth_values.to(dev, torch.float32).contiguous()
+        rows = {k: ops.proj_rows(proj_matrix[k]) for k in ("stage1", "stage2", "stage3")}
+        b = feats["stage1"].shape[0]
+        per = []
+        vws = []
+        for i in range(b):
+            o, vw = self._forward_one({k: v[i] for k, v in feats.items()}, {k: r[i:i + 1] for k, r in rows.items()},
+                                      dv[i:i + 1], img_hw, prep, view_shard)
+            per.append(o)
+            vws.append(vw)
+        outputs = {}
+        for s in range(self.num_stage):
+            name = f"stage{s + 1}"
+            outputs[name] = {k: torch.cat([p[name][k] for p in per], 0) for k in per[0][name]}
+            outputs.update(outputs[name])
+        if return_view_weights:
+            return outputs, torch.cat(vws, 0)
+        return outputs
+
+    def _fmt(self, s1, prep):
+        """FMT_with_pathway stage-1 part (models/FMT.py:212-226) -> tokens [N, h1*w1, 32]."""
+        n, c, h1, w1 = s1.shape
+        tokens = torch.empty(n, h1 * w1, c, device=s1.device)
+        ops.fmt_embed(s1, self._pe_slice(h1, w1, s1.device), tokens)
+        enc = prep["enc"]
+        ref, src = tokens[0:1], tokens[1:]
+        kv_cross = torch.empty(4, _lib.KV_NFLOATS, device=s1.device)
+        for i in range(0, 8, 2):  # ref view: self layers only; keep each output's cross K/V
+            kv = ops.fmt_kv(ref, enc[i])
+            ops.fmt_apply(ref, kv, enc[i])
+            ops.fmt_kv(ref, enc[i + 1], out=kv_cross[i // 2:i // 2 + 1])
+        if n > 1:
+            for i, name in enumerate(FMT_LAYERS):
+                if name == "self":
+                    kv = ops.fmt_kv(src, enc[i])
+                    ops.fmt_apply(src, kv, enc[i])
+                else:
+                    ops.fmt_apply(src, kv_cross[i // 2], enc[i], shared_kv=True)
+        return tokens
+
+    def _forward_one(self, f, rows, dv, img_hw, prep, view_shard):
+        s1, s2, s3 = f["stage1"], f["stage2"], f["stage3"]
+        n, _, h1, w1 = s1.shape
+        tokens = self._fmt(s1, prep)
+        st1 = tokens.view(n, h1, w1, 32)
+        st2 = ops.fmt_pathway(st1, s2, prep["red1"], prep["sm1"])
+        st3 = ops.fmt_pathway(st2, s3, prep["red2"], prep["sm2"])
+        nhwc = (st1, st2, st3)
+        outputs = {}
+        depth_raw = None
+        view_w = None
+        for s in range(self.num_stage):
+            name = f"stage{s + 1}"
+            hyp = ops.stage_hypotheses(dv, depth_raw, self.ndepths[s], self.depth_interals_ratio[s], img_hw,
+                                       STAGE_SCALES[s])
+            fs = nhwc[s]
+            if view_shard is None:
+                if s == 0:
+                    sim, _, view_w = ops.warp_corr(fs[0:1], fs[1:].unsqueeze(0), rows[name], hyp,
+                                                   pw_params=prep["pw"])
+                else:
+                    sim, _, _ = ops.warp_corr(fs[0:1], fs[1:].unsqueeze(0), rows[name], hyp, view_w_in=view_w,
+                                              vw_shift=s)
+            else:
+                sim, vw_new = view_shard.cost_volume(fs, rows[name], hyp, s, view_w, prep["pw"])
+                if s == 0:
+                    view_w = vw_new
+            logits = ops.costregnet(sim, prep["cr"][s][0])
+            prob, depth, depth_raw, conf = ops.softmax_wta(logits, hyp, DEPTH_CLAMP)
+            outputs[name] = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}
+        return outputs, view_w

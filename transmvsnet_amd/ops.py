@@ -1,0 +1,255 @@
+"""Torch-tensor wrappers over the C-ABI (device memory + current HIP stream in, status checked).
+
+Each op mirrors one reference callable (file:line in include/transmvs.h). Tensors must be
+fp32, contiguous and on the GPU; nothing here computes on the CPU except the 4x4 camera
+algebra that produces kernel arguments (proj_rows), which is done exactly as the
+reference does it so the warp coordinates match bit for bit.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_lib_h = _lib.load
+
+
+_TIMER = None
+
+
+def set_timer(timer):
+    """Install an object with begin(name) -> token / end(token) around every C-ABI launch
+    (bench.py uses HIP events on the launching stream); None disables."""
+    global _TIMER
+    _TIMER = timer
+
+
+class _Span:
+    __slots__ = ("tok",)
+
+    def __init__(self, name):
+        self.tok = _TIMER.begin(name) if _TIMER is not None else None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        if self.tok is not None:
+            _TIMER.end(self.tok)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _dev(t, name):
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a GPU tensor (the HIP path has no CPU fallback)")
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        raise RuntimeError(f"{name} must be contiguous float32")
+
+
+# ----------------------------------------------------------------- host-side parameter math
+def bn_fold(gamma, beta, mean, var, eps=1e-5):
+    """(alpha, shift) CPU float32 arrays, reference batch_norm eval semantics (tmvs_bn_fold)."""
+    g = np.ascontiguousarray(gamma.detach().cpu().numpy(), np.float32)
+    b = np.ascontiguousarray(beta.detach().cpu().numpy(), np.float32)
+    m = np.ascontiguousarray(mean.detach().cpu().numpy(), np.float32)
+    v = np.ascontiguousarray(var.detach().cpu().numpy(), np.float32)
+    a = np.empty_like(g)
+    s = np.empty_like(g)
+    with _Span("tmvs_bn_fold"):
+        _lib.check(_lib_h().tmvs_bn_fold(g.ctypes.data, b.ctypes.data, m.ctypes.data, v.ctypes.data, g.size,
+                                         ctypes.c_float(eps), a.ctypes.data, s.ctypes.data), "tmvs_bn_fold")
+    return a, s
+
+
+def compose_proj(proj):
+    """[B,2,4,4] -> [B,4,4] with rows 0..2 = K·E[:3,:4] (models/TransMVSNet.py:75-78), CPU fp32."""
+    new = proj[:, 0].clone()
+    new[:, :3, :4] = torch.matmul(proj[:, 1, :3, :3], proj[:, 0, :3, :4])
+    return new
+
+
+def proj_rows(proj_matrix_stage):
+    """[B,N,2,4,4] -> float32 [B, N-1, 12] = rows of P_src·P_ref^-1 (models/module.py:295-297).
+
+    Same torch-CPU fp32 ops as the reference, so the homography is bit-identical.
+    """
+    pm = proj_matrix_stage.detach().to("cpu", torch.float32)
+    ref = compose_proj(pm[:, 0])
+    inv = torch.inverse(ref)
+    rows = []
+    for v in range(1, pm.shape[1]):
+        p = torch.matmul(compose_proj(pm[:, v]), inv)
+        rows.append(p[:, :3, :4].reshape(pm.shape[0], 12))
+    return torch.stack(rows, 1).contiguous().numpy()
+
+
+# ----------------------------------------------------------------- ops
+def stage_hypotheses(depth_values, prev_depth, ndepth, ratio, full_hw, stage_scale):
+    """Stage glue (models/TransMVSNet.py:174-204): -> [B, D, H/s, W/s]."""
+    _dev(depth_values, "depth_values")
+    _dev(prev_depth, "prev_depth")
+    b = depth_values.shape[0]
+    h, w = full_hw
+    out = torch.empty(b, ndepth, h // stage_scale, w // stage_scale, device=depth_values.device)
+    ph, pw = (prev_depth.shape[1], prev_depth.shape[2]) if prev_depth is not None else (0, 0)
+    with _Span("tmvs_stage_hypotheses"):
+        _lib.check(_lib_h().tmvs_stage_hypotheses(_ptr(depth_values), depth_values.shape[1], _ptr(prev_depth), ph, pw, b,
+                                                  ndepth, ctypes.c_float(ratio), h, w, stage_scale, _ptr(out), _stream()),
+                   "tmvs_stage_hypotheses")
+    return out
+
+
+def warp_corr(ref_nhwc, src_nhwc, proj12, hyp, view_w_in=None, vw_shift=0, vw_offset=0, vw_total=None,
+              pw_params=None, partial=False, view_w_out=None):
+    """Fused cost volume (models/TransMVSNet.py:58-93). ref [B,H,W,C], src [B,V,H,W,C], proj12 HOST [B,V,12].
+
+    Returns sim [B,D,H,W] (and w_sum [B,H,W] when partial) ; stage 1 writes view_w_out [B,vw_total,H,W].
+    """
+    for t, n in ((ref_nhwc, "ref"), (src_nhwc, "src"), (hyp, "hyp"), (view_w_in, "view_w_in"), (view_w_out, "view_w_out")):
+        _dev(t, n)
+    b, v, h, w, c = src_nhwc.shape
+    d = hyp.shape[1]
+    vw_total = v if vw_total is None else vw_total
+    proj = np.ascontiguousarray(proj12, np.float32).reshape(b, v, 12)
+    sim = torch.empty(b, d, h, w, device=hyp.device)
+    wsum = torch.empty(b, h, w, device=hyp.device) if partial else None
+    if view_w_in is None:
+        if view_w_out is None:
+            view_w_out = torch.empty(b, vw_total, h, w, device=hyp.device)
+        pw = np.ascontiguousarray(pw_params, np.float32)
+        assert pw.size == _lib.PW_NPARAMS
+        pw_ptr = pw.ctypes.data
+    else:
+        pw_ptr = None
+    with _Span("tmvs_warp_corr"):
+        _lib.check(_lib_h().tmvs_warp_corr(_ptr(ref_nhwc), _ptr(src_nhwc), proj.ctypes.data, _ptr(hyp), _ptr(view_w_in),
+                                           vw_shift, vw_offset, vw_total, pw_ptr, b, v, c, d, h, w,
+                                           _lib.WARP_PARTIAL if partial else 0, _ptr(sim), _ptr(wsum),
+                                           _ptr(view_w_out if view_w_in is None else None), _stream()), "tmvs_warp_corr")
+    return sim, wsum, (view_w_out if view_w_in is None else None)
+
+
+def aggregate_finalize(sim_sum, w_sum):
+    _dev(sim_sum, "sim_sum")
+    _dev(w_sum, "w_sum")
+    b, d, h, w = sim_sum.shape
+    with _Span("tmvs_aggregate_finalize"):
+        _lib.check(_lib_h().tmvs_aggregate_finalize(_ptr(sim_sum), _ptr(w_sum), b, d, h, w, _stream()),
+                   "tmvs_aggregate_finalize")
+    return sim_sum
+
+
+def homo_warping(src_fea, src_proj, ref_proj, depth_values):
+    """Seam-compatible homo_warping (models/module.py:284-322): [B,C,H,W] -> [B,C,D,H,W]."""
+    _dev(src_fea, "src_fea")
+    _dev(depth_values, "depth_values")
+    b, c, h, w = src_fea.shape
+    d = depth_values.shape[1]
+    p = torch.matmul(src_proj.detach().cpu().float(), torch.inverse(ref_proj.detach().cpu().float()))
+    rows = np.ascontiguousarray(p[:, :3, :4].reshape(b, 12).numpy(), np.float32)
+    out = torch.empty(b, c, d, h, w, device=src_fea.device)
+    with _Span("tmvs_homo_warping"):
+        _lib.check(_lib_h().tmvs_homo_warping(_ptr(src_fea), rows.ctypes.data, _ptr(depth_values.contiguous()), b, c, d,
+                                              h, w, _ptr(out), _stream()), "tmvs_homo_warping")
+    return out
+
+
+def softmax_wta(logits, hyp, clamp=(425.0, 935.0)):
+    """prob, depth (clamped), depth_raw, conf (models/TransMVSNet.py:97-103,217-221)."""
+    _dev(logits, "logits")
+    _dev(hyp, "hyp")
+    b, d, h, w = logits.shape
+    prob = torch.empty_like(logits)
+    depth = torch.empty(b, h, w, device=logits.device)
+    raw = torch.empty_like(depth)
+    conf = torch.empty_like(depth)
+    with _Span("tmvs_softmax_wta"):
+        _lib.check(_lib_h().tmvs_softmax_wta(_ptr(logits), _ptr(hyp), b, d, h, w, ctypes.c_float(clamp[0]),
+                                             ctypes.c_float(clamp[1]), _ptr(prob), _ptr(depth), _ptr(raw), _ptr(conf),
+                                             _stream()), "tmvs_softmax_wta")
+    return prob, depth, raw, conf
+
+
+def costregnet(x, weights: "_lib.CostRegWeights", keepalive=None):
+    """CostRegNet forward (models/module.py:447-456): [B,D,H,W] -> logits [B,D,H,W]."""
+    _dev(x, "x")
+    b, d, h, w = x.shape
+    nbytes = _lib_h().tmvs_costregnet_workspace(b, d, h, w, weights.base_ch)
+    ws = torch.empty(nbytes // 4 + 64, device=x.device)
+    out = torch.empty_like(x)
+    with _Span("tmvs_costregnet"):
+        _lib.check(_lib_h().tmvs_costregnet(_ptr(x), b, d, h, w, ctypes.byref(weights), _ptr(ws), ws.numel() * 4,
+                                            _ptr(out), _stream()), "tmvs_costregnet")
+    return out
+
+
+def conv3d_bn_relu(x, wpk, alpha, shift, cout, stride):
+    b, d, h, w, cin = x.shape
+    do, ho, wo = ((d - 1) // 2 + 1, (h - 1) // 2 + 1, (w - 1) // 2 + 1) if stride == 2 else (d, h, w)
+    y = torch.empty(b, do, ho, wo, cout, device=x.device)
+    with _Span("tmvs_conv3d_bn_relu"):
+        _lib.check(_lib_h().tmvs_conv3d_bn_relu(_ptr(x), b, cin, d, h, w, _ptr(wpk), _ptr(alpha), _ptr(shift), cout,
+                                                stride, _ptr(y), _stream()), "tmvs_conv3d_bn_relu")
+    return y
+
+
+def deconv3d_bn_relu_add(x, wpk, alpha, shift, cout, skip):
+    b, d, h, w, cin = x.shape
+    y = torch.empty(b, 2 * d, 2 * h, 2 * w, cout, device=x.device)
+    with _Span("tmvs_deconv3d_bn_relu_add"):
+        _lib.check(_lib_h().tmvs_deconv3d_bn_relu_add(_ptr(x), b, cin, d, h, w, _ptr(wpk), _ptr(alpha), _ptr(shift),
+                                                      cout, _ptr(skip), _ptr(y), _stream()), "tmvs_deconv3d_bn_relu_add")
+    return y
+
+
+def fmt_embed(feat_nchw, pe, out_tokens):
+    """x + PE, 'n c h w -> n (h w) c' (FMT.py:152): feat [nv,C,H,W] -> tokens [nv,H*W,C] (written in place)."""
+    nv, c, h, w = feat_nchw.shape
+    with _Span("tmvs_fmt_embed"):
+        _lib.check(_lib_h().tmvs_fmt_embed(_ptr(feat_nchw), c * h * w, _ptr(pe), pe.shape[1], pe.shape[2], nv, c, h, w,
+                                           _ptr(out_tokens), _stream()), "tmvs_fmt_embed")
+    return out_tokens
+
+
+def fmt_kv(source_tokens, enc_w, out=None):
+    """(KV, Ksum) of one encoder layer over source tokens [nv,S,32] -> [nv,160]."""
+    nv, s, _ = source_tokens.shape
+    nbytes = _lib_h().tmvs_fmt_kv_workspace(nv, s)
+    ws = torch.empty(max(1, nbytes // 4), device=source_tokens.device)
+    kv = out if out is not None else torch.empty(nv, _lib.KV_NFLOATS, device=source_tokens.device)
+    with _Span("tmvs_fmt_kv"):
+        _lib.check(_lib_h().tmvs_fmt_kv(_ptr(source_tokens), nv, s, _ptr(enc_w), _ptr(ws), ws.numel() * 4, _ptr(kv),
+                                        _stream()), "tmvs_fmt_kv")
+    return kv
+
+
+def fmt_apply(x_tokens, kv, enc_w, shared_kv=False):
+    """Rest of EncoderLayer.forward in place on x [nv,L,32] (FMT.py:96-111)."""
+    nv, l, _ = x_tokens.shape
+    with _Span("tmvs_fmt_apply"):
+        _lib.check(_lib_h().tmvs_fmt_apply(_ptr(x_tokens), nv, l, _ptr(kv), 0 if shared_kv else _lib.KV_NFLOATS,
+                                           _ptr(enc_w), _stream()), "tmvs_fmt_apply")
+    return x_tokens
+
+
+def fmt_pathway(coarse_nhwc, lateral_nchw, w_reduce, w_smooth):
+    """smooth(up2(reduce(coarse)) + lateral) (FMT.py:221-228): coarse [nv,h,w,cc], lateral [nv,cf,2h,2w]."""
+    nv, h, w, cc = coarse_nhwc.shape
+    cf = lateral_nchw.shape[1]
+    out = torch.empty(nv, 2 * h, 2 * w, cf, device=coarse_nhwc.device)
+    with _Span("tmvs_fmt_pathway"):
+        _lib.check(_lib_h().tmvs_fmt_pathway(_ptr(coarse_nhwc), _ptr(lateral_nchw), cf * 4 * h * w, _ptr(w_reduce),
+                                             _ptr(w_smooth), nv, cc, cf, h, w, _ptr(out), _stream()), "tmvs_fmt_pathway")
+    return out
