@@ -139,10 +139,12 @@ def main():
 
         # instrumented steps (outside the timed region): per-launch HIP-event durations
         timer = EventTimer()
+        model.decomposed = True   # same kernels, one C-ABI call each, so each gets its own event pair
         ops.set_timer(timer)
         for _ in range(args.profile_steps):
             step()
         ops.set_timer(None)
+        model.decomposed = False
         spans = timer.durations()
 
     maps_per_step = 1 if args.mode == "views" else world

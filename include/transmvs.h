@@ -136,9 +136,10 @@ int tmvs_softmax_wta(const float* logits, const float* hyp, int batch, int ndept
 /* ------------------------------------------------------------------ FMT
  * Feature Matching Transformer (models/FMT.py), d_model 32, 8 heads x 4, linear attention.
  * Tokens are [nv][L][32] (= NHWC of the stage-1 map). Packed EncoderLayer weights
- * (TMVS_ENC_NPARAMS floats, offsets TMVS_ENC_*):
- *   Wq[32][32] bq[32] Wk[32][32] bk[32] Wv[32][32] bv[32] Wo[32][32] bo[32]
- *   W1[64][32] b1[64] W2[32][64] b2[32] ln1_g[32] ln1_b[32] ln2_g[32] ln2_b[32]            */
+ * (TMVS_ENC_NPARAMS floats, offsets TMVS_ENC_*); nn.Linear weights are [out][in] except the
+ * K/V projections and linear2, stored transposed ([in][out]) for the rank-1-update kernels:
+ *   Wq[32][32] bq[32] WkT[32][32] bk[32] WvT[32][32] bv[32] Wo[32][32] bo[32]
+ *   W1[64][32] b1[64] W2T[64][32] b2[32] ln1_g[32] ln1_b[32] ln2_g[32] ln2_b[32]            */
 #define TMVS_ENC_WQ 0
 #define TMVS_ENC_BQ 1024
 #define TMVS_ENC_WK 1056
@@ -149,7 +150,7 @@ int tmvs_softmax_wta(const float* logits, const float* hyp, int batch, int ndept
 #define TMVS_ENC_BO 4192
 #define TMVS_ENC_W1 4224
 #define TMVS_ENC_B1 6272
-#define TMVS_ENC_W2 6336
+#define TMVS_ENC_W2T 6336
 #define TMVS_ENC_B2 8384
 #define TMVS_ENC_LN1G 8416
 #define TMVS_ENC_LN1B 8448
@@ -177,10 +178,36 @@ int tmvs_fmt_apply(float* x, int nv, int l_tokens, const float* kv, long kv_view
 
 /* FMT_with_pathway lateral step (models/FMT.py:221-228): out = smooth(up2(reduce(coarse)) + lateral)
  *   coarse [nv][h][w][cc] (NHWC), lateral [nv][cf][2h][2w] (NCHW, per-view stride lat_view_stride),
- *   w_reduce [cf][cc] (1x1 conv, no bias), w_smooth [cf][cf][3][3] (3x3, pad 1, no bias)
+ *   w_reduce [cc][cf] (1x1 conv weight [cf][cc] transposed), w_smooth [cf_in][3][3][cf_out]
+ *   (3x3 conv weight [cf_out][cf_in][3][3] permuted (1,2,3,0)); both convs have no bias
  *   -> out [nv][2h][2w][cf] (NHWC).  Supported (cc,cf): (32,16), (16,8).                  */
 int tmvs_fmt_pathway(const float* coarse, const float* lateral, long lat_view_stride, const float* w_reduce,
                      const float* w_smooth, int nv, int cc, int cf, int h, int w, float* out, void* stream);
+
+/* ------------------------------------------------------------------ native orchestration
+ * Whole-FMT forward (models/FMT.py:147-177 inside FMT_with_pathway :212-226): embedding + PE,
+ * the reference view's 4 self layers (the K/V of each output is reduced once for the matching
+ * cross layer), then views 1..nv-1 through all 8 layers, batched.
+ *   stage1 [nv][32][H][W] (NCHW, per-view stride view_stride floats), pe [32][pe_h][pe_w],
+ *   enc_w  HOST array of 8 DEVICE pointers (packed EncoderLayer weights, layer order 0..7)
+ *   tokens [nv][H*W][32] out (NHWC stage-1 features after the FMT).                         */
+size_t tmvs_fmt_forward_workspace(int nv, int l_tokens);
+int tmvs_fmt_forward(const float* stage1, long view_stride, const float* pe, int pe_h, int pe_w, int nv, int height,
+                     int width, const float* const* enc_w, void* workspace, size_t workspace_bytes, float* tokens,
+                     void* stream);
+
+/* One cascade stage of TransMVSNet.forward for ONE sample (models/TransMVSNet.py:174-221):
+ * tmvs_stage_hypotheses -> tmvs_warp_corr -> tmvs_costregnet -> tmvs_softmax_wta.
+ *   feat [n_views][h][w][channels] NHWC, reference view first; proj HOST [n_views-1][12];
+ *   pw_params HOST (stage 1: view_w [n_views-1][h][w] is written) or NULL (view_w is read at
+ *   1/2^vw_shift resolution); outputs hyp/prob [ndepth][h][w], depth/depth_raw/conf [h][w]. */
+size_t tmvs_depth_stage_workspace(int ndepth, int height, int width, int base_ch);
+int tmvs_depth_stage(const float* depth_values, int n_values, const float* prev_depth, int prev_h, int prev_w,
+                     const float* feat, int n_views, int channels, int ndepth, float ratio, int full_h, int full_w,
+                     int stage_scale, const float* proj, const float* pw_params, float* view_w, int vw_shift,
+                     const TmvsCostRegWeights* cr, void* workspace, size_t workspace_bytes, float clamp_lo,
+                     float clamp_hi, float* hyp_out, float* prob_out, float* depth_out, float* depth_raw_out,
+                     float* conf_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -35,6 +35,10 @@ SIGNATURES = {
     "tmvs_fmt_kv": (I, [P, I, I, P, P, S, P, P]),
     "tmvs_fmt_apply": (I, [P, I, I, P, L, P, P]),
     "tmvs_fmt_pathway": (I, [P, P, L, P, P, I, I, I, I, I, P, P]),
+    "tmvs_fmt_forward_workspace": (S, [I, I]),
+    "tmvs_fmt_forward": (I, [P, L, P, I, I, I, I, I, P, P, S, P, P]),
+    "tmvs_depth_stage_workspace": (S, [I, I, I, I]),
+    "tmvs_depth_stage": (I, [P, I, P, I, I, P, I, I, I, F, I, I, I, P, P, P, I, P, P, S, F, F, P, P, P, P, P, P]),
 }
 
 ABI_VERSION = 1

@@ -3,7 +3,7 @@
 // Layout: NDHWC fp32 activations. Eval-mode BN is an (alpha, shift) epilogue,
 // y = relu(fmaf(acc, alpha, shift)) (tmvs_bn_fold; the reference CPU kernel's exact form).
 //
-// Mid layers (conv1..conv6, deconv conv7/9/11) are implicit GEMMs on the exact-fp32 matrix
+// Mid layers (conv1..conv6, deconv conv7/9/11) are LDS-staged implicit GEMMs on the exact-fp32 matrix
 // cores, v_mfma_f32_16x16x4_f32 (64 FLOP/clk/SIMD, the fp32 peak; no xf32 on gfx950):
 //   A (16 x 4) = weights   [cout][k]   lane l: cout = l&15, k = l>>4
 //   B (4 x 16) = input     [k][voxel]  lane l: k = l>>4,   voxel = l&15
@@ -54,8 +54,125 @@ struct Geo {
 };
 
 // ---------------------------------------------------------------- conv3d k3 p1, stride S
+// Workgroup tile: 16 output voxels along w x TH rows x TD depth slices, MBB blocks of 16
+// output channels. Per CK-channel chunk the input tile (+halo) is staged once into LDS
+// (voxel stride CK+4 floats: the 16 lanes of a row hit distinct banks), then each wave runs
+// its NBW = TD*TH/4 rows through the 27 taps: A (weights) from global/L2, B from LDS.
+template <int CIN, int COUT, int S, int TD, int TH, int MBB>
+__global__ __launch_bounds__(256) void conv3d_lds_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
+                                                         const float* __restrict__ alpha,
+                                                         const float* __restrict__ shift, float* __restrict__ y,
+                                                         Geo g) {
+  constexpr int CK = CIN < 16 ? CIN : 16;
+  constexpr int PL = CK / 4;
+  constexpr int MB = (COUT + 15) / 16;
+  constexpr int MG = MB / MBB;
+  constexpr int NBW = TD * TH / 4;
+  constexpr int LW = 15 * S + 3, LH = (TH - 1) * S + 3, LD = (TD - 1) * S + 3;
+  // voxel stride / quad swizzle chosen so the 4 lane groups of every ds_read_b128 are
+  // bank-conflict free (exhaustive search over the gfx950 b128 lane grouping)
+  constexpr bool SWZ = (S == 1 && CK == 16);
+  constexpr int VST = SWZ ? 16 : CK + 4;
+  constexpr int NVOX = LD * LH * LW;
+  static_assert(MB % MBB == 0 && (TD * TH) % 4 == 0, "tile");
+  __shared__ __attribute__((aligned(16))) float tile[NVOX * VST];
+
+  const int nws = (g.Wo + 15) / 16, nhs = (g.Ho + TH - 1) / TH, nds = (g.Do + TD - 1) / TD;
+  int t = blockIdx.x;
+  const int mg = t % MG;
+  t /= MG;
+  const int ws = t % nws;
+  t /= nws;
+  const int hs = t % nhs;
+  t /= nhs;
+  const int ds = t % nds;
+  const int n = t / nds;
+  const int ow0 = ws * 16, oh0 = hs * TH, od0 = ds * TD;
+  const int iw0 = ow0 * S - 1, ih0 = oh0 * S - 1, id0 = od0 * S - 1;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int col = lane & 15, kgrp = lane >> 4;
+  const size_t in_n = (size_t)n * g.Di * g.Hi * g.Wi;
+
+  floatx4 acc[NBW][MBB];
+#pragma unroll
+  for (int r = 0; r < NBW; ++r)
+#pragma unroll
+    for (int m = 0; m < MBB; ++m) acc[r][m] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll 1
+  for (int ch = 0; ch < CIN / CK; ++ch) {
+    if (ch) __syncthreads();
+    for (int idx = threadIdx.x; idx < NVOX * PL; idx += 256) {
+      const int vox = idx / PL, q = idx - vox * PL;
+      const int lw = vox % LW, rest = vox / LW, lh = rest % LH, ld = rest / LH;
+      const int iw = iw0 + lw, ih = ih0 + lh, id = id0 + ld;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (iw >= 0 && iw < g.Wi && ih >= 0 && ih < g.Hi && id >= 0 && id < g.Di)
+        v = *reinterpret_cast<const float4*>(x + (in_n + ((size_t)id * g.Hi + ih) * g.Wi + iw) * CIN + ch * CK + 4 * q);
+      const int qs = SWZ ? (q ^ ((vox >> 1) & 3)) : q;
+      *reinterpret_cast<float4*>(tile + vox * VST + 4 * qs) = v;
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int kd = 0; kd < 3; ++kd)
+#pragma unroll
+    for (int t9 = 0; t9 < 9; ++t9) {
+      const int kh = t9 / 3, kw = t9 % 3, tap = kd * 9 + t9;
+      VecN<PL> a[MBB];
+#pragma unroll
+      for (int m = 0; m < MBB; ++m) {
+        const int co = (mg * MBB + m) * 16 + col;
+        if (co < COUT)
+          a[m].load(wpk + ((size_t)tap * COUT + co) * CIN + ch * CK + kgrp * PL);
+        else
+          a[m].zero();
+      }
+      VecN<PL> b[NBW];
+#pragma unroll
+      for (int r = 0; r < NBW; ++r) {
+        const int rr = wv * NBW + r;
+        const int odl = rr / TH, ohl = rr - odl * TH;
+        const int lvox = ((odl * S + kd) * LH + ohl * S + kh) * LW + col * S + kw;
+        const int qs = SWZ ? (kgrp ^ ((lvox >> 1) & 3)) : kgrp;
+        b[r].load(tile + lvox * VST + qs * PL);
+      }
+#pragma unroll
+      for (int j = 0; j < PL; ++j)
+#pragma unroll
+        for (int r = 0; r < NBW; ++r)
+#pragma unroll
+          for (int m = 0; m < MBB; ++m)
+            acc[r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b[r].v[j], acc[r][m], 0, 0, 0);
+    }
+  }
+  const int ow = ow0 + col;
+  if (ow >= g.Wo) return;
+  const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
+#pragma unroll
+  for (int m = 0; m < MBB; ++m) {
+    const int co = (mg * MBB + m) * 16 + kgrp * 4;
+    if (co >= COUT) continue;
+    const float4 al = *reinterpret_cast<const float4*>(alpha + co);
+    const float4 sh = *reinterpret_cast<const float4*>(shift + co);
+#pragma unroll
+    for (int r = 0; r < NBW; ++r) {
+      const int rr = wv * NBW + r;
+      const int od = od0 + rr / TH, oh = oh0 + rr % TH;
+      if (od >= g.Do || oh >= g.Ho) continue;
+      float4 o;
+      o.x = relu(fmaf(acc[r][m][0], al.x, sh.x));
+      o.y = relu(fmaf(acc[r][m][1], al.y, sh.y));
+      o.z = relu(fmaf(acc[r][m][2], al.z, sh.z));
+      o.w = relu(fmaf(acc[r][m][3], al.w, sh.w));
+      *reinterpret_cast<float4*>(y + (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co) = o;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- conv3d, direct (no LDS)
+// Used for the stride-2 layers: no LDS footprint, high occupancy hides the per-tap L1/L2 latency.
 template <int CIN, int COUT, int S, int NBW, int MBW>
-__global__ __launch_bounds__(256) void conv3d_mfma_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
+__global__ __launch_bounds__(256) void conv3d_direct_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                           const float* __restrict__ alpha,
                                                           const float* __restrict__ shift, float* __restrict__ y,
                                                           Geo g, int n_tasks) {
@@ -156,238 +273,271 @@ __global__ __launch_bounds__(256) void conv3d_mfma_kernel(const float* __restric
 }
 
 // ---------------------------------------------------------------- ConvTranspose3d k3 s2 p1 op1
-// output o = 2i - 1 + k: parity 0 -> (k=1, i=o/2); parity 1 -> (k=0, i=o/2+1), (k=2, i=o/2)
-__device__ __forceinline__ void deconv_tap(int par, int t, int half, int& k, int& i) {
-  if (par == 0) {
-    k = 1;
-    i = half;
-  } else if (t == 0) {
-    k = 0;
-    i = half + 1;
-  } else {
-    k = 2;
-    i = half;
-  }
-}
-
-template <int CIN, int COUT, int NBW, int MBW>
-__global__ __launch_bounds__(256) void deconv3d_mfma_kernel(const float* __restrict__ x,
-                                                            const float* __restrict__ wpk,
-                                                            const float* __restrict__ alpha,
-                                                            const float* __restrict__ shift,
-                                                            const float* __restrict__ skip, float* __restrict__ y,
-                                                            Geo g, int n_tasks) {
+// output o = 2i - 1 + k: parity 0 -> (k=1, i=o/2); parity 1 -> (k=0, i=o/2+1), (k=2, i=o/2).
+// Workgroup tile in input-grid coordinates: 16 columns x THI rows x TDI slices (outputs
+// 32 x 2THI x 2TDI). Each wave owns TDI*THI/4 input-grid rows and all 8 output parity
+// classes of them (a class = 16 outputs with one parity per dimension = one tap set of
+// 1, 2, 4 or 8 taps), so the waves carry equal work. Input tile (+1 halo) staged in LDS.
+template <int CIN, int COUT, int TDI, int THI, int MBB>
+__global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restrict__ x,
+                                                           const float* __restrict__ wpk,
+                                                           const float* __restrict__ alpha,
+                                                           const float* __restrict__ shift,
+                                                           const float* __restrict__ skip, float* __restrict__ y,
+                                                           Geo g) {
   constexpr int CK = CIN < 16 ? CIN : 16;
   constexpr int PL = CK / 4;
   constexpr int MB = (COUT + 15) / 16;
-  constexpr int MG = MB / MBW;
-  static_assert(MB % MBW == 0, "MBW must divide MB");
-  const int lane = threadIdx.x & 63;
-  const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (task >= n_tasks) return;
-  // task -> (mg, pw, wseg, hgrp, ph, od, n); output w = 2*(wseg*16+col)+pw, h = 2*(hg*NBW+r)+ph
-  int t = task;
+  constexpr int MG = MB / MBB;
+  constexpr int NBW = TDI * THI / 4;
+  constexpr int LW = 17, LH = THI + 1, LD = TDI + 1;
+  constexpr bool SWZ = (CK == 16);  // conflict-free ds_read_b128 (see conv3d_lds_kernel)
+  constexpr int VST = SWZ ? 16 : CK + 4;
+  constexpr int NVOX = LD * LH * LW;
+  static_assert(MB % MBB == 0 && (TDI * THI) % 4 == 0, "tile");
+  __shared__ __attribute__((aligned(16))) float tile[NVOX * VST];
+
+  const int nws = (g.Wi + 15) / 16, nhs = (g.Hi + THI - 1) / THI, nds = (g.Di + TDI - 1) / TDI;
+  int t = blockIdx.x;
   const int mg = t % MG;
   t /= MG;
-  const int pw = t & 1;
-  t >>= 1;
-  const int nws = (g.Wi + 15) / 16;
-  const int wseg = t % nws;
+  const int ws = t % nws;
   t /= nws;
-  const int nhg = (g.Hi + NBW - 1) / NBW;
-  const int hg = t % nhg;
-  t /= nhg;
-  const int ph = t & 1;
-  t >>= 1;
-  const int od = t % g.Do;
-  const int n = t / g.Do;
-
-  const int col = lane & 15;
-  const int kgrp = lane >> 4;
-  const int mw = wseg * 16 + col;  // input-grid column of this lane's output
-  const int ow = 2 * mw + pw;
+  const int hs = t % nhs;
+  t /= nhs;
+  const int ds = t % nds;
+  const int n = t / nds;
+  const int mw0 = ws * 16, mh0 = hs * THI, md0 = ds * TDI;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int col = lane & 15, kgrp = lane >> 4;
   const size_t in_n = (size_t)n * g.Di * g.Hi * g.Wi;
-  const int pd = od & 1;
 
-  floatx4 acc[NBW][MBW];
+  floatx4 acc[NBW][8][MBB];
 #pragma unroll
   for (int r = 0; r < NBW; ++r)
 #pragma unroll
-    for (int m = 0; m < MBW; ++m) acc[r][m] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int m = 0; m < MBB; ++m) acc[r][c][m] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  for (int td = 0; td < 1 + pd; ++td) {
-    int kd, id;
-    deconv_tap(pd, td, od >> 1, kd, id);
-    if (id >= g.Di) continue;
-    for (int th = 0; th < 1 + ph; ++th) {
-      int kh, dh;
-      deconv_tap(ph, th, 0, kh, dh);  // dh = input-row offset relative to oh/2
-      for (int tw = 0; tw < 1 + pw; ++tw) {
-        int kw, iw;
-        deconv_tap(pw, tw, mw, kw, iw);
-        const int tap = kd * 9 + kh * 3 + kw;
-        const bool wok = mw < g.Wi && iw < g.Wi;
+#pragma unroll 1
+  for (int ch = 0; ch < CIN / CK; ++ch) {
+    if (ch) __syncthreads();
+    for (int idx = threadIdx.x; idx < NVOX * PL; idx += 256) {
+      const int vox = idx / PL, q = idx - vox * PL;
+      const int lw = vox % LW, rest = vox / LW, lh = rest % LH, ld = rest / LH;
+      const int iw = mw0 + lw, ih = mh0 + lh, id = md0 + ld;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (iw < g.Wi && ih < g.Hi && id < g.Di)
+        v = *reinterpret_cast<const float4*>(x + (in_n + ((size_t)id * g.Hi + ih) * g.Wi + iw) * CIN + ch * CK + 4 * q);
+      const int qs = SWZ ? (q ^ ((vox >> 1) & 3)) : q;
+      *reinterpret_cast<float4*>(tile + vox * VST + 4 * qs) = v;
+    }
+    __syncthreads();
 #pragma unroll
-        for (int ch = 0; ch < CIN / CK; ++ch) {
-          const int cbase = ch * CK + kgrp * PL;
-          VecN<PL> a[MBW];
+    for (int cls = 0; cls < 8; ++cls) {
+      const int pd = cls >> 2, ph = (cls >> 1) & 1, pw = cls & 1;
 #pragma unroll
-          for (int m = 0; m < MBW; ++m) {
-            const int co = (mg * MBW + m) * 16 + col;
-            if (co < COUT)
-              a[m].load(wpk + ((size_t)tap * COUT + co) * CIN + cbase);
-            else
-              a[m].zero();
+      for (int td = 0; td < 1 + pd; ++td)
+#pragma unroll
+        for (int th = 0; th < 1 + ph; ++th)
+#pragma unroll
+          for (int tw = 0; tw < 1 + pw; ++tw) {
+            const int kd = pd ? (td ? 2 : 0) : 1, od_off = (pd && !td) ? 1 : 0;
+            const int kh = ph ? (th ? 2 : 0) : 1, oh_off = (ph && !th) ? 1 : 0;
+            const int kw = pw ? (tw ? 2 : 0) : 1, ow_off = (pw && !tw) ? 1 : 0;
+            const int tap = kd * 9 + kh * 3 + kw;
+            VecN<PL> a[MBB];
+#pragma unroll
+            for (int m = 0; m < MBB; ++m) {
+              const int co = (mg * MBB + m) * 16 + col;
+              if (co < COUT)
+                a[m].load(wpk + ((size_t)tap * COUT + co) * CIN + ch * CK + kgrp * PL);
+              else
+                a[m].zero();
+            }
+#pragma unroll
+            for (int r = 0; r < NBW; ++r) {
+              const int rr = wv * NBW + r;
+              const int mdl = rr / THI, mhl = rr - mdl * THI;
+              VecN<PL> b;
+              const int lvox = ((mdl + od_off) * LH + mhl + oh_off) * LW + col + ow_off;
+              const int qs = SWZ ? (kgrp ^ ((lvox >> 1) & 3)) : kgrp;
+              b.load(tile + lvox * VST + qs * PL);
+#pragma unroll
+              for (int j = 0; j < PL; ++j)
+#pragma unroll
+                for (int m = 0; m < MBB; ++m)
+                  acc[r][cls][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b.v[j], acc[r][cls][m], 0, 0, 0);
+            }
           }
-          VecN<PL> b[NBW];
-#pragma unroll
-          for (int r = 0; r < NBW; ++r) {
-            const int mh = hg * NBW + r;
-            const int ih = mh + dh;
-            if (wok && mh < g.Hi && ih < g.Hi)
-              b[r].load(x + (in_n + ((size_t)id * g.Hi + ih) * g.Wi + iw) * CIN + cbase);
-            else
-              b[r].zero();
-          }
-#pragma unroll
-          for (int j = 0; j < PL; ++j)
-#pragma unroll
-            for (int r = 0; r < NBW; ++r)
-#pragma unroll
-              for (int m = 0; m < MBW; ++m)
-                acc[r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b[r].v[j], acc[r][m], 0, 0, 0);
-        }
-      }
     }
   }
+  const int mw = mw0 + col;
   if (mw >= g.Wi) return;
   const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
 #pragma unroll
-  for (int m = 0; m < MBW; ++m) {
-    const int co = (mg * MBW + m) * 16 + kgrp * 4;
+  for (int m = 0; m < MBB; ++m) {
+    const int co = (mg * MBB + m) * 16 + kgrp * 4;
     if (co >= COUT) continue;
     const float4 al = *reinterpret_cast<const float4*>(alpha + co);
     const float4 sh = *reinterpret_cast<const float4*>(shift + co);
 #pragma unroll
     for (int r = 0; r < NBW; ++r) {
-      const int mh = hg * NBW + r;
-      if (mh >= g.Hi) continue;
-      const int oh = 2 * mh + ph;
-      const size_t o = (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co;
-      const float4 s = *reinterpret_cast<const float4*>(skip + o);
-      float4 v;
-      v.x = s.x + relu(fmaf(acc[r][m][0], al.x, sh.x));
-      v.y = s.y + relu(fmaf(acc[r][m][1], al.y, sh.y));
-      v.z = s.z + relu(fmaf(acc[r][m][2], al.z, sh.z));
-      v.w = s.w + relu(fmaf(acc[r][m][3], al.w, sh.w));
-      *reinterpret_cast<float4*>(y + o) = v;
+      const int rr = wv * NBW + r;
+      const int md = md0 + rr / THI, mh = mh0 + rr % THI;
+      if (md >= g.Di || mh >= g.Hi) continue;
+#pragma unroll
+      for (int cls = 0; cls < 8; ++cls) {
+        const int od = 2 * md + (cls >> 2), oh = 2 * mh + ((cls >> 1) & 1), ow = 2 * mw + (cls & 1);
+        const size_t o = (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co;
+        const float4 s = *reinterpret_cast<const float4*>(skip + o);
+        float4 v;
+        v.x = s.x + relu(fmaf(acc[r][cls][m][0], al.x, sh.x));
+        v.y = s.y + relu(fmaf(acc[r][cls][m][1], al.y, sh.y));
+        v.z = s.z + relu(fmaf(acc[r][cls][m][2], al.z, sh.z));
+        v.w = s.w + relu(fmaf(acc[r][cls][m][3], al.w, sh.w));
+        *reinterpret_cast<float4*>(y + o) = v;
+      }
     }
   }
 }
 
+constexpr int kDChunk = 8;  // depth planes per thread in the full-resolution VALU convs
+
 // ---------------------------------------------------------------- conv0: Cin=1 -> 8, VALU
+// One thread per (h, w) column walks D; every input plane's 3x3 window is loaded once and
+// kept in a 3-plane ring, so each output sees its taps in (kd, kh, kw) order.
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, float* __restrict__ y, int D, int H,
                                                     int W, const float* __restrict__ wt,
                                                     const float* __restrict__ alpha,
                                                     const float* __restrict__ shift) {
   const int HW = H * W;
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= D * HW) return;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= HW) return;
   const int n = blockIdx.y;
-  const int d = v / HW, rem = v - d * HW, h = rem / W, w = rem - h * W;
+  const int d0 = blockIdx.z * kDChunk, d1 = min(D, d0 + kDChunk);
+  const int h = p / W, w = p - h * W;
   const float* xn = x + (size_t)n * D * HW;
-  float acc[8];
+  float win[3][9];
+  auto load_plane = [&](int d, float* o) {
 #pragma unroll
-  for (int c = 0; c < 8; ++c) acc[c] = 0.f;
-#pragma unroll
-  for (int kd = 0; kd < 3; ++kd) {
-    const int id = d - 1 + kd;
-#pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
-      const int ih = h - 1 + kh;
+    for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        const int iw = w - 1 + kw;
-        const bool ok = id >= 0 && id < D && ih >= 0 && ih < H && iw >= 0 && iw < W;
-        const float xv = ok ? xn[((size_t)id * H + ih) * W + iw] : 0.f;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) acc[c] = fmaf(wt[c * 27 + kd * 9 + kh * 3 + kw], xv, acc[c]);
+        const int ih = h - 1 + kh, iw = w - 1 + kw;
+        const bool ok = d >= 0 && d < D && ih >= 0 && ih < H && iw >= 0 && iw < W;
+        const int dc = min(max(d, 0), D - 1), ihc = min(max(ih, 0), H - 1), iwc = min(max(iw, 0), W - 1);
+        const float v = xn[((size_t)dc * H + ihc) * W + iwc];
+        o[kh * 3 + kw] = ok ? v : 0.f;
       }
+  };
+  load_plane(d0 - 1, win[0]);
+  load_plane(d0, win[1]);
+  float* yo = y + ((size_t)n * D * HW + p) * 8;
+  for (int d = d0; d < d1; ++d) {
+    load_plane(d + 1, win[2]);
+    float acc[8];
+#pragma unroll 2
+    for (int c = 0; c < 8; ++c) {
+      float a = 0.f;
+#pragma unroll
+      for (int kd = 0; kd < 3; ++kd)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) a = fmaf(wt[c * 27 + kd * 9 + t], win[kd][t], a);
+      acc[c] = relu(fmaf(a, alpha[c], shift[c]));
+    }
+    float4* o4 = reinterpret_cast<float4*>(yo + (size_t)d * HW * 8);
+    o4[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    o4[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      win[0][t] = win[1][t];
+      win[1][t] = win[2][t];
     }
   }
-  float4 o0, o1;
-  o0.x = relu(fmaf(acc[0], alpha[0], shift[0]));
-  o0.y = relu(fmaf(acc[1], alpha[1], shift[1]));
-  o0.z = relu(fmaf(acc[2], alpha[2], shift[2]));
-  o0.w = relu(fmaf(acc[3], alpha[3], shift[3]));
-  o1.x = relu(fmaf(acc[4], alpha[4], shift[4]));
-  o1.y = relu(fmaf(acc[5], alpha[5], shift[5]));
-  o1.z = relu(fmaf(acc[6], alpha[6], shift[6]));
-  o1.w = relu(fmaf(acc[7], alpha[7], shift[7]));
-  float4* yo = reinterpret_cast<float4*>(y + ((size_t)n * D * HW + v) * 8);
-  yo[0] = o0;
-  yo[1] = o1;
 }
 
 // ---------------------------------------------------------------- prob: 8 -> 1, VALU
+// One thread per (h, w) column walks D; input plane i (9 taps x 8 channels) is loaded once and
+// feeds outputs i+1 (kd=0), i (kd=1) and i-1 (kd=2) -- each output's FMA chain still runs in
+// (kd, kh, kw, c) order.
 __global__ __launch_bounds__(256) void prob_kernel(const float* __restrict__ x, float* __restrict__ y, int D, int H,
                                                    int W, const float* __restrict__ wt) {
   const int HW = H * W;
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= D * HW) return;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= HW) return;
   const int n = blockIdx.y;
-  const int d = v / HW, rem = v - d * HW, h = rem / W, w = rem - h * W;
+  const int h = p / W, w = p - h * W;
+  const int d0 = blockIdx.z * kDChunk, d1 = min(D, d0 + kDChunk);
   const float* xn = x + (size_t)n * D * HW * 8;
-  float acc = 0.f;
+  float* yn = y + (size_t)n * D * HW + p;
+  float acc_prev = 0.f, acc_cur = 0.f;  // outputs i-1 (has kd=0,1) and i (has kd=0)
+  for (int i = d0 - 1; i <= d1; ++i) {  // plane i feeds outputs i-1, i, i+1 (planes -1 and D are padding)
+    float acc_next = 0.f;                // output i+1, kd=0 from plane i
+    float c1 = acc_cur, c2 = acc_prev;
+    if (i >= 0 && i < D) {
 #pragma unroll
-  for (int kd = 0; kd < 3; ++kd) {
-    const int id = d - 1 + kd;
+      for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
-      const int ih = h - 1 + kh;
+        for (int kw = 0; kw < 3; ++kw) {
+          // branch-free: clamp the address, zero the value (padding taps add exact zeros)
+          const int ih = h - 1 + kh, iw = w - 1 + kw;
+          const bool ok = ih >= 0 && ih < H && iw >= 0 && iw < W;
+          const int ihc = min(max(ih, 0), H - 1), iwc = min(max(iw, 0), W - 1);
+          const float4* q = reinterpret_cast<const float4*>(xn + (((size_t)i * H + ihc) * W + iwc) * 8);
+          float4 u = q[0], v = q[1];
+          if (!ok) {
+            u = make_float4(0.f, 0.f, 0.f, 0.f);
+            v = u;
+          }
+          const float xv[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+          const int t = kh * 3 + kw;
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const int iw = w - 1 + kw;
-        const bool ok = id >= 0 && id < D && ih >= 0 && ih < H && iw >= 0 && iw < W;
-        if (!ok) continue;
-        const float4* p = reinterpret_cast<const float4*>(xn + (((size_t)id * H + ih) * W + iw) * 8);
-        const float4 u = p[0], q = p[1];
-        const int tap = kd * 9 + kh * 3 + kw;
-        acc = fmaf(wt[0 * 27 + tap], u.x, acc);
-        acc = fmaf(wt[1 * 27 + tap], u.y, acc);
-        acc = fmaf(wt[2 * 27 + tap], u.z, acc);
-        acc = fmaf(wt[3 * 27 + tap], u.w, acc);
-        acc = fmaf(wt[4 * 27 + tap], q.x, acc);
-        acc = fmaf(wt[5 * 27 + tap], q.y, acc);
-        acc = fmaf(wt[6 * 27 + tap], q.z, acc);
-        acc = fmaf(wt[7 * 27 + tap], q.w, acc);
-      }
+          for (int c = 0; c < 8; ++c) {
+            acc_next = fmaf(wt[c * 27 + t], xv[c], acc_next);
+            c1 = fmaf(wt[c * 27 + 9 + t], xv[c], c1);
+            c2 = fmaf(wt[c * 27 + 18 + t], xv[c], c2);
+          }
+        }
     }
+    if (i - 1 >= d0) yn[(size_t)(i - 1) * HW] = c2;  // output i-1 complete
+    acc_prev = c1;
+    acc_cur = acc_next;
   }
-  y[(size_t)n * D * HW + v] = acc;
 }
 
 // ---------------------------------------------------------------- launchers
-template <int CIN, int COUT, int S, int NBW, int MBW>
+template <int CIN, int COUT, int S, int TD, int TH, int MBB>
 static int launch_conv(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
                        const Geo& g, hipStream_t st) {
+  constexpr int MG = ((COUT + 15) / 16) / MBB;
+  const long nblk = (long)B * ((g.Do + TD - 1) / TD) * ((g.Ho + TH - 1) / TH) * ((g.Wo + 15) / 16) * MG;
+  hipLaunchKernelGGL((conv3d_lds_kernel<CIN, COUT, S, TD, TH, MBB>), dim3((unsigned)nblk), dim3(256), 0, st, x, w, al,
+                     sh, y, g);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+template <int CIN, int COUT, int S, int NBW, int MBW>
+static int launch_conv_direct(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
+                              const Geo& g, hipStream_t st) {
   constexpr int MG = ((COUT + 15) / 16) / MBW;
   const long n_tasks = (long)B * g.Do * ((g.Ho + NBW - 1) / NBW) * ((g.Wo + 15) / 16) * MG;
   const int nblk = (int)((n_tasks + 3) / 4);
-  hipLaunchKernelGGL((conv3d_mfma_kernel<CIN, COUT, S, NBW, MBW>), dim3(nblk), dim3(256), 0, st, x, w, al, sh, y, g,
+  hipLaunchKernelGGL((conv3d_direct_kernel<CIN, COUT, S, NBW, MBW>), dim3(nblk), dim3(256), 0, st, x, w, al, sh, y, g,
                      (int)n_tasks);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
 
-template <int CIN, int COUT, int NBW, int MBW>
+template <int CIN, int COUT, int TDI, int THI, int MBB>
 static int launch_deconv(const float* x, const float* w, const float* al, const float* sh, const float* skip,
                          float* y, int B, const Geo& g, hipStream_t st) {
-  constexpr int MG = ((COUT + 15) / 16) / MBW;
-  const long n_tasks = (long)B * g.Do * 2 * ((g.Hi + NBW - 1) / NBW) * ((g.Wi + 15) / 16) * 2 * MG;
-  const int nblk = (int)((n_tasks + 3) / 4);
-  hipLaunchKernelGGL((deconv3d_mfma_kernel<CIN, COUT, NBW, MBW>), dim3(nblk), dim3(256), 0, st, x, w, al, sh, skip,
-                     y, g, (int)n_tasks);
+  constexpr int MG = ((COUT + 15) / 16) / MBB;
+  const long nblk = (long)B * ((g.Di + TDI - 1) / TDI) * ((g.Hi + THI - 1) / THI) * ((g.Wi + 15) / 16) * MG;
+  hipLaunchKernelGGL((deconv3d_lds_kernel<CIN, COUT, TDI, THI, MBB>), dim3((unsigned)nblk), dim3(256), 0, st, x, w,
+                     al, sh, skip, y, g);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -407,17 +557,22 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
     g.Ho = (h - 1) / 2 + 1;
     g.Wo = (w - 1) / 2 + 1;
   }
-#define TMVS_CONV_CASE(CI, CO, S, NBW, MBW) \
-  if (cin == CI && cout == CO && stride == S) return launch_conv<CI, CO, S, NBW, MBW>(x, wpk, al, sh, y, B, g, st);
-  TMVS_CONV_CASE(8, 16, 2, 4, 1)
-  TMVS_CONV_CASE(16, 16, 1, 4, 1)
-  TMVS_CONV_CASE(16, 32, 2, 4, 1)
-  TMVS_CONV_CASE(32, 32, 1, 4, 1)
-  TMVS_CONV_CASE(32, 64, 2, 2, 1)
-  TMVS_CONV_CASE(64, 64, 1, 2, 1)
-  TMVS_CONV_CASE(8, 8, 1, 4, 1)
-  TMVS_CONV_CASE(16, 16, 2, 4, 1)
-#undef TMVS_CONV_CASE
+  // stride 1: LDS-staged tiles, one output depth slice x 8 rows x 16 columns per workgroup
+#define TMVS_CONV_LDS(CI, CO, TH, MBB)                                                          \
+  if (cin == CI && cout == CO && stride == 1) {                                               \
+    return launch_conv<CI, CO, 1, 1, TH, MBB>(x, wpk, al, sh, y, B, g, st);                  \
+  }
+  TMVS_CONV_LDS(16, 16, 8, 1)
+  TMVS_CONV_LDS(32, 32, 8, 2)
+  TMVS_CONV_LDS(64, 64, 8, 2)
+#undef TMVS_CONV_LDS
+  // stride 2: direct
+#define TMVS_CONV_DIRECT(CI, CO, NBW, MBW) \
+  if (cin == CI && cout == CO && stride == 2) return launch_conv_direct<CI, CO, 2, NBW, MBW>(x, wpk, al, sh, y, B, g, st);
+  TMVS_CONV_DIRECT(8, 16, 4, 1)
+  TMVS_CONV_DIRECT(16, 32, 4, 1)
+  TMVS_CONV_DIRECT(32, 64, 2, 1)
+#undef TMVS_CONV_DIRECT
   return TMVS_ERR_SHAPE;
 }
 
@@ -430,11 +585,14 @@ static int deconv_dispatch(const float* x, int B, int cin, int d, int h, int w, 
   g.Do = 2 * d;
   g.Ho = 2 * h;
   g.Wo = 2 * w;
-#define TMVS_DECONV_CASE(CI, CO, NBW, MBW) \
-  if (cin == CI && cout == CO) return launch_deconv<CI, CO, NBW, MBW>(x, wpk, al, sh, skip, y, B, g, st);
-  TMVS_DECONV_CASE(64, 32, 2, 1)
-  TMVS_DECONV_CASE(32, 16, 4, 1)
-  TMVS_DECONV_CASE(16, 8, 4, 1)
+#define TMVS_DECONV_CASE(CI, CO, MBB)                                                              \
+  if (cin == CI && cout == CO) {                                                                  \
+    if (g.Di % 2 == 0) return launch_deconv<CI, CO, 2, 2, MBB>(x, wpk, al, sh, skip, y, B, g, st); \
+    return launch_deconv<CI, CO, 1, 4, MBB>(x, wpk, al, sh, skip, y, B, g, st);                  \
+  }
+  TMVS_DECONV_CASE(64, 32, 1)
+  TMVS_DECONV_CASE(32, 16, 1)
+  TMVS_DECONV_CASE(16, 8, 1)
 #undef TMVS_DECONV_CASE
   return TMVS_ERR_SHAPE;
 }
@@ -513,7 +671,7 @@ extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height,
   const int D2 = D1 / 2, H2 = H1 / 2, W2 = W1 / 2;
   const int D3 = D2 / 2, H3 = H2 / 2, W3 = W2 / 2;
   int rc;
-  const dim3 g0((unsigned)((D0 * H0 * W0 + 255) / 256), (unsigned)batch);
+  const dim3 g0((unsigned)((H0 * W0 + 255) / 256), (unsigned)batch, (unsigned)((D0 + kDChunk - 1) / kDChunk));
   hipLaunchKernelGGL(conv0_kernel, g0, dim3(256), 0, st, x, c0, D0, H0, W0, w->w[0], w->alpha[0], w->shift[0]);
   TMVS_CHECK_LAUNCH();
   if ((rc = conv_dispatch(c0, batch, c, D0, H0, W0, w->w[1], w->alpha[1], w->shift[1], 2 * c, 2, c1, st))) return rc;

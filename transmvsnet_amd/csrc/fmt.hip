@@ -6,6 +6,7 @@
 //                     KV[h][m][d] = Σ_s K[h,d] V[h,m] and Ksum[h][d] = Σ_s K[h,d]  (FMT.py:23-32)
 //                     per workgroup -> partial slab [nv][nblk][160]
 //   fmt_kv_combine  : sums the slabs in a fixed order (bitwise reproducible; no atomics)
+// (dense 32x32 linears of the FFN use W2 transposed, TMVS_ENC_W2T)
 //   fmt_apply       : per query token: Q = elu(Wq x + bq) + 1, Z = 1/(Q·Ksum + 1e-6),
 //                     msg = (Q·KV) Z, x = LN1(x + Wo msg + bo), x = LN2(x + W2 relu(W1 x + b1) + b2)
 // Cross layers read the reference view's (KV, Ksum) for every source view (kv stride 0):
@@ -19,7 +20,6 @@ namespace tmvs {
 constexpr int kD = 32;
 constexpr int kKV = TMVS_KV_NFLOATS;
 constexpr int kKvBlock = 256;
-constexpr int kKvTokensPerThread = 2;
 
 __device__ __forceinline__ float elu1(float x) { return (x > 0.f ? x : expm1f(x)) + 1.f; }
 
@@ -34,17 +34,27 @@ __device__ __forceinline__ void load_token(const float* __restrict__ p, float (&
   }
 }
 
-// F.linear (addmm): bias + x·W^T, the dot product as an FMA chain over the input index
-template <int OUT, int IN>
-__device__ __forceinline__ void linear(const float* __restrict__ W, const float* __restrict__ b, const float* x,
-                                       float* y) {
+// F.linear (addmm) y = x·W^T + b with W stored transposed ([in][out]): for each input i the
+// OUT consecutive weights of row i arrive as one scalar load (SGPR operands of v_fma_f32) and
+// are accumulated into y[0..OUT) -- per output an FMA chain over the input index, in order.
+template <int IN, int OUT>
+__device__ __forceinline__ void linear_t(const float* __restrict__ WT, const float* __restrict__ b, const float* x,
+                                         float* y) {
 #pragma unroll
-  for (int o = 0; o < OUT; ++o) {
-    float acc = 0.f;
+  for (int o = 0; o < OUT; ++o) y[o] = 0.f;
+#pragma unroll 2
+  for (int i = 0; i < IN; ++i)
 #pragma unroll
-    for (int i = 0; i < IN; ++i) acc = fmaf(W[o * IN + i], x[i], acc);
-    y[o] = acc + b[o];
-  }
+    for (int o = 0; o < OUT; ++o) y[o] = fmaf(WT[i * OUT + o], x[i], y[o]);
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) y[o] = y[o] + b[o];
+}
+
+// Layer weights are staged once per workgroup into LDS (34 KB) and read back as wave-uniform
+// (broadcast) LDS loads; streaming them through the scalar cache from every wave thrashes it.
+__device__ __forceinline__ void stage_weights(float* __restrict__ lds, const float* __restrict__ w, int n) {
+  for (int i = threadIdx.x * 4; i < n; i += blockDim.x * 4)
+    *reinterpret_cast<float4*>(lds + i) = *reinterpret_cast<const float4*>(w + i);
 }
 
 __device__ __forceinline__ void layer_norm(float (&x)[kD], const float* __restrict__ g, const float* __restrict__ b) {
@@ -81,111 +91,320 @@ __global__ __launch_bounds__(256) void fmt_embed_kernel(const float* __restrict_
   for (int c4 = 0; c4 < kD / 4; ++c4) o[c4] = make_float4(t[4 * c4], t[4 * c4 + 1], t[4 * c4 + 2], t[4 * c4 + 3]);
 }
 
-// One token per thread computes (K, V); the block then contracts its 256 tokens out of LDS,
-// thread i < 160 owning one (h, m, d) entry of KV (or one Ksum entry), summing in token order.
-__global__ __launch_bounds__(kKvBlock) void fmt_kv_partial_kernel(const float* __restrict__ src, int S,
-                                                                   const float* __restrict__ w,
-                                                                   float* __restrict__ partial) {
-  __shared__ float sk[kD][kKvBlock + 1];
-  __shared__ float sv[kD][kKvBlock + 1];
-  const int v = blockIdx.y;
-  const float* srcv = src + (size_t)v * S * kD;
-  const int i = threadIdx.x;
-  // entry owned by thread i: KV[h][m][d] for i < 128, Ksum[h][d] for 128 <= i < 160
-  const int kidx = i < 128 ? (i >> 4) * 4 + (i & 3) : i - 128;
-  const int vidx = i < 128 ? (i >> 4) * 4 + ((i >> 2) & 3) : 0;
-  float acc = 0.f;
-  const int base = blockIdx.x * kKvBlock * kKvTokensPerThread;
-  for (int it = 0; it < kKvTokensPerThread; ++it) {
-    const int t0 = base + it * kKvBlock;
-    if (t0 >= S) break;  // block-uniform
-    const int s = t0 + threadIdx.x;
-    if (s < S) {
-      float x[kD], k[kD], val[kD];
-      load_token(srcv + (size_t)s * kD, x);
-      linear<kD, kD>(w + TMVS_ENC_WK, w + TMVS_ENC_BK, x, k);
-      linear<kD, kD>(w + TMVS_ENC_WV, w + TMVS_ENC_BV, x, val);
+// ============================================================================ MFMA formulation
+// The token-wise linears are dense 32x32 / 32x64 / 64x32 GEMMs over tokens. They run on the
+// exact-fp32 matrix cores (v_mfma_f32_16x16x4_f32: D = A.B + C as an fp32 FMA chain, the VALU
+// fp32 rate) with the weights resident in VGPRs as A fragments, loaded once per wave:
+//   D[o][t] = sum_k W[o][k] X[t][k]   A = W (16 outputs x 4 k),  B = X^T (4 k x 16 tokens)
+// Lane l holds D[o = 16mb + 4(l>>4) + r][t = l&15]: a token's 32 features live in lanes
+// t, t+16, t+32, t+48 (8 each), and head h = 4mb + (l>>4) is lane-local (4 consecutive features).
+// K-step s of a linear takes, in lane group g = l>>4, input feature f(s,g) = 16(s>>2) + 4g + (s&3):
+// exactly the register (mb = s>>2, r = s&3) that lane already holds from the previous linear's
+// accumulator -- so the linears chain with no data movement. Within a chain the input features
+// are summed in that permuted order (an exact fp32 FMA chain; the reference's BLAS order is
+// unknown anyway). VALU version of this file's history: bound by weight delivery (PMC).
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int kfeat(int s, int g) { return 16 * (s >> 2) + 4 * g + (s & 3); }
+
+// A fragments of a [OUT][IN] linear: frag[mb][s] = W[16mb + (l&15)][kfeat(s, l>>4)].
+// TRANS: the packed matrix is stored [IN][OUT].
+template <int OUT, int IN, bool TRANS>
+__device__ __forceinline__ void load_afrag(const float* __restrict__ W, float (&frag)[OUT / 16][IN / 4], int lane) {
 #pragma unroll
-      for (int c = 0; c < kD; ++c) {
-        sk[c][threadIdx.x] = elu1(k[c]);
-        sv[c][threadIdx.x] = val[c];
-      }
+  for (int mb = 0; mb < OUT / 16; ++mb)
+#pragma unroll
+    for (int s = 0; s < IN / 4; ++s) {
+      const int o = 16 * mb + (lane & 15), i = kfeat(s, lane >> 4);
+      frag[mb][s] = TRANS ? W[i * OUT + o] : W[o * IN + i];
     }
-    __syncthreads();
-    const int nt = min(kKvBlock, S - t0);
-    if (i < 128) {
-      for (int t = 0; t < nt; ++t) acc = fmaf(sk[kidx][t], sv[vidx][t], acc);
-    } else if (i < kKV) {
-      for (int t = 0; t < nt; ++t) acc += sk[kidx][t];
-    }
-    __syncthreads();
-  }
-  if (i < kKV) partial[((size_t)v * gridDim.x + blockIdx.x) * kKV + i] = acc;
 }
 
-__global__ void fmt_kv_combine_kernel(const float* __restrict__ partial, int nblk, float* __restrict__ kv) {
-  const int v = blockIdx.x;
-  const int i = threadIdx.x;
-  if (i >= kKV) return;
+// acc[mb] = sum_s A[mb][s] * in[s>>2][s&3]  (in: the B operand registers, D-layout of the input)
+template <int OUT, int IN>
+__device__ __forceinline__ void mfma_linear(const float (&frag)[OUT / 16][IN / 4], const floatx4 (&in)[IN / 16],
+                                            floatx4 (&acc)[OUT / 16]) {
+#pragma unroll
+  for (int mb = 0; mb < OUT / 16; ++mb) acc[mb] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < IN / 4; ++s)
+#pragma unroll
+    for (int mb = 0; mb < OUT / 16; ++mb)
+      acc[mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(frag[mb][s], in[s >> 2][s & 3], acc[mb], 0, 0, 0);
+}
+
+// NT independent tiles interleaved: NT x OUT/16 independent accumulation chains in flight
+template <int OUT, int IN, int NT>
+__device__ __forceinline__ void mfma_linear_n(const float (&frag)[OUT / 16][IN / 4], const floatx4 (&in)[NT][IN / 16],
+                                              floatx4 (&acc)[NT][OUT / 16]) {
+#pragma unroll
+  for (int p = 0; p < NT; ++p)
+#pragma unroll
+    for (int mb = 0; mb < OUT / 16; ++mb) acc[p][mb] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < IN / 4; ++s)
+#pragma unroll
+    for (int p = 0; p < NT; ++p)
+#pragma unroll
+      for (int mb = 0; mb < OUT / 16; ++mb)
+        acc[p][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(frag[mb][s], in[p][s >> 2][s & 3], acc[p][mb], 0, 0, 0);
+}
+
+// a token's 32 features are spread over lanes t, t+16, t+32, t+48 (8 per lane)
+__device__ __forceinline__ float token_sum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+__device__ __forceinline__ void layer_norm_frag(floatx4 (&x)[2], const float* __restrict__ g,
+                                                const float* __restrict__ b, int lane) {
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += partial[((size_t)v * nblk + b) * kKV + i];
-  kv[(size_t)v * kKV + i] = s;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s += x[mb][r];
+  const float mean = token_sum(s) / (float)kD;
+  float v = 0.f;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d = x[mb][r] - mean;
+      v = fmaf(d, d, v);
+    }
+  const float rstd = 1.f / sqrtf(token_sum(v) / (float)kD + 1e-5f);
+  const float bias = -rstd * mean;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 16 * mb + 4 * (lane >> 4) + r;
+      x[mb][r] = fmaf(fmaf(x[mb][r], rstd, bias), g[f], b[f]);
+    }
 }
 
+__device__ __forceinline__ void load_token_frag(const float* __restrict__ row, floatx4 (&x)[2], int lane) {
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+    const float4 t = *reinterpret_cast<const float4*>(row + 16 * mb + 4 * (lane >> 4));
+    x[mb] = floatx4{t.x, t.y, t.z, t.w};
+  }
+}
+
+constexpr int kTilesPerWave = 8;  // 16-token tiles per wave: amortises the weight-fragment loads
+
+// (KV, Ksum) partial sums: per wave, tiles of 16 source tokens; K, V by MFMA; per lane the
+// two heads it owns are accumulated over its tokens, then summed over the 16 token lanes.
+__global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __restrict__ src, int S,
+                                                              const float* __restrict__ w,
+                                                              float* __restrict__ partial) {
+  __shared__ float red[4][kKV];
+  const int v = blockIdx.y;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4;
+  float wk[2][8], wvv[2][8];
+  load_afrag<32, 32, true>(w + TMVS_ENC_WK, wk, lane);
+  load_afrag<32, 32, true>(w + TMVS_ENC_WV, wvv, lane);
+  float bk[2][4], bv[2][4];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bk[mb][r] = w[TMVS_ENC_BK + 16 * mb + 4 * g + r];
+      bv[mb][r] = w[TMVS_ENC_BV + 16 * mb + 4 * g + r];
+    }
+  float kv[2][16], ks[2][4];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) kv[mb][i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ks[mb][i] = 0.f;
+  }
+  const float* sv = src + (size_t)v * S * kD;
+  const int tile0 = (blockIdx.x * 4 + wv) * kTilesPerWave;
+#pragma unroll 1
+  for (int it = 0; it < kTilesPerWave; it += 2) {
+    if ((tile0 + it) * 16 >= S) break;  // wave-uniform
+    bool okp[2];
+    floatx4 xin[2][2], kk[2][2], vv[2][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int t = (tile0 + it + p) * 16 + (lane & 15);
+      okp[p] = t < S;
+      load_token_frag(sv + (size_t)(okp[p] ? t : S - 1) * kD, xin[p], lane);
+    }
+    mfma_linear_n<32, 32, 2>(wk, xin, kk);
+    mfma_linear_n<32, 32, 2>(wvv, xin, vv);
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      const bool ok = okp[p];
+      float kh[4], vh[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        kh[r] = ok ? elu1(kk[p][mb][r] + bk[mb][r]) : 0.f;
+        vh[r] = ok ? vv[p][mb][r] + bv[mb][r] : 0.f;
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) kv[mb][m * 4 + d] = fmaf(kh[d], vh[m], kv[mb][m * 4 + d]);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) ks[mb][d] += kh[d];
+    }
+  }
+  // sum over the 16 token lanes of each lane group (fixed butterfly)
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float x = kv[mb][i];
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) x += __shfl_xor(x, off, 64);
+      kv[mb][i] = x;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float x = ks[mb][i];
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) x += __shfl_xor(x, off, 64);
+      ks[mb][i] = x;
+    }
+  }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      const int h = 4 * mb + g;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) red[wv][h * 16 + i] = kv[mb][i];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wv][128 + h * 4 + i] = ks[mb][i];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kKV) {
+    const int i = threadIdx.x;
+    partial[((size_t)v * gridDim.x + blockIdx.x) * kKV + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+  }
+}
+
+// grid (nv, 5): 8 groups x 32 entries; group g sums partial blocks g, g+8, ... with all
+// loads independent, then the 8 group sums are added in a fixed order (bitwise reproducible).
+__global__ __launch_bounds__(256) void fmt_kv_combine_kernel(const float* __restrict__ partial, int nblk,
+                                                             float* __restrict__ kv) {
+  __shared__ float red[8][32];
+  const int v = blockIdx.x;
+  const int e = blockIdx.y * 32 + (threadIdx.x & 31);
+  const int g = threadIdx.x >> 5;
+  float s = 0.f;
+  for (int b = g; b < nblk; b += 8) s += partial[((size_t)v * nblk + b) * kKV + e];
+  red[g][threadIdx.x & 31] = s;
+  __syncthreads();
+  if (g == 0) {
+    float t = red[0][threadIdx.x];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) t += red[k][threadIdx.x];
+    kv[(size_t)v * kKV + e] = t;
+  }
+}
+
+// The rest of EncoderLayer.forward for tiles of 16 query tokens, entirely in registers;
+// kApplyNT tiles are processed together so their MFMA chains interleave.
+constexpr int kApplyNT = 2;
 __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, int L, const float* __restrict__ kvg,
                                                         long kv_stride, const float* __restrict__ w) {
-  const int l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= L) return;
+  __shared__ float kvs[kKV];
+  __shared__ float vec[TMVS_ENC_NPARAMS - TMVS_ENC_LN1G];  // LN params
   const int v = blockIdx.y;
-  const float* kv = kvg + (size_t)v * kv_stride;
-  float* xp = x + ((size_t)v * L + l) * kD;
-  float xs[kD];
-  load_token(xp, xs);
-  float msg[kD];
-  {
-    float q[kD];
-    linear<kD, kD>(w + TMVS_ENC_WQ, w + TMVS_ENC_BQ, xs, q);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4;
+  if (threadIdx.x < kKV) kvs[threadIdx.x] = kvg[(size_t)v * kv_stride + threadIdx.x];
+  if (threadIdx.x < 128) vec[threadIdx.x] = w[TMVS_ENC_LN1G + threadIdx.x];
+  float wq[2][8], wo[2][8], w1[4][8], w2[2][16];
+  load_afrag<32, 32, false>(w + TMVS_ENC_WQ, wq, lane);
+  load_afrag<32, 32, false>(w + TMVS_ENC_WO, wo, lane);
+  load_afrag<64, 32, false>(w + TMVS_ENC_W1, w1, lane);
+  load_afrag<32, 64, true>(w + TMVS_ENC_W2T, w2, lane);
+  __syncthreads();
+  float* xv = x + (size_t)v * L * kD;
+  const int tile0 = (blockIdx.x * 4 + wv) * kTilesPerWave;
+#pragma unroll 1
+  for (int it = 0; it < kTilesPerWave; it += kApplyNT) {
+    if ((tile0 + it) * 16 >= L) break;  // wave-uniform
+    constexpr int NT = kApplyNT;
+    float* row[NT];
+    bool ok[NT];
+    floatx4 xs[NT][2];
 #pragma unroll
-    for (int i = 0; i < kD; ++i) q[i] = elu1(q[i]);
+    for (int p = 0; p < NT; ++p) {
+      const int t = (tile0 + it + p) * 16 + (lane & 15);
+      ok[p] = t < L;
+      row[p] = xv + (size_t)(ok[p] ? t : L - 1) * kD;
+      load_token_frag(row[p], xs[p], lane);
+    }
+    floatx4 q[NT][2], msg[NT][2];
+    mfma_linear_n<32, 32, NT>(wq, xs, q);
 #pragma unroll
-    for (int h = 0; h < 8; ++h) {
-      float den = 0.f;
+    for (int p = 0; p < NT; ++p)
 #pragma unroll
-      for (int d = 0; d < 4; ++d) den = fmaf(q[h * 4 + d], kv[128 + h * 4 + d], den);
-      const float z = 1.f / (den + 1e-6f);
+      for (int mb = 0; mb < 2; ++mb) {
+        const int h = 4 * mb + g;
+        float qe[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        float num = 0.f;
+        for (int d = 0; d < 4; ++d) qe[d] = elu1(q[p][mb][d] + w[TMVS_ENC_BQ + 4 * h + d]);
+        float den = 0.f;
 #pragma unroll
-        for (int d = 0; d < 4; ++d) num = fmaf(q[h * 4 + d], kv[h * 16 + m * 4 + d], num);
-        msg[h * 4 + m] = num * z;
+        for (int d = 0; d < 4; ++d) den = fmaf(qe[d], kvs[128 + h * 4 + d], den);
+        const float z = 1.f / (den + 1e-6f);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          float num = 0.f;
+#pragma unroll
+          for (int d = 0; d < 4; ++d) num = fmaf(qe[d], kvs[h * 16 + m * 4 + d], num);
+          msg[p][mb][m] = num * z;
+        }
+      }
+    floatx4 a[NT][2];
+    mfma_linear_n<32, 32, NT>(wo, msg, a);
+#pragma unroll
+    for (int p = 0; p < NT; ++p) {
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xs[p][mb][r] = xs[p][mb][r] + (a[p][mb][r] + w[TMVS_ENC_BO + 16 * mb + 4 * g + r]);
+      layer_norm_frag(xs[p], vec, vec + kD, lane);
+    }
+    floatx4 hdn[NT][4], ff[NT][2];
+    mfma_linear_n<64, 32, NT>(w1, xs, hdn);
+#pragma unroll
+    for (int p = 0; p < NT; ++p)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hdn[p][mb][r] = relu(hdn[p][mb][r] + w[TMVS_ENC_B1 + 16 * mb + 4 * g + r]);
+    mfma_linear_n<32, 64, NT>(w2, hdn, ff);
+#pragma unroll
+    for (int p = 0; p < NT; ++p) {
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xs[p][mb][r] = xs[p][mb][r] + (ff[p][mb][r] + w[TMVS_ENC_B2 + 16 * mb + 4 * g + r]);
+      layer_norm_frag(xs[p], vec + 2 * kD, vec + 3 * kD, lane);
+      if (ok[p]) {
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+          *reinterpret_cast<float4*>(row[p] + 16 * mb + 4 * g) =
+              make_float4(xs[p][mb][0], xs[p][mb][1], xs[p][mb][2], xs[p][mb][3]);
       }
     }
   }
-  {
-    float a[kD];
-    linear<kD, kD>(w + TMVS_ENC_WO, w + TMVS_ENC_BO, msg, a);
-#pragma unroll
-    for (int i = 0; i < kD; ++i) xs[i] = xs[i] + a[i];
-  }
-  layer_norm(xs, w + TMVS_ENC_LN1G, w + TMVS_ENC_LN1B);
-  {
-    float hdn[2 * kD];
-    linear<2 * kD, kD>(w + TMVS_ENC_W1, w + TMVS_ENC_B1, xs, hdn);
-#pragma unroll
-    for (int i = 0; i < 2 * kD; ++i) hdn[i] = relu(hdn[i]);
-    float f[kD];
-    linear<kD, 2 * kD>(w + TMVS_ENC_W2, w + TMVS_ENC_B2, hdn, f);
-#pragma unroll
-    for (int i = 0; i < kD; ++i) xs[i] = xs[i] + f[i];
-  }
-  layer_norm(xs, w + TMVS_ENC_LN2G, w + TMVS_ENC_LN2B);
-  float4* o = reinterpret_cast<float4*>(xp);
-#pragma unroll
-  for (int c4 = 0; c4 < kD / 4; ++c4) o[c4] = make_float4(xs[4 * c4], xs[4 * c4 + 1], xs[4 * c4 + 2], xs[4 * c4 + 3]);
 }
 
-static int kv_nblk(int S) { return (S + kKvBlock * kKvTokensPerThread - 1) / (kKvBlock * kKvTokensPerThread); }
+static int kv_nblk(int S) { return (S + 16 * 4 * kTilesPerWave - 1) / (16 * 4 * kTilesPerWave); }
+static int apply_nblk(int L) { return (L + 16 * 4 * kTilesPerWave - 1) / (16 * 4 * kTilesPerWave); }
 
 }  // namespace tmvs
 
@@ -215,7 +434,7 @@ extern "C" int tmvs_fmt_kv(const float* source, int nv, int s_tokens, const floa
   hipLaunchKernelGGL(fmt_kv_partial_kernel, dim3(nblk, nv), dim3(kKvBlock), 0, st, source, s_tokens, enc_w,
                      (float*)workspace);
   TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(fmt_kv_combine_kernel, dim3(nv), dim3(kKV), 0, st, (const float*)workspace, nblk, kv);
+  hipLaunchKernelGGL(fmt_kv_combine_kernel, dim3(nv, kKV / 32), dim3(256), 0, st, (const float*)workspace, nblk, kv);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -223,7 +442,7 @@ extern "C" int tmvs_fmt_kv(const float* source, int nv, int s_tokens, const floa
 extern "C" int tmvs_fmt_apply(float* x, int nv, int l_tokens, const float* kv, long kv_view_stride,
                               const float* enc_w, void* stream) {
   if (!x || !kv || !enc_w || nv <= 0 || l_tokens <= 0 || kv_view_stride < 0) return TMVS_ERR_ARG;
-  hipLaunchKernelGGL(fmt_apply_kernel, dim3((l_tokens + 255) / 256, nv), dim3(256), 0, (hipStream_t)stream, x,
+  hipLaunchKernelGGL(fmt_apply_kernel, dim3(apply_nblk(l_tokens), nv), dim3(256), 0, (hipStream_t)stream, x,
                      l_tokens, kv, kv_view_stride, enc_w);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;

@@ -1,7 +1,8 @@
 // FMT_with_pathway lateral step (models/FMT.py:195-228), fused:
 //   out = smooth(bilinear_up2(reduce(coarse)) + lateral)
 // reduce = 1x1 conv (no bias), bilinear align_corners=False (F.interpolate default, :209),
-// smooth = 3x3 conv pad 1 (no bias). A workgroup owns a 16x16 output tile: it reduces the
+// smooth = 3x3 conv pad 1 (no bias). Weights arrive re-laid-out ([ci][co] and [ci][tap][co]) so
+// every input value meets CF consecutive weights (one scalar load). A workgroup owns a 16x16 output tile: it reduces the
 // 10x10 coarse pixels the tile's 18x18 halo interpolates from into LDS, builds the up-sampled
 // + lateral halo in LDS, then each thread convolves one output pixel for all channels and
 // writes it channels-last -- the layout the cost-volume kernel gathers from.
@@ -59,13 +60,15 @@ __global__ __launch_bounds__(256) void pathway_kernel(const float* __restrict__ 
       xin[4 * i4 + 2] = t.z;
       xin[4 * i4 + 3] = t.w;
     }
+    float acc[CF];
 #pragma unroll
-    for (int o = 0; o < CF; ++o) {
-      float acc = 0.f;
+    for (int o = 0; o < CF; ++o) acc[o] = 0.f;
+#pragma unroll 2
+    for (int i = 0; i < CC; ++i)
 #pragma unroll
-      for (int i = 0; i < CC; ++i) acc = fmaf(wred[o * CC + i], xin[i], acc);
-      red[o][r][c] = acc;
-    }
+      for (int o = 0; o < CF; ++o) acc[o] = fmaf(wred[i * CF + o], xin[i], acc[o]);
+#pragma unroll
+    for (int o = 0; o < CF; ++o) red[o][r][c] = acc[o];
   }
   __syncthreads();
   // 2) bilinear x2 up-sampling + lateral over the 18x18 halo (zero outside the image)
@@ -96,15 +99,15 @@ __global__ __launch_bounds__(256) void pathway_kernel(const float* __restrict__ 
   float acc[CF];
 #pragma unroll
   for (int o = 0; o < CF; ++o) acc[o] = 0.f;
-#pragma unroll
+#pragma unroll 1
   for (int i = 0; i < CF; ++i) {
-    float win[9];
+#pragma unroll 3
+    for (int k = 0; k < 9; ++k) {
+      const float xv = inb[i][ty + k / 3][tx + k % 3];
+      const float* __restrict__ wk = wsm + (i * 9 + k) * CF;  // 16 consecutive weights: one s_load
 #pragma unroll
-    for (int k = 0; k < 9; ++k) win[k] = inb[i][ty + k / 3][tx + k % 3];
-#pragma unroll
-    for (int o = 0; o < CF; ++o)
-#pragma unroll
-      for (int k = 0; k < 9; ++k) acc[o] = fmaf(wsm[(o * CF + i) * 9 + k], win[k], acc[o]);
+      for (int o = 0; o < CF; ++o) acc[o] = fmaf(wk[o], xv, acc[o]);
+    }
   }
   float4* op = reinterpret_cast<float4*>(out + (((size_t)v * H + y) * W + x) * CF);
 #pragma unroll

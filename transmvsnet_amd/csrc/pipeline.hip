@@ -1,0 +1,84 @@
+// Native orchestration of the hot path: whole-FMT and whole-DepthNet-stage entry points that
+// enqueue their kernels back to back on one stream (no per-kernel host round trip).
+#include "common.h"
+
+static size_t align_up256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+extern "C" size_t tmvs_fmt_forward_workspace(int nv, int l_tokens) {
+  // kv slabs (one per layer application in flight) + 4 cross-layer kv + per-view kv
+  return align_up256(tmvs_fmt_kv_workspace(nv, l_tokens)) + align_up256((size_t)(4 + nv) * TMVS_KV_NFLOATS * 4);
+}
+
+// FMT of FMT_with_pathway (models/FMT.py:147-177, 212-226), all views batched on the launch
+// grid's y dimension.
+extern "C" int tmvs_fmt_forward(const float* stage1, long view_stride, const float* pe, int pe_h, int pe_w, int nv,
+                                int height, int width, const float* const* enc_w, void* workspace,
+                                size_t workspace_bytes, float* tokens, void* stream) {
+  if (!stage1 || !pe || !enc_w || !workspace || !tokens || nv <= 0) return TMVS_ERR_ARG;
+  for (int i = 0; i < 8; ++i)
+    if (!enc_w[i]) return TMVS_ERR_ARG;
+  const int L = height * width;
+  if (workspace_bytes < tmvs_fmt_forward_workspace(nv, L)) return TMVS_ERR_ARG;
+  char* ws = (char*)workspace;
+  const size_t slab = align_up256(tmvs_fmt_kv_workspace(nv, L));
+  void* kv_ws = ws;
+  float* kv_cross = (float*)(ws + slab);
+  float* kv_self = kv_cross + 4 * TMVS_KV_NFLOATS;
+  int rc;
+  if ((rc = tmvs_fmt_embed(stage1, view_stride, pe, pe_h, pe_w, nv, 32, height, width, tokens, stream))) return rc;
+  // Self layers 0,2,4,6 carry the same weights for the reference view (FMT.py:155-158) and the
+  // source views (:171-172): each runs on all nv views in one launch (per-view K/V). The
+  // reference output of self layer 2j is ref_feature_list[j], the K/V source of cross layer 2j+1.
+  float* src = tokens + (size_t)L * 32;
+  for (int j = 0; j < 4; ++j) {
+    const int i = 2 * j;
+    if ((rc = tmvs_fmt_kv(tokens, nv, L, enc_w[i], kv_ws, slab, kv_self, stream))) return rc;
+    if ((rc = tmvs_fmt_apply(tokens, nv, L, kv_self, TMVS_KV_NFLOATS, enc_w[i], stream))) return rc;
+    if (nv == 1) continue;
+    if ((rc = tmvs_fmt_kv(tokens, 1, L, enc_w[i + 1], kv_ws, slab, kv_cross + j * TMVS_KV_NFLOATS, stream))) return rc;
+    if ((rc = tmvs_fmt_apply(src, nv - 1, L, kv_cross + j * TMVS_KV_NFLOATS, 0, enc_w[i + 1], stream))) return rc;
+  }
+  return TMVS_OK;
+}
+
+extern "C" size_t tmvs_depth_stage_workspace(int ndepth, int height, int width, int base_ch) {
+  const size_t vol = (size_t)ndepth * height * width * 4;
+  return 2 * align_up256(vol) + align_up256(tmvs_costregnet_workspace(1, ndepth, height, width, base_ch));
+}
+
+// One cascade stage of TransMVSNet.forward for one sample (models/TransMVSNet.py:174-221):
+// hypotheses -> fused cost volume -> CostRegNet -> softmax / winner-take-all.
+extern "C" int tmvs_depth_stage(const float* depth_values, int n_values, const float* prev_depth, int prev_h,
+                                int prev_w, const float* feat, int n_views, int channels, int ndepth, float ratio,
+                                int full_h, int full_w, int stage_scale, const float* proj, const float* pw_params,
+                                float* view_w, int vw_shift, const TmvsCostRegWeights* cr, void* workspace,
+                                size_t workspace_bytes, float clamp_lo, float clamp_hi, float* hyp_out,
+                                float* prob_out, float* depth_out, float* depth_raw_out, float* conf_out,
+                                void* stream) {
+  if (!feat || !view_w || !cr || !workspace || !hyp_out || n_views < 2) return TMVS_ERR_ARG;
+  const int h = full_h / stage_scale, w = full_w / stage_scale;
+  if (workspace_bytes < tmvs_depth_stage_workspace(ndepth, h, w, cr->base_ch)) return TMVS_ERR_ARG;
+  const size_t vol = (size_t)ndepth * h * w;
+  char* ws = (char*)workspace;
+  float* sim = (float*)ws;
+  float* logits = (float*)(ws + align_up256(vol * 4));
+  char* crws = ws + 2 * align_up256(vol * 4);
+  const size_t crbytes = workspace_bytes - 2 * align_up256(vol * 4);
+  const int V = n_views - 1;
+  int rc;
+  if ((rc = tmvs_stage_hypotheses(depth_values, n_values, prev_depth, prev_h, prev_w, 1, ndepth, ratio, full_h, full_w,
+                                  stage_scale, hyp_out, stream)))
+    return rc;
+  const float* ref = feat;
+  const float* src = feat + (size_t)h * w * channels;
+  if (pw_params)
+    rc = tmvs_warp_corr(ref, src, proj, hyp_out, nullptr, 0, 0, V, pw_params, 1, V, channels, ndepth, h, w, 0, sim,
+                        nullptr, view_w, stream);
+  else
+    rc = tmvs_warp_corr(ref, src, proj, hyp_out, view_w, vw_shift, 0, V, nullptr, 1, V, channels, ndepth, h, w, 0,
+                        sim, nullptr, nullptr, stream);
+  if (rc) return rc;
+  if ((rc = tmvs_costregnet(sim, 1, ndepth, h, w, cr, crws, crbytes, logits, stream))) return rc;
+  return tmvs_softmax_wta(logits, hyp_out, 1, ndepth, h, w, clamp_lo, clamp_hi, prob_out, depth_out, depth_raw_out,
+                          conf_out, stream);
+}

@@ -1,12 +1,10 @@
 // Fused cost-volume build for one cascade stage (DepthNet steps 1-2,
 // reference models/TransMVSNet.py:58-93 and homo_warping models/module.py:284-322).
 //
-// One thread owns one reference pixel and DPT consecutive depth planes; the G = D/DPT
-// threads of a pixel are adjacent lanes of one wave (the PixelwiseNet max over D is a
-// lane-shuffle reduction among them). Per source view the thread projects its pixel into
-// the view, bilinearly samples the channels-last source features (4 taps x C floats,
-// float4 loads) and forms the single-group correlation against the reference features it
-// keeps in registers; the warped [C,D,H,W] volume of the reference never exists.
+// A pixel is owned by C/4 adjacent lanes (see warp_corr_kernel); per source view they project
+// the pixel's depth planes into the view, bilinearly sample the channels-last source features
+// (one contiguous C*4-byte row per tap per lane group) and form the single-group correlation
+// against the reference features held in registers; the warped [C,D,H,W] volume never exists.
 //
 // fp32 op order follows the reference's PyTorch-CPU kernels (DESIGN.md "Numerics"):
 //   rot·(x,y,1)   : fmaf(r1, y, r0*x) + r2            (bmm, FMA chain)
@@ -14,6 +12,7 @@
 //   ix = (xn + 1) * ((W-1)/2)                          (grid_sample, align_corners=True)
 //   v  = fmaf(se_v,se, fmaf(sw_v,sw, fmaf(ne_v,ne, nw_v*nw)))  (zeros padding)
 //   sim = (Σ_c v_c*ref_c) / C ; sim_sum += sim*w ; w_sum = 1e-5 + Σ w ; sim_sum / w_sum
+// (the channel sum: serial within each lane's 4 channels, then a fixed xor tree over lanes)
 #include "common.h"
 
 namespace tmvs {
@@ -47,37 +46,69 @@ __device__ __forceinline__ float pixelwise_logit(float s, const float* __restric
   return out + b2;
 }
 
-template <int C, int DPT, int G, bool PW, bool PARTIAL>
+// Lane layout: a pixel is served by LPS = C/4 adjacent lanes ("group"); lane k of the group
+// owns channel quad k (4 channels, one 16-byte load per tap) and depth planes k, k+LPS, ...
+// For every depth plane the group issues one 16-byte load per lane per tap, i.e. the C
+// channels of a tap arrive as one contiguous row (C*4 bytes) per group: a wave-instruction
+// touches 64/LPS rows instead of 64 scattered 16-byte pieces. Each lane projects only its own
+// depth planes; the tap geometry (x0, y0, fractional x, fractional y) of plane j*LPS+t is
+// broadcast from lane t with lane shuffles, and the channel dot product is reduced across the
+// group with xor shuffles (channel order: 4-channel serial sums, then a fixed tree).
+template <int C>
+struct Tap {
+  int x0, y0;
+  float fx, fy;
+};
+
+__device__ __forceinline__ void project(const float rx, const float ry, const float rz, const float tx,
+                                        const float ty, const float tz, const float dep, const float halfw,
+                                        const float halfh, int& x0i, int& y0i, float& fx, float& fy) {
+  const float X = rx * dep + tx;
+  const float Y = ry * dep + ty;
+  const float Z = rz * dep + tz;
+  float xn = (X / Z) / halfw - 1.f;
+  float yn = (Y / Z) / halfh - 1.f;
+  if (Z < 1e-6f) {
+    xn = -99.f;
+    yn = -99.f;
+  }
+  const float ix = (xn + 1.f) * halfw;
+  const float iy = (yn + 1.f) * halfh;
+  const float x0 = floorf(ix), y0 = floorf(iy);
+  fx = ix - x0;
+  fy = iy - y0;
+  // clamp far-away samples (all four taps outside) to a sentinel that stays outside
+  x0i = (int)fminf(fmaxf(x0, -2.f), 65536.f);
+  y0i = (int)fminf(fmaxf(y0, -2.f), 65536.f);
+}
+
+template <int C, int D, bool PW, bool PARTIAL>
 __global__ __launch_bounds__(256) void warp_corr_kernel(
     const float* __restrict__ ref, const float* __restrict__ src, const float* __restrict__ hyp,
     const float* __restrict__ vw_in, float* __restrict__ sim_out, float* __restrict__ wsum_out,
     float* __restrict__ vw_out, int V, int H, int W, int vw_shift, int vw_offset, int vw_total, WarpArgs args) {
-  constexpr int PIX_PER_BLOCK = 256 / G;
+  constexpr int LPS = C / 4;          // lanes per pixel
+  constexpr int SPW = 64 / LPS;       // pixels per wave
+  constexpr int PIX = 4 * SPW;        // pixels per block
+  constexpr int DPT = D / LPS;        // depth planes owned per lane
+  static_assert(D % LPS == 0, "D must be a multiple of C/4");
   const int HW = H * W;
-  const int nblk = (HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK;
+  const int nblk = (HW + PIX - 1) / PIX;
   const int tile = xcd_remap(blockIdx.x, nblk);
-  const int g = threadIdx.x % G;
-  int p = tile * PIX_PER_BLOCK + threadIdx.x / G;
+  const int lane = threadIdx.x & 63;
+  const int k = lane % LPS;
+  const int gbase = lane - k;
+  int p = tile * PIX + (threadIdx.x >> 6) * SPW + lane / LPS;
   const bool active = p < HW;
-  if (!active) p = HW - 1;  // keep the lane alive for the G-lane shuffles; never stores
+  if (!active) p = HW - 1;
   const int py = p / W, px = p - py * W;
-  const float fx = (float)px, fy = (float)py;
-  const int d0 = g * DPT;
+  const float fxp = (float)px, fyp = (float)py;
 
-  float refv[C];
-#pragma unroll
-  for (int c4 = 0; c4 < C / 4; ++c4) {
-    const float4 r = *reinterpret_cast<const float4*>(ref + (size_t)p * C + c4 * 4);
-    refv[c4 * 4 + 0] = r.x;
-    refv[c4 * 4 + 1] = r.y;
-    refv[c4 * 4 + 2] = r.z;
-    refv[c4 * 4 + 3] = r.w;
-  }
+  const float4 r4 = *reinterpret_cast<const float4*>(ref + (size_t)p * C + 4 * k);
   float dep[DPT];
 #pragma unroll
-  for (int j = 0; j < DPT; ++j) dep[j] = hyp[(size_t)(d0 + j) * HW + p];
-
-  const float halfw = (float)(W - 1) / 2.f;  // (width - 1) / 2, exact
+  for (int j = 0; j < DPT; ++j) dep[j] = hyp[(size_t)(j * LPS + k) * HW + p];
+  const float halfw = (float)(W - 1) / 2.f;
   const float halfh = (float)(H - 1) / 2.f;
   float ssum[DPT];
 #pragma unroll
@@ -86,76 +117,62 @@ __global__ __launch_bounds__(256) void warp_corr_kernel(
 
   for (int v = 0; v < V; ++v) {
     const float* R = args.proj[v];
-    const float rx = fmaf(R[1], fy, R[0] * fx) + R[2];
-    const float ry = fmaf(R[5], fy, R[4] * fx) + R[6];
-    const float rz = fmaf(R[9], fy, R[8] * fx) + R[10];
-    const float tx = R[3], ty = R[7], tz = R[11];
-    const float* __restrict__ sv = src + (size_t)v * HW * C;
+    const float rx = fmaf(R[1], fyp, R[0] * fxp) + R[2];
+    const float ry = fmaf(R[5], fyp, R[4] * fxp) + R[6];
+    const float rz = fmaf(R[9], fyp, R[8] * fxp) + R[10];
+    const float* __restrict__ sv = src + (size_t)v * HW * C + 4 * k;
     float sim[DPT];
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
-      const float X = rx * dep[j] + tx;
-      const float Y = ry * dep[j] + ty;
-      const float Z = rz * dep[j] + tz;
-      float xn = (X / Z) / halfw - 1.f;
-      float yn = (Y / Z) / halfh - 1.f;
-      if (Z < 1e-6f) {
-        xn = -99.f;
-        yn = -99.f;
-      }
-      const float ix = (xn + 1.f) * halfw;
-      const float iy = (yn + 1.f) * halfh;
-      const float x0 = floorf(ix), y0 = floorf(iy);
-      const float we = ix - x0, ea = 1.f - we;
-      const float n = iy - y0, s = 1.f - n;
-      const float wnw = s * ea, wne = s * we, wsw = n * ea, wse = n * we;
-      const bool vx0 = x0 >= 0.f && x0 <= (float)(W - 1);
-      const bool vx1 = x0 + 1.f >= 0.f && x0 + 1.f <= (float)(W - 1);
-      const bool vy0 = y0 >= 0.f && y0 <= (float)(H - 1);
-      const bool vy1 = y0 + 1.f >= 0.f && y0 + 1.f <= (float)(H - 1);
-      const int xi0 = vx0 ? (int)x0 : 0, xi1 = vx1 ? (int)x0 + 1 : 0;
-      const int yi0 = vy0 ? (int)y0 : 0, yi1 = vy1 ? (int)y0 + 1 : 0;
-      const float* t00 = sv + ((size_t)yi0 * W + xi0) * C;
-      const float* t01 = sv + ((size_t)yi0 * W + xi1) * C;
-      const float* t10 = sv + ((size_t)yi1 * W + xi0) * C;
-      const float* t11 = sv + ((size_t)yi1 * W + xi1) * C;
-      const bool m00 = vy0 && vx0, m01 = vy0 && vx1, m10 = vy1 && vx0, m11 = vy1 && vx1;
-      float acc = 0.f;
+      int mx0, my0;
+      float mfx, mfy;
+      project(rx, ry, rz, R[3], R[7], R[11], dep[j], halfw, halfh, mx0, my0, mfx, mfy);
 #pragma unroll
-      for (int c4 = 0; c4 < C / 4; ++c4) {
-        float4 a = *reinterpret_cast<const float4*>(t00 + c4 * 4);
-        float4 b = *reinterpret_cast<const float4*>(t01 + c4 * 4);
-        float4 c = *reinterpret_cast<const float4*>(t10 + c4 * 4);
-        float4 d = *reinterpret_cast<const float4*>(t11 + c4 * 4);
-        if (!m00) a = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (!m01) b = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (!m10) c = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (!m11) d = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float va[4] = {a.x, a.y, a.z, a.w};
-        const float vb[4] = {b.x, b.y, b.z, b.w};
-        const float vc[4] = {c.x, c.y, c.z, c.w};
-        const float vd[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float val = fmaf(vd[k], wse, fmaf(vc[k], wsw, fmaf(vb[k], wne, va[k] * wnw)));
-          acc = acc + val * refv[c4 * 4 + k];
+      for (int t = 0; t < LPS; ++t) {
+        int x0 = mx0, y0 = my0;
+        float we = mfx, n = mfy;
+        if constexpr (LPS > 1) {
+          x0 = __shfl(mx0, gbase + t, 64);
+          y0 = __shfl(my0, gbase + t, 64);
+          we = __shfl(mfx, gbase + t, 64);
+          n = __shfl(mfy, gbase + t, 64);
         }
+        const float ea = 1.f - we, s = 1.f - n;
+        const float wnw = s * ea, wne = s * we, wsw = n * ea, wse = n * we;
+        const bool vx0 = x0 >= 0 && x0 <= W - 1, vx1 = x0 + 1 >= 0 && x0 + 1 <= W - 1;
+        const bool vy0 = y0 >= 0 && y0 <= H - 1, vy1 = y0 + 1 >= 0 && y0 + 1 <= H - 1;
+        const int xa = vx0 ? x0 : 0, xb = vx1 ? x0 + 1 : 0;
+        const int ya = vy0 ? y0 : 0, yb = vy1 ? y0 + 1 : 0;
+        float4 a = *reinterpret_cast<const float4*>(sv + ((size_t)ya * W + xa) * C);
+        float4 b = *reinterpret_cast<const float4*>(sv + ((size_t)ya * W + xb) * C);
+        float4 c = *reinterpret_cast<const float4*>(sv + ((size_t)yb * W + xa) * C);
+        float4 d = *reinterpret_cast<const float4*>(sv + ((size_t)yb * W + xb) * C);
+        if (!(vy0 && vx0)) a = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!(vy0 && vx1)) b = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!(vy1 && vx0)) c = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!(vy1 && vx1)) d = make_float4(0.f, 0.f, 0.f, 0.f);
+        float acc = 0.f;
+        acc = acc + fmaf(d.x, wse, fmaf(c.x, wsw, fmaf(b.x, wne, a.x * wnw))) * r4.x;
+        acc = acc + fmaf(d.y, wse, fmaf(c.y, wsw, fmaf(b.y, wne, a.y * wnw))) * r4.y;
+        acc = acc + fmaf(d.z, wse, fmaf(c.z, wsw, fmaf(b.z, wne, a.z * wnw))) * r4.z;
+        acc = acc + fmaf(d.w, wse, fmaf(c.w, wsw, fmaf(b.w, wne, a.w * wnw))) * r4.w;
+#pragma unroll
+        for (int off = 1; off < LPS; off <<= 1) acc += __shfl_xor(acc, off, 64);
+        if (k == t) sim[j] = acc / (float)C;
       }
-      sim[j] = acc / (float)C;
     }
     float w;
     if constexpr (PW) {
-      float wm = 0.f;  // sigmoid > 0, so 0 is a neutral start for the max
+      float wm = 0.f;  // sigmoid > 0: 0 is neutral for the max
 #pragma unroll
       for (int j = 0; j < DPT; ++j) {
         const float lg = pixelwise_logit(sim[j], args.pw);
-        const float sg = 1.f / (1.f + expf(-lg));
-        wm = fmaxf(wm, sg);
+        wm = fmaxf(wm, 1.f / (1.f + expf(-lg)));
       }
 #pragma unroll
-      for (int off = 1; off < G; off <<= 1) wm = fmaxf(wm, __shfl_xor(wm, off, G));
+      for (int off = 1; off < LPS; off <<= 1) wm = fmaxf(wm, __shfl_xor(wm, off, 64));
       w = wm;
-      if (active && g == 0) vw_out[(size_t)(vw_offset + v) * HW + p] = w;
+      if (active && k == 0) vw_out[(size_t)(vw_offset + v) * HW + p] = w;
     } else {
       const int Ws = W >> vw_shift, Hs = H >> vw_shift;
       w = vw_in[(size_t)(vw_offset + v) * Hs * Ws + (py >> vw_shift) * Ws + (px >> vw_shift)];
@@ -167,11 +184,11 @@ __global__ __launch_bounds__(256) void warp_corr_kernel(
   if (!active) return;
   if constexpr (PARTIAL) {
 #pragma unroll
-    for (int j = 0; j < DPT; ++j) sim_out[(size_t)(d0 + j) * HW + p] = ssum[j];
-    if (g == 0) wsum_out[p] = wsum;
+    for (int j = 0; j < DPT; ++j) sim_out[(size_t)(j * LPS + k) * HW + p] = ssum[j];
+    if (k == 0) wsum_out[p] = wsum;
   } else {
 #pragma unroll
-    for (int j = 0; j < DPT; ++j) sim_out[(size_t)(d0 + j) * HW + p] = ssum[j] / wsum;
+    for (int j = 0; j < DPT; ++j) sim_out[(size_t)(j * LPS + k) * HW + p] = ssum[j] / wsum;
   }
 }
 
@@ -222,14 +239,14 @@ __global__ void homo_warping_kernel(const float* __restrict__ src, const float* 
   }
 }
 
-template <int C, int DPT, int G, bool PW, bool PARTIAL>
+template <int C, int D, bool PW, bool PARTIAL>
 static int launch_warp(const float* ref, const float* src, const float* hyp, const float* vw_in, float* sim,
                        float* wsum, float* vw_out, int V, int H, int W, int vw_shift, int vw_offset, int vw_total,
                        const WarpArgs& args, hipStream_t st) {
-  constexpr int PIX = 256 / G;
+  constexpr int PIX = 4 * (64 / (C / 4));
   const int nblk = (H * W + PIX - 1) / PIX;
-  hipLaunchKernelGGL((warp_corr_kernel<C, DPT, G, PW, PARTIAL>), dim3(nblk), dim3(256), 0, st, ref, src, hyp, vw_in,
-                     sim, wsum, vw_out, V, H, W, vw_shift, vw_offset, vw_total, args);
+  hipLaunchKernelGGL((warp_corr_kernel<C, D, PW, PARTIAL>), dim3(nblk), dim3(256), 0, st, ref, src, hyp, vw_in, sim,
+                     wsum, vw_out, V, H, W, vw_shift, vw_offset, vw_total, args);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -238,17 +255,16 @@ template <int C, bool PW, bool PARTIAL>
 static int dispatch_depth(int D, const float* ref, const float* src, const float* hyp, const float* vw_in, float* sim,
                           float* wsum, float* vw_out, int V, int H, int W, int vw_shift, int vw_offset, int vw_total,
                           const WarpArgs& a, hipStream_t st) {
-#define TMVS_WARP_CASE(DD, DPT, G)                                                                                \
+#define TMVS_WARP_CASE(DD)                                                                                        \
   if (D == DD)                                                                                                    \
-    return launch_warp<C, DPT, G, PW, PARTIAL>(ref, src, hyp, vw_in, sim, wsum, vw_out, V, H, W, vw_shift,        \
-                                                vw_offset, vw_total, a, st);
-  TMVS_WARP_CASE(48, 12, 4)
-  TMVS_WARP_CASE(32, 8, 4)
-  TMVS_WARP_CASE(16, 8, 2)
-  TMVS_WARP_CASE(8, 8, 1)
-  TMVS_WARP_CASE(64, 16, 4)
-  TMVS_WARP_CASE(24, 12, 2)
-  TMVS_WARP_CASE(4, 4, 1)
+    return launch_warp<C, DD, PW, PARTIAL>(ref, src, hyp, vw_in, sim, wsum, vw_out, V, H, W, vw_shift, vw_offset, \
+                                           vw_total, a, st);
+  TMVS_WARP_CASE(48)
+  TMVS_WARP_CASE(32)
+  TMVS_WARP_CASE(16)
+  TMVS_WARP_CASE(8)
+  TMVS_WARP_CASE(64)
+  TMVS_WARP_CASE(24)
 #undef TMVS_WARP_CASE
   return TMVS_ERR_SHAPE;
 }

@@ -53,11 +53,12 @@ class EncoderLayer(nn.Module):
 
     def packed(self):
         a = self.attention
-        parts = [a.query_projection.weight, a.query_projection.bias, a.key_projection.weight, a.key_projection.bias,
-                 a.value_projection.weight, a.value_projection.bias, a.out_projection.weight, a.out_projection.bias,
-                 self.linear1.weight, self.linear1.bias, self.linear2.weight, self.linear2.bias,
-                 self.norm1.weight, self.norm1.bias, self.norm2.weight, self.norm2.bias]
-        flat = torch.cat([p.detach().float().reshape(-1) for p in parts])
+        parts = [a.query_projection.weight, a.query_projection.bias, a.key_projection.weight.t(),
+                 a.key_projection.bias, a.value_projection.weight.t(), a.value_projection.bias,
+                 a.out_projection.weight, a.out_projection.bias, self.linear1.weight, self.linear1.bias,
+                 self.linear2.weight.t(), self.linear2.bias, self.norm1.weight, self.norm1.bias, self.norm2.weight,
+                 self.norm2.bias]
+        flat = torch.cat([p.detach().float().contiguous().reshape(-1) for p in parts])
         assert flat.numel() == _lib.ENC_NPARAMS
         return flat
 
@@ -217,6 +218,7 @@ class TransMVSNet(nn.Module):
         self.DepthNet = DepthNet()
         self._prep = None
         self._pe = {}
+        self.decomposed = False  # True: one C-ABI call per op (instrumentation); False: native stage calls
         self.register_load_state_dict_post_hook(lambda m, k: m.invalidate())
 
     def invalidate(self):
@@ -233,10 +235,10 @@ class TransMVSNet(nn.Module):
         self._prep = {
             "device": device,
             "enc": enc,
-            "red1": fp.dim_reduction_1.weight.detach().float().reshape(16, 32).contiguous().to(device),
-            "red2": fp.dim_reduction_2.weight.detach().float().reshape(8, 16).contiguous().to(device),
-            "sm1": fp.smooth_1.weight.detach().float().contiguous().to(device),
-            "sm2": fp.smooth_2.weight.detach().float().contiguous().to(device),
+            "red1": fp.dim_reduction_1.weight.detach().float().reshape(16, 32).t().contiguous().to(device),
+            "red2": fp.dim_reduction_2.weight.detach().float().reshape(8, 16).t().contiguous().to(device),
+            "sm1": fp.smooth_1.weight.detach().float().permute(1, 2, 3, 0).contiguous().to(device),
+            "sm2": fp.smooth_2.weight.detach().float().permute(1, 2, 3, 0).contiguous().to(device),
             "cr": cr,
             "pw": self.DepthNet.pixel_wise_net.packed(),
         }
@@ -286,32 +288,19 @@ class TransMVSNet(nn.Module):
         outputs = {}
         for s in range(self.num_stage):
             name = f"stage{s + 1}"
-            outputs[name] = {k: torch.cat([p[name][k] for p in per], 0) for k in per[0][name]}
+            if b == 1:
+                outputs[name] = per[0][name]
+            else:
+                outputs[name] = {k: torch.cat([p[name][k] for p in per], 0) for k in per[0][name]}
             outputs.update(outputs[name])
         if return_view_weights:
-            return outputs, torch.cat(vws, 0)
+            return outputs, (vws[0] if b == 1 else torch.cat(vws, 0))
         return outputs
 
     def _fmt(self, s1, prep):
         """FMT_with_pathway stage-1 part (models/FMT.py:212-226) -> tokens [N, h1*w1, 32]."""
         n, c, h1, w1 = s1.shape
-        tokens = torch.empty(n, h1 * w1, c, device=s1.device)
-        ops.fmt_embed(s1, self._pe_slice(h1, w1, s1.device), tokens)
-        enc = prep["enc"]
-        ref, src = tokens[0:1], tokens[1:]
-        kv_cross = torch.empty(4, _lib.KV_NFLOATS, device=s1.device)
-        for i in range(0, 8, 2):  # ref view: self layers only; keep each output's cross K/V
-            kv = ops.fmt_kv(ref, enc[i])
-            ops.fmt_apply(ref, kv, enc[i])
-            ops.fmt_kv(ref, enc[i + 1], out=kv_cross[i // 2:i // 2 + 1])
-        if n > 1:
-            for i, name in enumerate(FMT_LAYERS):
-                if name == "self":
-                    kv = ops.fmt_kv(src, enc[i])
-                    ops.fmt_apply(src, kv, enc[i])
-                else:
-                    ops.fmt_apply(src, kv_cross[i // 2], enc[i], shared_kv=True)
-        return tokens
+        return ops.fmt_forward(s1, self._pe_slice(h1, w1, s1.device), prep["enc"])
 
     def _forward_one(self, f, rows, dv, img_hw, prep, view_shard):
         s1, s2, s3 = f["stage1"], f["stage2"], f["stage3"]
@@ -326,21 +315,28 @@ class TransMVSNet(nn.Module):
         view_w = None
         for s in range(self.num_stage):
             name = f"stage{s + 1}"
-            hyp = ops.stage_hypotheses(dv, depth_raw, self.ndepths[s], self.depth_interals_ratio[s], img_hw,
-                                       STAGE_SCALES[s])
             fs = nhwc[s]
-            if view_shard is None:
+            if view_shard is None and not self.decomposed:
                 if s == 0:
-                    sim, _, view_w = ops.warp_corr(fs[0:1], fs[1:].unsqueeze(0), rows[name], hyp,
-                                                   pw_params=prep["pw"])
+                    view_w = torch.empty(1, n - 1, fs.shape[1], fs.shape[2], device=fs.device)
+                out, depth_raw = ops.depth_stage(dv, depth_raw, fs, self.ndepths[s], self.depth_interals_ratio[s],
+                                                 img_hw, STAGE_SCALES[s], rows[name][0],
+                                                 prep["pw"] if s == 0 else None, view_w, s,
+                                                 prep["cr"][s][0], DEPTH_CLAMP)
+            else:  # per-op path: view-sharded mode, or per-kernel instrumentation (same kernels)
+                hyp = ops.stage_hypotheses(dv, depth_raw, self.ndepths[s], self.depth_interals_ratio[s], img_hw,
+                                           STAGE_SCALES[s])
+                if view_shard is not None:
+                    sim, vw_new = view_shard.cost_volume(fs, rows[name], hyp, s, view_w, prep["pw"])
+                elif s == 0:
+                    sim, _, vw_new = ops.warp_corr(fs[0:1], fs[1:].unsqueeze(0), rows[name], hyp, pw_params=prep["pw"])
                 else:
                     sim, _, _ = ops.warp_corr(fs[0:1], fs[1:].unsqueeze(0), rows[name], hyp, view_w_in=view_w,
                                               vw_shift=s)
-            else:
-                sim, vw_new = view_shard.cost_volume(fs, rows[name], hyp, s, view_w, prep["pw"])
                 if s == 0:
                     view_w = vw_new
-            logits = ops.costregnet(sim, prep["cr"][s][0])
-            prob, depth, depth_raw, conf = ops.softmax_wta(logits, hyp, DEPTH_CLAMP)
-            outputs[name] = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}
+                logits = ops.costregnet(sim, prep["cr"][s][0])
+                prob, depth, depth_raw, conf = ops.softmax_wta(logits, hyp, DEPTH_CLAMP)
+                out = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}
+            outputs[name] = out
         return outputs, view_w

@@ -253,3 +253,51 @@ def fmt_pathway(coarse_nhwc, lateral_nchw, w_reduce, w_smooth):
         _lib.check(_lib_h().tmvs_fmt_pathway(_ptr(coarse_nhwc), _ptr(lateral_nchw), cf * 4 * h * w, _ptr(w_reduce),
                                              _ptr(w_smooth), nv, cc, cf, h, w, _ptr(out), _stream()), "tmvs_fmt_pathway")
     return out
+
+
+# ----------------------------------------------------------------- native orchestration
+def fmt_forward(stage1_nchw, pe, enc_list, tokens=None):
+    """Whole FMT (models/FMT.py:147-177): stage1 [nv,32,H,W] -> tokens [nv,H*W,32]."""
+    _dev(stage1_nchw, "stage1")
+    nv, c, h, w = stage1_nchw.shape
+    tokens = torch.empty(nv, h * w, c, device=stage1_nchw.device) if tokens is None else tokens
+    nbytes = _lib_h().tmvs_fmt_forward_workspace(nv, h * w)
+    ws = torch.empty(nbytes // 4 + 64, device=stage1_nchw.device)
+    ptrs = (ctypes.c_void_p * 8)(*[e.data_ptr() for e in enc_list])
+    with _Span("tmvs_fmt_forward"):
+        _lib.check(_lib_h().tmvs_fmt_forward(_ptr(stage1_nchw), c * h * w, _ptr(pe), pe.shape[1], pe.shape[2], nv, h, w,
+                                             ptrs, _ptr(ws), ws.numel() * 4, _ptr(tokens), _stream()),
+                   "tmvs_fmt_forward")
+    return tokens
+
+
+def depth_stage(depth_values, prev_depth, feat_nhwc, ndepth, ratio, full_hw, stage_scale, proj12, pw_params,
+                view_w, vw_shift, cr_weights, clamp=(425.0, 935.0)):
+    """One cascade stage for one sample (models/TransMVSNet.py:174-221). feat [N,h,w,C] NHWC.
+
+    Returns dict(depth, photo_confidence, prob_volume, depth_values) with a batch dim of 1, and depth_raw.
+    """
+    _dev(depth_values, "depth_values")
+    _dev(prev_depth, "prev_depth")
+    _dev(feat_nhwc, "feat")
+    _dev(view_w, "view_w")
+    n, h, w, c = feat_nhwc.shape
+    dev = feat_nhwc.device
+    hyp = torch.empty(1, ndepth, h, w, device=dev)
+    prob = torch.empty_like(hyp)
+    depth = torch.empty(1, h, w, device=dev)
+    raw = torch.empty_like(depth)
+    conf = torch.empty_like(depth)
+    nbytes = _lib_h().tmvs_depth_stage_workspace(ndepth, h, w, cr_weights.base_ch)
+    ws = torch.empty(nbytes // 4 + 64, device=dev)
+    proj = np.ascontiguousarray(proj12, np.float32).reshape(n - 1, 12)
+    pw = None if pw_params is None else np.ascontiguousarray(pw_params, np.float32)
+    ph, pwd = (prev_depth.shape[-2], prev_depth.shape[-1]) if prev_depth is not None else (0, 0)
+    with _Span("tmvs_depth_stage"):
+        _lib.check(_lib_h().tmvs_depth_stage(_ptr(depth_values), depth_values.shape[-1], _ptr(prev_depth), ph, pwd,
+                                             _ptr(feat_nhwc), n, c, ndepth, ctypes.c_float(ratio), full_hw[0], full_hw[1],
+                                             stage_scale, proj.ctypes.data, None if pw is None else pw.ctypes.data,
+                                             _ptr(view_w), vw_shift, ctypes.byref(cr_weights), _ptr(ws), ws.numel() * 4,
+                                             ctypes.c_float(clamp[0]), ctypes.c_float(clamp[1]), _ptr(hyp), _ptr(prob),
+                                             _ptr(depth), _ptr(raw), _ptr(conf), _stream()), "tmvs_depth_stage")
+    return {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}, raw
