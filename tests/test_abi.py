@@ -1,0 +1,96 @@
+"""The C-ABI boundary without a GPU: the library builds for gfx950, loads, exports every
+function include/transmvs.h declares with the argument count the ctypes binding uses, and the
+host-only entry points behave (version, status strings, BN fold, argument validation).
+Also: the product path refuses CPU tensors (no fallback)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from transmvsnet_amd import _lib, build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "transmvs.h")
+
+
+def _declarations():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", " ", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", " ", src)
+    decls = {}
+    for m in re.finditer(r"\b(?:int|size_t|const\s+char\s*\*)\s*\*?\s*(tmvs_\w+)\s*\(([^)]*)\)\s*;", src):
+        args = m.group(2).strip()
+        n = 0 if args in ("", "void") else args.count(",") + 1
+        decls[m.group(1)] = n
+    return decls
+
+
+@pytest.fixture(scope="module")
+def lib():
+    build.build()
+    return _lib.load()
+
+
+def test_header_declarations_match_binding():
+    decls = _declarations()
+    assert len(decls) >= 20
+    assert set(decls) == set(_lib.SIGNATURES), set(decls) ^ set(_lib.SIGNATURES)
+    for name, n in decls.items():
+        assert len(_lib.SIGNATURES[name][1]) == n, name
+
+
+def test_library_exports_every_symbol(lib):
+    for name in _declarations():
+        assert hasattr(lib, name), name
+    assert lib.tmvs_abi_version() == _lib.ABI_VERSION
+
+
+def test_header_constants_match_binding():
+    src = open(HEADER).read()
+    consts = dict(re.findall(r"#define\s+(TMVS_\w+)\s+(-?\d+)", src))
+    assert int(consts["TMVS_ABI_VERSION"]) == _lib.ABI_VERSION
+    assert int(consts["TMVS_PW_NPARAMS"]) == _lib.PW_NPARAMS
+    assert int(consts["TMVS_ENC_NPARAMS"]) == _lib.ENC_NPARAMS
+    assert int(consts["TMVS_KV_NFLOATS"]) == _lib.KV_NFLOATS
+    assert int(consts["TMVS_WARP_PARTIAL"]) == _lib.WARP_PARTIAL
+
+
+def test_status_strings(lib):
+    for code in (0, -1, -2, -3):
+        assert lib.tmvs_status_string(code)
+    assert lib.tmvs_status_string(0) != lib.tmvs_status_string(-2)
+
+
+def test_bn_fold_host(lib):
+    """tmvs_bn_fold is host code: alpha = gamma/sqrt(var+eps) (reference op order), shift = beta - mean*alpha."""
+    g = np.random.default_rng(0)
+    gamma, beta, mean = (g.standard_normal(16).astype(np.float32) for _ in range(3))
+    var = g.random(16).astype(np.float32) + 0.1
+    alpha = np.empty(16, np.float32)
+    shift = np.empty(16, np.float32)
+    p = lambda a: a.ctypes.data
+    assert lib.tmvs_bn_fold(p(gamma), p(beta), p(mean), p(var), 16, 1e-5, p(alpha), p(shift)) == 0
+    ea = (np.float32(1) / np.sqrt(var + np.float32(1e-5))) * gamma
+    np.testing.assert_array_equal(alpha, ea)
+    np.testing.assert_allclose(shift, beta - mean * ea, rtol=0, atol=1e-6)
+
+
+def test_argument_validation_without_gpu(lib):
+    """Null pointers / unsupported shapes are rejected before any launch."""
+    assert lib.tmvs_warp_corr(None, None, None, None, None, 0, 0, 4, None, 1, 4, 32, 48, 8, 8, 0,
+                              None, None, None, None) == -1
+    assert lib.tmvs_softmax_wta(None, None, 1, 48, 8, 8, 425.0, 935.0, None, None, None, None, None) == -1
+    assert lib.tmvs_costregnet_workspace(1, 48, 216, 288, 8) > 0
+    assert lib.tmvs_depth_stage_workspace(48, 216, 288, 8) > lib.tmvs_costregnet_workspace(1, 48, 216, 288, 8)
+
+
+def test_forward_refuses_cpu_tensors():
+    from transmvsnet_amd import TransMVSNet, synthetic
+    m = TransMVSNet(ndepths=[8, 8, 8]).eval()
+    feats = synthetic.synthetic_features(3, 64, 80)
+    proj = synthetic.synthetic_cameras(3, 64, 80)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m.forward_features(feats, proj, synthetic.synthetic_depth_values(1), (64, 80))

@@ -1,0 +1,118 @@
+"""View sharding (transmvsnet_amd.distributed) on the gloo backend, world_size 2 and 3, CPU.
+
+The HIP partial cost volume is replaced by a restatement of the reference's per-view loop
+(models/TransMVSNet.py:58-93) restricted to the rank's views, so this checks the sharding and
+reduction protocol: every rank must end with the full-view aggregate of oracle.build_cost_volume.
+Tolerance: 1e-6 abs on O(1e-1) similarities (partial sums re-associate the view sum).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import transmvs_ref as oracle
+from transmvsnet_amd import synthetic
+from transmvsnet_amd.distributed import ViewShard, partition_views
+from tests._util import golden_state_dict
+
+N_VIEWS, C, D, H, W = 5, 8, 8, 12, 16
+
+
+def test_partition_views_covers_once():
+    for n_src in (1, 2, 3, 4, 7):
+        for world in (1, 2, 3, 4, 8):
+            parts = [partition_views(n_src, world, r) for r in range(world)]
+            flat = [v for p in parts for v in p]
+            assert flat == list(range(n_src))
+            sizes = [len(p) for p in parts]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_select_features_and_rows():
+    s = ViewShard(1, 2, 4)
+    assert s.src_views == [2, 3] and s.local_views == [0, 3, 4]
+    feats = {"stage1": torch.arange(5.).view(1, 5, 1, 1, 1).expand(1, 5, 2, 2, 2).contiguous()}
+    out = s.select_features(feats)
+    assert out["stage1"][0, :, 0, 0, 0].tolist() == [0., 3., 4.]
+    import numpy as np
+    rows = np.arange(4 * 12, dtype=np.float32).reshape(1, 4, 12)
+    assert (s.select_rows(rows) == rows[:, 2:]).all()
+
+
+def _inputs():
+    g = torch.Generator().manual_seed(7)
+    feats = [torch.randn(1, C, H, W, generator=g) for _ in range(N_VIEWS)]
+    proj = synthetic.synthetic_cameras(N_VIEWS, H * 4, W * 4, seed=1)["stage1"]
+    dv = torch.linspace(450.0, 900.0, D).view(1, D, 1, 1).expand(1, D, H, W).contiguous()
+    return feats, proj, dv
+
+
+def _oracle_partial(sd, feats, proj):
+    """Factory: partial (sum w*sim, sum w) over a rank's source views, reference op order."""
+    projs = torch.unbind(proj, 1)
+
+    def partial(fs, rows, hyp, stage, view_w, pw, sim_out, wsum_out, views=None):
+        ref = feats[0]
+        vws = []
+        for v in views:
+            warped = oracle.homo_warping(feats[1 + v], oracle.compose_proj(projs[1 + v]),
+                                         oracle.compose_proj(projs[0]), hyp)
+            sim = (warped * ref.unsqueeze(2)).mean(1, keepdim=True)
+            vw = oracle.pixelwise_net(sd, sim)
+            sim_out += (sim * vw.unsqueeze(1))[:, 0]
+            wsum_out += vw[:, 0]
+            vws.append(vw)
+        return torch.cat(vws, 1)
+    return partial
+
+
+def _finalize(sim_sum, w_sum):
+    sim_sum.div_(1e-5 + w_sum.unsqueeze(1))
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(1)
+        sd = golden_state_dict()
+        feats, proj, dv = _inputs()
+        part = _oracle_partial(sd, feats, proj)
+        shard = ViewShard(rank, world, N_VIEWS - 1, finalize_fn=_finalize)
+        shard._partial = lambda *a: part(*a, views=shard.src_views)
+        sim, vw = shard.cost_volume(None, None, dv, 0, None, None)
+        ref_sim, ref_vw = oracle.build_cost_volume(sd, feats, proj, dv)
+        err = float((sim - ref_sim[:, 0]).abs().max())
+        vw_err = 0.0
+        if shard.src_views:
+            vw_err = float((vw - ref_vw[:, shard.src_views]).abs().max())
+        q.put((rank, err, vw_err, float(ref_sim.abs().max())))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_view_sharded_cost_volume_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err, vw_err, scale in res:
+        assert scale > 1e-3
+        assert err <= 1e-6, (rank, err)
+        assert vw_err == 0.0, (rank, vw_err)

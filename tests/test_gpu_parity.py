@@ -230,6 +230,21 @@ def test_e2e_cascade_48_32_8(sd):
     print("e2e cascade", _e2e_check(out, vw, g))
 
 
+def test_e2e_cascade_view_sharded_path(sd):
+    """transmvsnet_amd.distributed on one rank: partial cost volume + finalize + replicated CostRegNet."""
+    from transmvsnet_amd.distributed import ViewShard
+    g = golden("e2e_cascade_256x320.npz")
+    m = TransMVSNet().eval()
+    m.load_state_dict(sd, strict=True)
+    m = m.to(DEV)
+    H, W, N = 256, 320, 3
+    feats = [{k: v.to(DEV) for k, v in f.items()} for f in synthetic.synthetic_features(N, H, W, seed=2)]
+    out, vw = m.forward_features(feats, synthetic.synthetic_cameras(N, H, W, seed=1),
+                                 synthetic.synthetic_depth_values(1).to(DEV), (H, W), return_view_weights=True,
+                                 view_shard=ViewShard(0, 1, N - 1))
+    print("e2e cascade (view-sharded path)", _e2e_check(out, vw, g))
+
+
 def test_e2e_images_full_forward(model):
     g = golden("e2e_c1_imgs.npz")
     H, W, N = 128, 160, 3

@@ -271,12 +271,16 @@ class TransMVSNet(nn.Module):
         view_shard: optional transmvsnet_amd.distributed.ViewShard (source views split over ranks).
         """
         feats = self.stack_features(features)
+        if view_shard is not None:  # reference view + this rank's source views only
+            feats = view_shard.select_features(feats)
         dev = feats["stage1"].device
         if not feats["stage1"].is_cuda:
             raise RuntimeError("TransMVSNet (HIP) needs GPU features; the HIP path has no CPU fallback")
         prep = self._prepared(dev)
         dv = depth_values.to(dev, torch.float32).contiguous()
         rows = {k: ops.proj_rows(proj_matrix[k]) for k in ("stage1", "stage2", "stage3")}
+        if view_shard is not None:
+            rows = {k: view_shard.select_rows(r) for k, r in rows.items()}
         b = feats["stage1"].shape[0]
         per = []
         vws = []

@@ -112,7 +112,7 @@ def stage_hypotheses(depth_values, prev_depth, ndepth, ratio, full_hw, stage_sca
 
 
 def warp_corr(ref_nhwc, src_nhwc, proj12, hyp, view_w_in=None, vw_shift=0, vw_offset=0, vw_total=None,
-              pw_params=None, partial=False, view_w_out=None):
+              pw_params=None, partial=False, view_w_out=None, sim_out=None, wsum_out=None):
     """Fused cost volume (models/TransMVSNet.py:58-93). ref [B,H,W,C], src [B,V,H,W,C], proj12 HOST [B,V,12].
 
     Returns sim [B,D,H,W] (and w_sum [B,H,W] when partial) ; stage 1 writes view_w_out [B,vw_total,H,W].
@@ -123,8 +123,12 @@ def warp_corr(ref_nhwc, src_nhwc, proj12, hyp, view_w_in=None, vw_shift=0, vw_of
     d = hyp.shape[1]
     vw_total = v if vw_total is None else vw_total
     proj = np.ascontiguousarray(proj12, np.float32).reshape(b, v, 12)
-    sim = torch.empty(b, d, h, w, device=hyp.device)
-    wsum = torch.empty(b, h, w, device=hyp.device) if partial else None
+    sim = torch.empty(b, d, h, w, device=hyp.device) if sim_out is None else sim_out
+    wsum = (torch.empty(b, h, w, device=hyp.device) if wsum_out is None else wsum_out) if partial else None
+    if sim.shape != (b, d, h, w) or not sim.is_contiguous():
+        raise ValueError(f"sim_out must be a contiguous [{b},{d},{h},{w}] tensor")
+    if wsum is not None and (wsum.numel() != b * h * w or not wsum.is_contiguous()):
+        raise ValueError(f"wsum_out must be a contiguous [{b},{h},{w}] tensor")
     if view_w_in is None:
         if view_w_out is None:
             view_w_out = torch.empty(b, vw_total, h, w, device=hyp.device)
