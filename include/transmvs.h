@@ -79,7 +79,8 @@ int tmvs_stage_hypotheses(const float* depth_values, int n_values, const float* 
  *                  all-reduce); 0 -> sim_out = the reference's normalised similarity.
  *   sim_out      : [B][D][H][W]       wsum_out : [B][H][W] (PARTIAL only, else may be NULL)
  *   view_w_out   : [B][vw_total][H][W] written at vw_offset.. when view_w_in == NULL
- * Supported: C in {8,16,32}; D % 4 == 0 (D <= 64 per pass); 1 <= V <= TMVS_MAX_VIEWS.     */
+ * Supported: C in {8,16,32}; D in {8,16,24,32,48,64}; 1 <= V <= TMVS_MAX_VIEWS;
+ *            V*H*W*C*4 < 2^30 bytes per sample (32-bit buffer offsets); H, W <= 32766.      */
 #define TMVS_WARP_PARTIAL 1
 #define TMVS_PW_NPARAMS 201 /* w0[16] a0[16] s0[16] w1[8][16] a1[8] s1[8] w2[8] b2 */
 int tmvs_warp_corr(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,

@@ -17,13 +17,17 @@
 
 namespace tmvs {
 
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
 struct WarpArgs {
   float proj[TMVS_MAX_VIEWS][12];
   float pw[TMVS_PW_NPARAMS];
 };
 
 __device__ __forceinline__ float pixelwise_logit(float s, const float* __restrict__ pw) {
-  // PixelwiseNet (TransMVSNet.py:20-26): 1x1x1 convs 1->16 (BN,ReLU) ->8 (BN,ReLU) ->1 (+bias)
+  // PixelwiseNet (TransMVSNet.py:20-26): 1x1x1 convs 1->16 (BN,ReLU) ->8 (BN,ReLU) ->1 (+bias).
+  // pw is in LDS; the hidden-unit loop is not unrolled so the 201 parameters are re-read
+  // (broadcast ds_read_b128) rather than hoisted into VGPRs.
   const float* w0 = pw;
   const float* a0 = pw + 16;
   const float* s0 = pw + 32;
@@ -31,35 +35,44 @@ __device__ __forceinline__ float pixelwise_logit(float s, const float* __restric
   const float* a1 = pw + 176;
   const float* s1 = pw + 184;
   const float* w2 = pw + 192;
-  const float b2 = pw[200];
   float h0[16];
 #pragma unroll
-  for (int o = 0; o < 16; ++o) h0[o] = relu(fmaf(w0[o] * s, a0[o], s0[o]));
+  for (int o4 = 0; o4 < 4; ++o4) {
+    const float4 w = reinterpret_cast<const float4*>(w0)[o4];
+    const float4 a = reinterpret_cast<const float4*>(a0)[o4];
+    const float4 sh = reinterpret_cast<const float4*>(s0)[o4];
+    h0[4 * o4 + 0] = relu(fmaf(w.x * s, a.x, sh.x));
+    h0[4 * o4 + 1] = relu(fmaf(w.y * s, a.y, sh.y));
+    h0[4 * o4 + 2] = relu(fmaf(w.z * s, a.z, sh.z));
+    h0[4 * o4 + 3] = relu(fmaf(w.w * s, a.w, sh.w));
+  }
   float out = 0.f;
-#pragma unroll
+#pragma unroll 1
   for (int p = 0; p < 8; ++p) {
     float acc = 0.f;
 #pragma unroll
-    for (int o = 0; o < 16; ++o) acc = fmaf(w1[p * 16 + o], h0[o], acc);
+    for (int o4 = 0; o4 < 4; ++o4) {
+      const float4 w = reinterpret_cast<const float4*>(w1 + p * 16)[o4];
+      acc = fmaf(w.x, h0[4 * o4 + 0], acc);
+      acc = fmaf(w.y, h0[4 * o4 + 1], acc);
+      acc = fmaf(w.z, h0[4 * o4 + 2], acc);
+      acc = fmaf(w.w, h0[4 * o4 + 3], acc);
+    }
     out = fmaf(w2[p], relu(fmaf(acc, a1[p], s1[p])), out);
   }
-  return out + b2;
+  return out + pw[200];
 }
 
 // Lane layout: a pixel is served by LPS = C/4 adjacent lanes ("group"); lane k of the group
-// owns channel quad k (4 channels, one 16-byte load per tap) and depth planes k, k+LPS, ...
-// For every depth plane the group issues one 16-byte load per lane per tap, i.e. the C
-// channels of a tap arrive as one contiguous row (C*4 bytes) per group: a wave-instruction
-// touches 64/LPS rows instead of 64 scattered 16-byte pieces. Each lane projects only its own
-// depth planes; the tap geometry (x0, y0, fractional x, fractional y) of plane j*LPS+t is
-// broadcast from lane t with lane shuffles, and the channel dot product is reduced across the
-// group with xor shuffles (channel order: 4-channel serial sums, then a fixed tree).
-template <int C>
-struct Tap {
-  int x0, y0;
-  float fx, fy;
-};
-
+// owns channel quad k (4 channels, one 16-byte load per tap) and depth planes j*LPS + k.
+// Each lane projects only its own planes. For plane slot j the group runs LPS rounds: in
+// round t all lanes take plane t's tap geometry (broadcast from lane t: DPP quad permute, or
+// ds_swizzle for groups of 8 -- no LDS memory traffic) and load their channel quad of the
+// four taps, so the C channels of a tap arrive as one contiguous C*4-byte row per group and a
+// wave-instruction touches 64/LPS full rows (measured: anything that splits a row over
+// several instructions, or mixes planes inside a group, costs up to 2x). All rounds' loads
+// are issued before any is consumed; a butterfly reduce-scatter then gives lane t the full
+// channel sum of plane t.
 __device__ __forceinline__ void project(const float rx, const float ry, const float rz, const float tx,
                                         const float ty, const float tz, const float dep, const float halfw,
                                         const float halfh, int& x0i, int& y0i, float& fx, float& fy) {
@@ -78,12 +91,167 @@ __device__ __forceinline__ void project(const float rx, const float ry, const fl
   fx = ix - x0;
   fy = iy - y0;
   // clamp far-away samples (all four taps outside) to a sentinel that stays outside
-  x0i = (int)fminf(fmaxf(x0, -2.f), 65536.f);
-  y0i = (int)fminf(fmaxf(y0, -2.f), 65536.f);
+  x0i = (int)fminf(fmaxf(x0, -2.f), 32766.f);
+  y0i = (int)fminf(fmaxf(y0, -2.f), 32766.f);
 }
 
+// x from lane (lane ^ R) inside an aligned group of 8 (R compile-time)
+template <int R>
+__device__ __forceinline__ int lane_xor(int x) {
+  if constexpr (R == 0) return x;
+  else if constexpr (R == 1) return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  else if constexpr (R == 2) return __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  else if constexpr (R == 3) return __builtin_amdgcn_mov_dpp(x, 0x1B, 0xF, 0xF, false);  // quad_perm [3,2,1,0]
+  else return __builtin_amdgcn_ds_swizzle(x, 0x1F | (R << 10));                           // bit mode, xor R
+}
+template <int R>
+__device__ __forceinline__ float lane_xor_f(float x) {
+  return __int_as_float(lane_xor<R>(__float_as_int(x)));
+}
+
+template <int LPS>
+__device__ __forceinline__ float group_max(float v) {
+  if constexpr (LPS >= 2) v = fmaxf(v, lane_xor_f<1>(v));
+  if constexpr (LPS >= 4) v = fmaxf(v, lane_xor_f<2>(v));
+  if constexpr (LPS >= 8) v = fmaxf(v, lane_xor_f<4>(v));
+  return v;
+}
+
+// Buffer resource over one sample's source views: raw (stride 0) addressing with 32-bit byte
+// offsets. An offset at or past num_records reads as 0 -- exactly grid_sample's zero padding --
+// so an out-of-image tap only needs an out-of-range offset: each axis term is kAxisOut when
+// invalid, and any sum containing one is >= kAxisOut >= num_records (< 2^30, checked).
+constexpr unsigned kAxisOut = 0x40000000u;
+constexpr int kRsrcWord3 = 0x00020000;
+
+struct Geom {
+  int x0, y0;
+  float fx, fy;
+};
+
+// x from lane t of this lane's aligned group of LPS lanes (t compile-time): the group's
+// lanes all receive the same value -- DPP quad permutes for LPS <= 4, ds_swizzle (bit mode,
+// no memory access) for LPS = 8
+template <int LPS, int T>
+__device__ __forceinline__ int group_bcast(int x) {
+  if constexpr (LPS == 1) return x;
+  else if constexpr (LPS == 2) return __builtin_amdgcn_mov_dpp(x, T | (T << 2) | ((T + 2) << 4) | ((T + 2) << 6), 0xF, 0xF, false);
+  else if constexpr (LPS == 4) return __builtin_amdgcn_mov_dpp(x, T * 0x55, 0xF, 0xF, false);
+  else return __builtin_amdgcn_ds_swizzle(x, 0x18 | (T << 5));  // lane' = (lane & 0x18) | T
+}
+
+template <int LPS, int T>
+__device__ __forceinline__ Geom geom_bcast(const Geom& g) {
+  return Geom{group_bcast<LPS, T>(g.x0), group_bcast<LPS, T>(g.y0),
+              __int_as_float(group_bcast<LPS, T>(__float_as_int(g.fx))),
+              __int_as_float(group_bcast<LPS, T>(__float_as_int(g.fy)))};
+}
+
+
+// Tap fetch for one round: 4 taps x this lane's channel quad; weights kept for the combine.
+struct Taps {
+  floatx4 a, b, c, d;
+  float wnw, wne, wsw, wse;
+};
+
+template <int C>
+__device__ __forceinline__ void fetch(const __amdgpu_buffer_rsrc_t rsrc, unsigned vbase, unsigned rowb, int W, int H,
+                                      const Geom& g, Taps& t) {
+  constexpr unsigned CB = C * 4;
+  const float we = g.fx, n = g.fy;
+  const float ea = 1.f - we, s = 1.f - n;
+  t.wnw = s * ea;
+  t.wne = s * we;
+  t.wsw = n * ea;
+  t.wse = n * we;
+  const unsigned xa = (unsigned)g.x0 < (unsigned)W ? (unsigned)g.x0 * CB : kAxisOut;
+  const unsigned xb = (unsigned)(g.x0 + 1) < (unsigned)W ? (unsigned)(g.x0 + 1) * CB : kAxisOut;
+  const unsigned yrow = vbase + (unsigned)g.y0 * rowb;
+  const unsigned ya = (unsigned)g.y0 < (unsigned)H ? yrow : kAxisOut;
+  const unsigned yb = (unsigned)(g.y0 + 1) < (unsigned)H ? yrow + rowb : kAxisOut;
+  t.a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(ya + xa), 0, 0);
+  t.b = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(ya + xb), 0, 0);
+  t.c = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(yb + xa), 0, 0);
+  t.d = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(yb + xb), 0, 0);
+}
+
+// bilinear value of each channel (grid_sample's fma order), times ref, summed in channel order
+__device__ __forceinline__ float combine(const Taps& t, const float4& r4) {
+  float acc = 0.f;
+  acc = acc + fmaf(t.d[0], t.wse, fmaf(t.c[0], t.wsw, fmaf(t.b[0], t.wne, t.a[0] * t.wnw))) * r4.x;
+  acc = acc + fmaf(t.d[1], t.wse, fmaf(t.c[1], t.wsw, fmaf(t.b[1], t.wne, t.a[1] * t.wnw))) * r4.y;
+  acc = acc + fmaf(t.d[2], t.wse, fmaf(t.c[2], t.wsw, fmaf(t.b[2], t.wne, t.a[2] * t.wnw))) * r4.z;
+  acc = acc + fmaf(t.d[3], t.wse, fmaf(t.c[3], t.wsw, fmaf(t.b[3], t.wne, t.a[3] * t.wnw))) * r4.w;
+  return acc;
+}
+
+
+// Partials of rounds R0..R0+3 (or fewer): every round's loads are issued before any is consumed.
+// Rounds R0..R0+N-1: in round t the whole group samples plane slot t (geometry broadcast from
+// lane t), so each load instruction covers one contiguous C*4-byte row per group.
+template <int C, int R0, int N>
+__device__ __forceinline__ void rounds(const __amdgpu_buffer_rsrc_t rsrc, unsigned vbase, unsigned rowb, int W,
+                                       int H, const Geom& own, const float4& r4, float* part) {
+  Taps t[N];
+  fetch<C>(rsrc, vbase, rowb, W, H, geom_bcast<C / 4, R0>(own), t[0]);
+  if constexpr (N > 1) fetch<C>(rsrc, vbase, rowb, W, H, geom_bcast<C / 4, R0 + 1>(own), t[1]);
+  if constexpr (N > 2) fetch<C>(rsrc, vbase, rowb, W, H, geom_bcast<C / 4, R0 + 2>(own), t[2]);
+  if constexpr (N > 3) fetch<C>(rsrc, vbase, rowb, W, H, geom_bcast<C / 4, R0 + 3>(own), t[3]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) part[R0 + i] = combine(t[i], r4);
+}
+
+// Full channel sum of this lane's own plane (slot k): LPS rounds, then a butterfly
+// reduce-scatter over lane bits (xor 4, xor 2, xor 1). At each step a lane keeps the half of
+// the planes whose slot bit matches its own lane bit and sends the other half to its partner;
+// the sum for slot t ends in lane t: no dependent shuffle chains, LPS-1 exchanges.
+template <int C>
+__device__ __forceinline__ float plane_corr(const __amdgpu_buffer_rsrc_t rsrc, unsigned vbase, unsigned rowb, int W,
+                                            int H, const Geom& own, const float4& r4, int k) {
+  constexpr int LPS = C / 4;
+  float p[LPS];
+  if constexpr (LPS <= 4) {
+    rounds<C, 0, LPS>(rsrc, vbase, rowb, W, H, own, r4, p);
+  } else {
+    rounds<C, 0, 4>(rsrc, vbase, rowb, W, H, own, r4, p);
+    rounds<C, 4, 4>(rsrc, vbase, rowb, W, H, own, r4, p);
+  }
+  float q[LPS];
+#pragma unroll
+  for (int i = 0; i < LPS; ++i) q[i] = p[i];
+  int n = LPS;
+  if constexpr (LPS >= 8) {
+    const bool hi = (k & 4) != 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float keep = hi ? q[4 + i] : q[i], send = hi ? q[i] : q[4 + i];
+      q[i] = keep + lane_xor_f<4>(send);
+    }
+    n = 4;
+  }
+  if constexpr (LPS >= 4) {
+    const bool hi = (k & 2) != 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float keep = hi ? q[2 + i] : q[i], send = hi ? q[i] : q[2 + i];
+      q[i] = keep + lane_xor_f<2>(send);
+    }
+    n = 2;
+  }
+  (void)n;
+  if constexpr (LPS >= 2) {
+    const bool hi = (k & 1) != 0;
+    const float keep = hi ? q[1] : q[0], send = hi ? q[0] : q[1];
+    q[0] = keep + lane_xor_f<1>(send);
+  }
+  return q[0];
+}
+
+// Views outer (a view's consecutive planes hit the same source lines: L1 reuse), planes inner
+// and not unrolled: the plane's depth and running weighted sum live in this thread's LDS
+// column, so the rounds' independent loads are the only large live set.
 template <int C, int D, bool PW, bool PARTIAL>
-__global__ __launch_bounds__(256) void warp_corr_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void warp_corr_kernel(
     const float* __restrict__ ref, const float* __restrict__ src, const float* __restrict__ hyp,
     const float* __restrict__ vw_in, float* __restrict__ sim_out, float* __restrict__ wsum_out,
     float* __restrict__ vw_out, int V, int H, int W, int vw_shift, int vw_offset, int vw_total, WarpArgs args) {
@@ -92,104 +260,80 @@ __global__ __launch_bounds__(256) void warp_corr_kernel(
   constexpr int PIX = 4 * SPW;        // pixels per block
   constexpr int DPT = D / LPS;        // depth planes owned per lane
   static_assert(D % LPS == 0, "D must be a multiple of C/4");
+  // PixelwiseNet parameters in LDS (uniform-address reads broadcast); as kernel arguments
+  // they would occupy ~200 SGPRs and spill
+  __shared__ __attribute__((aligned(16))) float pw_lds[PW ? TMVS_PW_NPARAMS + 3 : 4];
+  __shared__ float dep_lds[DPT][256];
+  __shared__ float acc_lds[DPT][256];
+  __shared__ float sim_lds[PW ? DPT : 1][PW ? 256 : 1];
+  const int tid = threadIdx.x;
+  if constexpr (PW) {
+    if (tid < TMVS_PW_NPARAMS) pw_lds[tid] = args.pw[tid];
+  }
   const int HW = H * W;
   const int nblk = (HW + PIX - 1) / PIX;
   const int tile = xcd_remap(blockIdx.x, nblk);
-  const int lane = threadIdx.x & 63;
+  const int lane = tid & 63;
   const int k = lane % LPS;
-  const int gbase = lane - k;
-  int p = tile * PIX + (threadIdx.x >> 6) * SPW + lane / LPS;
+  int p = tile * PIX + (tid >> 6) * SPW + lane / LPS;
   const bool active = p < HW;
   if (!active) p = HW - 1;
   const int py = p / W, px = p - py * W;
   const float fxp = (float)px, fyp = (float)py;
-
   const float4 r4 = *reinterpret_cast<const float4*>(ref + (size_t)p * C + 4 * k);
-  float dep[DPT];
 #pragma unroll
-  for (int j = 0; j < DPT; ++j) dep[j] = hyp[(size_t)(j * LPS + k) * HW + p];
+  for (int j = 0; j < DPT; ++j) {
+    dep_lds[j][tid] = hyp[(size_t)(j * LPS + k) * HW + p];
+    acc_lds[j][tid] = 0.f;
+  }
+  if constexpr (PW) __syncthreads();  // pw_lds is shared; the columns are per thread
   const float halfw = (float)(W - 1) / 2.f;
   const float halfh = (float)(H - 1) / 2.f;
-  float ssum[DPT];
-#pragma unroll
-  for (int j = 0; j < DPT; ++j) ssum[j] = 0.f;
   float wsum = PARTIAL ? 0.f : 1e-5f;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, V * HW * C * 4, kRsrcWord3);
+  const unsigned rowb = (unsigned)W * C * 4;
+  const int Ws = W >> vw_shift, Hs = H >> vw_shift;
 
   for (int v = 0; v < V; ++v) {
     const float* R = args.proj[v];
     const float rx = fmaf(R[1], fyp, R[0] * fxp) + R[2];
     const float ry = fmaf(R[5], fyp, R[4] * fxp) + R[6];
     const float rz = fmaf(R[9], fyp, R[8] * fxp) + R[10];
-    const float* __restrict__ sv = src + (size_t)v * HW * C + 4 * k;
-    float sim[DPT];
-#pragma unroll
+    const unsigned vbase = (unsigned)(v * HW * C * 4 + 16 * k);
+    float w = 0.f;
+    if constexpr (!PW) w = vw_in[(size_t)(vw_offset + v) * Hs * Ws + (py >> vw_shift) * Ws + (px >> vw_shift)];
+    float wm = 0.f;  // PW: running max of sigmoid (> 0, so 0 is neutral)
+#pragma unroll 1
     for (int j = 0; j < DPT; ++j) {
-      int mx0, my0;
-      float mfx, mfy;
-      project(rx, ry, rz, R[3], R[7], R[11], dep[j], halfw, halfh, mx0, my0, mfx, mfy);
-#pragma unroll
-      for (int t = 0; t < LPS; ++t) {
-        int x0 = mx0, y0 = my0;
-        float we = mfx, n = mfy;
-        if constexpr (LPS > 1) {
-          x0 = __shfl(mx0, gbase + t, 64);
-          y0 = __shfl(my0, gbase + t, 64);
-          we = __shfl(mfx, gbase + t, 64);
-          n = __shfl(mfy, gbase + t, 64);
-        }
-        const float ea = 1.f - we, s = 1.f - n;
-        const float wnw = s * ea, wne = s * we, wsw = n * ea, wse = n * we;
-        const bool vx0 = x0 >= 0 && x0 <= W - 1, vx1 = x0 + 1 >= 0 && x0 + 1 <= W - 1;
-        const bool vy0 = y0 >= 0 && y0 <= H - 1, vy1 = y0 + 1 >= 0 && y0 + 1 <= H - 1;
-        const int xa = vx0 ? x0 : 0, xb = vx1 ? x0 + 1 : 0;
-        const int ya = vy0 ? y0 : 0, yb = vy1 ? y0 + 1 : 0;
-        float4 a = *reinterpret_cast<const float4*>(sv + ((size_t)ya * W + xa) * C);
-        float4 b = *reinterpret_cast<const float4*>(sv + ((size_t)ya * W + xb) * C);
-        float4 c = *reinterpret_cast<const float4*>(sv + ((size_t)yb * W + xa) * C);
-        float4 d = *reinterpret_cast<const float4*>(sv + ((size_t)yb * W + xb) * C);
-        if (!(vy0 && vx0)) a = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (!(vy0 && vx1)) b = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (!(vy1 && vx0)) c = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (!(vy1 && vx1)) d = make_float4(0.f, 0.f, 0.f, 0.f);
-        float acc = 0.f;
-        acc = acc + fmaf(d.x, wse, fmaf(c.x, wsw, fmaf(b.x, wne, a.x * wnw))) * r4.x;
-        acc = acc + fmaf(d.y, wse, fmaf(c.y, wsw, fmaf(b.y, wne, a.y * wnw))) * r4.y;
-        acc = acc + fmaf(d.z, wse, fmaf(c.z, wsw, fmaf(b.z, wne, a.z * wnw))) * r4.z;
-        acc = acc + fmaf(d.w, wse, fmaf(c.w, wsw, fmaf(b.w, wne, a.w * wnw))) * r4.w;
-#pragma unroll
-        for (int off = 1; off < LPS; off <<= 1) acc += __shfl_xor(acc, off, 64);
-        if (k == t) sim[j] = acc / (float)C;
-      }
-    }
-    float w;
-    if constexpr (PW) {
-      float wm = 0.f;  // sigmoid > 0: 0 is neutral for the max
-#pragma unroll
-      for (int j = 0; j < DPT; ++j) {
-        const float lg = pixelwise_logit(sim[j], args.pw);
+      Geom own;
+      project(rx, ry, rz, R[3], R[7], R[11], dep_lds[j][tid], halfw, halfh, own.x0, own.y0, own.fx, own.fy);
+      const float sim = plane_corr<C>(rsrc, vbase, rowb, W, H, own, r4, k) * (1.f / (float)C);  // C = 2^n: == / C
+      if constexpr (PW) {
+        sim_lds[j][tid] = sim;
+        int salt = 0;  // opaque offset: keeps the parameter reads from being hoisted into VGPRs
+        asm volatile("" : "+v"(salt));
+        const float lg = pixelwise_logit(sim, pw_lds + salt);
         wm = fmaxf(wm, 1.f / (1.f + expf(-lg)));
+      } else {
+        acc_lds[j][tid] = acc_lds[j][tid] + sim * w;
       }
-#pragma unroll
-      for (int off = 1; off < LPS; off <<= 1) wm = fmaxf(wm, __shfl_xor(wm, off, 64));
-      w = wm;
-      if (active && k == 0) vw_out[(size_t)(vw_offset + v) * HW + p] = w;
-    } else {
-      const int Ws = W >> vw_shift, Hs = H >> vw_shift;
-      w = vw_in[(size_t)(vw_offset + v) * Hs * Ws + (py >> vw_shift) * Ws + (px >> vw_shift)];
     }
-#pragma unroll
-    for (int j = 0; j < DPT; ++j) ssum[j] = ssum[j] + sim[j] * w;
+    if constexpr (PW) {
+      w = group_max<LPS>(wm);
+      if (active && k == 0) vw_out[(size_t)(vw_offset + v) * HW + p] = w;
+#pragma unroll 4
+      for (int j = 0; j < DPT; ++j) acc_lds[j][tid] = acc_lds[j][tid] + sim_lds[j][tid] * w;
+    }
     wsum = wsum + w;
   }
   if (!active) return;
-  if constexpr (PARTIAL) {
-#pragma unroll
-    for (int j = 0; j < DPT; ++j) sim_out[(size_t)(j * LPS + k) * HW + p] = ssum[j];
-    if (k == 0) wsum_out[p] = wsum;
-  } else {
-#pragma unroll
-    for (int j = 0; j < DPT; ++j) sim_out[(size_t)(j * LPS + k) * HW + p] = ssum[j] / wsum;
+#pragma unroll 4
+  for (int j = 0; j < DPT; ++j) {
+    const size_t o = (size_t)(j * LPS + k) * HW + p;
+    sim_out[o] = PARTIAL ? acc_lds[j][tid] : acc_lds[j][tid] / wsum;
   }
+  if (PARTIAL && k == 0) wsum_out[p] = wsum;
 }
 
 __global__ void aggregate_finalize_kernel(float* __restrict__ sim, const float* __restrict__ wsum, int D, int HW) {
@@ -303,6 +447,9 @@ extern "C" int tmvs_warp_corr(const float* ref_fea, const float* src_fea, const 
   if (pw && (!pw_params || !view_w_out)) return TMVS_ERR_ARG;
   if (partial && !wsum_out) return TMVS_ERR_ARG;
   if (vw_offset < 0 || vw_offset + n_src > vw_total || vw_shift < 0) return TMVS_ERR_ARG;
+  // the kernel addresses one sample's source views with 32-bit byte offsets (< 2^30)
+  if ((long long)n_src * height * width * channels * 4 >= (1LL << 30)) return TMVS_ERR_SHAPE;
+  if (width > 32766 || height > 32766) return TMVS_ERR_SHAPE;
   hipStream_t st = (hipStream_t)stream;
   const size_t HW = (size_t)height * width;
   for (int b = 0; b < batch; ++b) {
