@@ -1,0 +1,23 @@
+"""Per-(kernel, grid) mean duration (us) and per-step total from a rocprofv3 kernel trace CSV."""
+import collections
+import csv
+import re
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+steps = max(1, sum(1 for r in rows if r["Kernel_Name"].startswith("fmt_embed") or "fmt_embed" in r["Kernel_Name"]))
+agg = collections.defaultdict(list)
+for r in rows:
+    name = re.sub(r"^void tmvs::|\(.*$", "", r["Kernel_Name"])
+    name = re.sub(r"^tmvs::", "", name)[:70]
+    agg[(name, r.get("Grid_Size", r.get("Grid_Size_X", "?")))].append(
+        (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+tot = 0.0
+out = []
+for (name, grid), v in agg.items():
+    per_step = sum(v) / steps
+    tot += per_step
+    out.append((per_step, name, grid, len(v) / steps, sum(v) / len(v)))
+for per_step, name, grid, calls, mean in sorted(out, reverse=True):
+    print(f"{per_step:9.1f} us/step  {calls:4.1f} calls x {mean:8.1f} us  grid={grid:>9}  {name}")
+print(f"{tot:9.1f} us/step total over {steps} steps")

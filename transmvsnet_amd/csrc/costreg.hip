@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const float* __restrict
   __shared__ __attribute__((aligned(16))) float tile[NVOX * VST];
 
   const int nws = (g.Wo + 15) / 16, nhs = (g.Ho + TH - 1) / TH, nds = (g.Do + TD - 1) / TD;
-  int t = blockIdx.x;
+  int t = xcd_remap(blockIdx.x, gridDim.x);  // contiguous tiles per XCD: halos share an L2
   const int mg = t % MG;
   t /= MG;
   const int ws = t % nws;
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void conv3d_direct_kernel(const float* __restr
   constexpr int MG = MB / MBW;             // wave groups along cout
   static_assert(MB % MBW == 0, "MBW must divide MB");
   const int lane = threadIdx.x & 63;
-  const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int task = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
   if (task >= n_tasks) return;
   // task -> (mg fastest, wseg, hgrp, od, n)
   int t = task;
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
   __shared__ __attribute__((aligned(16))) float tile[NVOX * VST];
 
   const int nws = (g.Wi + 15) / 16, nhs = (g.Hi + THI - 1) / THI, nds = (g.Di + TDI - 1) / TDI;
-  int t = blockIdx.x;
+  int t = xcd_remap(blockIdx.x, gridDim.x);  // contiguous tiles per XCD: halos share an L2
   const int mg = t % MG;
   t /= MG;
   const int ws = t % nws;
@@ -413,10 +413,17 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
                                                     const float* __restrict__ alpha,
                                                     const float* __restrict__ shift) {
   const int HW = H * W;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  // 1-D grid: logical block = (n, depth chunk, pixel chunk), pixel chunk fastest; remapped so
+  // that each XCD owns a contiguous range (the 3x3 row halo is then read from one L2)
+  const int npx = (HW + 255) / 256, ndc = (D + kDChunk - 1) / kDChunk;
+  int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int pc = lb % npx;
+  lb /= npx;
+  const int dc = lb % ndc;
+  const int n = lb / ndc;
+  const int p = pc * 256 + threadIdx.x;
   if (p >= HW) return;
-  const int n = blockIdx.y;
-  const int d0 = blockIdx.z * kDChunk, d1 = min(D, d0 + kDChunk);
+  const int d0 = dc * kDChunk, d1 = min(D, d0 + kDChunk);
   const int h = p / W, w = p - h * W;
   const float* xn = x + (size_t)n * D * HW;
   float win[3][9];
@@ -461,45 +468,67 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
 // ---------------------------------------------------------------- prob: 8 -> 1, VALU
 // One thread per (h, w) column walks D; input plane i (9 taps x 8 channels) is loaded once and
 // feeds outputs i+1 (kd=0), i (kd=1) and i-1 (kd=2) -- each output's FMA chain still runs in
-// (kd, kh, kw, c) order.
+// (kd, kh, kw, c) order. Loads are pipelined one tap row (3 taps x 8 channels) ahead.
 __global__ __launch_bounds__(256) void prob_kernel(const float* __restrict__ x, float* __restrict__ y, int D, int H,
                                                    int W, const float* __restrict__ wt) {
   const int HW = H * W;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int npx = (HW + 255) / 256, ndc = (D + kDChunk - 1) / kDChunk;
+  int lb = xcd_remap(blockIdx.x, gridDim.x);  // as conv0_kernel
+  const int pc = lb % npx;
+  lb /= npx;
+  const int dc = lb % ndc;
+  const int n = lb / ndc;
+  const int p = pc * 256 + threadIdx.x;
   if (p >= HW) return;
-  const int n = blockIdx.y;
   const int h = p / W, w = p - h * W;
-  const int d0 = blockIdx.z * kDChunk, d1 = min(D, d0 + kDChunk);
+  const int d0 = dc * kDChunk, d1 = min(D, d0 + kDChunk);
   const float* xn = x + (size_t)n * D * HW * 8;
   float* yn = y + (size_t)n * D * HW + p;
+  // tap row (plane i, row offset kh): 3 taps x 8 channels; planes outside [0, D) and
+  // out-of-image taps read as zeros (fmaf(w, 0, acc) == acc)
+  auto load_row = [&](int i, int kh, float4 (&o)[6]) {
+    const int ih = h - 1 + kh;
+    const bool okr = i >= 0 && i < D && ih >= 0 && ih < H;
+    const int ic = min(max(i, 0), D - 1), ihc = min(max(ih, 0), H - 1);
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int iw = w - 1 + kw;
+      const bool ok = okr && iw >= 0 && iw < W;
+      const int iwc = min(max(iw, 0), W - 1);
+      const float4* q = reinterpret_cast<const float4*>(xn + (((size_t)ic * H + ihc) * W + iwc) * 8);
+      float4 u = q[0], v = q[1];
+      if (!ok) {
+        u = make_float4(0.f, 0.f, 0.f, 0.f);
+        v = u;
+      }
+      o[2 * kw] = u;
+      o[2 * kw + 1] = v;
+    }
+  };
   float acc_prev = 0.f, acc_cur = 0.f;  // outputs i-1 (has kd=0,1) and i (has kd=0)
-  for (int i = d0 - 1; i <= d1; ++i) {  // plane i feeds outputs i-1, i, i+1 (planes -1 and D are padding)
+  float4 cur[6], nxt[6];
+  load_row(d0 - 1, 0, cur);
+  for (int i = d0 - 1; i <= d1; ++i) {  // plane i feeds outputs i-1, i, i+1
     float acc_next = 0.f;                // output i+1, kd=0 from plane i
     float c1 = acc_cur, c2 = acc_prev;
-    if (i >= 0 && i < D) {
+    // kh not unrolled: one row's 72 weights (3 taps x 8 channels x 3 kd) fit in SGPRs
+#pragma unroll 1
+    for (int kh = 0; kh < 3; ++kh) {
+      load_row(kh < 2 ? i : i + 1, kh < 2 ? kh + 1 : 0, nxt);
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh)
+      for (int kw = 0; kw < 3; ++kw) {
+        const float4 u = cur[2 * kw], v = cur[2 * kw + 1];
+        const float xv[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        const int t = kh * 3 + kw;
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          // branch-free: clamp the address, zero the value (padding taps add exact zeros)
-          const int ih = h - 1 + kh, iw = w - 1 + kw;
-          const bool ok = ih >= 0 && ih < H && iw >= 0 && iw < W;
-          const int ihc = min(max(ih, 0), H - 1), iwc = min(max(iw, 0), W - 1);
-          const float4* q = reinterpret_cast<const float4*>(xn + (((size_t)i * H + ihc) * W + iwc) * 8);
-          float4 u = q[0], v = q[1];
-          if (!ok) {
-            u = make_float4(0.f, 0.f, 0.f, 0.f);
-            v = u;
-          }
-          const float xv[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-          const int t = kh * 3 + kw;
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            acc_next = fmaf(wt[c * 27 + t], xv[c], acc_next);
-            c1 = fmaf(wt[c * 27 + 9 + t], xv[c], c1);
-            c2 = fmaf(wt[c * 27 + 18 + t], xv[c], c2);
-          }
+        for (int c = 0; c < 8; ++c) {
+          acc_next = fmaf(wt[c * 27 + t], xv[c], acc_next);
+          c1 = fmaf(wt[c * 27 + 9 + t], xv[c], c1);
+          c2 = fmaf(wt[c * 27 + 18 + t], xv[c], c2);
         }
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) cur[k] = nxt[k];
     }
     if (i - 1 >= d0) yn[(size_t)(i - 1) * HW] = c2;  // output i-1 complete
     acc_prev = c1;
@@ -671,7 +700,7 @@ extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height,
   const int D2 = D1 / 2, H2 = H1 / 2, W2 = W1 / 2;
   const int D3 = D2 / 2, H3 = H2 / 2, W3 = W2 / 2;
   int rc;
-  const dim3 g0((unsigned)((H0 * W0 + 255) / 256), (unsigned)batch, (unsigned)((D0 + kDChunk - 1) / kDChunk));
+  const dim3 g0((unsigned)(((H0 * W0 + 255) / 256) * batch * ((D0 + kDChunk - 1) / kDChunk)));
   hipLaunchKernelGGL(conv0_kernel, g0, dim3(256), 0, st, x, c0, D0, H0, W0, w->w[0], w->alpha[0], w->shift[0]);
   TMVS_CHECK_LAUNCH();
   if ((rc = conv_dispatch(c0, batch, c, D0, H0, W0, w->w[1], w->alpha[1], w->shift[1], 2 * c, 2, c1, st))) return rc;
