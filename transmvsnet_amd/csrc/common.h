@@ -33,4 +33,20 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   return base + (bid >> 3);
 }
 
+// Raw (stride 0) buffer resource over [base, base + bytes): 32-bit byte offsets, and any
+// offset at or past `bytes` reads as 0 -- used for zero padding without branches (an
+// out-of-image tap gets an out-of-range offset). Word 3 as for gfx9 raw buffers.
+constexpr int kRsrcWord3 = 0x00020000;
+constexpr unsigned kOffOut = 0x80000000u;  // an offset that is always out of range (bytes < 2^31)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, kRsrcWord3);
+}
+__device__ __forceinline__ float buf_load_f32(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));  // returns the raw bits
+}
+typedef float floatx4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ floatx4_t buf_load_f32x4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(floatx4_t, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+
 }  // namespace tmvs

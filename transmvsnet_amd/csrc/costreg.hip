@@ -407,11 +407,14 @@ constexpr int kDChunk = 8;  // depth planes per thread in the full-resolution VA
 
 // ---------------------------------------------------------------- conv0: Cin=1 -> 8, VALU
 // One thread per (h, w) column walks D; every input plane's 3x3 window is loaded once and
-// kept in a 3-plane ring, so each output sees its taps in (kd, kh, kw) order.
+// kept in a 3-plane ring, so each output sees its taps in (kd, kh, kw) order. Window loads are
+// unconditional buffer loads (padding taps get an out-of-range offset and read 0), so the
+// compiler cannot turn them into serialised branches.
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, float* __restrict__ y, int D, int H,
                                                     int W, const float* __restrict__ wt,
                                                     const float* __restrict__ alpha,
                                                     const float* __restrict__ shift) {
+  __shared__ __attribute__((aligned(16))) float stage[4 * 64 * 8];
   const int HW = H * W;
   // 1-D grid: logical block = (n, depth chunk, pixel chunk), pixel chunk fastest; remapped so
   // that each XCD owns a contiguous range (the 3x3 row halo is then read from one L2)
@@ -421,27 +424,34 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
   lb /= npx;
   const int dc = lb % ndc;
   const int n = lb / ndc;
-  const int p = pc * 256 + threadIdx.x;
-  if (p >= HW) return;
+  const int pw0 = pc * 256 + (threadIdx.x & ~63);  // first pixel of this wave
+  if (pw0 >= HW) return;                            // whole wave out of range
+  const bool full_wave = pw0 + 64 <= HW;
+  const int p = min(pc * 256 + (int)threadIdx.x, HW - 1);  // tail lanes compute a duplicate, store nothing
   const int d0 = dc * kDChunk, d1 = min(D, d0 + kDChunk);
   const int h = p / W, w = p - h * W;
-  const float* xn = x + (size_t)n * D * HW;
-  float win[3][9];
+  const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)n * D * HW, (unsigned)(D * HW * 4));
+  float* ybase = y + (size_t)n * D * HW * 8;
+  // per-axis byte offsets; an invalid axis makes the sum out of range
+  unsigned offw[3], offh[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    offw[k] = (unsigned)(w - 1 + k) < (unsigned)W ? (unsigned)(w - 1 + k) * 4u : kOffOut;
+    offh[k] = (unsigned)(h - 1 + k) < (unsigned)H ? (unsigned)((h - 1 + k) * W) * 4u : kOffOut;
+  }
   auto load_plane = [&](int d, float* o) {
+    const unsigned offd = (unsigned)d < (unsigned)D ? (unsigned)d * (unsigned)HW * 4u : kOffOut;
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        const int ih = h - 1 + kh, iw = w - 1 + kw;
-        const bool ok = d >= 0 && d < D && ih >= 0 && ih < H && iw >= 0 && iw < W;
-        const int dc = min(max(d, 0), D - 1), ihc = min(max(ih, 0), H - 1), iwc = min(max(iw, 0), W - 1);
-        const float v = xn[((size_t)dc * H + ihc) * W + iwc];
-        o[kh * 3 + kw] = ok ? v : 0.f;
+        const unsigned off = offd | offh[kh] | offw[kw];  // any kOffOut term keeps the top bit
+        o[kh * 3 + kw] = buf_load_f32(rx, (offd + offh[kh] + offw[kw]) | (off & kOffOut));
       }
   };
+  float win[3][9];
   load_plane(d0 - 1, win[0]);
   load_plane(d0, win[1]);
-  float* yo = y + ((size_t)n * D * HW + p) * 8;
   for (int d = d0; d < d1; ++d) {
     load_plane(d + 1, win[2]);
     float acc[8];
@@ -454,9 +464,24 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
         for (int t = 0; t < 9; ++t) a = fmaf(wt[c * 27 + kd * 9 + t], win[kd][t], a);
       acc[c] = relu(fmaf(a, alpha[c], shift[c]));
     }
-    float4* o4 = reinterpret_cast<float4*>(yo + (size_t)d * HW * 8);
-    o4[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-    o4[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    // store through LDS: the wave's 64 voxels x 32 B leave as two fully contiguous 1 KiB
+    // stores (every 4-lane quad writes 64 consecutive bytes)
+    float* st = stage + (threadIdx.x >> 6) * 64 * 8;
+    const int lane = threadIdx.x & 63;
+    *reinterpret_cast<float4*>(st + lane * 8) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *reinterpret_cast<float4*>(st + lane * 8 + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    __builtin_amdgcn_wave_barrier();
+    const float4 s0 = *reinterpret_cast<const float4*>(st + lane * 4);
+    const float4 s1 = *reinterpret_cast<const float4*>(st + 256 + lane * 4);
+    __builtin_amdgcn_wave_barrier();
+    float* wbase = ybase + ((size_t)d * HW + pw0) * 8;
+    if (full_wave) {
+      *reinterpret_cast<float4*>(wbase + lane * 4) = s0;
+      *reinterpret_cast<float4*>(wbase + 256 + lane * 4) = s1;
+    } else {
+      if (pw0 + (lane >> 1) < HW) *reinterpret_cast<float4*>(wbase + lane * 4) = s0;
+      if (pw0 + 32 + (lane >> 1) < HW) *reinterpret_cast<float4*>(wbase + 256 + lane * 4) = s1;
+    }
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       win[0][t] = win[1][t];
@@ -482,27 +507,25 @@ __global__ __launch_bounds__(256) void prob_kernel(const float* __restrict__ x, 
   if (p >= HW) return;
   const int h = p / W, w = p - h * W;
   const int d0 = dc * kDChunk, d1 = min(D, d0 + kDChunk);
-  const float* xn = x + (size_t)n * D * HW * 8;
+  const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)n * D * HW * 8, (unsigned)(D * HW * 32));
   float* yn = y + (size_t)n * D * HW + p;
-  // tap row (plane i, row offset kh): 3 taps x 8 channels; planes outside [0, D) and
-  // out-of-image taps read as zeros (fmaf(w, 0, acc) == acc)
+  unsigned offw[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) offw[k] = (unsigned)(w - 1 + k) < (unsigned)W ? (unsigned)(w - 1 + k) * 32u : kOffOut;
+  // tap row (plane i, row offset kh): 3 taps x 8 channels, unconditional buffer loads; planes
+  // outside [0, D) and out-of-image taps get an out-of-range offset and read 0 (fmaf(w, 0, acc) == acc)
   auto load_row = [&](int i, int kh, float4 (&o)[6]) {
     const int ih = h - 1 + kh;
-    const bool okr = i >= 0 && i < D && ih >= 0 && ih < H;
-    const int ic = min(max(i, 0), D - 1), ihc = min(max(ih, 0), H - 1);
+    const unsigned offr = ((unsigned)i < (unsigned)D && (unsigned)ih < (unsigned)H)
+                              ? ((unsigned)i * (unsigned)H + (unsigned)ih) * (unsigned)W * 32u
+                              : kOffOut;
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
-      const int iw = w - 1 + kw;
-      const bool ok = okr && iw >= 0 && iw < W;
-      const int iwc = min(max(iw, 0), W - 1);
-      const float4* q = reinterpret_cast<const float4*>(xn + (((size_t)ic * H + ihc) * W + iwc) * 8);
-      float4 u = q[0], v = q[1];
-      if (!ok) {
-        u = make_float4(0.f, 0.f, 0.f, 0.f);
-        v = u;
-      }
-      o[2 * kw] = u;
-      o[2 * kw + 1] = v;
+      const unsigned off = (offr + offw[kw]) | ((offr | offw[kw]) & kOffOut);
+      const floatx4 u = buf_load_f32x4(rx, off);
+      const floatx4 v = buf_load_f32x4(rx, off + 16u);
+      o[2 * kw] = make_float4(u[0], u[1], u[2], u[3]);
+      o[2 * kw + 1] = make_float4(v[0], v[1], v[2], v[3]);
     }
   };
   float acc_prev = 0.f, acc_cur = 0.f;  // outputs i-1 (has kd=0,1) and i (has kd=0)
@@ -670,6 +693,8 @@ extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height,
   if (!x || !w || !workspace || !logits || batch <= 0) return TMVS_ERR_ARG;
   if (depth % 8 || height % 8 || width % 8) return TMVS_ERR_SHAPE;
   if (w->base_ch != 8) return TMVS_ERR_SHAPE;
+  // conv0 / prob address one sample's 8-channel full-resolution volume with 32-bit offsets
+  if ((long long)depth * height * width * 32 >= (1LL << 31)) return TMVS_ERR_SHAPE;
   for (int i = 0; i < 11; ++i)
     if (!w->w[i]) return TMVS_ERR_ARG;
   for (int i = 0; i < 10; ++i)

@@ -122,7 +122,6 @@ __device__ __forceinline__ float group_max(float v) {
 // so an out-of-image tap only needs an out-of-range offset: each axis term is kAxisOut when
 // invalid, and any sum containing one is >= kAxisOut >= num_records (< 2^30, checked).
 constexpr unsigned kAxisOut = 0x40000000u;
-constexpr int kRsrcWord3 = 0x00020000;
 
 struct Geom {
   int x0, y0;
@@ -169,10 +168,10 @@ __device__ __forceinline__ void fetch(const __amdgpu_buffer_rsrc_t rsrc, unsigne
   const unsigned yrow = vbase + (unsigned)g.y0 * rowb;
   const unsigned ya = (unsigned)g.y0 < (unsigned)H ? yrow : kAxisOut;
   const unsigned yb = (unsigned)(g.y0 + 1) < (unsigned)H ? yrow + rowb : kAxisOut;
-  t.a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(ya + xa), 0, 0);
-  t.b = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(ya + xb), 0, 0);
-  t.c = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(yb + xa), 0, 0);
-  t.d = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(yb + xb), 0, 0);
+  t.a = buf_load_f32x4(rsrc, ya + xa);
+  t.b = buf_load_f32x4(rsrc, ya + xb);
+  t.c = buf_load_f32x4(rsrc, yb + xa);
+  t.d = buf_load_f32x4(rsrc, yb + xb);
 }
 
 // bilinear value of each channel (grid_sample's fma order), times ref, summed in channel order
