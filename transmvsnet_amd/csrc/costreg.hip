@@ -59,7 +59,7 @@ struct Geo {
 // (voxel stride CK+4 floats: the 16 lanes of a row hit distinct banks), then each wave runs
 // its NBW = TD*TH/4 rows through the 27 taps: A (weights) from global/L2, B from LDS.
 template <int CIN, int COUT, int S, int TD, int TH, int MBB>
-__global__ __launch_bounds__(256) void conv3d_lds_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv3d_lds_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                          const float* __restrict__ alpha,
                                                          const float* __restrict__ shift, float* __restrict__ y,
                                                          Geo g) {
@@ -114,19 +114,25 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const float* __restrict
     }
     __syncthreads();
 #pragma unroll 1
-    for (int kd = 0; kd < 3; ++kd)
+    for (int kd = 0; kd < 3; ++kd) {
+      // the kd slice's 9 weight fragments are requested together: one exposed latency per
+      // slice instead of one per tap (A fragments come from global/L2, B from LDS)
+      VecN<PL> aw[9][MBB];
+#pragma unroll
+      for (int t9 = 0; t9 < 9; ++t9)
+#pragma unroll
+        for (int m = 0; m < MBB; ++m) {
+          const int co = (mg * MBB + m) * 16 + col;
+          if (co < COUT)
+            aw[t9][m].load(wpk + ((size_t)(kd * 9 + t9) * COUT + co) * CIN + ch * CK + kgrp * PL);
+          else
+            aw[t9][m].zero();
+        }
+      __builtin_amdgcn_sched_barrier(0);  // keep the 9 requests ahead of the MFMAs
 #pragma unroll
     for (int t9 = 0; t9 < 9; ++t9) {
-      const int kh = t9 / 3, kw = t9 % 3, tap = kd * 9 + t9;
-      VecN<PL> a[MBB];
-#pragma unroll
-      for (int m = 0; m < MBB; ++m) {
-        const int co = (mg * MBB + m) * 16 + col;
-        if (co < COUT)
-          a[m].load(wpk + ((size_t)tap * COUT + co) * CIN + ch * CK + kgrp * PL);
-        else
-          a[m].zero();
-      }
+      const int kh = t9 / 3, kw = t9 % 3;
+      const VecN<PL>* a = aw[t9];
       VecN<PL> b[NBW];
 #pragma unroll
       for (int r = 0; r < NBW; ++r) {
@@ -143,6 +149,7 @@ __global__ __launch_bounds__(256) void conv3d_lds_kernel(const float* __restrict
 #pragma unroll
           for (int m = 0; m < MBB; ++m)
             acc[r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b[r].v[j], acc[r][m], 0, 0, 0);
+    }
     }
   }
   const int ow = ow0 + col;
@@ -295,7 +302,13 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
   constexpr int VST = SWZ ? 16 : CK + 4;
   constexpr int NVOX = LD * LH * LW;
   static_assert(MB % MBB == 0 && (TDI * THI) % 4 == 0, "tile");
+  static_assert(CK == 16 && MBB == 1, "LDS weight staging assumes 16-channel chunks, one 16-row block");
+  // weights of the current channel chunk: [27 taps][RM rows][16 ch], quad-swizzled like the
+  // tile so the A-fragment ds_read_b128 is bank-conflict free (a per-tap global load right
+  // before its MFMAs exposed a full memory latency per tap: MFMA busy 35 %)
+  constexpr int RM = COUT < 16 ? COUT : 16;
   __shared__ __attribute__((aligned(16))) float tile[NVOX * VST];
+  __shared__ __attribute__((aligned(16))) float wts[27 * RM * 16];
 
   const int nws = (g.Wi + 15) / 16, nhs = (g.Hi + THI - 1) / THI, nds = (g.Di + TDI - 1) / TDI;
   int t = xcd_remap(blockIdx.x, gridDim.x);  // contiguous tiles per XCD: halos share an L2
@@ -333,6 +346,11 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
       const int qs = SWZ ? (q ^ ((vox >> 1) & 3)) : q;
       *reinterpret_cast<float4*>(tile + vox * VST + 4 * qs) = v;
     }
+    for (int idx = threadIdx.x; idx < 27 * RM * 4; idx += 256) {
+      const int q = idx & 3, row = (idx >> 2) % RM, tap = (idx >> 2) / RM;
+      const float4 v = *reinterpret_cast<const float4*>(wpk + ((size_t)tap * COUT + mg * 16 + row) * CIN + ch * CK + 4 * q);
+      *reinterpret_cast<float4*>(wts + (tap * RM + row) * 16 + 4 * (q ^ ((row >> 1) & 3))) = v;
+    }
     __syncthreads();
 #pragma unroll
     for (int cls = 0; cls < 8; ++cls) {
@@ -348,14 +366,10 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
             const int kw = pw ? (tw ? 2 : 0) : 1, ow_off = (pw && !tw) ? 1 : 0;
             const int tap = kd * 9 + kh * 3 + kw;
             VecN<PL> a[MBB];
-#pragma unroll
-            for (int m = 0; m < MBB; ++m) {
-              const int co = (mg * MBB + m) * 16 + col;
-              if (co < COUT)
-                a[m].load(wpk + ((size_t)tap * COUT + co) * CIN + ch * CK + kgrp * PL);
-              else
-                a[m].zero();
-            }
+            if (col < RM)
+              a[0].load(wts + (tap * RM + col) * 16 + 4 * (kgrp ^ ((col >> 1) & 3)));
+            else
+              a[0].zero();
 #pragma unroll
             for (int r = 0; r < NBW; ++r) {
               const int rr = wv * NBW + r;
@@ -373,9 +387,51 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
           }
     }
   }
+  const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
+  if constexpr (COUT == 8) {
+    // 8-channel output (conv11, full resolution): the 32 output voxels of one (od, oh) row
+    // segment are exchanged through LDS so the skip read and the output store are single
+    // contiguous 1 KiB accesses (each 4-lane quad on 64 consecutive bytes) instead of 16-byte
+    // pieces at a 64-byte stride.
+    __shared__ __attribute__((aligned(16))) float ep[4][32 * 8];
+    float* eb = ep[wv];
+    const int co = kgrp * 4;
+    float4 al = make_float4(0.f, 0.f, 0.f, 0.f), sh = al;
+    if (kgrp < 2) {
+      al = *reinterpret_cast<const float4*>(alpha + co);
+      sh = *reinterpret_cast<const float4*>(shift + co);
+    }
+    const int ow = 2 * mw0 + (lane >> 1);  // voxel this lane stores (half lane & 1)
+#pragma unroll
+    for (int r = 0; r < NBW; ++r) {
+      const int rr = wv * NBW + r;
+      const int md = md0 + rr / THI, mh = mh0 + rr % THI;
+#pragma unroll
+      for (int pdh = 0; pdh < 4; ++pdh) {
+        if (kgrp < 2) {
+#pragma unroll
+          for (int pw = 0; pw < 2; ++pw) {
+            const floatx4 a = acc[r][pdh * 2 + pw][0];
+            *reinterpret_cast<float4*>(eb + (2 * col + pw) * 8 + co) =
+                make_float4(relu(fmaf(a[0], al.x, sh.x)), relu(fmaf(a[1], al.y, sh.y)),
+                            relu(fmaf(a[2], al.z, sh.z)), relu(fmaf(a[3], al.w, sh.w)));
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const float4 v = *reinterpret_cast<const float4*>(eb + lane * 4);
+        __builtin_amdgcn_wave_barrier();
+        const int od = 2 * md + (pdh >> 1), oh = 2 * mh + (pdh & 1);
+        if (md < g.Di && mh < g.Hi && ow < 2 * g.Wi) {
+          const size_t o = (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * 8 + (lane & 1) * 4;
+          const float4 s = *reinterpret_cast<const float4*>(skip + o);
+          *reinterpret_cast<float4*>(y + o) = make_float4(s.x + v.x, s.y + v.y, s.z + v.z, s.w + v.w);
+        }
+      }
+    }
+    return;
+  }
   const int mw = mw0 + col;
   if (mw >= g.Wi) return;
-  const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
 #pragma unroll
   for (int m = 0; m < MBB; ++m) {
     const int co = (mg * MBB + m) * 16 + kgrp * 4;
