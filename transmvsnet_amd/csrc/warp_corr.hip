@@ -147,73 +147,131 @@ __device__ __forceinline__ Geom geom_bcast(const Geom& g) {
 }
 
 
-// Tap fetch for one round: 4 taps x this lane's channel quad; weights kept for the combine.
-struct Taps {
-  floatx4 a, b, c, d;
-  float wnw, wne, wsw, wse;
+// Tap reuse across consecutive planes. A pixel's depth planes project to nearby points on the
+// epipolar line, so consecutive planes mostly share bilinear taps (unique taps per pixel-view,
+// synthetic DTU rig: 129 / 48 / 14 of 192 / 128 / 32 tap loads in stages 1 / 2 / 3). The 4
+// taps of a plane always occupy the 4 (x parity, y parity) classes, so tap (X, Y) is cached in
+// register slot (X&1, Y&1) with its position as tag: a plane loads only the slots whose tag
+// changed. The address unit's cost scales with the lanes that make a memory request (measured,
+// scripts/micro/ta_mask.hip: exec-masked and out-of-range lanes are equally free), so skipped
+// loads are skipped work.
+struct Slots {
+  floatx4 v[4];
+  unsigned pos[4];
 };
 
+__device__ __forceinline__ void slots_reset(Slots& S) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) S.pos[s] = 0xFFFFFFFFu;  // no position packs to this
+}
+
 template <int C>
-__device__ __forceinline__ void fetch(const __amdgpu_buffer_rsrc_t rsrc, unsigned vbase, unsigned rowb, int W, int H,
-                                      const Geom& g, Taps& t) {
+__device__ __forceinline__ void fetch_reuse(const __amdgpu_buffer_rsrc_t rsrc, unsigned vbase, unsigned rowb, int W,
+                                            int H, const Geom& g, Slots& S, floatx4 (&val)[4], float (&w)[4]) {
   constexpr unsigned CB = C * 4;
   const float we = g.fx, n = g.fy;
   const float ea = 1.f - we, s = 1.f - n;
-  t.wnw = s * ea;
-  t.wne = s * we;
-  t.wsw = n * ea;
-  t.wse = n * we;
+#pragma unroll
+  for (int sl = 0; sl < 4; ++sl) {
+    const int px = sl & 1, py = sl >> 1;
+    const int X = g.x0 + ((g.x0 ^ px) & 1), Y = g.y0 + ((g.y0 ^ py) & 1);
+    const unsigned key = (unsigned)(X + 2) | ((unsigned)(Y + 2) << 16);  // X, Y in [-2, 32767]
+    // branch-free: a lane whose slot still holds the tap issues the load with an out-of-range
+    // offset (no memory request; costs the address unit what an exec-masked lane costs, measured)
+    const bool need = key != S.pos[sl];
+    S.pos[sl] = key;
+    const bool inside = (unsigned)X < (unsigned)W && (unsigned)Y < (unsigned)H;  // outside: reads 0
+    const unsigned off = (need && inside) ? vbase + (unsigned)Y * rowb + (unsigned)X * CB : kOffOut;
+    const floatx4 ld = buf_load_f32x4(rsrc, off);
+    S.v[sl] = need ? ld : S.v[sl];
+    val[sl] = S.v[sl];
+    // grid_sample's weights: (y weight) * (x weight), nw = (1-fy)(1-fx) ...
+    w[sl] = ((Y == g.y0) ? s : n) * ((X == g.x0) ? ea : we);
+  }
+}
+
+// Without the cache (stage 1: uniform planes ~1.4 px apart share few taps): the 4 taps in
+// grid_sample's order nw, ne, sw, se, so the interpolation's fma chain is the reference's.
+template <int C>
+__device__ __forceinline__ void fetch_full(const __amdgpu_buffer_rsrc_t rsrc, unsigned vbase, unsigned rowb, int W,
+                                           int H, const Geom& g, floatx4 (&val)[4], float (&w)[4]) {
+  constexpr unsigned CB = C * 4;
+  const float we = g.fx, n = g.fy;
+  const float ea = 1.f - we, s = 1.f - n;
+  w[0] = s * ea;
+  w[1] = s * we;
+  w[2] = n * ea;
+  w[3] = n * we;
   const unsigned xa = (unsigned)g.x0 < (unsigned)W ? (unsigned)g.x0 * CB : kAxisOut;
   const unsigned xb = (unsigned)(g.x0 + 1) < (unsigned)W ? (unsigned)(g.x0 + 1) * CB : kAxisOut;
   const unsigned yrow = vbase + (unsigned)g.y0 * rowb;
   const unsigned ya = (unsigned)g.y0 < (unsigned)H ? yrow : kAxisOut;
   const unsigned yb = (unsigned)(g.y0 + 1) < (unsigned)H ? yrow + rowb : kAxisOut;
-  t.a = buf_load_f32x4(rsrc, ya + xa);
-  t.b = buf_load_f32x4(rsrc, ya + xb);
-  t.c = buf_load_f32x4(rsrc, yb + xa);
-  t.d = buf_load_f32x4(rsrc, yb + xb);
+  val[0] = buf_load_f32x4(rsrc, ya + xa);
+  val[1] = buf_load_f32x4(rsrc, ya + xb);
+  val[2] = buf_load_f32x4(rsrc, yb + xa);
+  val[3] = buf_load_f32x4(rsrc, yb + xb);
 }
 
-// bilinear value of each channel (grid_sample's fma order), times ref, summed in channel order
-__device__ __forceinline__ float combine(const Taps& t, const float4& r4) {
+// bilinear value of each channel (fixed slot order), times ref, summed in channel order
+__device__ __forceinline__ float combine(const floatx4 (&v)[4], const float (&w)[4], const float4& r4) {
   float acc = 0.f;
-  acc = acc + fmaf(t.d[0], t.wse, fmaf(t.c[0], t.wsw, fmaf(t.b[0], t.wne, t.a[0] * t.wnw))) * r4.x;
-  acc = acc + fmaf(t.d[1], t.wse, fmaf(t.c[1], t.wsw, fmaf(t.b[1], t.wne, t.a[1] * t.wnw))) * r4.y;
-  acc = acc + fmaf(t.d[2], t.wse, fmaf(t.c[2], t.wsw, fmaf(t.b[2], t.wne, t.a[2] * t.wnw))) * r4.z;
-  acc = acc + fmaf(t.d[3], t.wse, fmaf(t.c[3], t.wsw, fmaf(t.b[3], t.wne, t.a[3] * t.wnw))) * r4.w;
+  acc = acc + fmaf(v[3][0], w[3], fmaf(v[2][0], w[2], fmaf(v[1][0], w[1], v[0][0] * w[0]))) * r4.x;
+  acc = acc + fmaf(v[3][1], w[3], fmaf(v[2][1], w[2], fmaf(v[1][1], w[1], v[0][1] * w[0]))) * r4.y;
+  acc = acc + fmaf(v[3][2], w[3], fmaf(v[2][2], w[2], fmaf(v[1][2], w[1], v[0][2] * w[0]))) * r4.z;
+  acc = acc + fmaf(v[3][3], w[3], fmaf(v[2][3], w[2], fmaf(v[1][3], w[1], v[0][3] * w[0]))) * r4.w;
   return acc;
 }
 
-
-// Partials of rounds R0..R0+3 (or fewer): every round's loads are issued before any is consumed.
 // Rounds R0..R0+N-1: in round t the whole group samples plane slot t (geometry broadcast from
-// lane t), so each load instruction covers one contiguous C*4-byte row per group.
-template <int C, int R0, int N>
+// lane t), so each load instruction covers one contiguous C*4-byte row per group. Every
+// round's (masked) loads are issued before any is consumed.
+template <int C, bool REUSE, int R0, int N>
 __device__ __forceinline__ void rounds(const __amdgpu_buffer_rsrc_t rsrc, unsigned vbase, unsigned rowb, int W,
-                                       int H, const Geom& own, const float4& r4, float* part) {
-  Taps t[N];
-  fetch<C>(rsrc, vbase, rowb, W, H, geom_bcast<C / 4, R0>(own), t[0]);
-  if constexpr (N > 1) fetch<C>(rsrc, vbase, rowb, W, H, geom_bcast<C / 4, R0 + 1>(own), t[1]);
-  if constexpr (N > 2) fetch<C>(rsrc, vbase, rowb, W, H, geom_bcast<C / 4, R0 + 2>(own), t[2]);
-  if constexpr (N > 3) fetch<C>(rsrc, vbase, rowb, W, H, geom_bcast<C / 4, R0 + 3>(own), t[3]);
+                                       int H, const Geom& own, const float4& r4, Slots& S, float* part) {
+  floatx4 v[N][4];
+  float w[N][4];
+#define TMVS_FETCH(I)                                                                          \
+  if constexpr (REUSE)                                                                         \
+    fetch_reuse<C>(rsrc, vbase, rowb, W, H, geom_bcast<C / 4, R0 + I>(own), S, v[I], w[I]); \
+  else                                                                                         \
+    fetch_full<C>(rsrc, vbase, rowb, W, H, geom_bcast<C / 4, R0 + I>(own), v[I], w[I]);
+  TMVS_FETCH(0)
+  if constexpr (N > 1) { TMVS_FETCH(1) }
+  if constexpr (N > 2) { TMVS_FETCH(2) }
+  if constexpr (N > 3) { TMVS_FETCH(3) }
+#undef TMVS_FETCH
 #pragma unroll
-  for (int i = 0; i < N; ++i) part[R0 + i] = combine(t[i], r4);
+  for (int i = 0; i < N; ++i) part[R0 + i] = combine(v[i], w[i], r4);
 }
 
 // Full channel sum of this lane's own plane (slot k): LPS rounds, then a butterfly
 // reduce-scatter over lane bits (xor 4, xor 2, xor 1). At each step a lane keeps the half of
 // the planes whose slot bit matches its own lane bit and sends the other half to its partner;
 // the sum for slot t ends in lane t: no dependent shuffle chains, LPS-1 exchanges.
-template <int C>
+template <int C, bool REUSE>
 __device__ __forceinline__ float plane_corr(const __amdgpu_buffer_rsrc_t rsrc, unsigned vbase, unsigned rowb, int W,
-                                            int H, const Geom& own, const float4& r4, int k) {
+                                            int H, const Geom& own, const float4& r4, int k, Slots& S) {
   constexpr int LPS = C / 4;
   float p[LPS];
-  if constexpr (LPS <= 4) {
-    rounds<C, 0, LPS>(rsrc, vbase, rowb, W, H, own, r4, p);
+  if constexpr (REUSE) {
+    // batches of 2 rounds: the cached slots plus a batch's loads fit the VGPR budget
+    rounds<C, true, 0, 2>(rsrc, vbase, rowb, W, H, own, r4, S, p);
+    if constexpr (LPS >= 4) {
+      __builtin_amdgcn_sched_barrier(0);
+      rounds<C, true, 2, 2>(rsrc, vbase, rowb, W, H, own, r4, S, p);
+    }
+    if constexpr (LPS >= 8) {
+      __builtin_amdgcn_sched_barrier(0);
+      rounds<C, true, 4, 2>(rsrc, vbase, rowb, W, H, own, r4, S, p);
+      __builtin_amdgcn_sched_barrier(0);
+      rounds<C, true, 6, 2>(rsrc, vbase, rowb, W, H, own, r4, S, p);
+    }
+  } else if constexpr (LPS <= 4) {
+    rounds<C, false, 0, LPS>(rsrc, vbase, rowb, W, H, own, r4, S, p);
   } else {
-    rounds<C, 0, 4>(rsrc, vbase, rowb, W, H, own, r4, p);
-    rounds<C, 4, 4>(rsrc, vbase, rowb, W, H, own, r4, p);
+    rounds<C, false, 0, 4>(rsrc, vbase, rowb, W, H, own, r4, S, p);
+    rounds<C, false, 4, 4>(rsrc, vbase, rowb, W, H, own, r4, S, p);
   }
   float q[LPS];
 #pragma unroll
@@ -303,11 +361,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     float w = 0.f;
     if constexpr (!PW) w = vw_in[(size_t)(vw_offset + v) * Hs * Ws + (py >> vw_shift) * Ws + (px >> vw_shift)];
     float wm = 0.f;  // PW: running max of sigmoid (> 0, so 0 is neutral)
+    Slots S;  // tap cache, valid within one view: planes j*LPS + t run in depth order
+    slots_reset(S);
 #pragma unroll 1
     for (int j = 0; j < DPT; ++j) {
       Geom own;
       project(rx, ry, rz, R[3], R[7], R[11], dep_lds[j][tid], halfw, halfh, own.x0, own.y0, own.fx, own.fy);
-      const float sim = plane_corr<C>(rsrc, vbase, rowb, W, H, own, r4, k) * (1.f / (float)C);  // C = 2^n: == / C
+      const float sim = plane_corr<C, !PW>(rsrc, vbase, rowb, W, H, own, r4, k, S) * (1.f / (float)C);  // C = 2^n: == / C
       if constexpr (PW) {
         sim_lds[j][tid] = sim;
         int salt = 0;  // opaque offset: keeps the parameter reads from being hoisted into VGPRs
