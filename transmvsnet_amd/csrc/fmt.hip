@@ -133,6 +133,43 @@ __device__ __forceinline__ void mfma_linear(const float (&frag)[OUT / 16][IN / 4
       acc[mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(frag[mb][s], in[s >> 2][s & 3], acc[mb], 0, 0, 0);
 }
 
+// A fragments staged in LDS in read order [mb][s/4][lane][4]: one ds_read_b128 per lane
+// serves 4 consecutive k-steps of an MFMA chain, and the 64 lanes read 1 KiB contiguous
+// (conflict-free). Used by fmt_apply_kernel, whose 96 weight VGPRs otherwise capped it at
+// 2 waves/SIMD.
+template <int OUT, int IN, bool TRANS>
+__device__ __forceinline__ void stage_afrag(const float* __restrict__ W, float* __restrict__ lds) {
+  constexpr int N = OUT * IN;  // = (OUT/16) * (IN/16) * 64 lanes * 4
+  for (int idx = threadIdx.x; idx < N; idx += blockDim.x) {
+    const int j = idx & 3, l = (idx >> 2) & 63, rest = idx >> 8;
+    const int s4 = rest % (IN / 16), mb = rest / (IN / 16);
+    const int s = 4 * s4 + j;
+    const int o = 16 * mb + (l & 15), i = kfeat(s, l >> 4);
+    lds[idx] = TRANS ? W[i * OUT + o] : W[o * IN + i];
+  }
+}
+
+template <int OUT, int IN, int NT>
+__device__ __forceinline__ void mfma_linear_lds(const float* __restrict__ fl, const floatx4 (&in)[NT][IN / 16],
+                                                floatx4 (&acc)[NT][OUT / 16], int lane) {
+#pragma unroll
+  for (int p = 0; p < NT; ++p)
+#pragma unroll
+    for (int mb = 0; mb < OUT / 16; ++mb) acc[p][mb] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s4 = 0; s4 < IN / 16; ++s4)
+#pragma unroll
+    for (int mb = 0; mb < OUT / 16; ++mb) {
+      const float4 a4 = *reinterpret_cast<const float4*>(fl + ((mb * (IN / 16) + s4) * 64 + lane) * 4);
+      const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int p = 0; p < NT; ++p)
+          acc[p][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], in[p][s4][j], acc[p][mb], 0, 0, 0);
+    }
+}
+
 // NT independent tiles interleaved: NT x OUT/16 independent accumulation chains in flight
 template <int OUT, int IN, int NT>
 __device__ __forceinline__ void mfma_linear_n(const float (&frag)[OUT / 16][IN / 4], const floatx4 (&in)[NT][IN / 16],
@@ -192,7 +229,8 @@ __device__ __forceinline__ void load_token_frag(const float* __restrict__ row, f
   }
 }
 
-constexpr int kTilesPerWave = 8;  // 16-token tiles per wave: amortises the weight-fragment loads
+constexpr int kTilesPerWave = 8;  // 16-token tiles per wave (kv): amortises the weight-fragment loads
+constexpr int kApplyTilesPerWave = 4;  // apply: weights come from LDS; more, shorter waves
 
 // (KV, Ksum) partial sums: per wave, tiles of 16 source tokens; K, V by MFMA; per lane the
 // two heads it owns are accumulated over its tokens, then summed over the 16 token lanes.
@@ -313,7 +351,7 @@ __global__ __launch_bounds__(256) void fmt_kv_combine_kernel(const float* __rest
 
 // The rest of EncoderLayer.forward for tiles of 16 query tokens, entirely in registers;
 // kApplyNT tiles are processed together so their MFMA chains interleave.
-constexpr int kApplyNT = 2;
+constexpr int kApplyNT = 1;
 __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, int L, const float* __restrict__ kvg,
                                                         long kv_stride, const float* __restrict__ w) {
   __shared__ float kvs[kKV];
@@ -323,18 +361,21 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
   const int g = lane >> 4;
   if (threadIdx.x < kKV) kvs[threadIdx.x] = kvg[(size_t)v * kv_stride + threadIdx.x];
   if (threadIdx.x < 128) vec[threadIdx.x] = w[TMVS_ENC_LN1G + threadIdx.x];
-  float wq[2][8], wo[2][8], w1[4][8], w2[2][16];
-  load_afrag<32, 32, false>(w + TMVS_ENC_WQ, wq, lane);
-  load_afrag<32, 32, false>(w + TMVS_ENC_WO, wo, lane);
-  load_afrag<64, 32, false>(w + TMVS_ENC_W1, w1, lane);
-  load_afrag<32, 64, true>(w + TMVS_ENC_W2T, w2, lane);
+  __shared__ __attribute__((aligned(16))) float frag[32 * 32 * 2 + 64 * 32 * 2];  // Wq, Wo, W1, W2 fragments
+  stage_afrag<32, 32, false>(w + TMVS_ENC_WQ, frag);
+  stage_afrag<32, 32, false>(w + TMVS_ENC_WO, frag + 1024);
+  stage_afrag<64, 32, false>(w + TMVS_ENC_W1, frag + 2048);
+  stage_afrag<32, 64, true>(w + TMVS_ENC_W2T, frag + 4096);
   __syncthreads();
   float* xv = x + (size_t)v * L * kD;
-  const int tile0 = (blockIdx.x * 4 + wv) * kTilesPerWave;
+  const int tile0 = (blockIdx.x * 4 + wv) * kApplyTilesPerWave;
 #pragma unroll 1
-  for (int it = 0; it < kTilesPerWave; it += kApplyNT) {
+  for (int it = 0; it < kApplyTilesPerWave; it += kApplyNT) {
     if ((tile0 + it) * 16 >= L) break;  // wave-uniform
     constexpr int NT = kApplyNT;
+    int salt = 0;  // opaque offset: fragment reads stay in the loop (not hoisted back into VGPRs)
+    asm volatile("" : "+v"(salt));
+    const float* fr = frag + salt;
     float* row[NT];
     bool ok[NT];
     floatx4 xs[NT][2];
@@ -346,7 +387,7 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
       load_token_frag(row[p], xs[p], lane);
     }
     floatx4 q[NT][2], msg[NT][2];
-    mfma_linear_n<32, 32, NT>(wq, xs, q);
+    mfma_linear_lds<32, 32, NT>(fr, xs, q, lane);
 #pragma unroll
     for (int p = 0; p < NT; ++p)
 #pragma unroll
@@ -368,7 +409,7 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
         }
       }
     floatx4 a[NT][2];
-    mfma_linear_n<32, 32, NT>(wo, msg, a);
+    mfma_linear_lds<32, 32, NT>(fr + 1024, msg, a, lane);
 #pragma unroll
     for (int p = 0; p < NT; ++p) {
 #pragma unroll
@@ -378,14 +419,14 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
       layer_norm_frag(xs[p], vec, vec + kD, lane);
     }
     floatx4 hdn[NT][4], ff[NT][2];
-    mfma_linear_n<64, 32, NT>(w1, xs, hdn);
+    mfma_linear_lds<64, 32, NT>(fr + 2048, xs, hdn, lane);
 #pragma unroll
     for (int p = 0; p < NT; ++p)
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) hdn[p][mb][r] = relu(hdn[p][mb][r] + w[TMVS_ENC_B1 + 16 * mb + 4 * g + r]);
-    mfma_linear_n<32, 64, NT>(w2, hdn, ff);
+    mfma_linear_lds<32, 64, NT>(fr + 4096, hdn, ff, lane);
 #pragma unroll
     for (int p = 0; p < NT; ++p) {
 #pragma unroll
@@ -404,7 +445,7 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
 }
 
 static int kv_nblk(int S) { return (S + 16 * 4 * kTilesPerWave - 1) / (16 * 4 * kTilesPerWave); }
-static int apply_nblk(int L) { return (L + 16 * 4 * kTilesPerWave - 1) / (16 * 4 * kTilesPerWave); }
+static int apply_nblk(int L) { return (L + 16 * 4 * kApplyTilesPerWave - 1) / (16 * 4 * kApplyTilesPerWave); }
 
 }  // namespace tmvs
 
