@@ -69,6 +69,48 @@ def test_warp_corr_stage1_mode(sd, c, d):
     np.testing.assert_allclose(to_np(vw), to_np(vw_ref), rtol=0, atol=2e-5)
 
 
+@pytest.mark.parametrize("c,d,stage1", [(32, 48, True), (16, 32, False), (8, 8, False)])
+def test_warp_corr_ten_source_views(sd, c, d, stage1):
+    """N=11 (configs C3/C4: DTU / Tanks&Temples with 10 source views) through one launch."""
+    torch.manual_seed(100 + c)
+    n, h, w = 11, 20, 36  # TnT-like aspect
+    feats = [torch.randn(1, c, h, w) for _ in range(n)]
+    proj = synthetic.synthetic_cameras(n, h * 4, w * 4, seed=9)["stage1"]
+    hyp = torch.rand(1, d, h, w) * 500 + 425
+    nh = [_nhwc(f).to(DEV) for f in feats]
+    src = torch.stack([x[0] for x in nh[1:]], 0).unsqueeze(0).contiguous()
+    rows = ops.proj_rows(proj)
+    if stage1:
+        sim_ref, vw_ref = oracle.build_cost_volume(sd, feats, proj, hyp)
+        sim, _, vw = ops.warp_corr(nh[0], src, rows, hyp.to(DEV), pw_params=_pw_params(sd))
+        np.testing.assert_allclose(to_np(vw), to_np(vw_ref), rtol=0, atol=2e-5)
+    else:
+        vw = torch.rand(1, n - 1, h, w)
+        sim_ref, _ = oracle.build_cost_volume({}, feats, proj, hyp, view_weights=vw)
+        sim, _, _ = ops.warp_corr(nh[0], src, rows, hyp.to(DEV), view_w_in=vw.to(DEV), vw_shift=0)
+    np.testing.assert_allclose(to_np(sim)[:, None], to_np(sim_ref), rtol=0, atol=2e-5)
+
+
+def test_e2e_eleven_views_tnt_aspect(sd):
+    """Whole hot path at N=11 on a Tanks&Temples-shaped (1056x1920 / 4) frame vs the oracle."""
+    m = TransMVSNet().eval()
+    m.load_state_dict(sd, strict=True)
+    m = m.to(DEV)
+    H, W, N = 256, 480, 11
+    feats = synthetic.synthetic_features(N, H, W, seed=4)
+    proj = synthetic.synthetic_cameras(N, H, W, seed=3)
+    dv = synthetic.synthetic_depth_values(1)
+    ref = oracle.forward_from_features(sd, feats, proj, dv, (H, W))
+    with torch.no_grad():
+        out = m.forward_features([{k: v.to(DEV) for k, v in f.items()} for f in feats], proj, dv.to(DEV), (H, W))
+    for s in (1, 2, 3):
+        mean_l1, near, flips = depth_parity(to_np(out[f"stage{s}"]["depth"]), to_np(ref[f"stage{s}"]["depth"]),
+                                            to_np(ref[f"stage{s}"]["prob_volume"]))
+        assert flips == 0, (s, mean_l1, near, flips)
+    l1 = float(np.abs(to_np(out["depth"]).astype(np.float64) - to_np(ref["depth"]).astype(np.float64)).mean())
+    assert l1 <= 1e-4, l1
+
+
 def _pw_params(sd):
     m = TransMVSNet()
     m.load_state_dict(sd, strict=True)
