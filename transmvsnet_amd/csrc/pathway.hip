@@ -114,6 +114,117 @@ __global__ __launch_bounds__(256) void pathway_kernel(const float* __restrict__ 
   for (int o4 = 0; o4 < CF / 4; ++o4) op[o4] = make_float4(acc[4 * o4], acc[4 * o4 + 1], acc[4 * o4 + 2], acc[4 * o4 + 3]);
 }
 
+// 16-channel variant (stage-2 pathway, the larger one): the 3x3 smoothing conv runs on fp32
+// MFMA as an implicit GEMM -- M = 16 output channels, N = 16 pixels of a tile row,
+// K = 16 channels x 9 taps -- with B fragments from the LDS halo and A fragments (weights) in
+// VGPRs. The halo is stored [pixel][16 ch] with channels interleaved so a lane's 4 k-values
+// (channels kgrp, 4+kgrp, 8+kgrp, 12+kgrp) are one ds_read_b128, quad-swizzled by pixel
+// (bank-conflict free for 16 consecutive pixels, as in costreg.hip).
+typedef float floatx4_p __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int halo16_index(int vox, int o) {
+  const int q = (o & 3) ^ ((vox >> 1) & 3);
+  return vox * 16 + q * 4 + (o >> 2);
+}
+
+template <int CC>
+__global__ __launch_bounds__(256) void pathway16_mfma_kernel(const float* __restrict__ coarse,
+                                                             const float* __restrict__ lateral, long lat_stride,
+                                                             const float* __restrict__ wred,
+                                                             const float* __restrict__ wsm, int h, int w,
+                                                             float* __restrict__ out) {
+  constexpr int CF = 16;
+  __shared__ float red[CF][kCoarse][kCoarse + 1];
+  __shared__ __attribute__((aligned(16))) float inb[kHalo * kHalo * CF];
+  const int H = 2 * h, W = 2 * w;
+  const int v = blockIdx.z;
+  const int y0 = blockIdx.y * kTile, x0 = blockIdx.x * kTile;
+  const int cy0 = y0 / 2 - 1, cx0 = x0 / 2 - 1;
+  const float* cv = coarse + (size_t)v * h * w * CC;
+  // 1) 1x1 reduction of the coarse patch (as pathway_kernel)
+  for (int idx = threadIdx.x; idx < kCoarse * kCoarse; idx += blockDim.x) {
+    const int r = idx / kCoarse, c = idx - r * kCoarse;
+    const int cy = cy0 + r, cx = cx0 + c;
+    if (cy < 0 || cy >= h || cx < 0 || cx >= w) continue;
+    float xin[CC];
+    const float* p = cv + ((size_t)cy * w + cx) * CC;
+#pragma unroll
+    for (int i4 = 0; i4 < CC / 4; ++i4) {
+      const float4 t = *reinterpret_cast<const float4*>(p + 4 * i4);
+      xin[4 * i4] = t.x;
+      xin[4 * i4 + 1] = t.y;
+      xin[4 * i4 + 2] = t.z;
+      xin[4 * i4 + 3] = t.w;
+    }
+    float acc[CF];
+#pragma unroll
+    for (int o = 0; o < CF; ++o) acc[o] = 0.f;
+#pragma unroll 2
+    for (int i = 0; i < CC; ++i)
+#pragma unroll
+      for (int o = 0; o < CF; ++o) acc[o] = fmaf(wred[i * CF + o], xin[i], acc[o]);
+#pragma unroll
+    for (int o = 0; o < CF; ++o) red[o][r][c] = acc[o];
+  }
+  // A fragments meanwhile: lane (co = col, kgrp), tap t, k-step j -> W[co][ci = 4j + kgrp][t]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int col = lane & 15, kgrp = lane >> 4;
+  float wa[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wa[t][j] = wsm[((4 * j + kgrp) * 9 + t) * CF + col];
+  __syncthreads();
+  // 2) bilinear x2 up-sampling + lateral over the 18x18 halo (zero outside the image)
+  const float* lv = lateral + (size_t)v * lat_stride;
+  for (int idx = threadIdx.x; idx < kHalo * kHalo; idx += blockDim.x) {
+    const int r = idx / kHalo, c = idx - r * kHalo;
+    const int y = y0 - 1 + r, x = x0 - 1 + c;
+    if (y < 0 || y >= H || x < 0 || x >= W) {
+#pragma unroll
+      for (int o = 0; o < CF; ++o) inb[halo16_index(idx, o)] = 0.f;
+      continue;
+    }
+    const Axis ay = up_axis(y, h, H), ax = up_axis(x, w, W);
+    const int r0 = ay.i0 - cy0, r1 = ay.i1 - cy0, c0 = ax.i0 - cx0, c1 = ax.i1 - cx0;
+#pragma unroll
+    for (int o = 0; o < CF; ++o) {
+      const float t0 = fmaf(red[o][r0][c0], ax.l0, red[o][r0][c1] * ax.l1);
+      const float t1 = fmaf(red[o][r1][c0], ax.l0, red[o][r1][c1] * ax.l1);
+      const float up = fmaf(t0, ay.l0, t1 * ay.l1);
+      inb[halo16_index(idx, o)] = up + lv[((size_t)o * H + y) * W + x];
+    }
+  }
+  __syncthreads();
+  // 3) 3x3 conv on MFMA: wave wv owns tile rows 4wv .. 4wv+3
+  floatx4_p acc[4];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) acc[rr] = floatx4_p{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int kh = t / 3, kw = t % 3;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int vox = (4 * wv + rr + kh) * kHalo + col + kw;
+      const float4 b = *reinterpret_cast<const float4*>(inb + vox * 16 + 4 * (kgrp ^ ((vox >> 1) & 3)));
+      acc[rr] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t][0], b.x, acc[rr], 0, 0, 0);
+      acc[rr] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t][1], b.y, acc[rr], 0, 0, 0);
+      acc[rr] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t][2], b.z, acc[rr], 0, 0, 0);
+      acc[rr] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t][3], b.w, acc[rr], 0, 0, 0);
+    }
+  }
+  // D: lane (col, kgrp) holds output channels 4kgrp .. 4kgrp+3 of pixel (row, col)
+  const int x = x0 + col;
+  if (x >= W) return;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int y = y0 + 4 * wv + rr;
+    if (y >= H) continue;
+    *reinterpret_cast<float4*>(out + (((size_t)v * H + y) * W + x) * CF + 4 * kgrp) =
+        make_float4(acc[rr][0], acc[rr][1], acc[rr][2], acc[rr][3]);
+  }
+}
+
 }  // namespace tmvs
 
 using namespace tmvs;
@@ -125,8 +236,8 @@ extern "C" int tmvs_fmt_pathway(const float* coarse, const float* lateral, long 
   const dim3 grid((2 * w + kTile - 1) / kTile, (2 * h + kTile - 1) / kTile, nv);
   hipStream_t st = (hipStream_t)stream;
   if (cc == 32 && cf == 16)
-    hipLaunchKernelGGL((pathway_kernel<32, 16>), grid, dim3(256), 0, st, coarse, lateral, lat_view_stride, w_reduce,
-                       w_smooth, h, w, out);
+    hipLaunchKernelGGL((pathway16_mfma_kernel<32>), grid, dim3(256), 0, st, coarse, lateral, lat_view_stride,
+                       w_reduce, w_smooth, h, w, out);
   else if (cc == 16 && cf == 8)
     hipLaunchKernelGGL((pathway_kernel<16, 8>), grid, dim3(256), 0, st, coarse, lateral, lat_view_stride, w_reduce,
                        w_smooth, h, w, out);
