@@ -36,8 +36,8 @@ PEAK_F32_MFMA_TFS = 157.3  # MI355X_MICROARCH.md: fp32 MFMA dense peak
 def _args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--mode", choices=("replica", "views"), default="replica")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
