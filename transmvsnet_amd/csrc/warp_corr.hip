@@ -442,10 +442,175 @@ __global__ void homo_warping_kernel(const float* __restrict__ src, const float* 
   }
 }
 
+// C = 8 with given view weights (stage 3): "row pair" lane layout. A pixel is served by 4
+// lanes k = (tx, q): tx picks the tap column (x0 or x0+1), q the channel quad; in a round the
+// group's 4 lanes load one contiguous 64-byte span per tap row (x0 and x0+1, all 8 channels)
+// instead of two lanes loading 32-byte rows of different taps, so every lane quad of a load
+// instruction stays on one span (measured with the C/4 layout: 48 address-unit cycles per
+// instruction, stalled on the L1). Bilinear partial per lane: its column's two taps; the
+// reduce-scatter over the 4 lanes then adds the columns and the channel quads.
+// geometry of plane slot t (compile-time after unrolling) broadcast from lane t of the group
+template <int LPS>
+__device__ __forceinline__ Geom geom_round(const Geom& own, int t) {
+  if (t == 0) return geom_bcast<LPS, 0>(own);
+  if (t == 1) return geom_bcast<LPS, 1>(own);
+  if constexpr (LPS > 2) {
+    if (t == 2) return geom_bcast<LPS, 2>(own);
+    if (t == 3) return geom_bcast<LPS, 3>(own);
+  }
+  if constexpr (LPS > 4) {
+    if (t == 4) return geom_bcast<LPS, 4>(own);
+    if (t == 5) return geom_bcast<LPS, 5>(own);
+    if (t == 6) return geom_bcast<LPS, 6>(own);
+    return geom_bcast<LPS, 7>(own);
+  }
+  return own;
+}
+
+// Row-pair rounds R0..R0+N-1 (see warp_pair_kernel): in round t the group samples plane t;
+// this lane loads its tap column's two rows (one 16-byte channel quad each); all loads of the
+// batch are issued before any is consumed.
+template <int C, int R0, int N>
+__device__ __forceinline__ void pair_rounds(const __amdgpu_buffer_rsrc_t rsrc, unsigned vbase, unsigned rowb, int W,
+                                            int H, const Geom& own, const float4& r4, int tx, float* part) {
+  constexpr int LPS = C / 2;
+  floatx4 top[N], bot[N];
+  float wt[N], wb[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const Geom g = geom_round<LPS>(own, R0 + i);
+    const int X = g.x0 + tx;
+    const unsigned ox = (unsigned)X < (unsigned)W ? (unsigned)X * (unsigned)(C * 4) : kAxisOut;
+    const unsigned yrow = vbase + (unsigned)g.y0 * rowb;
+    const unsigned oa = (unsigned)g.y0 < (unsigned)H ? yrow : kAxisOut;
+    const unsigned ob = (unsigned)(g.y0 + 1) < (unsigned)H ? yrow + rowb : kAxisOut;
+    top[i] = buf_load_f32x4(rsrc, oa + ox);
+    bot[i] = buf_load_f32x4(rsrc, ob + ox);
+    const float wx = tx ? g.fx : 1.f - g.fx;
+    wt[i] = (1.f - g.fy) * wx;  // grid_sample: (y weight) * (x weight)
+    wb[i] = g.fy * wx;
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    float acc = 0.f;
+    acc = acc + fmaf(bot[i][0], wb[i], top[i][0] * wt[i]) * r4.x;
+    acc = acc + fmaf(bot[i][1], wb[i], top[i][1] * wt[i]) * r4.y;
+    acc = acc + fmaf(bot[i][2], wb[i], top[i][2] * wt[i]) * r4.z;
+    acc = acc + fmaf(bot[i][3], wb[i], top[i][3] * wt[i]) * r4.w;
+    part[R0 + i] = acc;
+  }
+}
+
+// Butterfly reduce-scatter over a lane group (xor LPS/2 ... 1): lane k ends with slot k's sum.
+template <int LPS>
+__device__ __forceinline__ float reduce_scatter(const float* p, int k) {
+  float q[LPS];
+#pragma unroll
+  for (int i = 0; i < LPS; ++i) q[i] = p[i];
+  if constexpr (LPS >= 8) {
+    const bool hi = (k & 4) != 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float keep = hi ? q[4 + i] : q[i], send = hi ? q[i] : q[4 + i];
+      q[i] = keep + lane_xor_f<4>(send);
+    }
+  }
+  if constexpr (LPS >= 4) {
+    const bool hi = (k & 2) != 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float keep = hi ? q[2 + i] : q[i], send = hi ? q[i] : q[2 + i];
+      q[i] = keep + lane_xor_f<2>(send);
+    }
+  }
+  if constexpr (LPS >= 2) {
+    const bool hi = (k & 1) != 0;
+    const float keep = hi ? q[1] : q[0], send = hi ? q[0] : q[1];
+    q[0] = keep + lane_xor_f<1>(send);
+  }
+  return q[0];
+}
+
+template <int C, int D, bool PARTIAL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void warp_pair_kernel(
+    const float* __restrict__ ref, const float* __restrict__ src, const float* __restrict__ hyp,
+    const float* __restrict__ vw_in, float* __restrict__ sim_out, float* __restrict__ wsum_out, int V, int H, int W,
+    int vw_shift, int vw_offset, WarpArgs args) {
+  constexpr int NQ = C / 4;             // channel quads
+  constexpr int LPS = 2 * NQ;           // lanes per pixel: (tap column, quad)
+  constexpr int SPW = 64 / LPS, PIX = 4 * SPW, DPT = D / LPS;
+  static_assert(C == 8 || C == 16, "row-pair layout for 8 or 16 channels");
+  static_assert(D % LPS == 0, "D must be a multiple of the lanes per pixel");
+  __shared__ float dep_lds[DPT][256];
+  __shared__ float acc_lds[DPT][256];
+  const int tid = threadIdx.x;
+  const int HW = H * W;
+  const int nblk = (HW + PIX - 1) / PIX;
+  const int tile = xcd_remap(blockIdx.x, nblk);
+  const int lane = tid & 63;
+  const int k = lane % LPS, tx = k / NQ, q = k % NQ;
+  int p = tile * PIX + (tid >> 6) * SPW + lane / LPS;
+  const bool active = p < HW;
+  if (!active) p = HW - 1;
+  const int py = p / W, px = p - py * W;
+  const float fxp = (float)px, fyp = (float)py;
+  const float4 r4 = *reinterpret_cast<const float4*>(ref + (size_t)p * C + 4 * q);
+#pragma unroll
+  for (int j = 0; j < DPT; ++j) {
+    dep_lds[j][tid] = hyp[(size_t)(j * LPS + k) * HW + p];
+    acc_lds[j][tid] = 0.f;
+  }
+  const float halfw = (float)(W - 1) / 2.f;
+  const float halfh = (float)(H - 1) / 2.f;
+  const int Ws = W >> vw_shift, Hs = H >> vw_shift;
+  const float* wv = vw_in + (size_t)vw_offset * Hs * Ws + (py >> vw_shift) * Ws + (px >> vw_shift);
+  float wsum = PARTIAL ? 0.f : 1e-5f;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, V * HW * C * 4, kRsrcWord3);
+  const unsigned rowb = (unsigned)W * C * 4;
+  for (int v = 0; v < V; ++v) {
+    const float* R = args.proj[v];
+    const float rx = fmaf(R[1], fyp, R[0] * fxp) + R[2];
+    const float ry = fmaf(R[5], fyp, R[4] * fxp) + R[6];
+    const float rz = fmaf(R[9], fyp, R[8] * fxp) + R[10];
+    const unsigned vbase = (unsigned)(v * HW * C * 4 + 16 * q);
+    const float w = wv[(size_t)v * Hs * Ws];
+#pragma unroll 1
+    for (int j = 0; j < DPT; ++j) {
+      Geom own;
+      project(rx, ry, rz, R[3], R[7], R[11], dep_lds[j][tid], halfw, halfh, own.x0, own.y0, own.fx, own.fy);
+      float part[LPS];
+      pair_rounds<C, 0, (LPS < 4 ? LPS : 4)>(rsrc, vbase, rowb, W, H, own, r4, tx, part);
+      if constexpr (LPS == 8) {
+        __builtin_amdgcn_sched_barrier(0);
+        pair_rounds<C, 4, 4>(rsrc, vbase, rowb, W, H, own, r4, tx, part);
+      }
+      float tot = reduce_scatter<LPS>(part, k);
+      acc_lds[j][tid] = acc_lds[j][tid] + (tot * (1.f / (float)C)) * w;
+    }
+    wsum = wsum + w;
+  }
+  if (!active) return;
+#pragma unroll 4
+  for (int j = 0; j < DPT; ++j) {
+    const size_t o = (size_t)(j * LPS + k) * HW + p;
+    sim_out[o] = PARTIAL ? acc_lds[j][tid] : acc_lds[j][tid] / wsum;
+  }
+  if (PARTIAL && k == 0) wsum_out[p] = wsum;
+}
+
 template <int C, int D, bool PW, bool PARTIAL>
 static int launch_warp(const float* ref, const float* src, const float* hyp, const float* vw_in, float* sim,
                        float* wsum, float* vw_out, int V, int H, int W, int vw_shift, int vw_offset, int vw_total,
                        const WarpArgs& args, hipStream_t st) {
+  if constexpr ((C == 8 || C == 16) && !PW) {
+    constexpr int PIXP = 4 * (64 / (C / 2));
+    const int nblk = (H * W + PIXP - 1) / PIXP;
+    hipLaunchKernelGGL((warp_pair_kernel<C, D, PARTIAL>), dim3(nblk), dim3(256), 0, st, ref, src, hyp, vw_in, sim,
+                       wsum, V, H, W, vw_shift, vw_offset, args);
+    TMVS_CHECK_LAUNCH();
+    return TMVS_OK;
+  }
   constexpr int PIX = 4 * (64 / (C / 4));
   const int nblk = (H * W + PIX - 1) / PIX;
   hipLaunchKernelGGL((warp_corr_kernel<C, D, PW, PARTIAL>), dim3(nblk), dim3(256), 0, st, ref, src, hyp, vw_in, sim,
