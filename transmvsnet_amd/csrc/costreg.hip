@@ -627,6 +627,94 @@ static int launch_conv(const float* x, const float* w, const float* al, const fl
   return TMVS_OK;
 }
 
+// ---------------------------------------------------------------- conv1: 8 -> 16, stride 2
+// Direct kernel with tap pairs: with 8 input channels a per-tap B fragment is 2 channels
+// (8 bytes) per lane, and a 64-lane load moves 512 bytes for a full address-unit cost. Here
+// the 27 taps are taken in pairs (a, b): lanes kgrp 0/1 load channel quads 0/1 of tap a,
+// lanes 2/3 of tap b, one 16-byte load each; MFMA j then contracts k = (tap, quad) over
+// channel j of each quad, and the A fragments are laid out to match. Same MFMA count (the
+// 14th pair is half empty), half the load instructions.
+template <int NBW>
+__global__ __launch_bounds__(256) void conv3d_s2c8_pairs_kernel(const float* __restrict__ x,
+                                                                const float* __restrict__ wpk,
+                                                                const float* __restrict__ alpha,
+                                                                const float* __restrict__ shift,
+                                                                float* __restrict__ y, Geo g, int n_tasks) {
+  constexpr int CIN = 8, COUT = 16;
+  const int lane = threadIdx.x & 63;
+  const int task = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  if (task >= n_tasks) return;
+  int t = task;
+  const int nws = (g.Wo + 15) / 16;
+  const int wseg = t % nws;
+  t /= nws;
+  const int nhg = (g.Ho + NBW - 1) / NBW;
+  const int hg = t % nhg;
+  t /= nhg;
+  const int od = t % g.Do;
+  const int n = t / g.Do;
+  const int col = lane & 15, kgrp = lane >> 4;
+  const int half = kgrp & 1, side = kgrp >> 1;  // channel quad, tap of the pair
+  const int ow = wseg * 16 + col;
+  const size_t in_n = (size_t)n * g.Di * g.Hi * g.Wi;
+  floatx4 acc[NBW];
+#pragma unroll
+  for (int r = 0; r < NBW; ++r) acc[r] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+  for (int pr = 0; pr < 14; ++pr) {
+    const int tap = 2 * pr + side;            // 27 = the empty second half of pair 13
+    const bool real = tap < 27;
+    const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+    const int id = od * 2 - 1 + kd;
+    const int iw = ow * 2 - 1 + kw;
+    const bool dwok = real && id >= 0 && id < g.Di && iw >= 0 && iw < g.Wi && ow < g.Wo;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (real) a = *reinterpret_cast<const float4*>(wpk + ((size_t)tap * COUT + col) * CIN + 4 * half);
+    float4 b[NBW];
+#pragma unroll
+    for (int r = 0; r < NBW; ++r) {
+      const int oh = hg * NBW + r;
+      const int ih = oh * 2 - 1 + kh;
+      b[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (dwok && oh < g.Ho && ih >= 0 && ih < g.Hi)
+        b[r] = *reinterpret_cast<const float4*>(x + (in_n + ((size_t)id * g.Hi + ih) * g.Wi + iw) * CIN + 4 * half);
+    }
+#pragma unroll
+    for (int r = 0; r < NBW; ++r) {
+      acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[r].x, acc[r], 0, 0, 0);
+      acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[r].y, acc[r], 0, 0, 0);
+      acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[r].z, acc[r], 0, 0, 0);
+      acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[r].w, acc[r], 0, 0, 0);
+    }
+  }
+  if (ow >= g.Wo) return;
+  const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
+  const int co = kgrp * 4;
+  const float4 al = *reinterpret_cast<const float4*>(alpha + co);
+  const float4 sh = *reinterpret_cast<const float4*>(shift + co);
+#pragma unroll
+  for (int r = 0; r < NBW; ++r) {
+    const int oh = hg * NBW + r;
+    if (oh >= g.Ho) continue;
+    float4 o;
+    o.x = relu(fmaf(acc[r][0], al.x, sh.x));
+    o.y = relu(fmaf(acc[r][1], al.y, sh.y));
+    o.z = relu(fmaf(acc[r][2], al.z, sh.z));
+    o.w = relu(fmaf(acc[r][3], al.w, sh.w));
+    *reinterpret_cast<float4*>(y + (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co) = o;
+  }
+}
+
+template <int NBW>
+static int launch_conv_s2c8_pairs(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
+                                  const Geo& g, hipStream_t st) {
+  const long n_tasks = (long)B * g.Do * ((g.Ho + NBW - 1) / NBW) * ((g.Wo + 15) / 16);
+  const int nblk = (int)((n_tasks + 3) / 4);
+  hipLaunchKernelGGL((conv3d_s2c8_pairs_kernel<NBW>), dim3(nblk), dim3(256), 0, st, x, w, al, sh, y, g, (int)n_tasks);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
 template <int CIN, int COUT, int S, int NBW, int MBW>
 static int launch_conv_direct(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
                               const Geo& g, hipStream_t st) {
@@ -674,6 +762,8 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
   TMVS_CONV_LDS(32, 32, 8, 2)
   TMVS_CONV_LDS(64, 64, 8, 2)
 #undef TMVS_CONV_LDS
+  // stride 2, 8 -> 16 (full-resolution input): tap pairs, 16-byte loads
+  if (cin == 8 && cout == 16 && stride == 2) return launch_conv_s2c8_pairs<4>(x, wpk, al, sh, y, B, g, st);
   // stride 2: direct
 #define TMVS_CONV_DIRECT(CI, CO, NBW, MBW) \
   if (cin == CI && cout == CO && stride == 2) return launch_conv_direct<CI, CO, 2, NBW, MBW>(x, wpk, al, sh, y, B, g, st);
