@@ -231,6 +231,7 @@ __device__ __forceinline__ void load_token_frag(const float* __restrict__ row, f
 
 constexpr int kTilesPerWave = 8;  // 16-token tiles per wave (kv): amortises the weight-fragment loads
 constexpr int kApplyTilesPerWave = 4;  // apply: weights come from LDS; more, shorter waves
+constexpr int kKvTilesPerWave = 8;     // kv: more tiles per wave keeps the partial slabs (and the combine) small
 
 // (KV, Ksum) partial sums: per wave, tiles of 16 source tokens; K, V by MFMA; per lane the
 // two heads it owns are accumulated over its tokens, then summed over the 16 token lanes.
@@ -238,12 +239,12 @@ __global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __rest
                                                               const float* __restrict__ w,
                                                               float* __restrict__ partial) {
   __shared__ float red[4][kKV];
+  __shared__ __attribute__((aligned(16))) float frag[2 * 32 * 32];  // Wk, Wv fragments (see stage_afrag)
   const int v = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4;
-  float wk[2][8], wvv[2][8];
-  load_afrag<32, 32, true>(w + TMVS_ENC_WK, wk, lane);
-  load_afrag<32, 32, true>(w + TMVS_ENC_WV, wvv, lane);
+  stage_afrag<32, 32, true>(w + TMVS_ENC_WK, frag);
+  stage_afrag<32, 32, true>(w + TMVS_ENC_WV, frag + 1024);
   float bk[2][4], bv[2][4];
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb)
@@ -260,23 +261,26 @@ __global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __rest
 #pragma unroll
     for (int i = 0; i < 4; ++i) ks[mb][i] = 0.f;
   }
+  __syncthreads();
   const float* sv = src + (size_t)v * S * kD;
-  const int tile0 = (blockIdx.x * 4 + wv) * kTilesPerWave;
+  const int tile0 = (blockIdx.x * 4 + wv) * kKvTilesPerWave;
 #pragma unroll 1
-  for (int it = 0; it < kTilesPerWave; it += 2) {
+  for (int it = 0; it < kKvTilesPerWave; ++it) {
     if ((tile0 + it) * 16 >= S) break;  // wave-uniform
-    bool okp[2];
-    floatx4 xin[2][2], kk[2][2], vv[2][2];
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int t = (tile0 + it + p) * 16 + (lane & 15);
-      okp[p] = t < S;
-      load_token_frag(sv + (size_t)(okp[p] ? t : S - 1) * kD, xin[p], lane);
+    int salt = 0;  // opaque offset: fragment reads stay in the loop (not hoisted back into VGPRs)
+    asm volatile("" : "+v"(salt));
+    const float* fr = frag + salt;
+    bool okp[1];
+    floatx4 xin[1][2], kk[1][2], vv[1][2];
+    {
+      const int t = (tile0 + it) * 16 + (lane & 15);
+      okp[0] = t < S;
+      load_token_frag(sv + (size_t)(okp[0] ? t : S - 1) * kD, xin[0], lane);
     }
-    mfma_linear_n<32, 32, 2>(wk, xin, kk);
-    mfma_linear_n<32, 32, 2>(wvv, xin, vv);
+    mfma_linear_lds<32, 32, 1>(fr, xin, kk, lane);
+    mfma_linear_lds<32, 32, 1>(fr + 1024, xin, vv, lane);
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
+    for (int p = 0; p < 1; ++p)
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
       const bool ok = okp[p];
@@ -444,7 +448,7 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
   }
 }
 
-static int kv_nblk(int S) { return (S + 16 * 4 * kTilesPerWave - 1) / (16 * 4 * kTilesPerWave); }
+static int kv_nblk(int S) { return (S + 16 * 4 * kKvTilesPerWave - 1) / (16 * 4 * kKvTilesPerWave); }
 static int apply_nblk(int L) { return (L + 16 * 4 * kApplyTilesPerWave - 1) / (16 * 4 * kApplyTilesPerWave); }
 
 }  // namespace tmvs
