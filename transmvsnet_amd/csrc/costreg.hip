@@ -462,87 +462,91 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
 constexpr int kDChunk = 8;  // depth planes per thread in the full-resolution VALU convs
 
 // ---------------------------------------------------------------- conv0: Cin=1 -> 8, VALU
-// One thread per (h, w) column walks D; every input plane's 3x3 window is loaded once and
-// kept in a 3-plane ring, so each output sees its taps in (kd, kh, kw) order. Window loads are
-// unconditional buffer loads (padding taps get an out-of-range offset and read 0), so the
-// compiler cannot turn them into serialised branches.
+// A thread owns 4 W-adjacent pixels (a 4-pixel group never straddles a row: W % 8 == 0) and
+// walks D with a 3-plane ring of their 3x6 input windows, so every scalar-loaded weight feeds 4
+// FMAs (one weight load per output per pixel left the kernel waiting on scalar memory).
+// Each output still sees its taps in (kd, kh, kw) order. Window loads are unconditional buffer
+// loads (padding taps get an out-of-range offset and read 0). Outputs leave through LDS as
+// contiguous 1 KiB rows.
+constexpr int kPx = 2;  // pixels per thread (conv0 / prob)
+
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, float* __restrict__ y, int D, int H,
                                                     int W, const float* __restrict__ wt,
                                                     const float* __restrict__ alpha,
                                                     const float* __restrict__ shift) {
-  __shared__ __attribute__((aligned(16))) float stage[4 * 64 * 8];
+  __shared__ __attribute__((aligned(16))) float stage[4][64 * kPx * 8];  // per wave: 256 voxels x 8 ch
   const int HW = H * W;
-  // 1-D grid: logical block = (n, depth chunk, pixel chunk), pixel chunk fastest; remapped so
-  // that each XCD owns a contiguous range (the 3x3 row halo is then read from one L2)
-  const int npx = (HW + 255) / 256, ndc = (D + kDChunk - 1) / kDChunk;
-  int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int npx = (HW + 256 * kPx - 1) / (256 * kPx), ndc = (D + kDChunk - 1) / kDChunk;
+  int lb = xcd_remap(blockIdx.x, gridDim.x);  // contiguous pixel ranges per XCD: row halos share an L2
   const int pc = lb % npx;
   lb /= npx;
   const int dc = lb % ndc;
   const int n = lb / ndc;
-  const int pw0 = pc * 256 + (threadIdx.x & ~63);  // first pixel of this wave
-  if (pw0 >= HW) return;                            // whole wave out of range
-  const bool full_wave = pw0 + 64 <= HW;
-  const int p = min(pc * 256 + (int)threadIdx.x, HW - 1);  // tail lanes compute a duplicate, store nothing
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int pw0 = pc * 256 * kPx + wv * 64 * kPx;  // first pixel of this wave
+  if (pw0 >= HW) return;                           // whole wave out of range
+  const int p = min(pw0 + lane * kPx, HW - kPx);   // tail lanes duplicate, store nothing
   const int d0 = dc * kDChunk, d1 = min(D, d0 + kDChunk);
   const int h = p / W, w = p - h * W;
   const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)n * D * HW, (unsigned)(D * HW * 4));
   float* ybase = y + (size_t)n * D * HW * 8;
-  // per-axis byte offsets; an invalid axis makes the sum out of range
-  unsigned offw[3], offh[3];
+  unsigned offw[kPx + 2], offh[3];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    offw[k] = (unsigned)(w - 1 + k) < (unsigned)W ? (unsigned)(w - 1 + k) * 4u : kOffOut;
-    offh[k] = (unsigned)(h - 1 + k) < (unsigned)H ? (unsigned)((h - 1 + k) * W) * 4u : kOffOut;
-  }
-  auto load_plane = [&](int d, float* o) {
+  for (int k = 0; k < kPx + 2; ++k) offw[k] = (unsigned)(w - 1 + k) < (unsigned)W ? (unsigned)(w - 1 + k) * 4u : kOffOut;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) offh[k] = (unsigned)(h - 1 + k) < (unsigned)H ? (unsigned)((h - 1 + k) * W) * 4u : kOffOut;
+  auto load_plane = [&](int d, float (&o)[3][kPx + 2]) {
     const unsigned offd = (unsigned)d < (unsigned)D ? (unsigned)d * (unsigned)HW * 4u : kOffOut;
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const unsigned off = offd | offh[kh] | offw[kw];  // any kOffOut term keeps the top bit
-        o[kh * 3 + kw] = buf_load_f32(rx, (offd + offh[kh] + offw[kw]) | (off & kOffOut));
+      for (int k = 0; k < kPx + 2; ++k) {
+        const unsigned off = offd | offh[kh] | offw[k];  // any out-of-range term keeps the top bit
+        o[kh][k] = buf_load_f32(rx, (offd + offh[kh] + offw[k]) | (off & kOffOut));
       }
   };
-  float win[3][9];
+  float win[3][3][kPx + 2];
   load_plane(d0 - 1, win[0]);
   load_plane(d0, win[1]);
+  float* st = stage[wv];
   for (int d = d0; d < d1; ++d) {
     load_plane(d + 1, win[2]);
-    float acc[8];
-#pragma unroll 2
+    // channel loop not unrolled: one channel's 27 weights fit in SGPRs; results go straight
+    // to the wave's LDS staging rows
+#pragma unroll 1
     for (int c = 0; c < 8; ++c) {
-      float a = 0.f;
+      float a[kPx];
+#pragma unroll
+      for (int q = 0; q < kPx; ++q) a[q] = 0.f;
 #pragma unroll
       for (int kd = 0; kd < 3; ++kd)
 #pragma unroll
-        for (int t = 0; t < 9; ++t) a = fmaf(wt[c * 27 + kd * 9 + t], win[kd][t], a);
-      acc[c] = relu(fmaf(a, alpha[c], shift[c]));
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const float wv_ = wt[c * 27 + kd * 9 + kh * 3 + kw];
+#pragma unroll
+            for (int q = 0; q < kPx; ++q) a[q] = fmaf(wv_, win[kd][kh][q + kw], a[q]);
+          }
+      const float al = alpha[c], sh = shift[c];
+#pragma unroll
+      for (int q = 0; q < kPx; ++q) st[(lane * kPx + q) * 8 + c] = relu(fmaf(a[q], al, sh));
     }
-    // store through LDS: the wave's 64 voxels x 32 B leave as two fully contiguous 1 KiB
-    // stores (every 4-lane quad writes 64 consecutive bytes)
-    float* st = stage + (threadIdx.x >> 6) * 64 * 8;
-    const int lane = threadIdx.x & 63;
-    *reinterpret_cast<float4*>(st + lane * 8) = make_float4(acc[0], acc[1], acc[2], acc[3]);
-    *reinterpret_cast<float4*>(st + lane * 8 + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
-    __builtin_amdgcn_wave_barrier();
-    const float4 s0 = *reinterpret_cast<const float4*>(st + lane * 4);
-    const float4 s1 = *reinterpret_cast<const float4*>(st + 256 + lane * 4);
     __builtin_amdgcn_wave_barrier();
     float* wbase = ybase + ((size_t)d * HW + pw0) * 8;
-    if (full_wave) {
-      *reinterpret_cast<float4*>(wbase + lane * 4) = s0;
-      *reinterpret_cast<float4*>(wbase + 256 + lane * 4) = s1;
-    } else {
-      if (pw0 + (lane >> 1) < HW) *reinterpret_cast<float4*>(wbase + lane * 4) = s0;
-      if (pw0 + 32 + (lane >> 1) < HW) *reinterpret_cast<float4*>(wbase + 256 + lane * 4) = s1;
-    }
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      win[0][t] = win[1][t];
-      win[1][t] = win[2][t];
+    for (int s = 0; s < 2 * kPx; ++s) {
+      const float4 v = *reinterpret_cast<const float4*>(st + s * 256 + lane * 4);
+      if (pw0 + s * 32 + (lane >> 1) < HW) *reinterpret_cast<float4*>(wbase + s * 256 + lane * 4) = v;
     }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int k = 0; k < kPx + 2; ++k) {
+        win[0][kh][k] = win[1][kh][k];
+        win[1][kh][k] = win[2][kh][k];
+      }
   }
 }
 
@@ -1006,8 +1010,8 @@ extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height,
   const int D2 = D1 / 2, H2 = H1 / 2, W2 = W1 / 2;
   const int D3 = D2 / 2, H3 = H2 / 2, W3 = W2 / 2;
   int rc;
-  const dim3 g0((unsigned)(((H0 * W0 + 255) / 256) * batch * ((D0 + kDChunk - 1) / kDChunk)));
-  hipLaunchKernelGGL(conv0_kernel, g0, dim3(256), 0, st, x, c0, D0, H0, W0, w->w[0], w->alpha[0], w->shift[0]);
+  const dim3 g0x((unsigned)(((H0 * W0 + 256 * kPx - 1) / (256 * kPx)) * batch * ((D0 + kDChunk - 1) / kDChunk)));
+  hipLaunchKernelGGL(conv0_kernel, g0x, dim3(256), 0, st, x, c0, D0, H0, W0, w->w[0], w->alpha[0], w->shift[0]);
   TMVS_CHECK_LAUNCH();
   if ((rc = conv_dispatch(c0, batch, c, D0, H0, W0, w->w[1], w->alpha[1], w->shift[1], 2 * c, 2, c1, st))) return rc;
   if ((rc = conv_dispatch(c1, batch, 2 * c, D1, H1, W1, w->w[2], w->alpha[2], w->shift[2], 2 * c, 1, c2, st)))
@@ -1026,7 +1030,8 @@ extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height,
     return rc;
   if ((rc = deconv_dispatch(x9, batch, 2 * c, D1, H1, W1, w->w[9], w->alpha[9], w->shift[9], c, c0, x11, st)))
     return rc;
-  hipLaunchKernelGGL(prob_kernel, g0, dim3(256), 0, st, x11, logits, D0, H0, W0, w->w[10]);
+  const dim3 g1((unsigned)(((H0 * W0 + 255) / 256) * batch * ((D0 + kDChunk - 1) / kDChunk)));
+  hipLaunchKernelGGL(prob_kernel, g1, dim3(256), 0, st, x11, logits, D0, H0, W0, w->w[10]);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
