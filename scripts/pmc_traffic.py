@@ -4,9 +4,10 @@
 
 Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half the bytes of a
 16 B/lane read, so bytes_read = 2 x FETCH_SIZE; WRITE_SIZE is exact for 16 B/lane stores. Both
-counters are in KiB. The passes run bench.py with --steps 2 --warmup 1 --profile-steps 0, i.e.
-3 forward steps; traffic per depth map = sum over one step's dispatches of the kernels behind
-one C-ABI entry point (the same grouping as bench.py's HIP-event `achieved`).
+counters are in KiB. The passes run bench.py with --steps 2 --warmup 1 --profile-steps 0 (3
+forward steps, counted by fmt_embed_kernel dispatches); traffic per depth map = sum over one
+step's dispatches of the kernels behind one C-ABI entry point (the same grouping as bench.py's
+HIP-event `achieved`).
 """
 import csv
 import json
@@ -15,23 +16,28 @@ import sys
 from collections import defaultdict
 
 ENTRY_KERNELS = {
-    "tmvs_warp_corr": ("warp_corr_kernel",),
-    "tmvs_costregnet": ("conv0_kernel", "conv3d_lds_kernel", "conv3d_direct_kernel", "deconv3d_lds_kernel",
-                        "prob_kernel"),
+    "tmvs_warp_corr": ("warp_corr_kernel", "warp_pair_kernel"),
+    "tmvs_costregnet": ("conv0_kernel", "conv3d_lds_kernel", "conv3d_direct_kernel", "conv3d_s2c8_pairs_kernel",
+                        "deconv3d_lds_kernel", "deconv3d_c8_kernel", "prob_kernel"),
 }
+STEP_KERNEL = "fmt_embed_kernel"  # launched exactly once per forward step
+
+
+def _is(kname, n):
+    return kname.startswith(n) or f"::{n}" in kname
 
 
 def load(path):
     per = defaultdict(float)
-    n_warp = 0
+    steps = 0
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"]
         for entry, names in ENTRY_KERNELS.items():
-            if any(k.startswith(n) or f"::{n}" in k for n in names):
+            if any(_is(k, n) for n in names):
                 per[entry] += float(r["Counter_Value"]) * 1024.0
-        if k.startswith("warp_corr_kernel") or "::warp_corr_kernel" in k:
-            n_warp += 1
-    return per, n_warp // 3
+        if _is(k, STEP_KERNEL):
+            steps += 1
+    return per, max(steps, 1)
 
 
 def main():
