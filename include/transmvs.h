@@ -102,9 +102,10 @@ int tmvs_homo_warping(const float* src_fea, const float* proj, const float* hyp,
  * per-channel (alpha, shift) epilogue (tmvs_bn_fold). Weight packing ("packed" below):
  *   Conv3d weight [Co][Ci][3][3][3]          -> [27][Co][Ci]  (tap = kd*9+kh*3+kw)
  *   ConvTranspose3d weight [Ci][Co][3][3][3] -> [27][Co][Ci]
- * conv0 (Ci=1) and prob (Co=1) keep their natural [Co][Ci][27] order.                     */
+ * conv0 (Ci=1) keeps its natural [Co][27] order. prob (Co=1, Ci=C) is packed per kh row:
+ *   [kh][ {W[c][kd=1][kh][kw], W[c][kd=2][kh][kw]} for (kw, c) | W[c][kd=0][kh][kw] for (kw, c) ]  */
 typedef struct {
-  const float* w[11];      /* conv0..conv6, conv7, conv9, conv11 (packed), prob [1][8][27]  */
+  const float* w[11];      /* conv0..conv6, conv7, conv9, conv11 (packed), prob [3][72]     */
   const float* alpha[10];  /* BN alpha of the first 10 layers                              */
   const float* shift[10];  /* BN shift                                                     */
   int base_ch;             /* cr_base_chs (models/TransMVSNet.py:115), 8                   */

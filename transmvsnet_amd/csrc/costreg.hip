@@ -551,71 +551,83 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
 }
 
 // ---------------------------------------------------------------- prob: 8 -> 1, VALU
-// One thread per (h, w) column walks D; input plane i (9 taps x 8 channels) is loaded once and
-// feeds outputs i+1 (kd=0), i (kd=1) and i-1 (kd=2) -- each output's FMA chain still runs in
-// (kd, kh, kw, c) order. Loads are pipelined one tap row (3 taps x 8 channels) ahead.
+// A wave owns one (h) row segment of 62 output columns; lane l holds column w0 + l - 1 (lanes
+// 0 and 63 are the kw halo and write nothing). Every input row is one coalesced 32-byte load
+// per lane (the segment's 64 pixels are 2 KB contiguous); the kw = 0 / 2 neighbours come from
+// lanes l -+ 1 by wave-wide DPP shifts instead of re-gathering them (the 3x re-read of the
+// 1-pixel-per-thread form made this kernel address-unit bound). The thread walks D: input plane
+// i (3 rows x 3 taps x 8 channels) feeds outputs i+1 (kd=0), i (kd=1) and i-1 (kd=2), and each
+// output's FMA chain runs in (kd, kh, kw, c) order. The next row's load is issued before the
+// current row is consumed.
+constexpr int kProbCols = 62;
+typedef float float2_v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float lane_from_left(float v) {  // lane l <- lane l-1 (wave_shr:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lane_from_right(float v) {  // lane l <- lane l+1 (wave_shl:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, false));
+}
+
 __global__ __launch_bounds__(256) void prob_kernel(const float* __restrict__ x, float* __restrict__ y, int D, int H,
                                                    int W, const float* __restrict__ wt) {
   const int HW = H * W;
-  const int npx = (HW + 255) / 256, ndc = (D + kDChunk - 1) / kDChunk;
-  int lb = xcd_remap(blockIdx.x, gridDim.x);  // as conv0_kernel
-  const int pc = lb % npx;
-  lb /= npx;
+  const int nseg = (W + kProbCols - 1) / kProbCols, nrow = (H + 3) / 4, ndc = (D + kDChunk - 1) / kDChunk;
+  int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int seg = lb % nseg;
+  lb /= nseg;
+  const int rowb = lb % nrow;
+  lb /= nrow;
   const int dc = lb % ndc;
   const int n = lb / ndc;
-  const int p = pc * 256 + threadIdx.x;
-  if (p >= HW) return;
-  const int h = p / W, w = p - h * W;
+  const int lane = threadIdx.x & 63;
+  const int h = rowb * 4 + (threadIdx.x >> 6);
+  if (h >= H) return;  // whole wave
+  const int w = seg * kProbCols + lane - 1;
+  const bool writes = lane >= 1 && lane <= kProbCols && w < W;
   const int d0 = dc * kDChunk, d1 = min(D, d0 + kDChunk);
   const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)n * D * HW * 8, (unsigned)(D * HW * 32));
-  float* yn = y + (size_t)n * D * HW + p;
-  unsigned offw[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) offw[k] = (unsigned)(w - 1 + k) < (unsigned)W ? (unsigned)(w - 1 + k) * 32u : kOffOut;
-  // tap row (plane i, row offset kh): 3 taps x 8 channels, unconditional buffer loads; planes
-  // outside [0, D) and out-of-image taps get an out-of-range offset and read 0 (fmaf(w, 0, acc) == acc)
-  auto load_row = [&](int i, int kh, float4 (&o)[6]) {
+  float* yn = y + (size_t)n * D * HW + (size_t)h * W + w;
+  const unsigned offw = (unsigned)w < (unsigned)W ? (unsigned)w * 32u : kOffOut;
+  auto load_row = [&](int i, int kh, float4 (&o)[2]) {
     const int ih = h - 1 + kh;
     const unsigned offr = ((unsigned)i < (unsigned)D && (unsigned)ih < (unsigned)H)
                               ? ((unsigned)i * (unsigned)H + (unsigned)ih) * (unsigned)W * 32u
                               : kOffOut;
-#pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      const unsigned off = (offr + offw[kw]) | ((offr | offw[kw]) & kOffOut);
-      const floatx4 u = buf_load_f32x4(rx, off);
-      const floatx4 v = buf_load_f32x4(rx, off + 16u);
-      o[2 * kw] = make_float4(u[0], u[1], u[2], u[3]);
-      o[2 * kw + 1] = make_float4(v[0], v[1], v[2], v[3]);
-    }
+    const unsigned off = (offr + offw) | ((offr | offw) & kOffOut);
+    const floatx4 u = buf_load_f32x4(rx, off);
+    const floatx4 v = buf_load_f32x4(rx, off + 16u);
+    o[0] = make_float4(u[0], u[1], u[2], u[3]);
+    o[1] = make_float4(v[0], v[1], v[2], v[3]);
   };
-  float acc_prev = 0.f, acc_cur = 0.f;  // outputs i-1 (has kd=0,1) and i (has kd=0)
-  float4 cur[6], nxt[6];
+  // c12 = {output i (kd=0 done, adds kd=1), output i-1 (kd=0,1 done, adds kd=2)}: one packed FMA
+  // per (tap, channel) with the weight pair {W[kd=1], W[kd=2]} (an aligned SGPR pair, see the
+  // host packing in include/transmvs.h) and x broadcast; acc_next (output i+1, kd=0) is scalar
+  float2_v c12 = {0.f, 0.f};
+  float4 cur[2], nxt[2];
   load_row(d0 - 1, 0, cur);
   for (int i = d0 - 1; i <= d1; ++i) {  // plane i feeds outputs i-1, i, i+1
-    float acc_next = 0.f;                // output i+1, kd=0 from plane i
-    float c1 = acc_cur, c2 = acc_prev;
-    // kh not unrolled: one row's 72 weights (3 taps x 8 channels x 3 kd) fit in SGPRs
+    float acc_next = 0.f;
 #pragma unroll 1
     for (int kh = 0; kh < 3; ++kh) {
       load_row(kh < 2 ? i : i + 1, kh < 2 ? kh + 1 : 0, nxt);
+      const float xc[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
+      const float* wk = wt + kh * 72;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        const float4 u = cur[2 * kw], v = cur[2 * kw + 1];
-        const float xv[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-        const int t = kh * 3 + kw;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          acc_next = fmaf(wt[c * 27 + t], xv[c], acc_next);
-          c1 = fmaf(wt[c * 27 + 9 + t], xv[c], c1);
-          c2 = fmaf(wt[c * 27 + 18 + t], xv[c], c2);
+          const float xv = kw == 0 ? lane_from_left(xc[c]) : kw == 1 ? xc[c] : lane_from_right(xc[c]);
+          const float2_v wp = *reinterpret_cast<const float2_v*>(wk + 2 * (kw * 8 + c));
+          acc_next = fmaf(wk[48 + kw * 8 + c], xv, acc_next);
+          c12 = __builtin_elementwise_fma(wp, float2_v{xv, xv}, c12);
         }
       }
-#pragma unroll
-      for (int k = 0; k < 6; ++k) cur[k] = nxt[k];
+      cur[0] = nxt[0];
+      cur[1] = nxt[1];
     }
-    if (i - 1 >= d0) yn[(size_t)(i - 1) * HW] = c2;  // output i-1 complete
-    acc_prev = c1;
-    acc_cur = acc_next;
+    if (i - 1 >= d0 && writes) yn[(size_t)(i - 1) * HW] = c12.y;  // output i-1 complete
+    c12 = float2_v{acc_next, c12.x};
   }
 }
 
@@ -1030,7 +1042,7 @@ extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height,
     return rc;
   if ((rc = deconv_dispatch(x9, batch, 2 * c, D1, H1, W1, w->w[9], w->alpha[9], w->shift[9], c, c0, x11, st)))
     return rc;
-  const dim3 g1((unsigned)(((H0 * W0 + 255) / 256) * batch * ((D0 + kDChunk - 1) / kDChunk)));
+  const dim3 g1((unsigned)(((W0 + kProbCols - 1) / kProbCols) * ((H0 + 3) / 4) * batch * ((D0 + kDChunk - 1) / kDChunk)));
   hipLaunchKernelGGL(prob_kernel, g1, dim3(256), 0, st, x11, logits, D0, H0, W0, w->w[10]);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;

@@ -141,7 +141,11 @@ class CostRegNet(nn.Module):
             a, s = ops.bn_fold(blk.bn.weight, blk.bn.bias, blk.bn.running_mean, blk.bn.running_var, blk.bn.eps)
             als.append(torch.from_numpy(a))
             shs.append(torch.from_numpy(s))
-        ws.append(self.prob.weight.detach().float().reshape(self.base_channels, 27).contiguous())
+        # prob [1][C][kd][kh][kw] -> per kh: 24 {kd1, kd2} pairs in (kw, c) order, then 24 kd0 in (kw, c) order
+        pw = self.prob.weight.detach().float().reshape(self.base_channels, 3, 3, 3)
+        pairs = pw[:, 1:3].permute(2, 3, 0, 1).reshape(3, -1)
+        single = pw[:, 0].permute(1, 2, 0).reshape(3, -1)
+        ws.append(torch.cat([pairs, single], 1).contiguous())
         ws = [t.to(device) for t in ws]
         als = [t.to(device) for t in als]
         shs = [t.to(device) for t in shs]
@@ -219,6 +223,10 @@ class TransMVSNet(nn.Module):
         self._prep = None
         self._pe = {}
         self.decomposed = False  # True: one C-ABI call per op (instrumentation); False: native stage calls
+        # the FMT pathway (stage-2/3 features) depends only on the FMT output: run it on a side
+        # stream, concurrently with stage 1 (whose small CostRegNet grids leave the GPU idle)
+        self.overlap_pathway = True
+        self._side = {}
         self.register_load_state_dict_post_hook(lambda m, k: m.invalidate())
 
     def invalidate(self):
@@ -311,23 +319,50 @@ class TransMVSNet(nn.Module):
         n, _, h1, w1 = s1.shape
         tokens = self._fmt(s1, prep)
         st1 = tokens.view(n, h1, w1, 32)
-        st2 = ops.fmt_pathway(st1, s2, prep["red1"], prep["sm1"])
-        st3 = ops.fmt_pathway(st2, s3, prep["red2"], prep["sm2"])
-        nhwc = (st1, st2, st3)
+        overlap = self.overlap_pathway and not self.decomposed
+        lateral = {}
+
+        def pathway():
+            lateral["st2"] = ops.fmt_pathway(st1, s2, prep["red1"], prep["sm1"])
+            lateral["st3"] = ops.fmt_pathway(lateral["st2"], s3, prep["red2"], prep["sm2"])
+
+        def pathway_side():
+            """Launch the pathway on a side stream once stage 1's cost volume is queued, so it runs
+            beside stage 1's CostRegNet (whose 1/16-resolution grids leave most CUs idle)."""
+            main = torch.cuda.current_stream(s1.device)
+            side = self._side.get(s1.device)
+            if side is None:
+                side = self._side[s1.device] = torch.cuda.Stream(s1.device)
+            ready = torch.cuda.Event()
+            ready.record(main)
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                pathway()
+            done = torch.cuda.Event()
+            done.record(side)
+            # allocator bookkeeping: st2/st3 are consumed on the main stream, st1/s2/s3 read on side
+            lateral["st2"].record_stream(main)
+            lateral["st3"].record_stream(main)
+            for t in (st1, s2, s3):
+                t.record_stream(side)
+            lateral["done"] = done
+
+        if not overlap:
+            pathway()
         outputs = {}
         depth_raw = None
         view_w = None
         for s in range(self.num_stage):
             name = f"stage{s + 1}"
-            fs = nhwc[s]
-            if view_shard is None and not self.decomposed:
-                if s == 0:
-                    view_w = torch.empty(1, n - 1, fs.shape[1], fs.shape[2], device=fs.device)
+            if s == 1 and overlap:
+                torch.cuda.current_stream(s1.device).wait_event(lateral["done"])
+            fs = (st1, lateral.get("st2"), lateral.get("st3"))[s]
+            if view_shard is None and not self.decomposed and s > 0:
                 out, depth_raw = ops.depth_stage(dv, depth_raw, fs, self.ndepths[s], self.depth_interals_ratio[s],
-                                                 img_hw, STAGE_SCALES[s], rows[name][0],
-                                                 prep["pw"] if s == 0 else None, view_w, s,
+                                                 img_hw, STAGE_SCALES[s], rows[name][0], None, view_w, s,
                                                  prep["cr"][s][0], DEPTH_CLAMP)
-            else:  # per-op path: view-sharded mode, or per-kernel instrumentation (same kernels)
+            else:  # per-op path: stage 1 (pathway launched between its cost volume and CostRegNet),
+                # view-sharded mode, or per-kernel instrumentation -- the same kernels
                 hyp = ops.stage_hypotheses(dv, depth_raw, self.ndepths[s], self.depth_interals_ratio[s], img_hw,
                                            STAGE_SCALES[s])
                 if view_shard is not None:
@@ -339,6 +374,8 @@ class TransMVSNet(nn.Module):
                                               vw_shift=s)
                 if s == 0:
                     view_w = vw_new
+                    if overlap:
+                        pathway_side()
                 logits = ops.costregnet(sim, prep["cr"][s][0])
                 prob, depth, depth_raw, conf = ops.softmax_wta(logits, hyp, DEPTH_CLAMP)
                 out = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}
