@@ -102,7 +102,7 @@ int tmvs_homo_warping(const float* src_fea, const float* proj, const float* hyp,
  * per-channel (alpha, shift) epilogue (tmvs_bn_fold). Weight packing ("packed" below):
  *   Conv3d weight [Co][Ci][3][3][3]          -> [27][Co][Ci]  (tap = kd*9+kh*3+kw)
  *   ConvTranspose3d weight [Ci][Co][3][3][3] -> [27][Co][Ci]
- * conv0 (Ci=1) keeps its natural [Co][27] order. prob (Co=1, Ci=C) is packed per kh row:
+ * (conv0, Ci=1, is thus [27][Co].) prob (Co=1, Ci=C) is packed per kh row:
  *   [kh][ {W[c][kd=1][kh][kw], W[c][kd=2][kh][kw]} for (kw, c) | W[c][kd=0][kh][kw] for (kw, c) ]  */
 typedef struct {
   const float* w[11];      /* conv0..conv6, conv7, conv9, conv11 (packed), prob [3][72]     */

@@ -462,92 +462,113 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
 constexpr int kDChunk = 8;  // depth planes per thread in the full-resolution VALU convs
 
 // ---------------------------------------------------------------- conv0: Cin=1 -> 8, VALU
-// A thread owns 4 W-adjacent pixels (a 4-pixel group never straddles a row: W % 8 == 0) and
-// walks D with a 3-plane ring of their 3x6 input windows, so every scalar-loaded weight feeds 4
-// FMAs (one weight load per output per pixel left the kernel waiting on scalar memory).
-// Each output still sees its taps in (kd, kh, kw) order. Window loads are unconditional buffer
-// loads (padding taps get an out-of-range offset and read 0). Outputs leave through LDS as
-// contiguous 1 KiB rows.
-constexpr int kPx = 2;  // pixels per thread (conv0 / prob)
+// Same row-segment layout as prob_kernel below: a wave owns 62 output columns of one row, lane l
+// column w0 + l - 1 (lanes 0 / 63 are the kw halo). Each input row is one coalesced dword per
+// lane; kw neighbours come by DPP. The thread walks D with a 3-plane ring of its 3x3 windows;
+// the next plane's raw rows are in flight while an output plane is computed.
+// The 8 output channels are 4 packed pairs: one v_pk_fma per (tap, pair) with the weight pair
+// {W[t][2cp], W[t][2cp+1]} (packing [27][Co]) and the tap value broadcast, the 4 chains
+// interleaved (a dependent v_pk_fma issued back to back stalls a cycle). Every output still
+// sees its taps in (kd, kh, kw) order. A lane stores its voxel's 8 channels (32 bytes): staging
+// them through LDS for lane-contiguous stores measured slower here.
+constexpr int kProbCols = 62;
+typedef float float2_v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float lane_from_left(float v) {  // lane l <- lane l-1 (wave_shr:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lane_from_right(float v) {  // lane l <- lane l+1 (wave_shl:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, false));
+}
 
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, float* __restrict__ y, int D, int H,
                                                     int W, const float* __restrict__ wt,
                                                     const float* __restrict__ alpha,
                                                     const float* __restrict__ shift) {
-  __shared__ __attribute__((aligned(16))) float stage[4][64 * kPx * 8];  // per wave: 256 voxels x 8 ch
   const int HW = H * W;
-  const int npx = (HW + 256 * kPx - 1) / (256 * kPx), ndc = (D + kDChunk - 1) / kDChunk;
-  int lb = xcd_remap(blockIdx.x, gridDim.x);  // contiguous pixel ranges per XCD: row halos share an L2
-  const int pc = lb % npx;
-  lb /= npx;
+  const int nseg = (W + kProbCols - 1) / kProbCols, nrow = (H + 3) / 4, ndc = (D + kDChunk - 1) / kDChunk;
+  int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int seg = lb % nseg;
+  lb /= nseg;
+  const int rowb = lb % nrow;
+  lb /= nrow;
   const int dc = lb % ndc;
   const int n = lb / ndc;
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int pw0 = pc * 256 * kPx + wv * 64 * kPx;  // first pixel of this wave
-  if (pw0 >= HW) return;                           // whole wave out of range
-  const int p = min(pw0 + lane * kPx, HW - kPx);   // tail lanes duplicate, store nothing
+  const int lane = threadIdx.x & 63;
+  const int h = rowb * 4 + (threadIdx.x >> 6);
+  if (h >= H) return;  // whole wave
+  const int w = seg * kProbCols + lane - 1;
+  const bool writes = lane >= 1 && lane <= kProbCols && w < W;
   const int d0 = dc * kDChunk, d1 = min(D, d0 + kDChunk);
-  const int h = p / W, w = p - h * W;
   const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)n * D * HW, (unsigned)(D * HW * 4));
-  float* ybase = y + (size_t)n * D * HW * 8;
-  unsigned offw[kPx + 2], offh[3];
-#pragma unroll
-  for (int k = 0; k < kPx + 2; ++k) offw[k] = (unsigned)(w - 1 + k) < (unsigned)W ? (unsigned)(w - 1 + k) * 4u : kOffOut;
+  float* yp = y + ((size_t)n * D * HW + (size_t)h * W + w) * 8;
+  const unsigned offw = (unsigned)w < (unsigned)W ? (unsigned)w * 4u : kOffOut;
+  unsigned offh[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) offh[k] = (unsigned)(h - 1 + k) < (unsigned)H ? (unsigned)((h - 1 + k) * W) * 4u : kOffOut;
-  auto load_plane = [&](int d, float (&o)[3][kPx + 2]) {
+  auto load_raw = [&](int d, float (&o)[3]) {
     const unsigned offd = (unsigned)d < (unsigned)D ? (unsigned)d * (unsigned)HW * 4u : kOffOut;
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-      for (int k = 0; k < kPx + 2; ++k) {
-        const unsigned off = offd | offh[kh] | offw[k];  // any out-of-range term keeps the top bit
-        o[kh][k] = buf_load_f32(rx, (offd + offh[kh] + offw[k]) | (off & kOffOut));
-      }
+    for (int kh = 0; kh < 3; ++kh) {
+      const unsigned off = offd | offh[kh] | offw;  // any out-of-range term keeps the top bit
+      o[kh] = buf_load_f32(rx, (offd + offh[kh] + offw) | (off & kOffOut));
+    }
   };
-  float win[3][3][kPx + 2];
-  load_plane(d0 - 1, win[0]);
-  load_plane(d0, win[1]);
-  float* st = stage[wv];
-  for (int d = d0; d < d1; ++d) {
-    load_plane(d + 1, win[2]);
-    // channel loop not unrolled: one channel's 27 weights fit in SGPRs; results go straight
-    // to the wave's LDS staging rows
-#pragma unroll 1
-    for (int c = 0; c < 8; ++c) {
-      float a[kPx];
+  auto expand = [&](const float (&r)[3], float (&o)[3][3]) {
 #pragma unroll
-      for (int q = 0; q < kPx; ++q) a[q] = 0.f;
-#pragma unroll
-      for (int kd = 0; kd < 3; ++kd)
-#pragma unroll
-        for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-          for (int kw = 0; kw < 3; ++kw) {
-            const float wv_ = wt[c * 27 + kd * 9 + kh * 3 + kw];
-#pragma unroll
-            for (int q = 0; q < kPx; ++q) a[q] = fmaf(wv_, win[kd][kh][q + kw], a[q]);
-          }
-      const float al = alpha[c], sh = shift[c];
-#pragma unroll
-      for (int q = 0; q < kPx; ++q) st[(lane * kPx + q) * 8 + c] = relu(fmaf(a[q], al, sh));
+    for (int kh = 0; kh < 3; ++kh) {
+      o[kh][0] = lane_from_left(r[kh]);
+      o[kh][1] = r[kh];
+      o[kh][2] = lane_from_right(r[kh]);
     }
-    __builtin_amdgcn_wave_barrier();
-    float* wbase = ybase + ((size_t)d * HW + pw0) * 8;
+  };
+  float al[8], sh[8];
 #pragma unroll
-    for (int s = 0; s < 2 * kPx; ++s) {
-      const float4 v = *reinterpret_cast<const float4*>(st + s * 256 + lane * 4);
-      if (pw0 + s * 32 + (lane >> 1) < HW) *reinterpret_cast<float4*>(wbase + s * 256 + lane * 4) = v;
+  for (int c = 0; c < 8; ++c) {
+    al[c] = alpha[c];
+    sh[c] = shift[c];
+  }
+  float win[3][3][3];
+  // one output plane; `raw` holds plane d+1's rows and is refilled with plane d+2's
+  auto step = [&](int d, float (&raw)[3]) {
+    expand(raw, win[2]);
+    load_raw(d + 2, raw);
+    const float* wk = wt;
+    float2_v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+    for (int t = 0; t < 27; ++t) {
+      const float xv = win[t / 9][(t / 3) % 3][t % 3];
+#pragma unroll
+      for (int cp = 0; cp < 4; ++cp)
+        a[cp] = __builtin_elementwise_fma(*reinterpret_cast<const float2_v*>(wk + t * 8 + 2 * cp), float2_v{xv, xv},
+                                          a[cp]);
     }
-    __builtin_amdgcn_wave_barrier();
+    float o[8];
+#pragma unroll
+    for (int cp = 0; cp < 4; ++cp) {
+      o[2 * cp] = relu(fmaf(a[cp].x, al[2 * cp], sh[2 * cp]));
+      o[2 * cp + 1] = relu(fmaf(a[cp].y, al[2 * cp + 1], sh[2 * cp + 1]));
+    }
+    if (writes) {
+      float4* q = reinterpret_cast<float4*>(yp + (size_t)d * HW * 8);
+      q[0] = make_float4(o[0], o[1], o[2], o[3]);
+      q[1] = make_float4(o[4], o[5], o[6], o[7]);
+    }
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-      for (int k = 0; k < kPx + 2; ++k) {
+      for (int k = 0; k < 3; ++k) {
         win[0][kh][k] = win[1][kh][k];
         win[1][kh][k] = win[2][kh][k];
       }
-  }
+  };
+  float ra[3];
+  load_raw(d0 - 1, ra);
+  expand(ra, win[0]);
+  load_raw(d0, ra);
+  expand(ra, win[1]);
+  load_raw(d0 + 1, ra);
+  for (int d = d0; d < d1; ++d) step(d, ra);
 }
 
 // ---------------------------------------------------------------- prob: 8 -> 1, VALU
@@ -559,15 +580,6 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
 // i (3 rows x 3 taps x 8 channels) feeds outputs i+1 (kd=0), i (kd=1) and i-1 (kd=2), and each
 // output's FMA chain runs in (kd, kh, kw, c) order. The next row's load is issued before the
 // current row is consumed.
-constexpr int kProbCols = 62;
-typedef float float2_v __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ float lane_from_left(float v) {  // lane l <- lane l-1 (wave_shr:1)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float lane_from_right(float v) {  // lane l <- lane l+1 (wave_shl:1)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, false));
-}
 
 __global__ __launch_bounds__(256) void prob_kernel(const float* __restrict__ x, float* __restrict__ y, int D, int H,
                                                    int W, const float* __restrict__ wt) {
@@ -902,13 +914,13 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
     g.Wo = (w - 1) / 2 + 1;
   }
   // stride 1: LDS-staged tiles, one output depth slice x 8 rows x 16 columns per workgroup
-#define TMVS_CONV_LDS(CI, CO, TH, MBB)                                                          \
+#define TMVS_CONV_LDS(CI, CO, TD, TH, MBB)                                                      \
   if (cin == CI && cout == CO && stride == 1) {                                               \
-    return launch_conv<CI, CO, 1, 1, TH, MBB>(x, wpk, al, sh, y, B, g, st);                  \
+    return launch_conv<CI, CO, 1, TD, TH, MBB>(x, wpk, al, sh, y, B, g, st);                 \
   }
-  TMVS_CONV_LDS(16, 16, 8, 1)
-  TMVS_CONV_LDS(32, 32, 8, 2)
-  TMVS_CONV_LDS(64, 64, 8, 2)
+  TMVS_CONV_LDS(16, 16, 2, 4, 1)
+  TMVS_CONV_LDS(32, 32, 2, 4, 2)
+  TMVS_CONV_LDS(64, 64, 1, 8, 2)
 #undef TMVS_CONV_LDS
   // stride 2, 8 -> 16 (full-resolution input): tap pairs, 16-byte loads
   if (cin == 8 && cout == 16 && stride == 2) return launch_conv_s2c8_pairs<4>(x, wpk, al, sh, y, B, g, st);
@@ -1022,7 +1034,7 @@ extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height,
   const int D2 = D1 / 2, H2 = H1 / 2, W2 = W1 / 2;
   const int D3 = D2 / 2, H3 = H2 / 2, W3 = W2 / 2;
   int rc;
-  const dim3 g0x((unsigned)(((H0 * W0 + 256 * kPx - 1) / (256 * kPx)) * batch * ((D0 + kDChunk - 1) / kDChunk)));
+  const dim3 g0x((unsigned)(((W0 + kProbCols - 1) / kProbCols) * ((H0 + 3) / 4) * batch * ((D0 + kDChunk - 1) / kDChunk)));
   hipLaunchKernelGGL(conv0_kernel, g0x, dim3(256), 0, st, x, c0, D0, H0, W0, w->w[0], w->alpha[0], w->shift[0]);
   TMVS_CHECK_LAUNCH();
   if ((rc = conv_dispatch(c0, batch, c, D0, H0, W0, w->w[1], w->alpha[1], w->shift[1], 2 * c, 2, c1, st))) return rc;

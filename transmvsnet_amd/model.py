@@ -132,9 +132,7 @@ class CostRegNet(nn.Module):
         for i, n in enumerate(names):
             blk = getattr(self, n)
             w = blk.conv.weight
-            if i == 0:
-                ws.append(w.detach().float().reshape(w.shape[0], 27).contiguous())
-            elif i < 7:
+            if i < 7:
                 ws.append(conv_w(w))
             else:
                 ws.append(deconv_w(w))
