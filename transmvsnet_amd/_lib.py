@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtransmvs_hip.so")
+LIB_PATH = os.environ.get("TMVS_LIB_PATH") or os.path.join(_HERE, "libtransmvs_hip.so")  # override: A/B experiments
 
 P = ctypes.c_void_p
 I = ctypes.c_int

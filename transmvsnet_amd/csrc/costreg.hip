@@ -760,129 +760,188 @@ static int launch_conv_direct(const float* x, const float* w, const float* al, c
 // the two W-parity outputs 2m and 2m+1 of one input column m: for each (d, h) tap the first
 // MFMA group applies kw=1 (rows 0-7) and kw=2 (rows 8-15) to input column m, the second
 // applies kw=0 (rows 8-15 only) to column m+1 -- 8 instead of 12 MFMAs per (d, h) tap and all
-// 64 lanes carry output. Input tile and weights staged in LDS as in deconv3d_lds_kernel.
+// 64 lanes carry output.
+// Persistent: a workgroup stages the 13.8 KB of weights in LDS once and then walks its share
+// of the tiles (restaging them per 4-row tile moved as many bytes as the input itself). Input
+// tiles are double-buffered in LDS -- the next tile's global loads are issued before the
+// current tile's MFMAs and land in the other buffer after them -- and the skip (conv0) rows
+// are requested before the MFMAs too, so neither latency sits between MFMA phases.
+// Tiles are dealt out XCD-contiguously (an XCD's workgroups share one L2: neighbouring tiles
+// share their halo voxels).
 template <int TDI, int THI>
-__global__ __launch_bounds__(256) void deconv3d_c8_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void deconv3d_c8_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                           const float* __restrict__ alpha,
                                                           const float* __restrict__ shift,
                                                           const float* __restrict__ skip, float* __restrict__ y,
-                                                          Geo g) {
+                                                          Geo g, int ntiles) {
   constexpr int CIN = 16, COUT = 8, PL = 4;
   constexpr int NBW = TDI * THI / 4;
   constexpr int LW = 17, LH = THI + 1, LD = TDI + 1, VST = 16;
   constexpr int NVOX = LD * LH * LW;
+  constexpr int NLD = (NVOX * 4 + 255) / 256;  // float4 staging loads per thread and tile
   static_assert((TDI * THI) % 4 == 0, "tile");
-  __shared__ __attribute__((aligned(16))) float tile[NVOX * VST];
+  __shared__ __attribute__((aligned(16))) float tile[2][NVOX * VST];
   __shared__ __attribute__((aligned(16))) float wts[27 * 8 * 16];
   __shared__ __attribute__((aligned(16))) float ep[4][32 * 8];
 
   const int nws = (g.Wi + 15) / 16, nhs = (g.Hi + THI - 1) / THI, nds = (g.Di + TDI - 1) / TDI;
-  int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int ws = t % nws;
-  t /= nws;
-  const int hs = t % nhs;
-  t /= nhs;
-  const int ds = t % nds;
-  const int n = t / nds;
-  const int mw0 = ws * 16, mh0 = hs * THI, md0 = ds * TDI;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int col = lane & 15, kgrp = lane >> 4;
-  const size_t in_n = (size_t)n * g.Di * g.Hi * g.Wi;
-  for (int idx = threadIdx.x; idx < NVOX * 4; idx += 256) {
-    const int vox = idx >> 2, q = idx & 3;
-    const int lw = vox % LW, rest = vox / LW, lh = rest % LH, ld = rest / LH;
-    const int iw = mw0 + lw, ih = mh0 + lh, id = md0 + ld;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (iw < g.Wi && ih < g.Hi && id < g.Di)
-      v = *reinterpret_cast<const float4*>(x + (in_n + ((size_t)id * g.Hi + ih) * g.Wi + iw) * CIN + 4 * q);
-    *reinterpret_cast<float4*>(tile + vox * VST + 4 * (q ^ ((vox >> 1) & 3))) = v;
-  }
+  // XCD-contiguous tile ranges: workgroup b runs on XCD b % 8 (round-robin dispatch)
+  const int nxcd = gridDim.x >= 8 ? 8 : 1, per_xcd = gridDim.x / nxcd;
+  const int xcd = blockIdx.x % nxcd, kx = blockIdx.x / nxcd;
+  const int t_lo = (int)((long)ntiles * xcd / nxcd), t_hi = (int)((long)ntiles * (xcd + 1) / nxcd);
+  if (kx >= per_xcd) return;  // grid not a multiple of 8: the remainder idles
+
+  struct TileCoord {
+    int n, md0, mh0, mw0;
+  };
+  auto coord = [&](int t) {
+    TileCoord c;
+    c.mw0 = (t % nws) * 16;
+    t /= nws;
+    c.mh0 = (t % nhs) * THI;
+    t /= nhs;
+    c.md0 = (t % nds) * TDI;
+    c.n = t / nds;
+    return c;
+  };
+  float4 pf[NLD];
+  auto fetch = [&](int t) {  // global -> registers
+    const TileCoord c = coord(t);
+    const size_t in_n = (size_t)c.n * g.Di * g.Hi * g.Wi;
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int vox = idx >> 2, q = idx & 3;
+      const int lw = vox % LW, rest = vox / LW, lh = rest % LH, ld = rest / LH;
+      const int iw = c.mw0 + lw, ih = c.mh0 + lh, id = c.md0 + ld;
+      pf[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (vox < NVOX && iw < g.Wi && ih < g.Hi && id < g.Di)
+        pf[k] = *reinterpret_cast<const float4*>(x + (in_n + ((size_t)id * g.Hi + ih) * g.Wi + iw) * CIN + 4 * q);
+    }
+  };
+  auto commit = [&](float* buf) {  // registers -> LDS (quad-swizzled voxels)
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int vox = idx >> 2, q = idx & 3;
+      if (vox < NVOX) *reinterpret_cast<float4*>(buf + vox * VST + 4 * (q ^ ((vox >> 1) & 3))) = pf[k];
+    }
+  };
+
   for (int idx = threadIdx.x; idx < 27 * 8 * 4; idx += 256) {
     const int q = idx & 3, row = (idx >> 2) & 7, tap = idx >> 5;
     const float4 v = *reinterpret_cast<const float4*>(wpk + ((size_t)tap * COUT + row) * CIN + 4 * q);
     *reinterpret_cast<float4*>(wts + (tap * 8 + row) * 16 + 4 * (q ^ ((row >> 1) & 3))) = v;
   }
-  __syncthreads();
-
-  const int co = col & 7;         // A row -> output channel
-  const bool hi = col >= 8;       // rows 8-15: the odd-w output
-  floatx4 acc[NBW][4];
-#pragma unroll
-  for (int r = 0; r < NBW; ++r)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[r][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-  auto wfrag = [&](int tap, VecN<PL>& a) {
-    a.load(wts + (tap * 8 + co) * 16 + 4 * (kgrp ^ ((co >> 1) & 3)));
-  };
-#pragma unroll
-  for (int pdh = 0; pdh < 4; ++pdh) {
-    const int pd = pdh >> 1, ph = pdh & 1;
-#pragma unroll
-    for (int td = 0; td < 1 + pd; ++td)
-#pragma unroll
-      for (int th = 0; th < 1 + ph; ++th) {
-        const int kd = pd ? (td ? 2 : 0) : 1, od_off = (pd && !td) ? 1 : 0;
-        const int kh = ph ? (th ? 2 : 0) : 1, oh_off = (ph && !th) ? 1 : 0;
-        const int tap_base = kd * 9 + kh * 3;
-        VecN<PL> a1, a2;
-        wfrag(tap_base + (hi ? 2 : 1), a1);  // rows 0-7: kw=1, rows 8-15: kw=2 (input column m)
-        if (hi)
-          wfrag(tap_base + 0, a2);           // rows 8-15: kw=0 (input column m+1)
-        else
-          a2.zero();
-#pragma unroll
-        for (int r = 0; r < NBW; ++r) {
-          const int rr = wv * NBW + r;
-          const int mdl = rr / THI, mhl = rr - mdl * THI;
-          const int lv = ((mdl + od_off) * LH + mhl + oh_off) * LW + col;
-          VecN<PL> b1, b2;
-          b1.load(tile + lv * VST + 4 * (kgrp ^ ((lv >> 1) & 3)));
-          b2.load(tile + (lv + 1) * VST + 4 * (kgrp ^ (((lv + 1) >> 1) & 3)));
-#pragma unroll
-          for (int j = 0; j < PL; ++j)
-            acc[r][pdh] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.v[j], b1.v[j], acc[r][pdh], 0, 0, 0);
-#pragma unroll
-          for (int j = 0; j < PL; ++j)
-            acc[r][pdh] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2.v[j], b2.v[j], acc[r][pdh], 0, 0, 0);
-        }
-      }
-  }
-  // epilogue: lane (col, kgrp) holds channels 4*(kgrp&1).. of output w 2*(mw0+col) + (kgrp>>1);
-  // exchanged through LDS so the skip read and the store are contiguous 1 KiB rows
-  const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
+  const int co = col & 7;    // A row -> output channel
+  const bool hi = col >= 8;  // rows 8-15: the odd-w output
   float* eb = ep[wv];
   const int cq = 4 * (kgrp & 1);
   const float4 al = *reinterpret_cast<const float4*>(alpha + cq);
   const float4 sh = *reinterpret_cast<const float4*>(shift + cq);
-  const int ow = 2 * mw0 + (lane >> 1);
+  auto wfrag = [&](int tap, VecN<PL>& a) { a.load(wts + (tap * 8 + co) * 16 + 4 * (kgrp ^ ((co >> 1) & 3))); };
+
+  int t = t_lo + kx;
+  if (t < t_hi) {
+    fetch(t);
+    commit(tile[0]);
+  }
+  __syncthreads();
+  for (int it = 0; t < t_hi; t += per_xcd, ++it) {
+    const float* cur = tile[it & 1];
+    const TileCoord c = coord(t);
+    const int tn = t + per_xcd;
+    if (tn < t_hi) fetch(tn);
+    // skip rows of this tile: lane (pair) j of a 1 KiB output row, as the epilogue stores it
+    const size_t out_n = (size_t)c.n * g.Do * g.Ho * g.Wo;
+    const int ow = 2 * c.mw0 + (lane >> 1);
+    const size_t plane = (size_t)g.Ho * g.Wo * 8, row = (size_t)g.Wo * 8;  // output strides (floats)
+    float4 sk[NBW][4];
+    size_t oo[NBW];
+    bool ok[NBW];
 #pragma unroll
-  for (int r = 0; r < NBW; ++r) {
-    const int rr = wv * NBW + r;
-    const int md = md0 + rr / THI, mh = mh0 + rr % THI;
+    for (int r = 0; r < NBW; ++r) {
+      const int rr = wv * NBW + r;
+      const int md = c.md0 + rr / THI, mh = c.mh0 + rr % THI;
+      ok[r] = md < g.Di && mh < g.Hi && ow < 2 * g.Wi;
+      oo[r] = (out_n + ((size_t)(2 * md) * g.Ho + 2 * mh) * g.Wo + ow) * 8 + (lane & 1) * 4;
+#pragma unroll
+      for (int pdh = 0; pdh < 4; ++pdh)
+        sk[r][pdh] = ok[r] ? *reinterpret_cast<const float4*>(skip + oo[r] + (pdh >> 1) * plane + (pdh & 1) * row)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    floatx4 acc[NBW][4];
+#pragma unroll
+    for (int r = 0; r < NBW; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[r][q] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int pdh = 0; pdh < 4; ++pdh) {
-      const floatx4 a = acc[r][pdh];
-      *reinterpret_cast<float4*>(eb + (2 * col + (kgrp >> 1)) * 8 + cq) =
-          make_float4(relu(fmaf(a[0], al.x, sh.x)), relu(fmaf(a[1], al.y, sh.y)), relu(fmaf(a[2], al.z, sh.z)),
-                      relu(fmaf(a[3], al.w, sh.w)));
-      __builtin_amdgcn_wave_barrier();
-      const float4 v = *reinterpret_cast<const float4*>(eb + lane * 4);
-      __builtin_amdgcn_wave_barrier();
-      const int od = 2 * md + (pdh >> 1), oh = 2 * mh + (pdh & 1);
-      if (md < g.Di && mh < g.Hi && ow < 2 * g.Wi) {
-        const size_t o = (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * 8 + (lane & 1) * 4;
-        const float4 s = *reinterpret_cast<const float4*>(skip + o);
-        *reinterpret_cast<float4*>(y + o) = make_float4(s.x + v.x, s.y + v.y, s.z + v.z, s.w + v.w);
-      }
+      const int pd = pdh >> 1, ph = pdh & 1;
+#pragma unroll
+      for (int td = 0; td < 1 + pd; ++td)
+#pragma unroll
+        for (int th = 0; th < 1 + ph; ++th) {
+          const int kd = pd ? (td ? 2 : 0) : 1, od_off = (pd && !td) ? 1 : 0;
+          const int kh = ph ? (th ? 2 : 0) : 1, oh_off = (ph && !th) ? 1 : 0;
+          const int tap_base = kd * 9 + kh * 3;
+          VecN<PL> a1, a2;
+          wfrag(tap_base + (hi ? 2 : 1), a1);  // rows 0-7: kw=1, rows 8-15: kw=2 (input column m)
+          if (hi)
+            wfrag(tap_base + 0, a2);           // rows 8-15: kw=0 (input column m+1)
+          else
+            a2.zero();
+#pragma unroll
+          for (int r = 0; r < NBW; ++r) {
+            const int rr = wv * NBW + r;
+            const int mdl = rr / THI, mhl = rr - mdl * THI;
+            const int lv = ((mdl + od_off) * LH + mhl + oh_off) * LW + col;
+            VecN<PL> b1, b2;
+            b1.load(cur + lv * VST + 4 * (kgrp ^ ((lv >> 1) & 3)));
+            b2.load(cur + (lv + 1) * VST + 4 * (kgrp ^ (((lv + 1) >> 1) & 3)));
+#pragma unroll
+            for (int j = 0; j < PL; ++j)
+              acc[r][pdh] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.v[j], b1.v[j], acc[r][pdh], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < PL; ++j)
+              acc[r][pdh] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2.v[j], b2.v[j], acc[r][pdh], 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);  // one tap's fragments live at a time (VGPR budget)
+        }
     }
+    // epilogue: lane (col, kgrp) holds channels 4*(kgrp&1).. of output w 2*(mw0+col) + (kgrp>>1);
+    // exchanged through LDS so the skip read and the store are contiguous 1 KiB rows
+#pragma unroll
+    for (int r = 0; r < NBW; ++r)
+#pragma unroll
+      for (int pdh = 0; pdh < 4; ++pdh) {
+        const floatx4 a = acc[r][pdh];
+        *reinterpret_cast<float4*>(eb + (2 * col + (kgrp >> 1)) * 8 + cq) =
+            make_float4(relu(fmaf(a[0], al.x, sh.x)), relu(fmaf(a[1], al.y, sh.y)), relu(fmaf(a[2], al.z, sh.z)),
+                        relu(fmaf(a[3], al.w, sh.w)));
+        __builtin_amdgcn_wave_barrier();
+        const float4 v = *reinterpret_cast<const float4*>(eb + lane * 4);
+        __builtin_amdgcn_wave_barrier();
+        const float4 sv = sk[r][pdh];
+        if (ok[r])
+          *reinterpret_cast<float4*>(y + oo[r] + (pdh >> 1) * plane + (pdh & 1) * row) =
+              make_float4(sv.x + v.x, sv.y + v.y, sv.z + v.z, sv.w + v.w);
+      }
+    if (tn < t_hi) commit(tile[(it + 1) & 1]);
+    __syncthreads();
   }
 }
 
 template <int TDI, int THI>
 static int launch_deconv_c8(const float* x, const float* w, const float* al, const float* sh, const float* skip,
                             float* y, int B, const Geo& g, hipStream_t st) {
-  const long nblk = (long)B * ((g.Di + TDI - 1) / TDI) * ((g.Hi + THI - 1) / THI) * ((g.Wi + 15) / 16);
-  hipLaunchKernelGGL((deconv3d_c8_kernel<TDI, THI>), dim3((unsigned)nblk), dim3(256), 0, st, x, w, al, sh, skip, y, g);
+  const long ntiles = (long)B * ((g.Di + TDI - 1) / TDI) * ((g.Hi + THI - 1) / THI) * ((g.Wi + 15) / 16);
+  // 4 resident workgroups per CU (LDS: 2 tiles + weights + epilogue rows)
+  const long grid = std::min<long>(ntiles, 256 * 4);
+  hipLaunchKernelGGL((deconv3d_c8_kernel<TDI, THI>), dim3((unsigned)grid), dim3(256), 0, st, x, w, al, sh, skip, y, g,
+                     (int)ntiles);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
