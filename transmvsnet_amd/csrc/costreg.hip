@@ -643,6 +643,157 @@ __global__ __launch_bounds__(256) void prob_kernel(const float* __restrict__ x, 
   }
 }
 
+// ---------------------------------------------------------------- conv 16 -> 16, stride 1 (conv2)
+// Persistent form of conv3d_lds_kernel for the one stride-1 layer whose weights fit in LDS next
+// to a tile (27 x 16 x 16 fp32 = 27 KB): a workgroup stages them once, then walks its share of
+// 2x4x16-voxel output tiles; the next tile's input is fetched into registers while the
+// current tile's 27 taps run on the MFMAs, and committed to LDS between two barriers.
+// Same fragment layouts, tap order and epilogue as conv3d_lds_kernel.
+template <int TD, int TH>
+__global__ __launch_bounds__(256) void conv3d_c16_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
+                                                         const float* __restrict__ alpha,
+                                                         const float* __restrict__ shift, float* __restrict__ y, Geo g,
+                                                         int ntiles) {
+  constexpr int C = 16, PL = 4, NBW = TD * TH / 4;
+  constexpr int LW = 18, LH = TH + 2, LD = TD + 2, VST = 16;
+  constexpr int NVOX = LD * LH * LW;
+  constexpr int NLD = (NVOX * 4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float tile[NVOX * VST];
+  __shared__ __attribute__((aligned(16))) float wts[27 * 16 * 16];
+  const int nws = (g.Wo + 15) / 16, nhs = (g.Ho + TH - 1) / TH, nds = (g.Do + TD - 1) / TD;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int col = lane & 15, kgrp = lane >> 4;
+  const int nxcd = gridDim.x >= 8 ? 8 : 1, per_xcd = gridDim.x / nxcd;
+  const int xcd = blockIdx.x % nxcd, kx = blockIdx.x / nxcd;
+  const int t_lo = (int)((long)ntiles * xcd / nxcd), t_hi = (int)((long)ntiles * (xcd + 1) / nxcd);
+  if (kx >= per_xcd) return;
+  struct TileCoord {
+    int n, od0, oh0, ow0;
+  };
+  auto coord = [&](int t) {
+    TileCoord c;
+    c.ow0 = (t % nws) * 16;
+    t /= nws;
+    c.oh0 = (t % nhs) * TH;
+    t /= nhs;
+    c.od0 = (t % nds) * TD;
+    c.n = t / nds;
+    return c;
+  };
+  float4 pf[NLD];
+  auto fetch = [&](int t) {
+    const TileCoord c = coord(t);
+    const size_t in_n = (size_t)c.n * g.Di * g.Hi * g.Wi;
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int vox = idx >> 2, q = idx & 3;
+      const int lw = vox % LW, rest = vox / LW, lh = rest % LH, ld = rest / LH;
+      const int iw = c.ow0 - 1 + lw, ih = c.oh0 - 1 + lh, id = c.od0 - 1 + ld;
+      pf[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (vox < NVOX && (unsigned)iw < (unsigned)g.Wi && (unsigned)ih < (unsigned)g.Hi && (unsigned)id < (unsigned)g.Di)
+        pf[k] = *reinterpret_cast<const float4*>(x + (in_n + ((size_t)id * g.Hi + ih) * g.Wi + iw) * C + 4 * q);
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int vox = idx >> 2, q = idx & 3;
+      if (vox < NVOX) *reinterpret_cast<float4*>(tile + vox * VST + 4 * (q ^ ((vox >> 1) & 3))) = pf[k];
+    }
+  };
+  for (int idx = threadIdx.x; idx < 27 * 16 * 4; idx += 256) {
+    const int q = idx & 3, row = (idx >> 2) & 15, tap = idx >> 6;
+    const float4 v = *reinterpret_cast<const float4*>(wpk + ((size_t)tap * C + row) * C + 4 * q);
+    *reinterpret_cast<float4*>(wts + (tap * 16 + row) * 16 + 4 * (q ^ ((row >> 1) & 3))) = v;
+  }
+  const float4 al = *reinterpret_cast<const float4*>(alpha + kgrp * 4);
+  const float4 sh = *reinterpret_cast<const float4*>(shift + kgrp * 4);
+  int t = t_lo + kx;
+  if (t < t_hi) {
+    fetch(t);
+    commit();
+  }
+  __syncthreads();
+  for (; t < t_hi; t += per_xcd) {
+    const TileCoord c = coord(t);
+    const int tn = t + per_xcd;
+    if (tn < t_hi) fetch(tn);
+    floatx4 acc[NBW];
+#pragma unroll
+    for (int r = 0; r < NBW; ++r) acc[r] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 27; ++tap) {
+      const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+      VecN<PL> a;
+      a.load(wts + (tap * 16 + col) * 16 + 4 * (kgrp ^ ((col >> 1) & 3)));
+      VecN<PL> b[NBW];
+#pragma unroll
+      for (int r = 0; r < NBW; ++r) {
+        const int rr = wv * NBW + r;
+        const int odl = rr / TH, ohl = rr - odl * TH;
+        const int lvox = ((odl + kd) * LH + ohl + kh) * LW + col + kw;
+        b[r].load(tile + lvox * VST + 4 * (kgrp ^ ((lvox >> 1) & 3)));
+      }
+#pragma unroll
+      for (int j = 0; j < PL; ++j)
+#pragma unroll
+        for (int r = 0; r < NBW; ++r)
+          acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[j], b[r].v[j], acc[r], 0, 0, 0);
+      if (tap % 9 == 8) __builtin_amdgcn_sched_barrier(0);  // bound the fragments in flight
+    }
+    const int ow = c.ow0 + col;
+    const size_t out_n = (size_t)c.n * g.Do * g.Ho * g.Wo;
+#pragma unroll
+    for (int r = 0; r < NBW; ++r) {
+      const int rr = wv * NBW + r;
+      const int od = c.od0 + rr / TH, oh = c.oh0 + rr % TH;
+      if (ow >= g.Wo || od >= g.Do || oh >= g.Ho) continue;
+      float4 o;
+      o.x = relu(fmaf(acc[r][0], al.x, sh.x));
+      o.y = relu(fmaf(acc[r][1], al.y, sh.y));
+      o.z = relu(fmaf(acc[r][2], al.z, sh.z));
+      o.w = relu(fmaf(acc[r][3], al.w, sh.w));
+      *reinterpret_cast<float4*>(y + (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * C + kgrp * 4) = o;
+    }
+    __syncthreads();  // every wave is done with the tile
+    if (tn < t_hi) commit();
+    __syncthreads();
+  }
+}
+
+// residency of a persistent kernel: resident workgroups per CU x CUs (queried once per kernel)
+template <typename K>
+static int persistent_grid(K kernel, long ntiles) {
+  struct Entry {
+    const void* fn;
+    int dev, cap;
+  };
+  static Entry cache[16];
+  static int used = 0;
+  int dev = 0;
+  hipGetDevice(&dev);
+  for (int i = 0; i < used; ++i)
+    if (cache[i].fn == (const void*)kernel && cache[i].dev == dev) return (int)std::min<long>(ntiles, cache[i].cap);
+  int cus = 0, per = 0;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0);
+  const int cap = std::max(8, cus * std::max(per, 1));
+  if (used < 16) cache[used++] = Entry{(const void*)kernel, dev, cap};
+  return (int)std::min<long>(ntiles, cap);
+}
+
+template <int TD, int TH>
+static int launch_conv_c16(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
+                           const Geo& g, hipStream_t st) {
+  const long ntiles = (long)B * ((g.Do + TD - 1) / TD) * ((g.Ho + TH - 1) / TH) * ((g.Wo + 15) / 16);
+  const int grid = persistent_grid(conv3d_c16_kernel<TD, TH>, ntiles);
+  hipLaunchKernelGGL((conv3d_c16_kernel<TD, TH>), dim3(grid), dim3(256), 0, st, x, w, al, sh, y, g, (int)ntiles);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
 // ---------------------------------------------------------------- launchers
 template <int CIN, int COUT, int S, int TD, int TH, int MBB>
 static int launch_conv(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
@@ -938,8 +1089,7 @@ template <int TDI, int THI>
 static int launch_deconv_c8(const float* x, const float* w, const float* al, const float* sh, const float* skip,
                             float* y, int B, const Geo& g, hipStream_t st) {
   const long ntiles = (long)B * ((g.Di + TDI - 1) / TDI) * ((g.Hi + THI - 1) / THI) * ((g.Wi + 15) / 16);
-  // 4 resident workgroups per CU (LDS: 2 tiles + weights + epilogue rows)
-  const long grid = std::min<long>(ntiles, 256 * 4);
+  const long grid = persistent_grid(deconv3d_c8_kernel<TDI, THI>, ntiles);
   hipLaunchKernelGGL((deconv3d_c8_kernel<TDI, THI>), dim3((unsigned)grid), dim3(256), 0, st, x, w, al, sh, skip, y, g,
                      (int)ntiles);
   TMVS_CHECK_LAUNCH();
@@ -977,7 +1127,12 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
   if (cin == CI && cout == CO && stride == 1) {                                               \
     return launch_conv<CI, CO, 1, TD, TH, MBB>(x, wpk, al, sh, y, B, g, st);                 \
   }
-  TMVS_CONV_LDS(16, 16, 2, 4, 1)
+#ifndef TMVS_C16_TD
+#define TMVS_C16_TD 2
+#define TMVS_C16_TH 4
+#endif
+  if (cin == 16 && cout == 16 && stride == 1)
+    return launch_conv_c16<TMVS_C16_TD, TMVS_C16_TH>(x, wpk, al, sh, y, B, g, st);
   TMVS_CONV_LDS(32, 32, 2, 4, 2)
   TMVS_CONV_LDS(64, 64, 1, 8, 2)
 #undef TMVS_CONV_LDS
