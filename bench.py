@@ -42,6 +42,7 @@ def _args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--profile-steps", type=int, default=3)
+    ap.add_argument("--no-overlap", action="store_true", help="run the FMT pathway on the main stream (A/B)")
     return ap.parse_args()
 
 
@@ -106,6 +107,7 @@ def main():
     model = TransMVSNet().eval()
     model.load_state_dict(synthetic.synthetic_state_dict(synthetic.state_dict_shapes(model), seed=0, sharpen=100.0))
     model = model.to(dev)
+    model.overlap_pathway = not args.no_overlap
     feats_cpu, proj, dv = make_inputs(dev)
     feats = {k: v.to(dev) for k, v in feats_cpu.items()}
     dv_dev = dv.to(dev)

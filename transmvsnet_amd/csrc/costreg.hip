@@ -794,6 +794,149 @@ static int launch_conv_c16(const float* x, const float* w, const float* al, cons
   return TMVS_OK;
 }
 
+// ---------------------------------------------------------------- conv1: 8 -> 16, stride 2, persistent
+// A persistent workgroup keeps the 13.8 KB of
+// weights in LDS and walks 2x4x16-output tiles; a tile's 5x9x33-voxel input footprint (8
+// channels, 32 B per voxel) is staged with W split by parity -- [d][h][w&1][w>>1][8] -- so the
+// stride-2 taps of 16 consecutive outputs read 16 consecutive voxels (kw 0/1/2 -> parity
+// 0/1/0, index col + kw/2): conflict-free ds_read_b128 with no address-unit waste. The next
+// tile is fetched into registers during the current tile's MFMAs.
+// Tap pairs: with 8 input channels a per-tap B fragment would be 2 channels per lane. The 27
+// taps are taken in pairs (a, b): lanes kgrp 0/1 read channel quads 0/1 of tap a, lanes 2/3
+// of tap b, one 16-byte read each; MFMA j contracts k = (tap, quad) over channel j of each
+// quad, and the A fragments are laid out to match (the 14th pair is half empty).
+template <int TD, int TH>
+__global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __restrict__ x,
+                                                               const float* __restrict__ wpk,
+                                                               const float* __restrict__ alpha,
+                                                               const float* __restrict__ shift, float* __restrict__ y,
+                                                               Geo g, int ntiles) {
+  constexpr int CIN = 8, COUT = 16, NBW = TD * TH / 4;
+  constexpr int LW = 33, LH = 2 * TH + 1, LD = 2 * TD + 1, SW = 17;
+  constexpr int NROW = LD * LH, NQ = NROW * LW * 2;  // float4 quads per tile
+  constexpr int NLD = (NQ + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float tile[NROW * 2 * SW * 8];
+  __shared__ __attribute__((aligned(16))) float wts[28 * 16 * 8];
+  const int nws = (g.Wo + 15) / 16, nhs = (g.Ho + TH - 1) / TH, nds = (g.Do + TD - 1) / TD;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int col = lane & 15, kgrp = lane >> 4;
+  const int half = kgrp & 1, side = kgrp >> 1;
+  const int nxcd = gridDim.x >= 8 ? 8 : 1, per_xcd = gridDim.x / nxcd;
+  const int xcd = blockIdx.x % nxcd, kx = blockIdx.x / nxcd;
+  const int t_lo = (int)((long)ntiles * xcd / nxcd), t_hi = (int)((long)ntiles * (xcd + 1) / nxcd);
+  if (kx >= per_xcd) return;
+  struct TileCoord {
+    int n, od0, oh0, ow0;
+  };
+  auto coord = [&](int t) {
+    TileCoord c;
+    c.ow0 = (t % nws) * 16;
+    t /= nws;
+    c.oh0 = (t % nhs) * TH;
+    t /= nhs;
+    c.od0 = (t % nds) * TD;
+    c.n = t / nds;
+    return c;
+  };
+  float4 pf[NLD];
+  auto fetch = [&](int t) {
+    const TileCoord c = coord(t);
+    const size_t in_n = (size_t)c.n * g.Di * g.Hi * g.Wi;
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int q = idx & 1, v = idx >> 1;
+      const int lw = v % LW, row = v / LW, lh = row % LH, ld = row / LH;
+      const int iw = 2 * c.ow0 - 1 + lw, ih = 2 * c.oh0 - 1 + lh, id = 2 * c.od0 - 1 + ld;
+      pf[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (idx < NQ && (unsigned)iw < (unsigned)g.Wi && (unsigned)ih < (unsigned)g.Hi && (unsigned)id < (unsigned)g.Di)
+        pf[k] = *reinterpret_cast<const float4*>(x + (in_n + ((size_t)id * g.Hi + ih) * g.Wi + iw) * CIN + 4 * q);
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int q = idx & 1, v = idx >> 1;
+      const int lw = v % LW, row = v / LW;
+      if (idx < NQ) *reinterpret_cast<float4*>(tile + ((row * 2 + (lw & 1)) * SW + (lw >> 1)) * 8 + 4 * q) = pf[k];
+    }
+  };
+  for (int idx = threadIdx.x; idx < 28 * 16 * 2; idx += 256) {  // tap 27: zero (the empty half of pair 13)
+    const int q = idx & 1, row = (idx >> 1) & 15, tap = idx >> 5;
+    const float4 v = tap < 27 ? *reinterpret_cast<const float4*>(wpk + ((size_t)tap * COUT + row) * CIN + 4 * q)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(wts + (tap * 16 + row) * 8 + 4 * q) = v;
+  }
+  const int co = kgrp * 4;
+  const float4 al = *reinterpret_cast<const float4*>(alpha + co);
+  const float4 sh = *reinterpret_cast<const float4*>(shift + co);
+  int t = t_lo + kx;
+  if (t < t_hi) {
+    fetch(t);
+    commit();
+  }
+  __syncthreads();
+  for (; t < t_hi; t += per_xcd) {
+    const TileCoord c = coord(t);
+    const int tn = t + per_xcd;
+    if (tn < t_hi) fetch(tn);
+    floatx4 acc[NBW];
+#pragma unroll
+    for (int r = 0; r < NBW; ++r) acc[r] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int pr = 0; pr < 14; ++pr) {
+      const int tap = 2 * pr + side;
+      const int tp = tap < 27 ? tap : 26;  // the empty tap reads a real voxel against zero weights
+      const int kd = tp / 9, kh = (tp / 3) % 3, kw = tp % 3;
+      const float4 a = *reinterpret_cast<const float4*>(wts + (tap * 16 + col) * 8 + 4 * half);
+      float4 b[NBW];
+#pragma unroll
+      for (int r = 0; r < NBW; ++r) {
+        const int rr = wv * NBW + r;
+        const int odl = rr / TH, ohl = rr - odl * TH;
+        const int row = (2 * odl + kd) * LH + 2 * ohl + kh;
+        b[r] = *reinterpret_cast<const float4*>(tile + ((row * 2 + (kw & 1)) * SW + col + (kw >> 1)) * 8 + 4 * half);
+      }
+#pragma unroll
+      for (int r = 0; r < NBW; ++r) {
+        acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[r].x, acc[r], 0, 0, 0);
+        acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[r].y, acc[r], 0, 0, 0);
+        acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[r].z, acc[r], 0, 0, 0);
+        acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[r].w, acc[r], 0, 0, 0);
+      }
+    }
+    const int ow = c.ow0 + col;
+    const size_t out_n = (size_t)c.n * g.Do * g.Ho * g.Wo;
+#pragma unroll
+    for (int r = 0; r < NBW; ++r) {
+      const int rr = wv * NBW + r;
+      const int od = c.od0 + rr / TH, oh = c.oh0 + rr % TH;
+      if (ow >= g.Wo || od >= g.Do || oh >= g.Ho) continue;
+      float4 o;
+      o.x = relu(fmaf(acc[r][0], al.x, sh.x));
+      o.y = relu(fmaf(acc[r][1], al.y, sh.y));
+      o.z = relu(fmaf(acc[r][2], al.z, sh.z));
+      o.w = relu(fmaf(acc[r][3], al.w, sh.w));
+      *reinterpret_cast<float4*>(y + (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co) = o;
+    }
+    __syncthreads();
+    if (tn < t_hi) commit();
+    __syncthreads();
+  }
+}
+
+template <int TD, int TH>
+static int launch_conv_s2c8_tile(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
+                                 const Geo& g, hipStream_t st) {
+  const long ntiles = (long)B * ((g.Do + TD - 1) / TD) * ((g.Ho + TH - 1) / TH) * ((g.Wo + 15) / 16);
+  const int grid = persistent_grid(conv3d_s2c8_tile_kernel<TD, TH>, ntiles);
+  hipLaunchKernelGGL((conv3d_s2c8_tile_kernel<TD, TH>), dim3(grid), dim3(256), 0, st, x, w, al, sh, y, g,
+                     (int)ntiles);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
 // ---------------------------------------------------------------- launchers
 template <int CIN, int COUT, int S, int TD, int TH, int MBB>
 static int launch_conv(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
@@ -802,94 +945,6 @@ static int launch_conv(const float* x, const float* w, const float* al, const fl
   const long nblk = (long)B * ((g.Do + TD - 1) / TD) * ((g.Ho + TH - 1) / TH) * ((g.Wo + 15) / 16) * MG;
   hipLaunchKernelGGL((conv3d_lds_kernel<CIN, COUT, S, TD, TH, MBB>), dim3((unsigned)nblk), dim3(256), 0, st, x, w, al,
                      sh, y, g);
-  TMVS_CHECK_LAUNCH();
-  return TMVS_OK;
-}
-
-// ---------------------------------------------------------------- conv1: 8 -> 16, stride 2
-// Direct kernel with tap pairs: with 8 input channels a per-tap B fragment is 2 channels
-// (8 bytes) per lane, and a 64-lane load moves 512 bytes for a full address-unit cost. Here
-// the 27 taps are taken in pairs (a, b): lanes kgrp 0/1 load channel quads 0/1 of tap a,
-// lanes 2/3 of tap b, one 16-byte load each; MFMA j then contracts k = (tap, quad) over
-// channel j of each quad, and the A fragments are laid out to match. Same MFMA count (the
-// 14th pair is half empty), half the load instructions.
-template <int NBW>
-__global__ __launch_bounds__(256) void conv3d_s2c8_pairs_kernel(const float* __restrict__ x,
-                                                                const float* __restrict__ wpk,
-                                                                const float* __restrict__ alpha,
-                                                                const float* __restrict__ shift,
-                                                                float* __restrict__ y, Geo g, int n_tasks) {
-  constexpr int CIN = 8, COUT = 16;
-  const int lane = threadIdx.x & 63;
-  const int task = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
-  if (task >= n_tasks) return;
-  int t = task;
-  const int nws = (g.Wo + 15) / 16;
-  const int wseg = t % nws;
-  t /= nws;
-  const int nhg = (g.Ho + NBW - 1) / NBW;
-  const int hg = t % nhg;
-  t /= nhg;
-  const int od = t % g.Do;
-  const int n = t / g.Do;
-  const int col = lane & 15, kgrp = lane >> 4;
-  const int half = kgrp & 1, side = kgrp >> 1;  // channel quad, tap of the pair
-  const int ow = wseg * 16 + col;
-  const size_t in_n = (size_t)n * g.Di * g.Hi * g.Wi;
-  floatx4 acc[NBW];
-#pragma unroll
-  for (int r = 0; r < NBW; ++r) acc[r] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-  for (int pr = 0; pr < 14; ++pr) {
-    const int tap = 2 * pr + side;            // 27 = the empty second half of pair 13
-    const bool real = tap < 27;
-    const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
-    const int id = od * 2 - 1 + kd;
-    const int iw = ow * 2 - 1 + kw;
-    const bool dwok = real && id >= 0 && id < g.Di && iw >= 0 && iw < g.Wi && ow < g.Wo;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (real) a = *reinterpret_cast<const float4*>(wpk + ((size_t)tap * COUT + col) * CIN + 4 * half);
-    float4 b[NBW];
-#pragma unroll
-    for (int r = 0; r < NBW; ++r) {
-      const int oh = hg * NBW + r;
-      const int ih = oh * 2 - 1 + kh;
-      b[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (dwok && oh < g.Ho && ih >= 0 && ih < g.Hi)
-        b[r] = *reinterpret_cast<const float4*>(x + (in_n + ((size_t)id * g.Hi + ih) * g.Wi + iw) * CIN + 4 * half);
-    }
-#pragma unroll
-    for (int r = 0; r < NBW; ++r) {
-      acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[r].x, acc[r], 0, 0, 0);
-      acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[r].y, acc[r], 0, 0, 0);
-      acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[r].z, acc[r], 0, 0, 0);
-      acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[r].w, acc[r], 0, 0, 0);
-    }
-  }
-  if (ow >= g.Wo) return;
-  const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
-  const int co = kgrp * 4;
-  const float4 al = *reinterpret_cast<const float4*>(alpha + co);
-  const float4 sh = *reinterpret_cast<const float4*>(shift + co);
-#pragma unroll
-  for (int r = 0; r < NBW; ++r) {
-    const int oh = hg * NBW + r;
-    if (oh >= g.Ho) continue;
-    float4 o;
-    o.x = relu(fmaf(acc[r][0], al.x, sh.x));
-    o.y = relu(fmaf(acc[r][1], al.y, sh.y));
-    o.z = relu(fmaf(acc[r][2], al.z, sh.z));
-    o.w = relu(fmaf(acc[r][3], al.w, sh.w));
-    *reinterpret_cast<float4*>(y + (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co) = o;
-  }
-}
-
-template <int NBW>
-static int launch_conv_s2c8_pairs(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
-                                  const Geo& g, hipStream_t st) {
-  const long n_tasks = (long)B * g.Do * ((g.Ho + NBW - 1) / NBW) * ((g.Wo + 15) / 16);
-  const int nblk = (int)((n_tasks + 3) / 4);
-  hipLaunchKernelGGL((conv3d_s2c8_pairs_kernel<NBW>), dim3(nblk), dim3(256), 0, st, x, w, al, sh, y, g, (int)n_tasks);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -1137,7 +1192,7 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
   TMVS_CONV_LDS(64, 64, 1, 8, 2)
 #undef TMVS_CONV_LDS
   // stride 2, 8 -> 16 (full-resolution input): tap pairs, 16-byte loads
-  if (cin == 8 && cout == 16 && stride == 2) return launch_conv_s2c8_pairs<4>(x, wpk, al, sh, y, B, g, st);
+  if (cin == 8 && cout == 16 && stride == 2) return launch_conv_s2c8_tile<2, 4>(x, wpk, al, sh, y, B, g, st);
   // stride 2: direct
 #define TMVS_CONV_DIRECT(CI, CO, NBW, MBW) \
   if (cin == CI && cout == CO && stride == 2) return launch_conv_direct<CI, CO, 2, NBW, MBW>(x, wpk, al, sh, y, B, g, st);
