@@ -57,9 +57,14 @@ struct Geo {
 // Workgroup tile: 16 output voxels along w x TH rows x TD depth slices, MBB blocks of 16
 // output channels. Per CK-channel chunk the input tile (+halo) is staged once into LDS
 // (voxel stride CK+4 floats: the 16 lanes of a row hit distinct banks), then each wave runs
-// its NBW = TD*TH/4 rows through the 27 taps: A (weights) from global/L2, B from LDS.
+// its NBW = TD*TH/4 rows through the 27 taps: A (weights) from global/L2, requested two taps
+// ahead, B from LDS. The next chunk's tile is fetched into registers during the current
+// chunk's MFMAs.
 template <int CIN, int COUT, int S, int TD, int TH, int MBB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv3d_lds_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
+#ifndef TMVS_LDS_WPE
+#define TMVS_LDS_WPE 3
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WPE, TMVS_LDS_WPE))) void conv3d_lds_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                          const float* __restrict__ alpha,
                                                          const float* __restrict__ shift, float* __restrict__ y,
                                                          Geo g) {
@@ -99,40 +104,55 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
     for (int m = 0; m < MBB; ++m) acc[r][m] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll 1
-  for (int ch = 0; ch < CIN / CK; ++ch) {
-    if (ch) __syncthreads();
-    for (int idx = threadIdx.x; idx < NVOX * PL; idx += 256) {
+  // channel chunk ch's tile: global -> registers (issued one chunk ahead) -> LDS
+  constexpr int NCH = CIN / CK, NLD = (NVOX * PL + 255) / 256;
+  float4 pf[NLD];
+  auto fetch = [&](int ch) {
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      const int idx = threadIdx.x + 256 * k;
       const int vox = idx / PL, q = idx - vox * PL;
       const int lw = vox % LW, rest = vox / LW, lh = rest % LH, ld = rest / LH;
       const int iw = iw0 + lw, ih = ih0 + lh, id = id0 + ld;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (iw >= 0 && iw < g.Wi && ih >= 0 && ih < g.Hi && id >= 0 && id < g.Di)
-        v = *reinterpret_cast<const float4*>(x + (in_n + ((size_t)id * g.Hi + ih) * g.Wi + iw) * CIN + ch * CK + 4 * q);
-      const int qs = SWZ ? (q ^ ((vox >> 1) & 3)) : q;
-      *reinterpret_cast<float4*>(tile + vox * VST + 4 * qs) = v;
+      pf[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (idx < NVOX * PL && iw >= 0 && iw < g.Wi && ih >= 0 && ih < g.Hi && id >= 0 && id < g.Di)
+        pf[k] = *reinterpret_cast<const float4*>(x + (in_n + ((size_t)id * g.Hi + ih) * g.Wi + iw) * CIN + ch * CK + 4 * q);
     }
-    __syncthreads();
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int vox = idx / PL, q = idx - vox * PL;
+      const int qs = SWZ ? (q ^ ((vox >> 1) & 3)) : q;
+      if (idx < NVOX * PL) *reinterpret_cast<float4*>(tile + vox * VST + 4 * qs) = pf[k];
+    }
+  };
+  fetch(0);
+  commit();
+  __syncthreads();
 #pragma unroll 1
-    for (int kd = 0; kd < 3; ++kd) {
-      // the kd slice's 9 weight fragments are requested together: one exposed latency per
-      // slice instead of one per tap (A fragments come from global/L2, B from LDS)
-      VecN<PL> aw[9][MBB];
+  for (int ch = 0; ch < NCH; ++ch) {
+    if (ch + 1 < NCH) fetch(ch + 1);  // lands during this chunk's MFMAs
+    // A fragments from global/L2, requested two taps ahead of their MFMAs
+    auto wload = [&](int tap, VecN<PL>(&a)[MBB]) {
 #pragma unroll
-      for (int t9 = 0; t9 < 9; ++t9)
+      for (int m = 0; m < MBB; ++m) {
+        const int co = (mg * MBB + m) * 16 + col;
+        if (co < COUT)
+          a[m].load(wpk + ((size_t)tap * COUT + co) * CIN + ch * CK + kgrp * PL);
+        else
+          a[m].zero();
+      }
+    };
+    VecN<PL> aw[3][MBB];
+    wload(0, aw[0]);
+    wload(1, aw[1]);
 #pragma unroll
-        for (int m = 0; m < MBB; ++m) {
-          const int co = (mg * MBB + m) * 16 + col;
-          if (co < COUT)
-            aw[t9][m].load(wpk + ((size_t)(kd * 9 + t9) * COUT + co) * CIN + ch * CK + kgrp * PL);
-          else
-            aw[t9][m].zero();
-        }
-      __builtin_amdgcn_sched_barrier(0);  // keep the 9 requests ahead of the MFMAs
-#pragma unroll
-    for (int t9 = 0; t9 < 9; ++t9) {
-      const int kh = t9 / 3, kw = t9 % 3;
-      const VecN<PL>* a = aw[t9];
+    for (int tap = 0; tap < 27; ++tap) {
+      const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+      if (tap + 2 < 27) wload(tap + 2, aw[(tap + 2) % 3]);
+      const VecN<PL>* a = aw[tap % 3];
       VecN<PL> b[NBW];
 #pragma unroll
       for (int r = 0; r < NBW; ++r) {
@@ -149,7 +169,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
           for (int m = 0; m < MBB; ++m)
             acc[r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b[r].v[j], acc[r][m], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // keep the 2-tap-ahead schedule (and the VGPR budget)
     }
+    if (ch + 1 < NCH) {
+      __syncthreads();
+      commit();
+      __syncthreads();
     }
   }
   const int ow = ow0 + col;
@@ -1189,7 +1214,7 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
   if (cin == 16 && cout == 16 && stride == 1)
     return launch_conv_c16<TMVS_C16_TD, TMVS_C16_TH>(x, wpk, al, sh, y, B, g, st);
   TMVS_CONV_LDS(32, 32, 2, 4, 2)
-  TMVS_CONV_LDS(64, 64, 1, 8, 2)
+  TMVS_CONV_LDS(64, 64, 1, 4, 2)
 #undef TMVS_CONV_LDS
   // stride 2, 8 -> 16 (full-resolution input): tap pairs, 16-byte loads
   if (cin == 8 && cout == 16 && stride == 2) return launch_conv_s2c8_tile<2, 4>(x, wpk, al, sh, y, B, g, st);
