@@ -91,6 +91,49 @@ def test_warp_corr_ten_source_views(sd, c, d, stage1):
     np.testing.assert_allclose(to_np(sim)[:, None], to_np(sim_ref), rtol=0, atol=2e-5)
 
 
+@pytest.mark.parametrize("given", [False, True])
+def test_warp_corr_dtu_stage1_size(sd, given):
+    """Fused cost volume at the DTU stage-1 size (216x288, C=32, D=48, 4 src views) with the
+    forward's uniform fronto-parallel planes, against the oracle. 3M outputs: the channel-sum order
+    leaves 5 of them between 2e-5 and 2.7e-5 in given-weight mode, hence 3e-5 here."""
+    torch.manual_seed(7)
+    n, h, w, c, d = 5, 216, 288, 32, 48
+    feats = [torch.randn(1, c, h, w) for _ in range(n)]
+    proj = synthetic.synthetic_cameras(n, h * 4, w * 4, seed=1)["stage1"]
+    dv = synthetic.synthetic_depth_values(1)
+    hyp = oracle.stage_hypotheses(None, dv, 0, (h * 4, w * 4), (48, 32, 8), (4.0, 1.0, 0.5))
+    nh = [_nhwc(f).to(DEV) for f in feats]
+    src = torch.stack([x[0] for x in nh[1:]], 0).unsqueeze(0).contiguous()
+    rows = ops.proj_rows(proj)
+    if given:
+        vw = torch.rand(1, n - 1, h, w)
+        sim_ref, _ = oracle.build_cost_volume({}, feats, proj, hyp, view_weights=vw)
+        sim, _, _ = ops.warp_corr(nh[0], src, rows, hyp.to(DEV), view_w_in=vw.to(DEV), vw_shift=0)
+    else:
+        sim_ref, vw_ref = oracle.build_cost_volume(sd, feats, proj, hyp)
+        sim, _, vw_out = ops.warp_corr(nh[0], src, rows, hyp.to(DEV), pw_params=_pw_params(sd))
+        np.testing.assert_allclose(to_np(vw_out), to_np(vw_ref), rtol=0, atol=2e-5)
+    np.testing.assert_allclose(to_np(sim)[:, None], to_np(sim_ref), rtol=0, atol=3e-5)
+
+
+def test_warp_corr_incoherent_depth_and_degenerate_planes(sd):
+    """C=32 with per-pixel random hypotheses over the whole DTU range, one coherent tile and a
+    patch of planes behind the camera (z < 1e-6 -> zero samples), against the oracle."""
+    torch.manual_seed(8)
+    n, h, w, c, d = 4, 40, 72, 32, 32
+    feats = [torch.randn(1, c, h, w) for _ in range(n)]
+    proj = synthetic.synthetic_cameras(n, h * 4, w * 4, seed=2)["stage1"]
+    hyp = torch.sort(torch.rand(1, d, h, w) * 480 + 425, dim=1).values
+    hyp[:, :, :8, :16] = hyp[:, :, :8, :16] * 0 + torch.linspace(600, 640, d).view(1, d, 1, 1)
+    hyp[0, 3, 20:24, 30:40] = -30.0
+    nh = [_nhwc(f).to(DEV) for f in feats]
+    src = torch.stack([x[0] for x in nh[1:]], 0).unsqueeze(0).contiguous()
+    sim_ref, vw_ref = oracle.build_cost_volume(sd, feats, proj, hyp)
+    sim, _, vw = ops.warp_corr(nh[0], src, ops.proj_rows(proj), hyp.to(DEV), pw_params=_pw_params(sd))
+    np.testing.assert_allclose(to_np(sim)[:, None], to_np(sim_ref), rtol=0, atol=2e-5)
+    np.testing.assert_allclose(to_np(vw), to_np(vw_ref), rtol=0, atol=2e-5)
+
+
 def test_e2e_eleven_views_tnt_aspect(sd):
     """Whole hot path at N=11 on a Tanks&Temples-shaped (1056x1920 / 4) frame vs the oracle."""
     m = TransMVSNet().eval()
