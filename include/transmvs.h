@@ -211,6 +211,24 @@ int tmvs_depth_stage(const float* depth_values, int n_values, const float* prev_
                      float clamp_hi, float* hyp_out, float* prob_out, float* depth_out, float* depth_raw_out,
                      float* conf_out, void* stream);
 
+/* ------------------------------------------------------------------ FeatureNet heads
+ * Modulated deformable convolution of DCN.forward (models/dcn.py:66-80; torchvision.ops.deform_conv2d,
+ * torchvision 0.10.1): 3x3, stride 1, padding 1, dilation 1, one offset group, with the head's bias,
+ * optional eval BatchNorm (tmvs_bn_fold's alpha/shift) and ReLU fused (models/module.py:362-395).
+ *   x_nhwc      : [B][H][W][cin] (cin = 32)
+ *   offset_mask : [B][27][H][W] = conv_offset_mask(x) (NCHW): channels 2k / 2k+1 = dy / dx of tap k,
+ *                 18+k = mask logit of tap k (sigmoid applied inside)
+ *   w_packed    : tmvs_deform_conv2d_packed_floats(cout) floats from tmvs_deform_conv2d_pack (HOST
+ *                 packing of the [cout][cin][3][3] weight; copy to the device once per load_state_dict)
+ *   bias        : [cout]; bn_alpha / bn_shift: [cout] or both NULL; relu: 0/1
+ *   out         : [B][cout][H][W] (NCHW);  out_nhwc: optional [B][H][W][cout] copy, or NULL
+ * Supported: cin = 32, cout in {8, 16, 32}; H*W*cin*4 < 2^31; H, W <= 32766.                      */
+size_t tmvs_deform_conv2d_packed_floats(int cout);
+int tmvs_deform_conv2d_pack(const float* weight, int cout, int cin, float* packed);
+int tmvs_deform_conv2d(const float* x_nhwc, const float* offset_mask, const float* w_packed, const float* bias,
+                       const float* bn_alpha, const float* bn_shift, int relu, int batch, int cin, int cout,
+                       int height, int width, float* out, float* out_nhwc, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

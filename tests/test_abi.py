@@ -94,3 +94,23 @@ def test_forward_refuses_cpu_tensors():
     proj = synthetic.synthetic_cameras(3, 64, 80)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         m.forward_features(feats, proj, synthetic.synthetic_depth_values(1), (64, 80))
+
+
+def test_deform_conv2d_pack_host(lib):
+    """tmvs_deform_conv2d_pack (HOST): A-fragment order [tap][s][mtile][lane], K = channel 8*(lane/16)+s."""
+    import numpy as np
+    import torch
+    from transmvsnet_amd import ops
+    for co in (8, 16, 32):
+        w = torch.randn(co, 32, 3, 3)
+        pk = ops.deform_conv2d_pack(w).numpy()
+        mt_n = (co + 15) // 16
+        assert pk.size == 9 * 8 * mt_n * 64
+        wn = w.numpy()
+        for k in (0, 4, 8):
+            for s in (0, 3, 7):
+                for mt in range(mt_n):
+                    for lane in (0, 5, 17, 63):
+                        c_o, c_i = 16 * mt + lane % 16, 8 * (lane // 16) + s
+                        want = wn[c_o, c_i, k // 3, k % 3] if c_o < co else 0.0
+                        assert pk[((k * 8 + s) * mt_n + mt) * 64 + lane] == want

@@ -39,6 +39,9 @@ SIGNATURES = {
     "tmvs_fmt_forward": (I, [P, L, P, I, I, I, I, I, P, P, S, P, P]),
     "tmvs_depth_stage_workspace": (S, [I, I, I, I]),
     "tmvs_depth_stage": (I, [P, I, P, I, I, P, I, I, I, F, I, I, I, P, P, P, I, P, P, S, F, F, P, P, P, P, P, P]),
+    "tmvs_deform_conv2d_packed_floats": (S, [I]),
+    "tmvs_deform_conv2d_pack": (I, [P, I, I, P]),
+    "tmvs_deform_conv2d": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P, P, P]),
 }
 
 ABI_VERSION = 1

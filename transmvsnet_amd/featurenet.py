@@ -1,9 +1,10 @@
-"""FeatureNet + DCN (models/module.py:343-422, models/dcn.py:43-80) -- OUTSIDE the hot path.
+"""FeatureNet + DCN (models/module.py:343-422, models/dcn.py:43-80) -- SURVEY.md 8f, the #1 "next" row.
 
-SURVEY.md section 8f ranks this the #1 "next" row (80 % of the FLOPs of a full forward, but
-not named by the north star). Until its HIP kernels land it runs on the GPU through
-PyTorch-ROCm (MIOpen convolutions) with a torch formulation of the modulated deformable
-convolution (torchvision.ops.deform_conv2d, torchvision 0.10.1 -- absent in this image).
+The 3-scale trunk, the lateral 1x1 convs and each DCN's offset/mask conv run as PyTorch-ROCm
+(MIOpen) convolutions. The modulated deformable convolution itself -- torchvision.ops.deform_conv2d
+(torchvision 0.10.1, absent in this image) -- runs as the HIP kernel ``tmvs_deform_conv2d``
+(csrc/featurenet.hip), with the head's bias, BatchNorm and ReLU fused into its epilogue
+(models/module.py:362-395: DCN -> BN -> ReLU -> DCN -> BN -> ReLU -> DCN). There is no CPU path.
 The module/parameter names are the reference's, so checkpoints load strict=True.
 """
 from __future__ import annotations
@@ -13,6 +14,8 @@ import math
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from . import ops
 
 
 class Conv2dBlock(nn.Module):
@@ -27,45 +30,13 @@ class Conv2dBlock(nn.Module):
         return F.relu(self.bn(self.conv(x)))
 
 
-def deform_conv2d(x, offset, weight, bias, padding, mask):
-    """Modulated deformable conv, stride 1 / dilation 1 / one offset group (torchvision layout:
-    channel 2k = dy, 2k+1 = dx of tap k; bilinear, zeros outside)."""
-    b, c, h, w = x.shape
-    co, _, kh, kw = weight.shape
-    ys = torch.arange(h, dtype=x.dtype, device=x.device).view(1, h, 1).expand(b, h, w)
-    xs = torch.arange(w, dtype=x.dtype, device=x.device).view(1, 1, w).expand(b, h, w)
-    flat = x.reshape(b, c, h * w)
-    cols = []
-    for i in range(kh):
-        for j in range(kw):
-            k = i * kw + j
-            py = ys + float(i - padding) + offset[:, 2 * k]
-            px = xs + float(j - padding) + offset[:, 2 * k + 1]
-            inside = (py > -1) & (py < h) & (px > -1) & (px < w)
-            y0 = torch.floor(py)
-            x0 = torch.floor(px)
-            ly, lx = py - y0, px - x0
-            hy, hx = 1 - ly, 1 - lx
-            y0i, x0i = y0.long(), x0.long()
-            val = 0
-            for dy, dx, wt in ((0, 0, hy * hx), (0, 1, hy * lx), (1, 0, ly * hx), (1, 1, ly * lx)):
-                yy, xx = y0i + dy, x0i + dx
-                ok = inside & (yy >= 0) & (yy <= h - 1) & (xx >= 0) & (xx <= w - 1)
-                lin = (yy.clamp(0, h - 1) * w + xx.clamp(0, w - 1)).view(b, 1, h * w).expand(b, c, h * w)
-                tap = torch.gather(flat, 2, lin).view(b, c, h, w) * ok.unsqueeze(1)
-                val = val + wt.unsqueeze(1) * tap
-            cols.append(mask[:, k:k + 1] * val)
-    col = torch.stack(cols, dim=2).view(b, c * kh * kw, h * w)
-    out = torch.matmul(weight.view(co, -1), col).view(b, co, h, w)
-    return out if bias is None else out + bias.view(1, -1, 1, 1)
-
-
 class DCN(nn.Module):
     """DCNv2 (models/dcn.py:15-80): weight/bias + zero-initialised offset/mask conv."""
 
     def __init__(self, cin, cout, k=3, padding=1):
         super().__init__()
         self.padding = padding
+        self.cout = cout
         self.weight = nn.Parameter(torch.empty(cout, cin, k, k))
         self.bias = nn.Parameter(torch.zeros(cout))
         std = 1.0 / math.sqrt(cin * k * k)
@@ -73,10 +44,36 @@ class DCN(nn.Module):
         self.conv_offset_mask = nn.Conv2d(cin, 3 * k * k, k, padding=padding, bias=True)
         nn.init.zeros_(self.conv_offset_mask.weight)
         nn.init.zeros_(self.conv_offset_mask.bias)
+        self._packed = None
+        self.register_load_state_dict_post_hook(lambda m, k: m.invalidate())
 
-    def forward(self, x):
-        o1, o2, m = torch.chunk(self.conv_offset_mask(x), 3, dim=1)
-        return deform_conv2d(x, torch.cat((o1, o2), 1), self.weight, self.bias, self.padding, torch.sigmoid(m))
+    def invalidate(self):
+        self._packed = None
+
+    def _prepared(self, device, bn):
+        bnv = None if bn is None else (id(bn), bn.weight._version, bn.bias._version, bn.running_mean._version,
+                                       bn.running_var._version)
+        key = (str(device), self.weight._version, self.bias._version, bnv)
+        if self._packed is None or self._packed[0] != key:
+            w = ops.deform_conv2d_pack(self.weight).to(device)
+            b = self.bias.detach().float().contiguous().to(device)
+            fold = None
+            if bn is not None:
+                a, s = ops.bn_fold(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
+                fold = (torch.from_numpy(a).to(device), torch.from_numpy(s).to(device))
+            self._packed = (key, w, b, fold)
+        return self._packed[1:]
+
+    def forward(self, x, bn=None, relu=False, x_nhwc=None, want_nhwc=False):
+        """deform_conv2d(x, offset, weight, bias, mask) (models/dcn.py:71-80), then the head's
+        eval BatchNorm ``bn`` and ReLU if given (fused)."""
+        if not x.is_cuda:
+            raise RuntimeError("FeatureNet DCN runs on the GPU only (tmvs_deform_conv2d); no CPU fallback")
+        om = self.conv_offset_mask(x).contiguous()
+        if x_nhwc is None:
+            x_nhwc = x.permute(0, 2, 3, 1).contiguous()
+        w, b, fold = self._prepared(x.device, bn)
+        return ops.deform_conv2d(x_nhwc, om, w, b, self.cout, bn=fold, relu=relu, want_nhwc=want_nhwc)
 
 
 def _head(cin, cmid, cout, first_k):
@@ -85,6 +82,14 @@ def _head(cin, cmid, cout, first_k):
         DCN(cmid, cmid), nn.BatchNorm2d(cmid), nn.ReLU(inplace=True),
         DCN(cmid, cmid), nn.BatchNorm2d(cmid), nn.ReLU(inplace=True),
         DCN(cmid, cout))
+
+
+def _run_head(seq, x):
+    """out{1,2,3} Sequential (models/module.py:362-395) with BN + ReLU fused into the DCN kernels."""
+    x = seq[0](x)
+    x, xh = seq[1](x, bn=seq[2], relu=True, want_nhwc=True)
+    x, xh = seq[4](x, bn=seq[5], relu=True, x_nhwc=xh, want_nhwc=True)
+    return seq[7](x, x_nhwc=xh)
 
 
 class FeatureNet(nn.Module):
@@ -105,12 +110,14 @@ class FeatureNet(nn.Module):
         self.out3 = _head(4 * b, 4 * b, b, 3)
 
     def forward(self, x):
+        """x [B,3,H,W] -> {stage1: [B,32,H/4,W/4], stage2: [B,16,H/2,W/2], stage3: [B,8,H,W]}.
+        Views may be batched on B (eval BatchNorm is per sample)."""
         conv0 = self.conv0(x)
         conv1 = self.conv1(conv0)
         conv2 = self.conv2(conv1)
-        out = {"stage1": self.out1(conv2)}
+        out = {"stage1": _run_head(self.out1, conv2)}
         intra = F.interpolate(conv2, scale_factor=2.0, mode="nearest") + self.inner1(conv1)
-        out["stage2"] = self.out2(intra)
+        out["stage2"] = _run_head(self.out2, intra)
         intra = F.interpolate(intra, scale_factor=2.0, mode="nearest") + self.inner2(conv0)
-        out["stage3"] = self.out3(intra)
+        out["stage3"] = _run_head(self.out3, intra)
         return out

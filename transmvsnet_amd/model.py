@@ -258,8 +258,11 @@ class TransMVSNet(nn.Module):
 
     # --------------------------------------------------------- forward
     def forward(self, imgs, proj_matrix, depth_values):
-        """models/TransMVSNet.py:141-226."""
-        feats = [self.feature(imgs[:, v]) for v in range(imgs.size(1))]
+        """models/TransMVSNet.py:141-226. FeatureNet runs once over all B*N views (the reference
+        loops over views, :151-153; eval BatchNorm is per sample, so batching is exact)."""
+        b, n = imgs.shape[:2]
+        f = self.feature(imgs.reshape(b * n, *imgs.shape[2:]))
+        feats = {k: v.reshape(b, n, *v.shape[1:]) for k, v in f.items()}
         return self.forward_features(feats, proj_matrix, depth_values, (imgs.shape[3], imgs.shape[4]))
 
     @staticmethod

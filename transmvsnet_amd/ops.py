@@ -305,3 +305,33 @@ def depth_stage(depth_values, prev_depth, feat_nhwc, ndepth, ratio, full_hw, sta
                                              ctypes.c_float(clamp[0]), ctypes.c_float(clamp[1]), _ptr(hyp), _ptr(prob),
                                              _ptr(depth), _ptr(raw), _ptr(conf), _stream()), "tmvs_depth_stage")
     return {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}, raw
+
+
+def deform_conv2d_pack(weight):
+    """HOST packing of a DCN weight [Co][32][3][3] into the kernel's A-fragment order (CPU float32)."""
+    w = np.ascontiguousarray(weight.detach().float().cpu().numpy(), np.float32)
+    co, ci = w.shape[:2]
+    out = np.empty(_lib_h().tmvs_deform_conv2d_packed_floats(co), np.float32)
+    _lib.check(_lib_h().tmvs_deform_conv2d_pack(w.ctypes.data, co, ci, out.ctypes.data), "tmvs_deform_conv2d_pack")
+    return torch.from_numpy(out)
+
+
+def deform_conv2d(x_nhwc, offset_mask, w_packed, bias, cout, bn=None, relu=False, want_nhwc=False):
+    """DCN.forward's deform_conv2d (models/dcn.py:71-80) + optional folded BN / ReLU of the head.
+
+    x_nhwc [B,H,W,32], offset_mask [B,27,H,W] (conv_offset_mask output), w_packed from
+    deform_conv2d_pack (on the device). Returns out [B,cout,H,W] (and [B,H,W,cout] if want_nhwc).
+    """
+    for t, n in ((x_nhwc, "x_nhwc"), (offset_mask, "offset_mask"), (w_packed, "w_packed"), (bias, "bias")):
+        _dev(t, n)
+    b, h, w, cin = x_nhwc.shape
+    if offset_mask.shape != (b, 27, h, w) or not offset_mask.is_contiguous() or not x_nhwc.is_contiguous():
+        raise ValueError("deform_conv2d: expects contiguous x_nhwc [B,H,W,C] and offset_mask [B,27,H,W]")
+    out = torch.empty(b, cout, h, w, device=x_nhwc.device)
+    out_nhwc = torch.empty(b, h, w, cout, device=x_nhwc.device) if want_nhwc else None
+    alpha, shift = bn if bn is not None else (None, None)
+    with _Span("tmvs_deform_conv2d"):
+        _lib.check(_lib_h().tmvs_deform_conv2d(_ptr(x_nhwc), _ptr(offset_mask), _ptr(w_packed), _ptr(bias),
+                                               _ptr(alpha), _ptr(shift), int(relu), b, cin, cout, h, w, _ptr(out),
+                                               _ptr(out_nhwc), _stream()), "tmvs_deform_conv2d")
+    return (out, out_nhwc) if want_nhwc else out
