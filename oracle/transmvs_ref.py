@@ -161,8 +161,8 @@ def warp_grid(src_proj, ref_proj, depth_values, height, width):
         proj = torch.matmul(src_proj, torch.inverse(ref_proj))
         rot = proj[:, :3, :3]
         trans = proj[:, :3, 3:4]
-        y, x = torch.meshgrid([torch.arange(0, height, dtype=torch.float32),
-                               torch.arange(0, width, dtype=torch.float32)], indexing="ij")
+        y, x = torch.meshgrid([torch.arange(0, height, dtype=depth_values.dtype),
+                               torch.arange(0, width, dtype=depth_values.dtype)], indexing="ij")
         y, x = y.contiguous().view(height * width), x.contiguous().view(height * width)
         xyz = torch.stack((x, y, torch.ones_like(x)))
         xyz = torch.unsqueeze(xyz, 0).repeat(batch, 1, 1)

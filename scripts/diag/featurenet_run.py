@@ -1,0 +1,18 @@
+"""FeatureNet over the 5 DTU views (batched, as TransMVSNet.forward does), K times: the command
+profiled by rocprofv3 to see where FeatureNet's time goes. Usage: featurenet_run.py [K]"""
+import os, sys
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
+import torch
+from transmvsnet_amd import TransMVSNet, synthetic
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+H, W, N = 864, 1152, 5
+dev = torch.device("cuda")
+m = TransMVSNet().eval()
+m.load_state_dict(synthetic.synthetic_state_dict(synthetic.state_dict_shapes(m), seed=0, sharpen=100.0))
+m = m.to(dev)
+imgs = synthetic.synthetic_images(N, H, W).to(dev)
+with torch.no_grad():
+    for i in range(K + 2):
+        f = m.feature(imgs.reshape(N, 3, H, W))
+    torch.cuda.synchronize()
+print("done", {k: tuple(v.shape) for k, v in f.items()})
