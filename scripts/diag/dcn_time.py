@@ -1,0 +1,29 @@
+"""Time tmvs_deform_conv2d at the FeatureNet head sizes (5 DTU views batched), offsets ~N(0, 1.5) px.
+HIP events on the current stream, median of 10 after 3 warm-ups. Variant via TMVS_DCN_* env."""
+import os, sys
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
+import numpy as np, torch
+from transmvsnet_amd import ops
+dev = "cuda"
+g = torch.Generator(device="cpu").manual_seed(0)
+res = []
+CFGS = ((864, 1152, 32), (864, 1152, 8), (432, 576, 32), (432, 576, 16), (216, 288, 32))
+only = os.environ.get("DCN_ONLY")
+for (h, w, co) in ([CFGS[int(only)]] if only else CFGS):
+    x = torch.randn(5, h, w, 32, generator=g).to(dev)
+    om = torch.randn(5, 27, h, w, generator=g)
+    om[:, :18] *= float(os.environ.get("DCN_OFFSET_STD", "1.5"))
+    om = om.to(dev)
+    wp = ops.deform_conv2d_pack(torch.randn(co, 32, 3, 3, generator=g) * 0.06).to(dev)
+    bias = torch.zeros(co, device=dev)
+    ts = []
+    for i in range(13):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ops.deform_conv2d(x, om, wp, bias, co, want_nhwc=True)
+        e1.record()
+        torch.cuda.synchronize()
+        if i >= 3:
+            ts.append(e0.elapsed_time(e1) * 1e3)
+    res.append(f"{h}x{w}->{co}: {np.median(ts):.1f} us")
+print(os.environ.get("TMVS_DCN_TAG", "default"), "offset std", os.environ.get("DCN_OFFSET_STD", "1.5"), " | ".join(res))

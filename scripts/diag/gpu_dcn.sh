@@ -1,0 +1,8 @@
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/dcn; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_featurenet.py -q -x --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+tail -2 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
+for sd in 0 0.5 1.5; do
+DCN_OFFSET_STD=$sd timeout -k 10 120 python scripts/diag/dcn_time.py > $O/t_$sd.txt 2>&1 || exit $?
+done
+cat $O/t_*.txt | grep us

@@ -38,6 +38,14 @@ for (name, grid), d in sorted(vals.items(), key=lambda x: (x[0][0], x[0][1])):
         line.append(f"ldsconf={m.get('SQ_LDS_BANK_CONFLICT', 0) / m['SQ_LDS_IDX_ACTIVE']:4.2f}")
     if cyc and "TA_ADDR_STALLED_BY_TC_CYCLES_sum" in m:
         line.append(f"TAstallTC={m['TA_ADDR_STALLED_BY_TC_CYCLES_sum'] / 256 / cyc:4.2f}")
+    if "TCC_HIT_sum" in m and "TCC_MISS_sum" in m:
+        line.append(f"L2hit={m['TCC_HIT_sum'] / max(m['TCC_HIT_sum'] + m['TCC_MISS_sum'], 1):4.2f}")
+    if "TCP_TOTAL_CACHE_ACCESSES_sum" in m and "TCP_TCC_READ_REQ_sum" in m:
+        line.append(f"L1miss={m['TCP_TCC_READ_REQ_sum'] / max(m['TCP_TOTAL_CACHE_ACCESSES_sum'], 1):4.2f}")
+    if cyc and "SQ_WAIT_ANY" in m and "SQ_WAVE_CYCLES" in m:
+        line.append(f"parked={m['SQ_WAIT_ANY'] / max(m['SQ_WAVE_CYCLES'], 1):4.2f}")
+    if "SQ_WAVE_CYCLES" in m and cyc:
+        line.append(f"waves/SIMD={m['SQ_WAVE_CYCLES'] / 1024 / cyc:4.1f}")
     if cyc and "SQ_WAIT_INST_ANY" in m and "SQ_WAVE_CYCLES" in m:
         line.append(f"wait={m['SQ_WAIT_INST_ANY'] / max(m['SQ_WAVE_CYCLES'], 1):4.2f}")
     print(" ".join(x for x in line if x))

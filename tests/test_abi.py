@@ -97,7 +97,8 @@ def test_forward_refuses_cpu_tensors():
 
 
 def test_deform_conv2d_pack_host(lib):
-    """tmvs_deform_conv2d_pack (HOST): A-fragment order [tap][s][mtile][lane], K = channel 8*(lane/16)+s."""
+    """tmvs_deform_conv2d_pack (HOST): A fragments [tap][mtile][half][lane][e], k-step s = 4*half + e feeds
+    channel 16*half + 4*(lane/16) + e (the kernel's B lanes hold channels 4j..4j+3 and 16+4j..16+4j+3)."""
     import numpy as np
     import torch
     from transmvsnet_amd import ops
@@ -111,6 +112,7 @@ def test_deform_conv2d_pack_host(lib):
             for s in (0, 3, 7):
                 for mt in range(mt_n):
                     for lane in (0, 5, 17, 63):
-                        c_o, c_i = 16 * mt + lane % 16, 8 * (lane // 16) + s
+                        h, e = s // 4, s % 4
+                        c_o, c_i = 16 * mt + lane % 16, 16 * h + 4 * (lane // 16) + e
                         want = wn[c_o, c_i, k // 3, k % 3] if c_o < co else 0.0
-                        assert pk[((k * 8 + s) * mt_n + mt) * 64 + lane] == want
+                        assert pk[((((k * mt_n + mt) * 2 + h) * 64) + lane) * 4 + e] == want

@@ -11,118 +11,233 @@
 // first 18 channels ARE cat(o1, o2) (models/dcn.py:75-77): channel 2k = dy_k, 2k+1 = dx_k.
 //
 // Implicit GEMM on fp32 MFMA (v_mfma_f32_16x16x4f32, exact fp32 products): M = 16 output
-// channels, N = 16 pixels, K = 9 taps x 32 input channels. The B operand is produced in registers
-// by the bilinear sampler itself: lane (j = lane/16, n = lane%16) samples pixel n's tap and holds
-// input channels 8j .. 8j+7 -- two 16-byte loads per corner from the NHWC input -- and k-step s of
-// the tap feeds channel 8j + s (the weights are packed in that K order). A wave owns 4 N-tiles
-// (64 pixels); the A fragments (all taps) sit in LDS.
+// channels, N = 16 pixels, K = 9 taps x 32 input channels. Lane (j, n) of the B operand samples
+// pixel n itself and holds channels {4j..4j+3} (k-steps 0-3) and {16+4j..16+4j+3} (k-steps 4-7)
+// of the tap: the weights are packed in that K order, as the kernel's LDS image.
+//
+// Work unit = (image, 8-row band, 16-pixel column step); wave w of the 512-thread block owns row
+// 8*band + w of the unit. Per unit the block stages the source window rows [8*band - 4, +16) x
+// columns [x0 - 4, +24) x 32 channels (48 KB) in LDS, so the 4 bilinear corners of every tap whose
+// offsets stay within the window (|offset| up to ~2 px; the reference's zero-initialised offsets,
+// models/dcn.py:62-64, always) are LDS reads; a wave whose unit has a sample beyond the window runs
+// the same taps with per-lane global fallback gathers. The next unit's window is fetched into
+// registers during the current unit's taps. Window layout: 16-byte chunk c of window pixel P at
+// P*8 + (c ^ (P & 7)), which makes both the staging writes (one 128-byte pixel row per 8 lanes)
+// and the B-layout reads (chunks j and j+4 of 16 pixels per lane group) bank-conflict-free.
+// Per (tap, pixel) sampling records (window index, 4 bilinear weights, mask) are built once per
+// unit and shared by the 4 lanes of a pixel.
 #include "common.h"
+
+#include <algorithm>
 
 namespace tmvs {
 
 namespace dcn {
-constexpr int CI = 32;  // input channels (FeatureNet heads: 4 * base_channels)
-constexpr int NT = 4;   // 16-pixel N-tiles per wave
+constexpr int CI = 32;     // input channels (FeatureNet heads: 4 * base_channels)
+constexpr int WAVES = 8;   // waves per block = rows per unit
+constexpr int TW = 16;     // pixels per wave row
+constexpr int HALO = 4;    // window margin (pixels) on every side
+constexpr int WR = WAVES + 2 * HALO, WC = TW + 2 * HALO;  // window rows, columns
+constexpr int WIN4 = WR * WC * 8;                          // window float4s (8 per pixel)
+constexpr int STAGE = WIN4 / (WAVES * 64);                 // float4 per thread per window copy
+static_assert(WIN4 % (WAVES * 64) == 0, "window copy must split evenly over the block");
+constexpr int NREC = 9 * TW;                               // (tap, pixel) records per wave
 }  // namespace dcn
 
-template <int CO>
-__global__ __launch_bounds__(256) void dcn_kernel(const float* __restrict__ x, const float* __restrict__ om,
-                                                  const float* __restrict__ wpk, const float* __restrict__ bias,
-                                                  const float* __restrict__ alpha, const float* __restrict__ shift,
-                                                  int relu, int H, int W, float* __restrict__ out,
-                                                  float* __restrict__ out_nhwc) {
-  constexpr int MT = (CO + 15) / 16;
-  constexpr int NA = 9 * 8 * MT * 64;
-  __shared__ float wl[NA];  // A fragments [tap][s][mt][lane]
-  const int tid = threadIdx.x, lane = tid & 63;
-  for (int i = tid; i < NA; i += 256) wl[i] = wpk[i];
-  __syncthreads();
-  const int HW = H * W, b = blockIdx.y;
+// Window slot of chunk c of window pixel P.
+__device__ __forceinline__ int dcn_slot(int P, int c) { return P * 8 + (c ^ (P & 7)); }
+
+// The 9 taps of one wave-unit: gather (window LDS; beyond it, global, unless FAST), blend,
+// modulate, MT x 8 MFMAs per tap.
+template <int MT, bool FAST>
+__device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* __restrict__ wl,
+                                         const floatx4_t* __restrict__ win, const floatx4_t* __restrict__ recw,
+                                         const int2* __restrict__ recb, const int2* __restrict__ recyx,
+                                         __amdgpu_buffer_rsrc_t rx, int H, int W, int lane) {
   const int j = lane >> 4, n = lane & 15;
-  const int base = (blockIdx.x * 4 + (tid >> 6)) * (16 * dcn::NT);
-  const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)b * HW * dcn::CI, (unsigned)HW * dcn::CI * 4);
-  const float* omb = om + (size_t)b * 27 * HW;
-  int pix[dcn::NT], yy[dcn::NT], xx[dcn::NT];
-#pragma unroll
-  for (int t = 0; t < dcn::NT; ++t) {
-    pix[t] = min(base + 16 * t + n, HW - 1);
-    yy[t] = pix[t] / W;
-    xx[t] = pix[t] - yy[t] * W;
-  }
-  floatx4_t acc[dcn::NT][MT];
-#pragma unroll
-  for (int t = 0; t < dcn::NT; ++t)
-#pragma unroll
-    for (int m = 0; m < MT; ++m) acc[t][m] = floatx4_t{0.f, 0.f, 0.f, 0.f};
-  const float fH = (float)H, fW = (float)W;
-#pragma unroll 1
-  for (int k = 0; k < 9; ++k) {
-    const int ki = k / 3, kj = k - 3 * ki;
-    float col[dcn::NT][8];
-#pragma unroll
-    for (int t = 0; t < dcn::NT; ++t) {
-      const float dy = omb[(size_t)(2 * k) * HW + pix[t]];
-      const float dx = omb[(size_t)(2 * k + 1) * HW + pix[t]];
-      const float ml = omb[(size_t)(18 + k) * HW + pix[t]];
-      const float mk = 1.f / (1.f + expf(-ml));
-      const float py = (float)(yy[t] + ki - 1) + dy;
-      const float px = (float)(xx[t] + kj - 1) + dx;
-      const bool inside = py > -1.f && py < fH && px > -1.f && px < fW;
-      const float y0 = floorf(py), x0 = floorf(px);
-      const float ly = py - y0, lx = px - x0;
-      const float hy = 1.f - ly, hx = 1.f - lx;
-      const int y0i = (int)fmaxf(fminf(y0, 32766.f), -2.f), x0i = (int)fmaxf(fminf(x0, 32766.f), -2.f);
-      const float w4[4] = {hy * hx, hy * lx, ly * hx, ly * lx};
-      floatx4_t v[4][2];
+  floatx4_t v[2][4][2], w4[2];
+  float mk[2];
+  // gathers of tap k into buffer bb (issued one tap ahead of their use)
+  auto gather = [&](int k, int bb) {
+    const int rr = k * dcn::TW + n;
+    w4[bb] = recw[rr];
+    const int2 bm = recb[rr];  // (window pixel of corner (y0, x0) or -1, mask bits)
+    mk[bb] = __int_as_float(bm.y);
+    if (FAST || bm.x >= 0) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const int cy = y0i + (c >> 1), cx = x0i + (c & 1);
-        const bool ok = inside && (unsigned)cy < (unsigned)H && (unsigned)cx < (unsigned)W;
-        const unsigned o = ok ? ((unsigned)(cy * W + cx) * dcn::CI + 8u * j) * 4u : kOffOut;  // outside: reads 0
-        v[c][0] = buf_load_f32x4(rx, o);
-        v[c][1] = buf_load_f32x4(rx, o + 16u);
+        const int Pc = bm.x + (c >> 1) * dcn::WC + (c & 1);
+        v[bb][c][0] = win[dcn_slot(Pc, j)];
+        v[bb][c][1] = win[dcn_slot(Pc, j + 4)];
       }
+    } else {  // sample beyond the window: global gather (corners outside the image read 0)
+      const int2 yx = recyx[rr];
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        float val = w4[0] * v[0][s >> 2][s & 3];
-        val = val + w4[1] * v[1][s >> 2][s & 3];
-        val = val + w4[2] * v[2][s >> 2][s & 3];
-        val = val + w4[3] * v[3][s >> 2][s & 3];
-        col[t][s] = mk * val;
+      for (int c = 0; c < 4; ++c) {
+        const int cy = yx.x + (c >> 1), cx = yx.y + (c & 1);
+        const bool ok = (unsigned)cy < (unsigned)H && (unsigned)cx < (unsigned)W;
+        const unsigned off = ok ? ((unsigned)(cy * W + cx) * dcn::CI + 4u * j) * 4u : kOffOut;
+        v[bb][c][0] = buf_load_f32x4(rx, off);
+        v[bb][c][1] = buf_load_f32x4(rx, off == kOffOut ? kOffOut : off + 64u);
       }
     }
+  };
+  gather(0, 0);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      float a[MT];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) a[m] = wl[((k * 8 + s) * MT + m) * 64 + lane];
-#pragma unroll
-      for (int t = 0; t < dcn::NT; ++t)
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-          acc[t][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], col[t][s], acc[t][m], 0, 0, 0);
-    }
-  }
-  // D fragment: lane (j, n) holds output channels 16m + 4j .. +3 of pixel n of each N-tile
-#pragma unroll
-  for (int t = 0; t < dcn::NT; ++t) {
-    const int p = base + 16 * t + n;
-    if (p >= HW) continue;
+  for (int k = 0; k < 9; ++k) {
+    const int bb = k & 1;
+    floatx4_t a[MT][2];
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const int co0 = 16 * m + 4 * j;
-      if (co0 >= CO) continue;
-      float r[4];
+      a[m][0] = wl[((k * MT + m) * 2 + 0) * 64 + lane];
+      a[m][1] = wl[((k * MT + m) * 2 + 1) * 64 + lane];
+    }
+    float b[8];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float v = acc[t][m][i] + bias[co0 + i];
-        if (alpha) v = fmaf(v, alpha[co0 + i], shift[co0 + i]);
-        if (relu) v = fmaxf(v, 0.f);
-        r[i] = v;
-        out[((size_t)b * CO + co0 + i) * HW + p] = v;
+    for (int e = 0; e < 8; ++e) {
+      float val = w4[bb][0] * v[bb][0][e >> 2][e & 3];
+      val = val + w4[bb][1] * v[bb][1][e >> 2][e & 3];
+      val = val + w4[bb][2] * v[bb][2][e >> 2][e & 3];
+      val = val + w4[bb][3] * v[bb][3][e >> 2][e & 3];
+      b[e] = mk[bb] * val;
+    }
+    if (k < 8) gather(k + 1, bb ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s >> 2][s & 3], b[s], acc[m], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int CO>
+__global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict__ x, const float* __restrict__ om,
+                                                         const float* __restrict__ wpk,
+                                                         const float* __restrict__ bias,
+                                                         const float* __restrict__ alpha,
+                                                         const float* __restrict__ shift, int relu, int B, int H,
+                                                         int W, float* __restrict__ out,
+                                                         float* __restrict__ out_nhwc) {
+  constexpr int MT = (CO + 15) / 16;
+  constexpr int NA4 = 9 * MT * 2 * 64;  // A fragments [tap][mt][half][lane] float4
+  __shared__ floatx4_t wl[NA4];
+  __shared__ floatx4_t win[dcn::WIN4];                  // swizzled [row][col] pixels of 8 chunks
+  __shared__ floatx4_t recw[dcn::WAVES][dcn::NREC];     // [tap][px] bilinear weights (0 outside)
+  __shared__ int2 recb[dcn::WAVES][dcn::NREC];          // [tap][px] (window pixel | -1, mask bits)
+  __shared__ int2 recyx[dcn::WAVES][dcn::NREC];         // [tap][px] (y0, x0) for global fallback
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < NA4; i += 512) wl[i] = reinterpret_cast<const floatx4_t*>(wpk)[i];
+  const int HW = H * W, nbx = (W + dcn::TW - 1) / dcn::TW, nby = (H + dcn::WAVES - 1) / dcn::WAVES;
+  const int nunits = B * nby * nbx;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int u_begin = (int)((long long)nunits * bid / gridDim.x);
+  const int u_end = (int)((long long)nunits * (bid + 1) / gridDim.x);
+  const int j = lane >> 4, n = lane & 15;  // MFMA layout
+  const float fH = (float)H, fW = (float)W;
+
+  // global -> register copy of a unit's window (zeros outside the image) and of the offsets/mask
+  // logits of the (tap, pixel) records this lane builds (r = lane + 64 i < 144)
+  floatx4_t stg[dcn::STAGE];
+  float omv[9];
+  auto fetch = [&](int u) {
+    const int b = u / (nby * nbx), rem = u - b * (nby * nbx), band = rem / nbx, xs = rem - band * nbx;
+    const int wy0 = band * dcn::WAVES - dcn::HALO, wx0 = xs * dcn::TW - dcn::HALO;
+    const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)b * HW * dcn::CI, (unsigned)HW * dcn::CI * 4);
+#pragma unroll
+    for (int i = 0; i < dcn::STAGE; ++i) {
+      const int idx = tid + 512 * i, pix = idx >> 3, ch = idx & 7;
+      const int r = pix / dcn::WC, c = pix - r * dcn::WC;
+      const int gy = wy0 + r, gx = wx0 + c;
+      const bool ok = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+      stg[i] = buf_load_f32x4(rx, ok ? ((unsigned)(gy * W + gx) * dcn::CI + 4u * ch) * 4u : kOffOut);
+    }
+    const int row = min(band * dcn::WAVES + wv, H - 1), x0t = xs * dcn::TW;
+    const float* omb = om + (size_t)b * 27 * HW + (size_t)row * W + x0t;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int r = lane + 64 * i, tap = r >> 4, px = min(r & 15, W - 1 - x0t);
+      if (r < dcn::NREC) {
+        omv[3 * i + 0] = omb[(size_t)(2 * tap) * HW + px];
+        omv[3 * i + 1] = omb[(size_t)(2 * tap + 1) * HW + px];
+        omv[3 * i + 2] = omb[(size_t)(18 + tap) * HW + px];
       }
-      if (out_nhwc)
-        *reinterpret_cast<float4*>(out_nhwc + ((size_t)b * HW + p) * CO + co0) = make_float4(r[0], r[1], r[2], r[3]);
+    }
+  };
+
+  if (u_begin < u_end) fetch(u_begin);
+  for (int u = u_begin; u < u_end; ++u) {
+    const int b = u / (nby * nbx), rem = u - b * (nby * nbx), band = rem / nbx, xs = rem - band * nbx;
+    const int wy0 = band * dcn::WAVES - dcn::HALO, wx0 = xs * dcn::TW - dcn::HALO;
+    __syncthreads();  // previous unit's window reads are done (and, first time, the weights are staged)
+#pragma unroll
+    for (int i = 0; i < dcn::STAGE; ++i) {
+      const int idx = tid + 512 * i;
+      win[dcn_slot(idx >> 3, idx & 7)] = stg[i];
+    }
+    const int row = band * dcn::WAVES + wv;
+    const int x0t = xs * dcn::TW, nvalid = min(dcn::TW, W - x0t);
+    // sampling records of this wave's 16 pixels x 9 taps: window pixel of corner (y0, x0) (or -1:
+    // beyond the window), the 4 bilinear weights (zero when the sample point is outside the image:
+    // the column is then 0, as in torchvision), the modulation mask, and (y0, x0) for the fallback
+    bool lane_fast = true;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int r = lane + 64 * i;
+      if (r < dcn::NREC) {
+        const int tap = r >> 4, px = r & 15, ki = tap / 3, kj = tap - 3 * ki;
+        const float py = (float)(row + ki - 1) + omv[3 * i + 0];
+        const float pxf = (float)(x0t + min(px, nvalid - 1) + kj - 1) + omv[3 * i + 1];
+        const bool inside = py > -1.f && py < fH && pxf > -1.f && pxf < fW;
+        const float y0 = floorf(py), x0 = floorf(pxf);
+        const float ly = py - y0, lx = pxf - x0;
+        const float hy = 1.f - ly, hx = 1.f - lx;
+        const int y0i = (int)fmaxf(fminf(y0, 32766.f), -2.f), x0i = (int)fmaxf(fminf(x0, 32766.f), -2.f);
+        const int ry = y0i - wy0, rxw = x0i - wx0;
+        const bool inwin = (unsigned)ry < (unsigned)(dcn::WR - 1) && (unsigned)rxw < (unsigned)(dcn::WC - 1);
+        lane_fast = lane_fast && (inwin || !inside);
+        const float mk = 1.f / (1.f + expf(-omv[3 * i + 2]));
+        recb[wv][r] = make_int2(!inside ? 0 : inwin ? ry * dcn::WC + rxw : -1, __float_as_int(mk));
+        recw[wv][r] = inside ? floatx4_t{hy * hx, hy * lx, ly * hx, ly * lx} : floatx4_t{0.f, 0.f, 0.f, 0.f};
+        recyx[wv][r] = make_int2(y0i, x0i);
+      }
+    }
+    // every sample of the wave's unit inside the window: the branch-free tap loop
+    const bool fast = __all(lane_fast);
+    __syncthreads();
+    if (u + 1 < u_end) fetch(u + 1);  // next window in flight during this unit's taps
+
+    if (row < H) {
+      const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)b * HW * dcn::CI, (unsigned)HW * dcn::CI * 4);
+      floatx4_t acc[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+      if (fast)
+        dcn_taps<MT, true>(acc, wl, win, recw[wv], recb[wv], recyx[wv], rx, H, W, lane);
+      else
+        dcn_taps<MT, false>(acc, wl, win, recw[wv], recb[wv], recyx[wv], rx, H, W, lane);
+      // D fragment: lane (j, n) holds output channels 16m + 4j .. +3 of pixel (row, x0t + n)
+      if (n < nvalid) {
+        const int pq = row * W + x0t + n;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int co0 = 16 * m + 4 * j;
+          if (co0 >= CO) continue;
+          float r[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float y = acc[m][i] + bias[co0 + i];
+            if (alpha) y = fmaf(y, alpha[co0 + i], shift[co0 + i]);
+            if (relu) y = fmaxf(y, 0.f);
+            r[i] = y;
+            out[((size_t)b * CO + co0 + i) * HW + pq] = y;
+          }
+          if (out_nhwc)
+            *reinterpret_cast<float4*>(out_nhwc + ((size_t)b * HW + pq) * CO + co0) =
+                make_float4(r[0], r[1], r[2], r[3]);
+        }
+      }
     }
   }
 }
@@ -133,16 +248,20 @@ using namespace tmvs;
 
 extern "C" size_t tmvs_deform_conv2d_packed_floats(int cout) { return (size_t)9 * 8 * ((cout + 15) / 16) * 64; }
 
+// A fragments in the kernel's LDS order [tap k][m-tile][half h][lane l][e], k-step s = 4h + e:
+// lane l holds W[co = 16m + (l & 15)][ci = 16h + 4 (l >> 4) + e][k] (zero for co >= cout).
 extern "C" int tmvs_deform_conv2d_pack(const float* weight, int cout, int cin, float* packed) {
   if (!weight || !packed || cin != dcn::CI || (cout != 8 && cout != 16 && cout != 32)) return TMVS_ERR_ARG;
   const int mt_n = (cout + 15) / 16;
   for (int k = 0; k < 9; ++k)
-    for (int s = 0; s < 8; ++s)
-      for (int mt = 0; mt < mt_n; ++mt)
-        for (int l = 0; l < 64; ++l) {
-          const int co = 16 * mt + (l & 15), ci = 8 * (l >> 4) + s;
-          packed[((k * 8 + s) * mt_n + mt) * 64 + l] = co < cout ? weight[((size_t)co * cin + ci) * 9 + k] : 0.f;
-        }
+    for (int mt = 0; mt < mt_n; ++mt)
+      for (int h = 0; h < 2; ++h)
+        for (int l = 0; l < 64; ++l)
+          for (int e = 0; e < 4; ++e) {
+            const int co = 16 * mt + (l & 15), ci = 16 * h + 4 * (l >> 4) + e;
+            packed[((((size_t)k * mt_n + mt) * 2 + h) * 64 + l) * 4 + e] =
+                co < cout ? weight[((size_t)co * cin + ci) * 9 + k] : 0.f;
+          }
   return TMVS_OK;
 }
 
@@ -155,12 +274,27 @@ extern "C" int tmvs_deform_conv2d(const float* x_nhwc, const float* offset_mask,
   if ((bn_alpha == nullptr) != (bn_shift == nullptr)) return TMVS_ERR_ARG;
   if (cin != dcn::CI || (cout != 8 && cout != 16 && cout != 32)) return TMVS_ERR_SHAPE;
   if ((long long)height * width * cin * 4 >= (1LL << 31) || height > 32766 || width > 32766) return TMVS_ERR_SHAPE;
-  const int HW = height * width;
-  const dim3 grid((HW + 4 * 16 * dcn::NT - 1) / (4 * 16 * dcn::NT), batch);
   hipStream_t st = (hipStream_t)stream;
-#define TMVS_DCN(CO)                                                                                             \
-  hipLaunchKernelGGL(dcn_kernel<CO>, grid, dim3(256), 0, st, x_nhwc, offset_mask, w_packed, bias, bn_alpha, \
-                     bn_shift, relu, height, width, out, out_nhwc)
+  // persistent grid: one block per CU slot the kernel's LDS/VGPR footprint allows
+  static int grid_cache[3] = {0, 0, 0};
+  const int ci = cout == 32 ? 0 : cout == 16 ? 1 : 2;
+  if (!grid_cache[ci]) {
+    int dev = 0, ncu = 0, occ = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return TMVS_ERR_HIP;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cout == 32)
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dcn_window_kernel<32>, 512, 0);
+    else if (cout == 16)
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dcn_window_kernel<16>, 512, 0);
+    else
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dcn_window_kernel<8>, 512, 0);
+    grid_cache[ci] = std::max(1, ncu * std::max(occ, 1));
+  }
+  const long long nunits = (long long)batch * ((height + dcn::WAVES - 1) / dcn::WAVES) * ((width + dcn::TW - 1) / dcn::TW);
+  const int nblk = (int)std::min<long long>(grid_cache[ci], nunits);
+#define TMVS_DCN(CO)                                                                                           \
+  hipLaunchKernelGGL(dcn_window_kernel<CO>, dim3(nblk), dim3(512), 0, st, x_nhwc, offset_mask, w_packed, bias, \
+                     bn_alpha, bn_shift, relu, batch, height, width, out, out_nhwc)
   if (cout == 32)
     TMVS_DCN(32);
   else if (cout == 16)
