@@ -43,6 +43,8 @@ def _args():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--profile-steps", type=int, default=3)
     ap.add_argument("--no-overlap", action="store_true", help="run the FMT pathway on the main stream (A/B)")
+    ap.add_argument("--e2e-steps", type=int, default=10,
+                    help="timed full forward() passes (images -> depth, FeatureNet included); 0 = skip")
     return ap.parse_args()
 
 
@@ -149,6 +151,8 @@ def main():
         model.decomposed = False
         spans = timer.durations()
 
+        e2e = end_to_end(model, args.e2e_steps, proj, dv_dev, dev) if args.e2e_steps > 0 and shard is None else None
+
     maps_per_step = 1 if args.mode == "views" else world
     value = maps_per_step * args.steps / elapsed
     per_kernel = {}
@@ -220,10 +224,38 @@ def main():
             "kernel_ms_per_depth_map": breakdown,
             "cpu_baseline": cpu,
             "abs_depth_l1_vs_ref": l1,
+            "end_to_end": e2e,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def end_to_end(model, steps, proj, dv_dev, dev):
+    """The whole TransMVSNet.forward (images -> depth, FeatureNet + DCN included) beside the hot-path
+    step: synthetic U[0,1) images [1,N,3,H,W] resident in HBM, HIP events on the current stream,
+    median of `steps` after 2 warm-ups. FeatureNet alone is timed the same way."""
+    from transmvsnet_amd import synthetic
+    imgs = synthetic.synthetic_images(NVIEWS, H, W).to(dev)
+
+    def timed(fn):
+        ts = []
+        for i in range(steps + 2):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            if i >= 2:
+                ts.append(e0.elapsed_time(e1))
+        return float(np.median(ts))
+
+    t_all = timed(lambda: model.forward(imgs, proj, dv_dev))
+    t_feat = timed(lambda: model.feature(imgs.reshape(NVIEWS, 3, H, W)))
+    return {"depth_maps_per_s": round(1e3 / t_all, 3), "ms_per_depth_map": round(t_all, 3),
+            "featurenet_ms": round(t_feat, 3), "steps": steps,
+            "workload": "TransMVSNet.forward(imgs [1,5,3,864,1152], proj, depth_values): FeatureNet (MIOpen "
+                        "convs + tmvs_deform_conv2d) + the hot path above"}
 
 
 def cpu_baseline(threads, feats_cpu, proj, dv, gpu_out):
