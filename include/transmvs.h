@@ -222,12 +222,38 @@ int tmvs_depth_stage(const float* depth_values, int n_values, const float* prev_
  *                 packing of the [cout][cin][3][3] weight; copy to the device once per load_state_dict)
  *   bias        : [cout]; bn_alpha / bn_shift: [cout] or both NULL; relu: 0/1
  *   out         : [B][cout][H][W] (NCHW);  out_nhwc: optional [B][H][W][cout] copy, or NULL
- * Supported: cin = 32, cout in {8, 16, 32}; H*W*cin*4 < 2^31; H, W <= 32766.                      */
+ * Supported: cin = 32, cout in {8, 16, 32}; H*W*cin*4 < 2^31; H, W <= 32766. tmvs_deform_conv2d_pack also
+ * takes cout = 27 (a conv_offset_mask weight, for tmvs_dcn_fused).                                */
 size_t tmvs_deform_conv2d_packed_floats(int cout);
 int tmvs_deform_conv2d_pack(const float* weight, int cout, int cin, float* packed);
 int tmvs_deform_conv2d(const float* x_nhwc, const float* offset_mask, const float* w_packed, const float* bias,
                        const float* bn_alpha, const float* bn_shift, int relu, int batch, int cin, int cout,
                        int height, int width, float* out, float* out_nhwc, void* stream);
+
+/* The whole DCN.forward (models/dcn.py:66-80) in one launch: conv_offset_mask (3x3, 32 -> 27, bias;
+ * models/dcn.py:58-64) computed in-kernel from the same staged input window, then the modulated
+ * deformable convolution as above. The [B][27][H][W] offset/mask tensor never reaches HBM.
+ *   wom_packed : tmvs_deform_conv2d_packed_floats(27) floats = tmvs_deform_conv2d_pack(conv_offset_mask.weight,
+ *                27, 32, ...);  bom: conv_offset_mask.bias [27]
+ *   out (NCHW) and out_nhwc are both optional (at least one).                                        */
+int tmvs_dcn_fused(const float* x_nhwc, const float* wom_packed, const float* bom, const float* w_packed,
+                   const float* bias, const float* bn_alpha, const float* bn_shift, int relu, int batch, int cin,
+                   int cout, int height, int width, float* out, float* out_nhwc, void* stream);
+
+/* FeatureNet heads' first layer Conv2d(32, 32, 3, 1, 1, bias=False) -> BatchNorm -> ReLU
+ * (models/module.py:24-61 as used at :373 / :385), NHWC: x_nhwc [B][H][W][32] -> out [B][32][H][W]
+ * and/or out_nhwc [B][H][W][32] (either may be NULL, not both). w_packed = tmvs_deform_conv2d_pack of
+ * the [32][32][3][3] weight; bias optional (NULL for the reference's bias-free conv).            */
+int tmvs_conv3x3_nhwc(const float* x_nhwc, const float* w_packed, const float* bias, const float* bn_alpha,
+                      const float* bn_shift, int relu, int batch, int cin, int cout, int height, int width,
+                      float* out, float* out_nhwc, void* stream);
+
+/* FeatureNet FPN merge (models/module.py:409-417): intra = interpolate(prev, 2, nearest) + inner(lat),
+ * inner = Conv2d(lat_channels, 32, 1, bias=True) with w_inner [32][lat_channels], b_inner [32].
+ * prev_nhwc [B][height][width][32], lat_nhwc [B][2 height][2 width][lat_channels] (8 or 16),
+ * out_nhwc [B][2 height][2 width][32].                                                            */
+int tmvs_fpn_merge(const float* prev_nhwc, const float* lat_nhwc, int lat_channels, const float* w_inner,
+                   const float* b_inner, int batch, int height, int width, float* out_nhwc, void* stream);
 
 #ifdef __cplusplus
 }

@@ -46,6 +46,52 @@ def test_deform_conv2d_random_offsets(cout, bn, relu):
     np.testing.assert_array_equal(to_np(out_nhwc), to_np(out.permute(0, 2, 3, 1)))
 
 
+@pytest.mark.parametrize("cout,bn,relu,h,w", [(32, True, True, 20, 28), (16, False, False, 37, 45),
+                                              (8, True, False, 9, 70), (32, False, True, 64, 48)])
+def test_dcn_fused_vs_oracle(cout, bn, relu, h, w):
+    """tmvs_dcn_fused: conv_offset_mask (3x3, 32 -> 27, bias) in-kernel + deform_conv2d, against the
+    oracle's F.conv2d + deform_conv2d. Offsets of several pixels (samples beyond the LDS window take
+    the global fallback), ragged H/W (partial 16-pixel steps and 8-row bands). Tolerance: the DCN's
+    2e-5 abs + 1e-5 rel, widened to 5e-5 abs since the offsets themselves carry MFMA-order rounding."""
+    torch.manual_seed(100 + cout + h)
+    b = 2
+    x = torch.randn(b, 32, h, w)
+    wom = torch.randn(27, 32, 3, 3) * 0.05
+    bom = torch.randn(27) * 0.5
+    weight = torch.randn(cout, 32, 3, 3) * 0.06
+    bias = torch.randn(cout) * 0.1
+    om = F.conv2d(x, wom, bom, padding=1)
+    ref = oracle.deform_conv2d(x, om[:, :18], weight, bias, 1, torch.sigmoid(om[:, 18:]))
+    fold = None
+    if bn:
+        gamma, beta = torch.rand(cout) + 0.5, torch.randn(cout) * 0.1
+        mean, var = torch.randn(cout) * 0.1, torch.rand(cout) + 0.5
+        ref = F.batch_norm(ref, mean, var, gamma, beta, False, 0.1, 1e-5)
+        a, s_ = ops.bn_fold(gamma, beta, mean, var)
+        fold = (torch.from_numpy(a).to(DEV), torch.from_numpy(s_).to(DEV))
+    if relu:
+        ref = F.relu(ref)
+    out, out_nhwc = ops.dcn_fused(x.permute(0, 2, 3, 1).contiguous().to(DEV), ops.deform_conv2d_pack(wom).to(DEV),
+                                  bom.to(DEV), ops.deform_conv2d_pack(weight).to(DEV), bias.to(DEV), cout, bn=fold,
+                                  relu=relu, want_nchw=True, want_nhwc=True)
+    np.testing.assert_allclose(to_np(out), to_np(ref), rtol=1e-5, atol=5e-5)
+    np.testing.assert_array_equal(to_np(out_nhwc), to_np(out.permute(0, 2, 3, 1)))
+
+
+def test_dcn_fused_zero_offsets_is_masked_conv():
+    """The reference's initial state (zero offset/mask conv, models/dcn.py:62-64): every tap samples an
+    integer position with mask sigmoid(0) = 0.5, i.e. 0.5 * conv2d(x, W) + bias."""
+    torch.manual_seed(7)
+    x = torch.randn(3, 32, 24, 40)
+    weight = torch.randn(32, 32, 3, 3) * 0.06
+    bias = torch.randn(32) * 0.1
+    ref = F.conv2d(0.5 * x, weight, bias, padding=1)
+    out, _ = ops.dcn_fused(x.permute(0, 2, 3, 1).contiguous().to(DEV),
+                           ops.deform_conv2d_pack(torch.zeros(27, 32, 3, 3)).to(DEV), torch.zeros(27, device=DEV),
+                           ops.deform_conv2d_pack(weight).to(DEV), bias.to(DEV), 32)
+    np.testing.assert_allclose(to_np(out), to_np(ref), rtol=1e-5, atol=2e-5)
+
+
 def test_featurenet_nonzero_offsets_vs_oracle():
     """Whole FeatureNet (3 scales, 9 DCNs) with trained-like nonzero offset/mask convs, 2 views batched."""
     m = TransMVSNet().eval()
@@ -63,3 +109,36 @@ def test_featurenet_nonzero_offsets_vs_oracle():
             ref = oracle.feature_net(sd, imgs[v:v + 1])
             for s in ("stage1", "stage2", "stage3"):
                 np.testing.assert_allclose(to_np(out[s][v:v + 1]), to_np(ref[s]), rtol=0, atol=1e-4, err_msg=s)
+
+
+def test_conv3x3_nhwc_bn_relu():
+    """tmvs_conv3x3_nhwc = Conv2d(32, 32, 3, 1, 1, bias=False) -> eval BN -> ReLU (models/module.py:24-61),
+    ragged sizes; 2e-5 abs + 1e-5 rel (MFMA K-order vs the CPU conv)."""
+    torch.manual_seed(3)
+    for (b, h, w) in ((2, 20, 28), (1, 9, 70), (3, 33, 17)):
+        x = torch.randn(b, 32, h, w)
+        weight = torch.randn(32, 32, 3, 3) * 0.06
+        gamma, beta = torch.rand(32) + 0.5, torch.randn(32) * 0.1
+        mean, var = torch.randn(32) * 0.1, torch.rand(32) + 0.5
+        ref = F.relu(F.batch_norm(F.conv2d(x, weight, padding=1), mean, var, gamma, beta, False, 0.1, 1e-5))
+        a, s_ = ops.bn_fold(gamma, beta, mean, var)
+        fold = (torch.from_numpy(a).to(DEV), torch.from_numpy(s_).to(DEV))
+        out, out_nhwc = ops.conv3x3_nhwc(x.permute(0, 2, 3, 1).contiguous().to(DEV), ops.deform_conv2d_pack(weight).to(DEV),
+                                         bn=fold, relu=True, want_nchw=True, want_nhwc=True)
+        np.testing.assert_allclose(to_np(out), to_np(ref), rtol=1e-5, atol=2e-5)
+        np.testing.assert_array_equal(to_np(out_nhwc), to_np(out.permute(0, 2, 3, 1)))
+
+
+@pytest.mark.parametrize("cl", [8, 16])
+def test_fpn_merge(cl):
+    """tmvs_fpn_merge = interpolate(prev, 2, nearest) + Conv2d(cl, 32, 1, bias) (models/module.py:413,417)."""
+    torch.manual_seed(cl)
+    b, h, w = 2, 11, 13
+    prev = torch.randn(b, 32, h, w)
+    lat = torch.randn(b, cl, 2 * h, 2 * w)
+    conv = torch.nn.Conv2d(cl, 32, 1, bias=True)
+    with torch.no_grad():
+        ref = F.interpolate(prev, scale_factor=2.0, mode="nearest") + conv(lat)
+    out = ops.fpn_merge(prev.permute(0, 2, 3, 1).contiguous().to(DEV), lat.permute(0, 2, 3, 1).contiguous().to(DEV),
+                        conv.weight.detach().reshape(32, cl).contiguous().to(DEV), conv.bias.detach().to(DEV))
+    np.testing.assert_allclose(to_np(out), to_np(ref.permute(0, 2, 3, 1)), rtol=1e-5, atol=1e-5)

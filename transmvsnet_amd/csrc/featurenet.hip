@@ -52,8 +52,8 @@ __device__ __forceinline__ int dcn_slot(int P, int c) { return P * 8 + (c ^ (P &
 template <int MT, bool FAST>
 __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* __restrict__ wl,
                                          const floatx4_t* __restrict__ win, const floatx4_t* __restrict__ recw,
-                                         const int2* __restrict__ recb, const int2* __restrict__ recyx,
-                                         __amdgpu_buffer_rsrc_t rx, int H, int W, int lane) {
+                                         const int2* __restrict__ recb, __amdgpu_buffer_rsrc_t rx, int H, int W,
+                                         int lane) {
   const int j = lane >> 4, n = lane & 15;
   floatx4_t v[2][4][2], w4[2];
   float mk[2];
@@ -61,7 +61,7 @@ __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* 
   auto gather = [&](int k, int bb) {
     const int rr = k * dcn::TW + n;
     w4[bb] = recw[rr];
-    const int2 bm = recb[rr];  // (window pixel of corner (y0, x0) or -1, mask bits)
+    const int2 bm = recb[rr];  // (window pixel of corner (y0, x0) | fallback code, mask bits)
     mk[bb] = __int_as_float(bm.y);
     if (FAST || bm.x >= 0) {
 #pragma unroll
@@ -71,10 +71,10 @@ __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* 
         v[bb][c][1] = win[dcn_slot(Pc, j + 4)];
       }
     } else {  // sample beyond the window: global gather (corners outside the image read 0)
-      const int2 yx = recyx[rr];
+      const int code = -1 - bm.x, y0 = (code >> 15) - 1, x0 = (code & 32767) - 1;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const int cy = yx.x + (c >> 1), cx = yx.y + (c & 1);
+        const int cy = y0 + (c >> 1), cx = x0 + (c & 1);
         const bool ok = (unsigned)cy < (unsigned)H && (unsigned)cx < (unsigned)W;
         const unsigned off = ok ? ((unsigned)(cy * W + cx) * dcn::CI + 4u * j) * 4u : kOffOut;
         v[bb][c][0] = buf_load_f32x4(rx, off);
@@ -112,8 +112,12 @@ __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* 
   }
 }
 
-template <int CO>
+// FUSED: the DCN's offset/mask conv (conv_offset_mask, models/dcn.py:58-64: 3x3, 32 -> 27, bias)
+// is computed in-kernel from the same LDS window (implicit GEMM on MFMA, M = 27 padded to 32), so
+// the [27][H][W] offset/mask tensor never exists in HBM; otherwise `om` is read from global.
+template <int CO, bool FUSED>
 __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict__ x, const float* __restrict__ om,
+                                                         const float* __restrict__ wom, const float* __restrict__ bom,
                                                          const float* __restrict__ wpk,
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ alpha,
@@ -122,13 +126,17 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
                                                          float* __restrict__ out_nhwc) {
   constexpr int MT = (CO + 15) / 16;
   constexpr int NA4 = 9 * MT * 2 * 64;  // A fragments [tap][mt][half][lane] float4
+  constexpr int NO4 = FUSED ? 9 * 2 * 2 * 64 : 1;  // offset-conv A fragments (27 rows padded to 32)
   __shared__ floatx4_t wl[NA4];
+  __shared__ floatx4_t wo[NO4];
   __shared__ floatx4_t win[dcn::WIN4];                  // swizzled [row][col] pixels of 8 chunks
   __shared__ floatx4_t recw[dcn::WAVES][dcn::NREC];     // [tap][px] bilinear weights (0 outside)
-  __shared__ int2 recb[dcn::WAVES][dcn::NREC];          // [tap][px] (window pixel | -1, mask bits)
-  __shared__ int2 recyx[dcn::WAVES][dcn::NREC];         // [tap][px] (y0, x0) for global fallback
+                                                        // (FUSED: first the [px][32] offset/mask tile)
+  __shared__ int2 recb[dcn::WAVES][dcn::NREC];          // [tap][px] (window pixel | fallback code, mask bits)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int i = tid; i < NA4; i += 512) wl[i] = reinterpret_cast<const floatx4_t*>(wpk)[i];
+  if (FUSED)
+    for (int i = tid; i < NO4; i += 512) wo[i] = reinterpret_cast<const floatx4_t*>(wom)[i];
   const int HW = H * W, nbx = (W + dcn::TW - 1) / dcn::TW, nby = (H + dcn::WAVES - 1) / dcn::WAVES;
   const int nunits = B * nby * nbx;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -137,8 +145,8 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
   const int j = lane >> 4, n = lane & 15;  // MFMA layout
   const float fH = (float)H, fW = (float)W;
 
-  // global -> register copy of a unit's window (zeros outside the image) and of the offsets/mask
-  // logits of the (tap, pixel) records this lane builds (r = lane + 64 i < 144)
+  // global -> register copy of a unit's window (zeros outside the image) and (not FUSED) of the
+  // offsets/mask logits of the (tap, pixel) records this lane builds (r = lane + 64 i < 144)
   floatx4_t stg[dcn::STAGE];
   float omv[9];
   auto fetch = [&](int u) {
@@ -153,15 +161,17 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
       const bool ok = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
       stg[i] = buf_load_f32x4(rx, ok ? ((unsigned)(gy * W + gx) * dcn::CI + 4u * ch) * 4u : kOffOut);
     }
-    const int row = min(band * dcn::WAVES + wv, H - 1), x0t = xs * dcn::TW;
-    const float* omb = om + (size_t)b * 27 * HW + (size_t)row * W + x0t;
+    if (!FUSED) {
+      const int row = min(band * dcn::WAVES + wv, H - 1), x0t = xs * dcn::TW;
+      const float* omb = om + (size_t)b * 27 * HW + (size_t)row * W + x0t;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int r = lane + 64 * i, tap = r >> 4, px = min(r & 15, W - 1 - x0t);
-      if (r < dcn::NREC) {
-        omv[3 * i + 0] = omb[(size_t)(2 * tap) * HW + px];
-        omv[3 * i + 1] = omb[(size_t)(2 * tap + 1) * HW + px];
-        omv[3 * i + 2] = omb[(size_t)(18 + tap) * HW + px];
+      for (int i = 0; i < 3; ++i) {
+        const int r = lane + 64 * i, tap = r >> 4, px = min(r & 15, W - 1 - x0t);
+        if (r < dcn::NREC) {
+          omv[3 * i + 0] = omb[(size_t)(2 * tap) * HW + px];
+          omv[3 * i + 1] = omb[(size_t)(2 * tap + 1) * HW + px];
+          omv[3 * i + 2] = omb[(size_t)(18 + tap) * HW + px];
+        }
       }
     }
   };
@@ -176,11 +186,58 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
       const int idx = tid + 512 * i;
       win[dcn_slot(idx >> 3, idx & 7)] = stg[i];
     }
+    __syncthreads();
+    if (u + 1 < u_end) fetch(u + 1);  // next window in flight during this unit's work
     const int row = band * dcn::WAVES + wv;
     const int x0t = xs * dcn::TW, nvalid = min(dcn::TW, W - x0t);
-    // sampling records of this wave's 16 pixels x 9 taps: window pixel of corner (y0, x0) (or -1:
-    // beyond the window), the 4 bilinear weights (zero when the sample point is outside the image:
-    // the column is then 0, as in torchvision), the modulation mask, and (y0, x0) for the fallback
+    if (row >= H) continue;
+    if (FUSED) {
+      // conv_offset_mask of this wave's 16 pixels from the window: B lane (j, n) = chunks j, j+4 of
+      // window pixel (wv + HALO + ki - 1, HALO + n + kj - 1); D lane (j, n) = channels 16m + 4j + i
+      floatx4_t ao[2] = {floatx4_t{0.f, 0.f, 0.f, 0.f}, floatx4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int ki = k / 3, kj = k - 3 * ki;
+        const int P = (wv + dcn::HALO + ki - 1) * dcn::WC + dcn::HALO + n + kj - 1;
+        const floatx4_t b0 = win[dcn_slot(P, j)], b1 = win[dcn_slot(P, j + 4)];
+        floatx4_t a[2][2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          a[m][0] = wo[((k * 2 + m) * 2 + 0) * 64 + lane];
+          a[m][1] = wo[((k * 2 + m) * 2 + 1) * 64 + lane];
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+            ao[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s >> 2][s & 3], s < 4 ? b0[s] : b1[s - 4], ao[m], 0,
+                                                         0, 0);
+      }
+      float* omt = reinterpret_cast<float*>(recw[wv]);  // [px][32] tile, consumed before the records
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        floatx4_t o = ao[m];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 16 * m + 4 * j + i;
+          o[i] = o[i] + (c < 27 ? bom[c] : 0.f);
+        }
+        *reinterpret_cast<floatx4_t*>(omt + n * 32 + 16 * m + 4 * j) = o;
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int r = lane + 64 * i;
+        if (r < dcn::NREC) {
+          const int tap = r >> 4, px = r & 15;
+          omv[3 * i + 0] = omt[px * 32 + 2 * tap];
+          omv[3 * i + 1] = omt[px * 32 + 2 * tap + 1];
+          omv[3 * i + 2] = omt[px * 32 + 18 + tap];
+        }
+      }
+    }
+    // sampling records of this wave's 16 pixels x 9 taps: window pixel of corner (y0, x0), or for a
+    // sample beyond the window -1 - ((y0 + 1) << 15 | (x0 + 1)); the 4 bilinear weights (zero when
+    // the sample point is outside the image: the column is then 0, as in torchvision); the mask
     bool lane_fast = true;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -198,48 +255,186 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
         const bool inwin = (unsigned)ry < (unsigned)(dcn::WR - 1) && (unsigned)rxw < (unsigned)(dcn::WC - 1);
         lane_fast = lane_fast && (inwin || !inside);
         const float mk = 1.f / (1.f + expf(-omv[3 * i + 2]));
-        recb[wv][r] = make_int2(!inside ? 0 : inwin ? ry * dcn::WC + rxw : -1, __float_as_int(mk));
+        // inside => y0 in [-1, H-1], x0 in [-1, W-1]: the fallback code fits 30 bits
+        const int code = !inside ? 0 : inwin ? ry * dcn::WC + rxw : -1 - (((y0i + 1) << 15) | (x0i + 1));
+        recb[wv][r] = make_int2(code, __float_as_int(mk));
         recw[wv][r] = inside ? floatx4_t{hy * hx, hy * lx, ly * hx, ly * lx} : floatx4_t{0.f, 0.f, 0.f, 0.f};
-        recyx[wv][r] = make_int2(y0i, x0i);
       }
     }
     // every sample of the wave's unit inside the window: the branch-free tap loop
     const bool fast = __all(lane_fast);
-    __syncthreads();
-    if (u + 1 < u_end) fetch(u + 1);  // next window in flight during this unit's taps
-
-    if (row < H) {
-      const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)b * HW * dcn::CI, (unsigned)HW * dcn::CI * 4);
-      floatx4_t acc[MT];
+    const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)b * HW * dcn::CI, (unsigned)HW * dcn::CI * 4);
+    floatx4_t acc[MT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) acc[m] = floatx4_t{0.f, 0.f, 0.f, 0.f};
-      if (fast)
-        dcn_taps<MT, true>(acc, wl, win, recw[wv], recb[wv], recyx[wv], rx, H, W, lane);
-      else
-        dcn_taps<MT, false>(acc, wl, win, recw[wv], recb[wv], recyx[wv], rx, H, W, lane);
-      // D fragment: lane (j, n) holds output channels 16m + 4j .. +3 of pixel (row, x0t + n)
-      if (n < nvalid) {
-        const int pq = row * W + x0t + n;
+    for (int m = 0; m < MT; ++m) acc[m] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+    if (fast)
+      dcn_taps<MT, true>(acc, wl, win, recw[wv], recb[wv], rx, H, W, lane);
+    else
+      dcn_taps<MT, false>(acc, wl, win, recw[wv], recb[wv], rx, H, W, lane);
+    // D fragment: lane (j, n) holds output channels 16m + 4j .. +3 of pixel (row, x0t + n)
+    if (n < nvalid) {
+      const int pq = row * W + x0t + n;
 #pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          const int co0 = 16 * m + 4 * j;
-          if (co0 >= CO) continue;
-          float r[4];
+      for (int m = 0; m < MT; ++m) {
+        const int co0 = 16 * m + 4 * j;
+        if (co0 >= CO) continue;
+        float r[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float y = acc[m][i] + bias[co0 + i];
-            if (alpha) y = fmaf(y, alpha[co0 + i], shift[co0 + i]);
-            if (relu) y = fmaxf(y, 0.f);
-            r[i] = y;
-            out[((size_t)b * CO + co0 + i) * HW + pq] = y;
-          }
-          if (out_nhwc)
-            *reinterpret_cast<float4*>(out_nhwc + ((size_t)b * HW + pq) * CO + co0) =
-                make_float4(r[0], r[1], r[2], r[3]);
+        for (int i = 0; i < 4; ++i) {
+          float y = acc[m][i] + bias[co0 + i];
+          if (alpha) y = fmaf(y, alpha[co0 + i], shift[co0 + i]);
+          if (relu) y = fmaxf(y, 0.f);
+          r[i] = y;
+          if (out) out[((size_t)b * CO + co0 + i) * HW + pq] = y;
         }
+        if (out_nhwc)
+          *reinterpret_cast<float4*>(out_nhwc + ((size_t)b * HW + pq) * CO + co0) = make_float4(r[0], r[1], r[2], r[3]);
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The heads' first layer Conv2d(32, 32, 3, 1, 1, bias=False) + BatchNorm + ReLU (models/module.py:24-61,
+// 373/385) in NHWC: the DCN kernel's unit/window scheme with a 1-pixel halo (23 KB window, two
+// blocks per CU) and its B-layout window reads feeding MFMA directly (the weights packed as a DCN
+// weight). Output NHWC (the next DCN's input) and optionally NCHW.
+namespace c3 {
+constexpr int HALO = 1;
+constexpr int WR = dcn::WAVES + 2 * HALO, WC = dcn::TW + 2 * HALO;
+constexpr int WIN4 = WR * WC * 8;
+constexpr int STAGE = (WIN4 + 511) / 512;
+}  // namespace c3
+
+__global__ __launch_bounds__(512) void conv3x3_window_kernel(const float* __restrict__ x,
+                                                             const float* __restrict__ wpk,
+                                                             const float* __restrict__ bias,
+                                                             const float* __restrict__ alpha,
+                                                             const float* __restrict__ shift, int relu, int B, int H,
+                                                             int W, float* __restrict__ out,
+                                                             float* __restrict__ out_nhwc) {
+  constexpr int NA4 = 9 * 2 * 2 * 64;
+  __shared__ floatx4_t wl[NA4];
+  __shared__ floatx4_t win[c3::WIN4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < NA4; i += 512) wl[i] = reinterpret_cast<const floatx4_t*>(wpk)[i];
+  const int HW = H * W, nbx = (W + dcn::TW - 1) / dcn::TW, nby = (H + dcn::WAVES - 1) / dcn::WAVES;
+  const int nunits = B * nby * nbx;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int u_begin = (int)((long long)nunits * bid / gridDim.x);
+  const int u_end = (int)((long long)nunits * (bid + 1) / gridDim.x);
+  const int j = lane >> 4, n = lane & 15;
+  floatx4_t stg[c3::STAGE];
+  auto fetch = [&](int u) {
+    const int b = u / (nby * nbx), rem = u - b * (nby * nbx), band = rem / nbx, xs = rem - band * nbx;
+    const int wy0 = band * dcn::WAVES - c3::HALO, wx0 = xs * dcn::TW - c3::HALO;
+    const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)b * HW * dcn::CI, (unsigned)HW * dcn::CI * 4);
+#pragma unroll
+    for (int i = 0; i < c3::STAGE; ++i) {
+      const int idx = min(tid + 512 * i, c3::WIN4 - 1), pix = idx >> 3, ch = idx & 7;
+      const int r = pix / c3::WC, c = pix - r * c3::WC;
+      const int gy = wy0 + r, gx = wx0 + c;
+      const bool ok = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+      stg[i] = buf_load_f32x4(rx, ok ? ((unsigned)(gy * W + gx) * dcn::CI + 4u * ch) * 4u : kOffOut);
+    }
+  };
+  if (u_begin < u_end) fetch(u_begin);
+  for (int u = u_begin; u < u_end; ++u) {
+    const int b = u / (nby * nbx), rem = u - b * (nby * nbx), band = rem / nbx, xs = rem - band * nbx;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < c3::STAGE; ++i) {
+      const int idx = tid + 512 * i;
+      if (idx < c3::WIN4) win[dcn_slot(idx >> 3, idx & 7)] = stg[i];
+    }
+    __syncthreads();
+    if (u + 1 < u_end) fetch(u + 1);
+    const int row = band * dcn::WAVES + wv;
+    const int x0t = xs * dcn::TW, nvalid = min(dcn::TW, W - x0t);
+    if (row >= H) continue;
+    floatx4_t acc[2] = {floatx4_t{0.f, 0.f, 0.f, 0.f}, floatx4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int ki = k / 3, kj = k - 3 * ki;
+      const int P = (wv + c3::HALO + ki - 1) * c3::WC + c3::HALO + n + kj - 1;
+      const floatx4_t b0 = win[dcn_slot(P, j)], b1 = win[dcn_slot(P, j + 4)];
+      floatx4_t a[2][2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        a[m][0] = wl[((k * 2 + m) * 2 + 0) * 64 + lane];
+        a[m][1] = wl[((k * 2 + m) * 2 + 1) * 64 + lane];
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s >> 2][s & 3], s < 4 ? b0[s] : b1[s - 4], acc[m], 0, 0,
+                                                        0);
+    }
+    if (n < nvalid) {
+      const int pq = row * W + x0t + n;
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int co0 = 16 * m + 4 * j;
+        float r[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float y = acc[m][i];
+          if (bias) y = y + bias[co0 + i];
+          if (alpha) y = fmaf(y, alpha[co0 + i], shift[co0 + i]);
+          if (relu) y = fmaxf(y, 0.f);
+          r[i] = y;
+          if (out) out[((size_t)b * 32 + co0 + i) * HW + pq] = y;
+        }
+        if (out_nhwc)
+          *reinterpret_cast<float4*>(out_nhwc + ((size_t)b * HW + pq) * 32 + co0) = make_float4(r[0], r[1], r[2], r[3]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// FPN merge of FeatureNet.forward (models/module.py:409-417):
+//   intra = interpolate(prev, scale 2, nearest) + inner(lat)      inner = Conv2d(cl, 32, 1, bias=True)
+// NHWC in and out: prev [B][h][w][32], lat [B][2h][2w][cl], out [B][2h][2w][32]. Four lanes per
+// pixel, 8 output channels each; inner's weights/bias in LDS. HBM-bound elementwise work.
+template <int CL>
+__global__ __launch_bounds__(256) void fpn_merge_kernel(const float* __restrict__ prev, const float* __restrict__ lat,
+                                                        const float* __restrict__ wi, const float* __restrict__ bi,
+                                                        int B, int h, int w, float* __restrict__ out) {
+  __shared__ float ws[32 * CL + 32];
+  for (int i = threadIdx.x; i < 32 * CL; i += 256) ws[i] = wi[i];  // [co][ci]
+  if (threadIdx.x < 32) ws[32 * CL + threadIdx.x] = bi[threadIdx.x];
+  __syncthreads();
+  const int H2 = 2 * h, W2 = 2 * w;
+  const long long npix = (long long)B * H2 * W2;
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long pix = t >> 2;
+  if (pix >= npix) return;
+  const int g = (int)(t & 3);  // output channels 8g .. 8g+7
+  const int b = (int)(pix / ((long long)H2 * W2));
+  const int rem = (int)(pix - (long long)b * H2 * W2), y = rem / W2, xx = rem - y * W2;
+  float lv[CL];
+#pragma unroll
+  for (int c = 0; c < CL; c += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(lat + pix * CL + c);
+    lv[c] = v.x; lv[c + 1] = v.y; lv[c + 2] = v.z; lv[c + 3] = v.w;
+  }
+  const float* pv = prev + (((size_t)b * h + (y >> 1)) * w + (xx >> 1)) * 32 + 8 * g;
+  const float4 p0 = *reinterpret_cast<const float4*>(pv), p1 = *reinterpret_cast<const float4*>(pv + 4);
+  const float up[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+  float r[8];
+#pragma unroll
+  for (int o = 0; o < 8; ++o) {
+    const int co = 8 * g + o;
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < CL; ++c) acc = fmaf(ws[co * CL + c], lv[c], acc);
+    r[o] = up[o] + (acc + ws[32 * CL + co]);
+  }
+  float* ov = out + pix * 32 + 8 * g;
+  *reinterpret_cast<float4*>(ov) = make_float4(r[0], r[1], r[2], r[3]);
+  *reinterpret_cast<float4*>(ov + 4) = make_float4(r[4], r[5], r[6], r[7]);
 }
 
 }  // namespace tmvs
@@ -250,8 +445,10 @@ extern "C" size_t tmvs_deform_conv2d_packed_floats(int cout) { return (size_t)9 
 
 // A fragments in the kernel's LDS order [tap k][m-tile][half h][lane l][e], k-step s = 4h + e:
 // lane l holds W[co = 16m + (l & 15)][ci = 16h + 4 (l >> 4) + e][k] (zero for co >= cout).
+// cout 8 / 16 / 32: a DCN weight; 27: a conv_offset_mask weight (for tmvs_dcn_fused).
 extern "C" int tmvs_deform_conv2d_pack(const float* weight, int cout, int cin, float* packed) {
-  if (!weight || !packed || cin != dcn::CI || (cout != 8 && cout != 16 && cout != 32)) return TMVS_ERR_ARG;
+  if (!weight || !packed || cin != dcn::CI || (cout != 8 && cout != 16 && cout != 27 && cout != 32))
+    return TMVS_ERR_ARG;
   const int mt_n = (cout + 15) / 16;
   for (int k = 0; k < 9; ++k)
     for (int mt = 0; mt < mt_n; ++mt)
@@ -265,43 +462,114 @@ extern "C" int tmvs_deform_conv2d_pack(const float* weight, int cout, int cin, f
   return TMVS_OK;
 }
 
+namespace {
+
+template <int CO, bool FUSED>
+int dcn_launch(const float* x, const float* om, const float* wom, const float* bom, const float* w,
+               const float* bias, const float* alpha, const float* shift, int relu, int batch, int height, int width,
+               float* out, float* out_nhwc, hipStream_t st) {
+  // persistent grid: one block per CU slot the kernel's LDS/VGPR footprint allows
+  static int grid = 0;
+  if (!grid) {
+    int dev = 0, ncu = 0, occ = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return TMVS_ERR_HIP;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dcn_window_kernel<CO, FUSED>, 512, 0);
+    grid = std::max(1, ncu * std::max(occ, 1));
+  }
+  const long long nunits =
+      (long long)batch * ((height + dcn::WAVES - 1) / dcn::WAVES) * ((width + dcn::TW - 1) / dcn::TW);
+  const int nblk = (int)std::min<long long>(grid, nunits);
+  hipLaunchKernelGGL((dcn_window_kernel<CO, FUSED>), dim3(nblk), dim3(512), 0, st, x, om, wom, bom, w, bias, alpha,
+                     shift, relu, batch, height, width, out, out_nhwc);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+int dcn_check(const float* x_nhwc, const float* w_packed, const float* bias, const float* bn_alpha,
+              const float* bn_shift, int batch, int cin, int cout, int height, int width) {
+  if (!x_nhwc || !w_packed || !bias || batch <= 0 || height <= 0 || width <= 0) return TMVS_ERR_ARG;
+  if ((bn_alpha == nullptr) != (bn_shift == nullptr)) return TMVS_ERR_ARG;
+  if (cin != dcn::CI || (cout != 8 && cout != 16 && cout != 32)) return TMVS_ERR_SHAPE;
+  if ((long long)height * width * cin * 4 >= (1LL << 31) || height > 32766 || width > 32766) return TMVS_ERR_SHAPE;
+  return TMVS_OK;
+}
+
+}  // namespace
+
 extern "C" int tmvs_deform_conv2d(const float* x_nhwc, const float* offset_mask, const float* w_packed,
                                   const float* bias, const float* bn_alpha, const float* bn_shift, int relu,
                                   int batch, int cin, int cout, int height, int width, float* out,
                                   float* out_nhwc, void* stream) {
-  if (!x_nhwc || !offset_mask || !w_packed || !bias || !out || batch <= 0 || height <= 0 || width <= 0)
-    return TMVS_ERR_ARG;
-  if ((bn_alpha == nullptr) != (bn_shift == nullptr)) return TMVS_ERR_ARG;
-  if (cin != dcn::CI || (cout != 8 && cout != 16 && cout != 32)) return TMVS_ERR_SHAPE;
-  if ((long long)height * width * cin * 4 >= (1LL << 31) || height > 32766 || width > 32766) return TMVS_ERR_SHAPE;
+  if (!offset_mask || !out) return TMVS_ERR_ARG;
+  const int rc = dcn_check(x_nhwc, w_packed, bias, bn_alpha, bn_shift, batch, cin, cout, height, width);
+  if (rc != TMVS_OK) return rc;
   hipStream_t st = (hipStream_t)stream;
-  // persistent grid: one block per CU slot the kernel's LDS/VGPR footprint allows
-  static int grid_cache[3] = {0, 0, 0};
-  const int ci = cout == 32 ? 0 : cout == 16 ? 1 : 2;
-  if (!grid_cache[ci]) {
+  if (cout == 32)
+    return dcn_launch<32, false>(x_nhwc, offset_mask, nullptr, nullptr, w_packed, bias, bn_alpha, bn_shift, relu,
+                                 batch, height, width, out, out_nhwc, st);
+  if (cout == 16)
+    return dcn_launch<16, false>(x_nhwc, offset_mask, nullptr, nullptr, w_packed, bias, bn_alpha, bn_shift, relu,
+                                 batch, height, width, out, out_nhwc, st);
+  return dcn_launch<8, false>(x_nhwc, offset_mask, nullptr, nullptr, w_packed, bias, bn_alpha, bn_shift, relu, batch,
+                              height, width, out, out_nhwc, st);
+}
+
+extern "C" int tmvs_dcn_fused(const float* x_nhwc, const float* wom_packed, const float* bom, const float* w_packed,
+                              const float* bias, const float* bn_alpha, const float* bn_shift, int relu, int batch,
+                              int cin, int cout, int height, int width, float* out, float* out_nhwc, void* stream) {
+  if (!wom_packed || !bom || (!out && !out_nhwc)) return TMVS_ERR_ARG;
+  const int rc = dcn_check(x_nhwc, w_packed, bias, bn_alpha, bn_shift, batch, cin, cout, height, width);
+  if (rc != TMVS_OK) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (cout == 32)
+    return dcn_launch<32, true>(x_nhwc, nullptr, wom_packed, bom, w_packed, bias, bn_alpha, bn_shift, relu, batch,
+                                height, width, out, out_nhwc, st);
+  if (cout == 16)
+    return dcn_launch<16, true>(x_nhwc, nullptr, wom_packed, bom, w_packed, bias, bn_alpha, bn_shift, relu, batch,
+                                height, width, out, out_nhwc, st);
+  return dcn_launch<8, true>(x_nhwc, nullptr, wom_packed, bom, w_packed, bias, bn_alpha, bn_shift, relu, batch,
+                             height, width, out, out_nhwc, st);
+}
+
+extern "C" int tmvs_conv3x3_nhwc(const float* x_nhwc, const float* w_packed, const float* bias, const float* bn_alpha,
+                                 const float* bn_shift, int relu, int batch, int cin, int cout, int height, int width,
+                                 float* out, float* out_nhwc, void* stream) {
+  if (!x_nhwc || !w_packed || (!out && !out_nhwc) || batch <= 0 || height <= 0 || width <= 0) return TMVS_ERR_ARG;
+  if ((bn_alpha == nullptr) != (bn_shift == nullptr)) return TMVS_ERR_ARG;
+  if (cin != 32 || cout != 32) return TMVS_ERR_SHAPE;
+  if ((long long)height * width * cin * 4 >= (1LL << 31)) return TMVS_ERR_SHAPE;
+  static int grid = 0;
+  if (!grid) {
     int dev = 0, ncu = 0, occ = 0;
     if (hipGetDevice(&dev) != hipSuccess) return TMVS_ERR_HIP;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cout == 32)
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dcn_window_kernel<32>, 512, 0);
-    else if (cout == 16)
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dcn_window_kernel<16>, 512, 0);
-    else
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dcn_window_kernel<8>, 512, 0);
-    grid_cache[ci] = std::max(1, ncu * std::max(occ, 1));
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv3x3_window_kernel, 512, 0);
+    grid = std::max(1, ncu * std::max(occ, 1));
   }
-  const long long nunits = (long long)batch * ((height + dcn::WAVES - 1) / dcn::WAVES) * ((width + dcn::TW - 1) / dcn::TW);
-  const int nblk = (int)std::min<long long>(grid_cache[ci], nunits);
-#define TMVS_DCN(CO)                                                                                           \
-  hipLaunchKernelGGL(dcn_window_kernel<CO>, dim3(nblk), dim3(512), 0, st, x_nhwc, offset_mask, w_packed, bias, \
-                     bn_alpha, bn_shift, relu, batch, height, width, out, out_nhwc)
-  if (cout == 32)
-    TMVS_DCN(32);
-  else if (cout == 16)
-    TMVS_DCN(16);
+  const long long nunits =
+      (long long)batch * ((height + dcn::WAVES - 1) / dcn::WAVES) * ((width + dcn::TW - 1) / dcn::TW);
+  const int nblk = (int)std::min<long long>(grid, nunits);
+  hipLaunchKernelGGL(conv3x3_window_kernel, dim3(nblk), dim3(512), 0, (hipStream_t)stream, x_nhwc, w_packed, bias,
+                     bn_alpha, bn_shift, relu, batch, height, width, out, out_nhwc);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+extern "C" int tmvs_fpn_merge(const float* prev_nhwc, const float* lat_nhwc, int lat_channels, const float* w_inner,
+                              const float* b_inner, int batch, int height, int width, float* out_nhwc, void* stream) {
+  if (!prev_nhwc || !lat_nhwc || !w_inner || !b_inner || !out_nhwc || batch <= 0 || height <= 0 || width <= 0)
+    return TMVS_ERR_ARG;
+  if (lat_channels != 8 && lat_channels != 16) return TMVS_ERR_SHAPE;
+  const long long threads = (long long)batch * 4 * height * width * 4;
+  if (threads / 256 + 1 >= (1LL << 31)) return TMVS_ERR_SHAPE;
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  if (lat_channels == 8)
+    hipLaunchKernelGGL(fpn_merge_kernel<8>, grid, dim3(256), 0, (hipStream_t)stream, prev_nhwc, lat_nhwc, w_inner,
+                       b_inner, batch, height, width, out_nhwc);
   else
-    TMVS_DCN(8);
-#undef TMVS_DCN
+    hipLaunchKernelGGL(fpn_merge_kernel<16>, grid, dim3(256), 0, (hipStream_t)stream, prev_nhwc, lat_nhwc, w_inner,
+                       b_inner, batch, height, width, out_nhwc);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }

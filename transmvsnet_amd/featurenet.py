@@ -1,11 +1,12 @@
 """FeatureNet + DCN (models/module.py:343-422, models/dcn.py:43-80) -- SURVEY.md 8f, the #1 "next" row.
 
-The 3-scale trunk, the lateral 1x1 convs and each DCN's offset/mask conv run as PyTorch-ROCm
-(MIOpen) convolutions. The modulated deformable convolution itself -- torchvision.ops.deform_conv2d
-(torchvision 0.10.1, absent in this image) -- runs as the HIP kernel ``tmvs_deform_conv2d``
-(csrc/featurenet.hip), with the head's bias, BatchNorm and ReLU fused into its epilogue
-(models/module.py:362-395: DCN -> BN -> ReLU -> DCN -> BN -> ReLU -> DCN). There is no CPU path.
-The module/parameter names are the reference's, so checkpoints load strict=True.
+The 3-scale trunk, the lateral 1x1 convs and each head's first conv run as PyTorch-ROCm (MIOpen)
+convolutions in channels_last (NHWC) memory format. Each DCN -- its conv_offset_mask conv AND the
+modulated deformable convolution (torchvision.ops.deform_conv2d, torchvision 0.10.1, absent in
+this image) -- is ONE HIP launch, ``tmvs_dcn_fused`` (csrc/featurenet.hip), with the head's bias,
+BatchNorm and ReLU fused into its epilogue (models/module.py:362-395: DCN -> BN -> ReLU -> DCN ->
+BN -> ReLU -> DCN); the offset/mask tensor never reaches HBM, and DCN -> DCN hand-offs stay NHWC.
+There is no CPU path. Module/parameter names are the reference's, so checkpoints load strict=True.
 """
 from __future__ import annotations
 
@@ -25,9 +26,22 @@ class Conv2dBlock(nn.Module):
         super().__init__()
         self.conv = nn.Conv2d(cin, cout, k, stride=stride, padding=padding, bias=False)
         self.bn = nn.BatchNorm2d(cout, momentum=0.1)
+        self._packed = None
+        self.register_load_state_dict_post_hook(lambda m, k: setattr(m, "_packed", None))
 
     def forward(self, x):
         return F.relu(self.bn(self.conv(x)))
+
+    def forward_nhwc(self, x_nhwc):
+        """The heads' 3x3 32 -> 32 block on NHWC input as one HIP kernel (tmvs_conv3x3_nhwc) -> NHWC."""
+        bn = self.bn
+        key = (str(x_nhwc.device), self.conv.weight._version, bn.weight._version, bn.bias._version,
+               bn.running_mean._version, bn.running_var._version)
+        if self._packed is None or self._packed[0] != key:
+            a, s = ops.bn_fold(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
+            self._packed = (key, ops.deform_conv2d_pack(self.conv.weight).to(x_nhwc.device),
+                            (torch.from_numpy(a).to(x_nhwc.device), torch.from_numpy(s).to(x_nhwc.device)))
+        return ops.conv3x3_nhwc(x_nhwc, self._packed[1], bn=self._packed[2], relu=True)[1]
 
 
 class DCN(nn.Module):
@@ -53,27 +67,28 @@ class DCN(nn.Module):
     def _prepared(self, device, bn):
         bnv = None if bn is None else (id(bn), bn.weight._version, bn.bias._version, bn.running_mean._version,
                                        bn.running_var._version)
-        key = (str(device), self.weight._version, self.bias._version, bnv)
+        com = self.conv_offset_mask
+        key = (str(device), self.weight._version, self.bias._version, com.weight._version, com.bias._version, bnv)
         if self._packed is None or self._packed[0] != key:
             w = ops.deform_conv2d_pack(self.weight).to(device)
             b = self.bias.detach().float().contiguous().to(device)
+            wom = ops.deform_conv2d_pack(com.weight).to(device)
+            bom = com.bias.detach().float().contiguous().to(device)
             fold = None
             if bn is not None:
                 a, s = ops.bn_fold(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
                 fold = (torch.from_numpy(a).to(device), torch.from_numpy(s).to(device))
-            self._packed = (key, w, b, fold)
+            self._packed = (key, w, b, wom, bom, fold)
         return self._packed[1:]
 
-    def forward(self, x, bn=None, relu=False, x_nhwc=None, want_nhwc=False):
-        """deform_conv2d(x, offset, weight, bias, mask) (models/dcn.py:71-80), then the head's
-        eval BatchNorm ``bn`` and ReLU if given (fused)."""
-        if not x.is_cuda:
-            raise RuntimeError("FeatureNet DCN runs on the GPU only (tmvs_deform_conv2d); no CPU fallback")
-        om = self.conv_offset_mask(x).contiguous()
-        if x_nhwc is None:
-            x_nhwc = x.permute(0, 2, 3, 1).contiguous()
-        w, b, fold = self._prepared(x.device, bn)
-        return ops.deform_conv2d(x_nhwc, om, w, b, self.cout, bn=fold, relu=relu, want_nhwc=want_nhwc)
+    def forward(self, x_nhwc, bn=None, relu=False, want_nchw=True, want_nhwc=False):
+        """DCN.forward (models/dcn.py:66-80) on x_nhwc [B,H,W,32]: conv_offset_mask, deform_conv2d, then
+        the head's eval BatchNorm ``bn`` and ReLU if given -- one fused kernel. Returns (nchw, nhwc)."""
+        if not x_nhwc.is_cuda:
+            raise RuntimeError("FeatureNet DCN runs on the GPU only (tmvs_dcn_fused); no CPU fallback")
+        w, b, wom, bom, fold = self._prepared(x_nhwc.device, bn)
+        return ops.dcn_fused(x_nhwc.contiguous(), wom, bom, w, b, self.cout, bn=fold, relu=relu, want_nchw=want_nchw,
+                             want_nhwc=want_nhwc)
 
 
 def _head(cin, cmid, cout, first_k):
@@ -84,12 +99,16 @@ def _head(cin, cmid, cout, first_k):
         DCN(cmid, cout))
 
 
-def _run_head(seq, x):
-    """out{1,2,3} Sequential (models/module.py:362-395) with BN + ReLU fused into the DCN kernels."""
-    x = seq[0](x)
-    x, xh = seq[1](x, bn=seq[2], relu=True, want_nhwc=True)
-    x, xh = seq[4](x, bn=seq[5], relu=True, x_nhwc=xh, want_nhwc=True)
-    return seq[7](x, x_nhwc=xh)
+def _run_head(seq, x, x_nhwc=None):
+    """out{1,2,3} Sequential (models/module.py:362-395) with BN + ReLU fused into the DCN kernels.
+    With x_nhwc (stages 2/3) the first 3x3 block also runs natively."""
+    if x_nhwc is not None:
+        xh = seq[0].forward_nhwc(x_nhwc)
+    else:
+        xh = seq[0](x).permute(0, 2, 3, 1).contiguous()  # channels_last storage: already NHWC
+    _, xh = seq[1](xh, bn=seq[2], relu=True, want_nchw=False, want_nhwc=True)
+    _, xh = seq[4](xh, bn=seq[5], relu=True, want_nchw=False, want_nhwc=True)
+    return seq[7](xh)[0]
 
 
 class FeatureNet(nn.Module):
@@ -112,12 +131,20 @@ class FeatureNet(nn.Module):
     def forward(self, x):
         """x [B,3,H,W] -> {stage1: [B,32,H/4,W/4], stage2: [B,16,H/2,W/2], stage3: [B,8,H,W]}.
         Views may be batched on B (eval BatchNorm is per sample)."""
+        x = x.contiguous(memory_format=torch.channels_last)  # MIOpen NHWC convs; NHWC into the DCNs
         conv0 = self.conv0(x)
         conv1 = self.conv1(conv0)
         conv2 = self.conv2(conv1)
         out = {"stage1": _run_head(self.out1, conv2)}
-        intra = F.interpolate(conv2, scale_factor=2.0, mode="nearest") + self.inner1(conv1)
-        out["stage2"] = _run_head(self.out2, intra)
-        intra = F.interpolate(intra, scale_factor=2.0, mode="nearest") + self.inner2(conv0)
-        out["stage3"] = _run_head(self.out3, intra)
+        nhwc = lambda t: t.permute(0, 2, 3, 1).contiguous()  # free for channels_last storage
+        # intra = interpolate(., 2, nearest) + inner(.) as one NHWC kernel (models/module.py:413, 417)
+        intra = ops.fpn_merge(nhwc(conv2), nhwc(conv1), *self._inner(self.inner1, conv2.device))
+        out["stage2"] = _run_head(self.out2, None, intra)
+        intra = ops.fpn_merge(intra, nhwc(conv0), *self._inner(self.inner2, conv2.device))
+        out["stage3"] = _run_head(self.out3, None, intra)
         return out
+
+    @staticmethod
+    def _inner(conv, device):
+        w = conv.weight.detach().float().reshape(conv.out_channels, conv.in_channels).contiguous().to(device)
+        return w, conv.bias.detach().float().contiguous().to(device)

@@ -308,7 +308,8 @@ def depth_stage(depth_values, prev_depth, feat_nhwc, ndepth, ratio, full_hw, sta
 
 
 def deform_conv2d_pack(weight):
-    """HOST packing of a DCN weight [Co][32][3][3] into the kernel's A-fragment order (CPU float32)."""
+    """HOST packing of a DCN weight [Co][32][3][3] (Co 8/16/32, or 27 for conv_offset_mask) into the
+    kernel's A-fragment order (CPU float32)."""
     w = np.ascontiguousarray(weight.detach().float().cpu().numpy(), np.float32)
     co, ci = w.shape[:2]
     out = np.empty(_lib_h().tmvs_deform_conv2d_packed_floats(co), np.float32)
@@ -335,3 +336,59 @@ def deform_conv2d(x_nhwc, offset_mask, w_packed, bias, cout, bn=None, relu=False
                                                _ptr(alpha), _ptr(shift), int(relu), b, cin, cout, h, w, _ptr(out),
                                                _ptr(out_nhwc), _stream()), "tmvs_deform_conv2d")
     return (out, out_nhwc) if want_nhwc else out
+
+
+def dcn_fused(x_nhwc, wom_packed, bom, w_packed, bias, cout, bn=None, relu=False, want_nchw=True, want_nhwc=False):
+    """The whole DCN.forward (models/dcn.py:66-80): conv_offset_mask computed in-kernel, then the
+    modulated deformable conv + optional folded BN / ReLU. x_nhwc [B,H,W,32] -> out [B,cout,H,W]
+    and/or [B,H,W,cout] (returned as (out_nchw, out_nhwc), None where not requested)."""
+    for t, n in ((x_nhwc, "x_nhwc"), (wom_packed, "wom_packed"), (bom, "bom"), (w_packed, "w_packed"), (bias, "bias")):
+        _dev(t, n)
+    if not (want_nchw or want_nhwc):
+        raise ValueError("dcn_fused: request at least one output layout")
+    b, h, w, cin = x_nhwc.shape
+    if not x_nhwc.is_contiguous():
+        raise ValueError("dcn_fused: expects a contiguous x_nhwc [B,H,W,C]")
+    out = torch.empty(b, cout, h, w, device=x_nhwc.device) if want_nchw else None
+    out_nhwc = torch.empty(b, h, w, cout, device=x_nhwc.device) if want_nhwc else None
+    alpha, shift = bn if bn is not None else (None, None)
+    with _Span("tmvs_dcn_fused"):
+        _lib.check(_lib_h().tmvs_dcn_fused(_ptr(x_nhwc), _ptr(wom_packed), _ptr(bom), _ptr(w_packed), _ptr(bias),
+                                           _ptr(alpha), _ptr(shift), int(relu), b, cin, cout, h, w, _ptr(out),
+                                           _ptr(out_nhwc), _stream()), "tmvs_dcn_fused")
+    return out, out_nhwc
+
+
+def conv3x3_nhwc(x_nhwc, w_packed, bn=None, relu=False, bias=None, want_nchw=False, want_nhwc=True):
+    """Conv2d(32, 32, 3, 1, 1) [+ bias] + folded BN + ReLU on x_nhwc [B,H,W,32] (models/module.py:24-61).
+    Returns (out_nchw, out_nhwc), None where not requested."""
+    for t, n in ((x_nhwc, "x_nhwc"), (w_packed, "w_packed")):
+        _dev(t, n)
+    if not x_nhwc.is_contiguous():
+        raise ValueError("conv3x3_nhwc: expects a contiguous x_nhwc [B,H,W,32]")
+    b, h, w, cin = x_nhwc.shape
+    out = torch.empty(b, 32, h, w, device=x_nhwc.device) if want_nchw else None
+    out_nhwc = torch.empty(b, h, w, 32, device=x_nhwc.device) if want_nhwc else None
+    alpha, shift = bn if bn is not None else (None, None)
+    with _Span("tmvs_conv3x3_nhwc"):
+        _lib.check(_lib_h().tmvs_conv3x3_nhwc(_ptr(x_nhwc), _ptr(w_packed), _ptr(bias), _ptr(alpha), _ptr(shift),
+                                              int(relu), b, cin, 32, h, w, _ptr(out), _ptr(out_nhwc), _stream()),
+                   "tmvs_conv3x3_nhwc")
+    return out, out_nhwc
+
+
+def fpn_merge(prev_nhwc, lat_nhwc, w_inner, b_inner):
+    """interpolate(prev, 2, nearest) + Conv2d_1x1(lat) (models/module.py:409-417), all NHWC:
+    prev [B,h,w,32], lat [B,2h,2w,cl] (cl 8/16), w_inner [32,cl] -> [B,2h,2w,32]."""
+    for t, n in ((prev_nhwc, "prev_nhwc"), (lat_nhwc, "lat_nhwc"), (w_inner, "w_inner"), (b_inner, "b_inner")):
+        _dev(t, n)
+    b, h, w, c = prev_nhwc.shape
+    cl = lat_nhwc.shape[-1]
+    if c != 32 or tuple(lat_nhwc.shape) != (b, 2 * h, 2 * w, cl) or not prev_nhwc.is_contiguous() \
+            or not lat_nhwc.is_contiguous():
+        raise ValueError("fpn_merge: expects contiguous prev [B,h,w,32] and lat [B,2h,2w,cl]")
+    out = torch.empty(b, 2 * h, 2 * w, 32, device=prev_nhwc.device)
+    with _Span("tmvs_fpn_merge"):
+        _lib.check(_lib_h().tmvs_fpn_merge(_ptr(prev_nhwc), _ptr(lat_nhwc), cl, _ptr(w_inner), _ptr(b_inner), b, h, w,
+                                           _ptr(out), _stream()), "tmvs_fpn_merge")
+    return out
