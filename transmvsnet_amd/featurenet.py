@@ -132,6 +132,7 @@ class FeatureNet(nn.Module):
         """x [B,3,H,W] -> {stage1: [B,32,H/4,W/4], stage2: [B,16,H/2,W/2], stage3: [B,8,H,W]}.
         Views may be batched on B (eval BatchNorm is per sample)."""
         x = x.contiguous(memory_format=torch.channels_last)  # MIOpen NHWC convs; NHWC into the DCNs
+        self._weights_channels_last()
         conv0 = self.conv0(x)
         conv1 = self.conv1(conv0)
         conv2 = self.conv2(conv1)
@@ -144,7 +145,18 @@ class FeatureNet(nn.Module):
         out["stage3"] = _run_head(self.out3, None, intra)
         return out
 
-    @staticmethod
-    def _inner(conv, device):
-        w = conv.weight.detach().float().reshape(conv.out_channels, conv.in_channels).contiguous().to(device)
-        return w, conv.bias.detach().float().contiguous().to(device)
+    def _weights_channels_last(self):
+        """MIOpen's NHWC convs want NHWC weights: convert the trunk/head conv weights once (in place,
+        values unchanged) instead of on every call."""
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d) and not m.weight.is_contiguous(memory_format=torch.channels_last):
+                m.weight.data = m.weight.data.contiguous(memory_format=torch.channels_last)
+
+    def _inner(self, conv, device):
+        """inner{1,2} 1x1 conv weight [32, cl] and bias, cached per parameter version."""
+        key = (id(conv), str(device), conv.weight._version, conv.bias._version)
+        cache = self.__dict__.setdefault("_inner_cache", {})
+        if cache.get(id(conv), (None,))[0] != key:
+            w = conv.weight.detach().float().reshape(conv.out_channels, conv.in_channels).contiguous().to(device)
+            cache[id(conv)] = (key, w, conv.bias.detach().float().contiguous().to(device))
+        return cache[id(conv)][1:]
