@@ -255,6 +255,17 @@ int tmvs_conv3x3_nhwc(const float* x_nhwc, const float* w_packed, const float* b
 int tmvs_fpn_merge(const float* prev_nhwc, const float* lat_nhwc, int lat_channels, const float* w_inner,
                    const float* b_inner, int batch, int height, int width, float* out_nhwc, void* stream);
 
+/* FeatureNet Conv2d(bias=False) -> eval BatchNorm -> ReLU blocks (models/module.py:24-61) of the trunk
+ * (:349-360) and the stage-1 head's 1x1 (:362), NHWC out. Shapes (cin, cout, k, stride): (3,8,3,1) --
+ * x is the NCHW image [B][3][H][W] --, (8,8,3,1), (8,16,5,2), (16,16,3,1), (16,32,5,2), (32,32,3,1),
+ * (32,32,1,1) -- x is NHWC [B][H][W][cin]; padding k/2; out_nhwc [B][Ho][Wo][cout].
+ * w_packed = tmvs_conv2d_packed_floats(cout, cin, k) floats from tmvs_conv2d_pack (HOST).            */
+size_t tmvs_conv2d_packed_floats(int cout, int cin, int k);
+int tmvs_conv2d_pack(const float* weight, int cout, int cin, int k, float* packed);
+int tmvs_conv2d_bn_relu(const float* x, int batch, int cin, int height, int width, const float* w_packed, int cout,
+                        int k, int stride, const float* bn_alpha, const float* bn_shift, int relu, float* out_nhwc,
+                        void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -116,3 +116,31 @@ def test_deform_conv2d_pack_host(lib):
                         c_o, c_i = 16 * mt + lane % 16, 16 * h + 4 * (lane // 16) + e
                         want = wn[c_o, c_i, k // 3, k % 3] if c_o < co else 0.0
                         assert pk[((((k * mt_n + mt) * 2 + h) * 64) + lane) * 4 + e] == want
+
+
+def test_conv2d_pack_host(lib):
+    """tmvs_conv2d_pack (HOST): [k-block][mtile][lane][e]; lane group j of k-block b owns the (tap, chunk) pair
+    idx = 4b + j, element e = channel 4*chunk + e; zero padding past cin / cout / the last pair."""
+    import numpy as np
+    import torch
+    from transmvsnet_amd import ops
+    for (co, ci, k) in ((8, 3, 3), (16, 8, 5), (32, 32, 1), (32, 16, 3)):
+        w = torch.randn(co, ci, k, k)
+        pk = ops.conv2d_pack(w).numpy()
+        cip = max(ci, 4)
+        g = cip // 4
+        nidx = k * k * g
+        nb, mt = (nidx + 3) // 4, (co + 15) // 16
+        assert pk.size == nb * mt * 64 * 4
+        wn = w.numpy()
+        for b in range(nb):
+            for m in range(mt):
+                for lane in (0, 7, 21, 63):
+                    for e in range(4):
+                        idx, c_o = 4 * b + lane // 16, 16 * m + lane % 16
+                        want = 0.0
+                        if idx < nidx and c_o < co:
+                            tap, c = idx // g, 4 * (idx % g) + e
+                            if c < ci:
+                                want = wn[c_o, c, tap // k, tap % k]
+                        assert pk[((b * mt + m) * 64 + lane) * 4 + e] == want

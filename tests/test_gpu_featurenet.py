@@ -142,3 +142,26 @@ def test_fpn_merge(cl):
     out = ops.fpn_merge(prev.permute(0, 2, 3, 1).contiguous().to(DEV), lat.permute(0, 2, 3, 1).contiguous().to(DEV),
                         conv.weight.detach().reshape(32, cl).contiguous().to(DEV), conv.bias.detach().to(DEV))
     np.testing.assert_allclose(to_np(out), to_np(ref.permute(0, 2, 3, 1)), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,h,w", [(3, 8, 3, 1, 37, 50), (8, 8, 3, 1, 20, 33), (8, 16, 5, 2, 41, 70),
+                                                   (16, 16, 3, 1, 17, 40), (16, 32, 5, 2, 36, 48),
+                                                   (32, 32, 3, 1, 19, 21), (32, 32, 1, 1, 9, 35)])
+def test_conv2d_bn_relu_shapes(cin, cout, k, stride, h, w):
+    """tmvs_conv2d_bn_relu for every FeatureNet Conv2d block shape (models/module.py:349-362): Conv2d(k,
+    stride, padding k//2, no bias) -> eval BN -> ReLU, ragged sizes; the first layer reads the NCHW
+    image. 2e-5 abs + 1e-5 rel (MFMA K-order vs the CPU conv)."""
+    torch.manual_seed(cin * 7 + cout + k)
+    b = 2
+    x = torch.randn(b, cin, h, w)
+    weight = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
+    gamma, beta = torch.rand(cout) + 0.5, torch.randn(cout) * 0.1
+    mean, var = torch.randn(cout) * 0.1, torch.rand(cout) + 0.5
+    ref = F.relu(F.batch_norm(F.conv2d(x, weight, stride=stride, padding=k // 2), mean, var, gamma, beta, False, 0.1,
+                              1e-5))
+    a, s_ = ops.bn_fold(gamma, beta, mean, var)
+    fold = (torch.from_numpy(a).to(DEV), torch.from_numpy(s_).to(DEV))
+    xin = x.contiguous() if cin == 3 else x.permute(0, 2, 3, 1).contiguous()
+    out = ops.conv2d_bn_relu(xin.to(DEV), ops.conv2d_pack(weight).to(DEV), cout, k, stride, bn=fold, relu=True,
+                             nchw_input=(cin == 3))
+    np.testing.assert_allclose(to_np(out), to_np(ref.permute(0, 2, 3, 1)), rtol=1e-5, atol=2e-5)

@@ -45,6 +45,9 @@ SIGNATURES = {
     "tmvs_dcn_fused": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P]),
     "tmvs_conv3x3_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, P, P, P]),
     "tmvs_fpn_merge": (I, [P, P, I, P, P, I, I, I, P, P]),
+    "tmvs_conv2d_packed_floats": (S, [I, I, I]),
+    "tmvs_conv2d_pack": (I, [P, I, I, I, P]),
+    "tmvs_conv2d_bn_relu": (I, [P, I, I, I, I, P, I, I, I, P, P, I, P, P]),
 }
 
 ABI_VERSION = 1

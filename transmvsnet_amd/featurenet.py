@@ -1,12 +1,14 @@
 """FeatureNet + DCN (models/module.py:343-422, models/dcn.py:43-80) -- SURVEY.md 8f, the #1 "next" row.
 
-The 3-scale trunk, the lateral 1x1 convs and each head's first conv run as PyTorch-ROCm (MIOpen)
-convolutions in channels_last (NHWC) memory format. Each DCN -- its conv_offset_mask conv AND the
-modulated deformable convolution (torchvision.ops.deform_conv2d, torchvision 0.10.1, absent in
-this image) -- is ONE HIP launch, ``tmvs_dcn_fused`` (csrc/featurenet.hip), with the head's bias,
-BatchNorm and ReLU fused into its epilogue (models/module.py:362-395: DCN -> BN -> ReLU -> DCN ->
-BN -> ReLU -> DCN); the offset/mask tensor never reaches HBM, and DCN -> DCN hand-offs stay NHWC.
-There is no CPU path. Module/parameter names are the reference's, so checkpoints load strict=True.
+Every layer is a HIP kernel behind the C-ABI, NHWC end to end: the trunk's Conv+BN+ReLU blocks
+and the stage-1 head's 1x1 (``tmvs_conv2d_bn_relu``, csrc/conv2d.hip), the FPN merges
+(``tmvs_fpn_merge``), the stage-2/3 heads' 3x3 blocks (``tmvs_conv3x3_nhwc``), and each DCN -- its
+conv_offset_mask conv AND the modulated deformable convolution (torchvision.ops.deform_conv2d,
+torchvision 0.10.1, absent in this image) -- as ONE launch, ``tmvs_dcn_fused`` (csrc/featurenet.hip),
+with the head's bias, BatchNorm and ReLU fused into its epilogue (models/module.py:362-395: DCN ->
+BN -> ReLU -> DCN -> BN -> ReLU -> DCN); the offset/mask tensor never reaches HBM. The stage
+outputs are NCHW, as the reference's. There is no CPU path. Module/parameter names are the
+reference's, so checkpoints load strict=True.
 """
 from __future__ import annotations
 
@@ -32,10 +34,22 @@ class Conv2dBlock(nn.Module):
     def forward(self, x):
         return F.relu(self.bn(self.conv(x)))
 
+    def forward_native(self, x, nchw_input=False):
+        """This block as one HIP kernel (tmvs_conv2d_bn_relu): NHWC in (or the NCHW image), NHWC out."""
+        bn, conv = self.bn, self.conv
+        key = ("c2d", str(x.device), conv.weight._version, bn.weight._version, bn.bias._version,
+               bn.running_mean._version, bn.running_var._version)
+        if self._packed is None or self._packed[0] != key:
+            a, s = ops.bn_fold(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
+            self._packed = (key, ops.conv2d_pack(conv.weight).to(x.device),
+                            (torch.from_numpy(a).to(x.device), torch.from_numpy(s).to(x.device)))
+        return ops.conv2d_bn_relu(x, self._packed[1], conv.out_channels, conv.kernel_size[0], conv.stride[0],
+                                  bn=self._packed[2], relu=True, nchw_input=nchw_input)
+
     def forward_nhwc(self, x_nhwc):
         """The heads' 3x3 32 -> 32 block on NHWC input as one HIP kernel (tmvs_conv3x3_nhwc) -> NHWC."""
         bn = self.bn
-        key = (str(x_nhwc.device), self.conv.weight._version, bn.weight._version, bn.bias._version,
+        key = ("dcnpk", str(x_nhwc.device), self.conv.weight._version, bn.weight._version, bn.bias._version,
                bn.running_mean._version, bn.running_var._version)
         if self._packed is None or self._packed[0] != key:
             a, s = ops.bn_fold(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
@@ -102,10 +116,10 @@ def _head(cin, cmid, cout, first_k):
 def _run_head(seq, x, x_nhwc=None):
     """out{1,2,3} Sequential (models/module.py:362-395) with BN + ReLU fused into the DCN kernels.
     With x_nhwc (stages 2/3) the first 3x3 block also runs natively."""
-    if x_nhwc is not None:
+    if x_nhwc is not None:  # 3x3 first block (stages 2/3)
         xh = seq[0].forward_nhwc(x_nhwc)
-    else:
-        xh = seq[0](x).permute(0, 2, 3, 1).contiguous()  # channels_last storage: already NHWC
+    else:  # 1x1 first block (stage 1) on the NHWC trunk output
+        xh = seq[0].forward_native(x)
     _, xh = seq[1](xh, bn=seq[2], relu=True, want_nchw=False, want_nhwc=True)
     _, xh = seq[4](xh, bn=seq[5], relu=True, want_nchw=False, want_nhwc=True)
     return seq[7](xh)[0]
@@ -131,26 +145,23 @@ class FeatureNet(nn.Module):
     def forward(self, x):
         """x [B,3,H,W] -> {stage1: [B,32,H/4,W/4], stage2: [B,16,H/2,W/2], stage3: [B,8,H,W]}.
         Views may be batched on B (eval BatchNorm is per sample)."""
-        x = x.contiguous(memory_format=torch.channels_last)  # MIOpen NHWC convs; NHWC into the DCNs
-        self._weights_channels_last()
-        conv0 = self.conv0(x)
-        conv1 = self.conv1(conv0)
-        conv2 = self.conv2(conv1)
+        x = x.contiguous()
+        if not x.is_cuda:
+            raise RuntimeError("FeatureNet runs on the GPU only (HIP kernels); no CPU fallback")
+        conv0 = self.conv0[1].forward_native(self.conv0[0].forward_native(x, nchw_input=True))  # NHWC from here on
+        conv1 = conv0
+        for blk in self.conv1:
+            conv1 = blk.forward_native(conv1)
+        conv2 = conv1
+        for blk in self.conv2:
+            conv2 = blk.forward_native(conv2)
         out = {"stage1": _run_head(self.out1, conv2)}
-        nhwc = lambda t: t.permute(0, 2, 3, 1).contiguous()  # free for channels_last storage
         # intra = interpolate(., 2, nearest) + inner(.) as one NHWC kernel (models/module.py:413, 417)
-        intra = ops.fpn_merge(nhwc(conv2), nhwc(conv1), *self._inner(self.inner1, conv2.device))
+        intra = ops.fpn_merge(conv2, conv1, *self._inner(self.inner1, conv2.device))
         out["stage2"] = _run_head(self.out2, None, intra)
-        intra = ops.fpn_merge(intra, nhwc(conv0), *self._inner(self.inner2, conv2.device))
+        intra = ops.fpn_merge(intra, conv0, *self._inner(self.inner2, conv2.device))
         out["stage3"] = _run_head(self.out3, None, intra)
         return out
-
-    def _weights_channels_last(self):
-        """MIOpen's NHWC convs want NHWC weights: convert the trunk/head conv weights once (in place,
-        values unchanged) instead of on every call."""
-        for m in self.modules():
-            if isinstance(m, nn.Conv2d) and not m.weight.is_contiguous(memory_format=torch.channels_last):
-                m.weight.data = m.weight.data.contiguous(memory_format=torch.channels_last)
 
     def _inner(self, conv, device):
         """inner{1,2} 1x1 conv weight [32, cl] and bias, cached per parameter version."""

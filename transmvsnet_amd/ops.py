@@ -392,3 +392,33 @@ def fpn_merge(prev_nhwc, lat_nhwc, w_inner, b_inner):
         _lib.check(_lib_h().tmvs_fpn_merge(_ptr(prev_nhwc), _ptr(lat_nhwc), cl, _ptr(w_inner), _ptr(b_inner), b, h, w,
                                            _ptr(out), _stream()), "tmvs_fpn_merge")
     return out
+
+
+def conv2d_pack(weight):
+    """HOST packing of a Conv2d weight [Co][Ci][k][k] into tmvs_conv2d_bn_relu's k-block order."""
+    w = np.ascontiguousarray(weight.detach().float().cpu().numpy(), np.float32)
+    co, ci, k, _ = w.shape
+    out = np.empty(_lib_h().tmvs_conv2d_packed_floats(co, ci, k), np.float32)
+    _lib.check(_lib_h().tmvs_conv2d_pack(w.ctypes.data, co, ci, k, out.ctypes.data), "tmvs_conv2d_pack")
+    return torch.from_numpy(out)
+
+
+def conv2d_bn_relu(x, w_packed, cout, k, stride, bn=None, relu=True, nchw_input=False):
+    """Conv2d(k, stride, padding k//2, no bias) + folded BN + ReLU (models/module.py:24-61) -> NHWC.
+    x: NHWC [B,H,W,Ci], or the NCHW image [B,3,H,W] with nchw_input=True."""
+    _dev(x, "x")
+    _dev(w_packed, "w_packed")
+    if not x.is_contiguous():
+        raise ValueError("conv2d_bn_relu: expects a contiguous input")
+    if nchw_input:
+        b, cin, h, w = x.shape
+    else:
+        b, h, w, cin = x.shape
+    pad = k // 2
+    ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+    out = torch.empty(b, ho, wo, cout, device=x.device)
+    alpha, shift = bn if bn is not None else (None, None)
+    with _Span("tmvs_conv2d_bn_relu"):
+        _lib.check(_lib_h().tmvs_conv2d_bn_relu(_ptr(x), b, cin, h, w, _ptr(w_packed), cout, k, stride, _ptr(alpha),
+                                                _ptr(shift), int(relu), _ptr(out), _stream()), "tmvs_conv2d_bn_relu")
+    return out
