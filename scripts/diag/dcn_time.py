@@ -16,11 +16,18 @@ for (h, w, co) in ([CFGS[int(only)]] if only else CFGS):
     om = om.to(dev)
     wp = ops.deform_conv2d_pack(torch.randn(co, 32, 3, 3, generator=g) * 0.06).to(dev)
     bias = torch.zeros(co, device=dev)
+    # fused: conv_offset_mask weights scaled so offsets have about DCN_OFFSET_STD pixels
+    wom = ops.deform_conv2d_pack(torch.randn(27, 32, 3, 3, generator=g) * float(os.environ.get("DCN_OFFSET_STD", "1.5")) / 17).to(dev)
+    bom = torch.zeros(27, device=dev)
+    fused = os.environ.get("DCN_FUSED") is not None
     ts = []
     for i in range(13):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        ops.deform_conv2d(x, om, wp, bias, co, want_nhwc=True)
+        if fused:
+            ops.dcn_fused(x, wom, bom, wp, bias, co, want_nchw=False, want_nhwc=True)
+        else:
+            ops.deform_conv2d(x, om, wp, bias, co, want_nhwc=True)
         e1.record()
         torch.cuda.synchronize()
         if i >= 3:

@@ -1,0 +1,7 @@
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/dcn; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_featurenet.py -q -x --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+tail -2 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
+for sd in 0 1.5; do
+DCN_FUSED=1 DCN_OFFSET_STD=$sd timeout -k 10 120 python scripts/diag/dcn_time.py 2>&1 | grep us || exit 1
+done

@@ -55,6 +55,7 @@ __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* 
                                          const int2* __restrict__ recb, __amdgpu_buffer_rsrc_t rx, int H, int W,
                                          int lane) {
   const int j = lane >> 4, n = lane & 15;
+  floatx4_t alt = floatx4_t{0.f, 0.f, 0.f, 0.f};
   floatx4_t v[2][4][2], w4[2];
   float mk[2];
   // gathers of tap k into buffer bb (issued one tap ahead of their use)
@@ -106,10 +107,15 @@ __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* 
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s >> 2][s & 3], b[s], acc[m], 0, 0, 0);
+      for (int m = 0; m < MT; ++m) {
+        if (MT == 1 && (s & 1))  // one output tile: two interleaved chains hide the dependent latency
+          alt = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s >> 2][s & 3], b[s], alt, 0, 0, 0);
+        else
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s >> 2][s & 3], b[s], acc[m], 0, 0, 0);
+      }
     __builtin_amdgcn_sched_barrier(0);
   }
+  if (MT == 1) acc[0] = acc[0] + alt;
 }
 
 // FUSED: the DCN's offset/mask conv (conv_offset_mask, models/dcn.py:58-64: 3x3, 32 -> 27, bias)
@@ -213,25 +219,24 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
             ao[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s >> 2][s & 3], s < 4 ? b0[s] : b1[s - 4], ao[m], 0,
                                                          0, 0);
       }
-      float* omt = reinterpret_cast<float*>(recw[wv]);  // [px][32] tile, consumed before the records
+      // [px][33] tile (odd row stride: the record builders' column reads hit 16 distinct banks),
+      // consumed before the records overwrite it
+      float* omt = reinterpret_cast<float*>(recw[wv]);
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        floatx4_t o = ao[m];
+      for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int c = 16 * m + 4 * j + i;
-          o[i] = o[i] + (c < 27 ? bom[c] : 0.f);
+          if (c < 27) omt[n * 33 + c] = ao[m][i] + bom[c];
         }
-        *reinterpret_cast<floatx4_t*>(omt + n * 32 + 16 * m + 4 * j) = o;
-      }
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const int r = lane + 64 * i;
         if (r < dcn::NREC) {
           const int tap = r >> 4, px = r & 15;
-          omv[3 * i + 0] = omt[px * 32 + 2 * tap];
-          omv[3 * i + 1] = omt[px * 32 + 2 * tap + 1];
-          omv[3 * i + 2] = omt[px * 32 + 18 + tap];
+          omv[3 * i + 0] = omt[px * 33 + 2 * tap];
+          omv[3 * i + 1] = omt[px * 33 + 2 * tap + 1];
+          omv[3 * i + 2] = omt[px * 33 + 18 + tap];
         }
       }
     }
@@ -254,7 +259,7 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
         const int ry = y0i - wy0, rxw = x0i - wx0;
         const bool inwin = (unsigned)ry < (unsigned)(dcn::WR - 1) && (unsigned)rxw < (unsigned)(dcn::WC - 1);
         lane_fast = lane_fast && (inwin || !inside);
-        const float mk = 1.f / (1.f + expf(-omv[3 * i + 2]));
+        const float mk = __frcp_rn(1.f + __expf(-omv[3 * i + 2]));  // sigmoid (fast exp / rcp)
         // inside => y0 in [-1, H-1], x0 in [-1, W-1]: the fallback code fits 30 bits
         const int code = !inside ? 0 : inwin ? ry * dcn::WC + rxw : -1 - (((y0i + 1) << 15) | (x0i + 1));
         recb[wv][r] = make_int2(code, __float_as_int(mk));
