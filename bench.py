@@ -254,8 +254,9 @@ def end_to_end(model, steps, proj, dv_dev, dev):
     t_feat = timed(lambda: model.feature(imgs.reshape(NVIEWS, 3, H, W)))
     return {"depth_maps_per_s": round(1e3 / t_all, 3), "ms_per_depth_map": round(t_all, 3),
             "featurenet_ms": round(t_feat, 3), "steps": steps,
-            "workload": "TransMVSNet.forward(imgs [1,5,3,864,1152], proj, depth_values): FeatureNet (MIOpen "
-                        "convs + tmvs_deform_conv2d) + the hot path above"}
+            "workload": "TransMVSNet.forward(imgs [1,5,3,864,1152], proj, depth_values): FeatureNet (HIP: "
+                        "tmvs_conv2d_bn_relu trunk, tmvs_fpn_merge, tmvs_conv3x3_nhwc, tmvs_dcn_fused) + the hot "
+                        "path above"}
 
 
 def cpu_baseline(threads, feats_cpu, proj, dv, gpu_out):
