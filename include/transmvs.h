@@ -266,6 +266,16 @@ int tmvs_conv2d_bn_relu(const float* x, int batch, int cin, int height, int widt
                         int k, int stride, const float* bn_alpha, const float* bn_shift, int relu, float* out_nhwc,
                         void* stream);
 
+/* ------------------------------------------------------------------ output side
+ * gipuma depth-map fusion kernel (gipuma/fusibile/fusibile.cu:89-173) for one reference camera:
+ *   rgbd    : [V][H][W][4] float (B, G, R, depth), depth = 425 + 512 * alpha / 255 (main.cpp:136)
+ *   cams    : [V][32] float: P (3x4 row-major), inv(P[:, :3]) (3x3), camera centre (3), fx, pad
+ *   coord / texture : [H][W][4] point buffer; pixels fused with >= consistent_threshold agreeing
+ *             views are overwritten with the averaged point / colour (.w = 0), others are left as
+ *             they are (the reference reuses one buffer across cameras).                         */
+int tmvs_fusibile(const float* rgbd, const float* cams, int n_views, int height, int width, int ref_view,
+                  int consistent_threshold, float depth_threshold, float* coord, float* texture, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

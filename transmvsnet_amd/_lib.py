@@ -48,6 +48,7 @@ SIGNATURES = {
     "tmvs_conv2d_packed_floats": (S, [I, I, I]),
     "tmvs_conv2d_pack": (I, [P, I, I, I, P]),
     "tmvs_conv2d_bn_relu": (I, [P, I, I, I, I, P, I, I, I, P, P, I, P, P]),
+    "tmvs_fusibile": (I, [P, P, I, I, I, I, I, F, P, P, P]),
 }
 
 ABI_VERSION = 1
