@@ -107,8 +107,9 @@ def test_load_sample_synthetic_scan():
                 os.path.join(td, "scan1", "images", "{:0>8}.jpg".format(v)))
             open(os.path.join(td, "scan1", "cams", "{:0>8}_cam.txt".format(v)), "w").write(CAM_TXT)
         s = data.load_sample(td, "scan1", 0, [1, 2, 3], nviews=4, max_h=216, max_w=288)
-    assert s["imgs"].shape == (4, 3, 192, 256)  # 300x400 -> 0.72 -> 216x288 -> multiples of 32
+    assert s["imgs"].shape == (4, 3, 192, 288)  # 300x400 -> x0.72 -> 216x288 -> multiples of 32: 192x288
     p1, p3 = s["proj_matrix"]["stage1"], s["proj_matrix"]["stage3"]
     np.testing.assert_allclose(p3[:, 1, :2, :], p1[:, 1, :2, :] * 4)
-    np.testing.assert_allclose(p1[0, 1, 0, 0], 2892.33 / 4 * 256 / 400, rtol=1e-6)
+    np.testing.assert_allclose(p1[0, 1, 0, 0], 2892.33 / 4 * 288 / 400, rtol=1e-6)
+    np.testing.assert_allclose(p1[0, 1, 1, 1], 2883.18 / 4 * 192 / 300, rtol=1e-6)
     assert len(s["depth_values"]) == 192 and s["depth_values"][1] == np.float32(427.5)
