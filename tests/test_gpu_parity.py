@@ -339,3 +339,24 @@ def test_e2e_images_full_forward(model):
     l1 = float(np.abs(to_np(out["depth"]).astype(np.float64) - g["stage3_depth"]).mean())
     assert l1 <= 1e-4, l1
     assert set(out) == {"stage1", "stage2", "stage3", "depth", "photo_confidence", "prob_volume", "depth_values"}
+
+
+def test_e2e_images_batch_of_two(sd, model):
+    """forward() on a batch of 2 different samples (FeatureNet batches all B*N views; the hot path
+    loops over B): each sample's outputs equal the oracle's single-sample forward."""
+    from oracle import transmvs_ref as oracle
+    H, W, N = 64, 96, 3
+    imgs = torch.cat([synthetic.synthetic_images(N, H, W, seed=10), synthetic.synthetic_images(N, H, W, seed=11)], 0)
+    cams = [synthetic.synthetic_cameras(N, H, W, seed=20), synthetic.synthetic_cameras(N, H, W, seed=21)]
+    proj = {k: torch.cat([c[k] for c in cams], 0) for k in cams[0]}
+    dv = torch.cat([synthetic.synthetic_depth_values(1), synthetic.synthetic_depth_values(1) + 5.0], 0)
+    with torch.no_grad():
+        out = model(imgs.to(DEV), proj, dv.to(DEV))
+        for b in range(2):
+            ref = oracle.forward(sd, imgs[b:b + 1], {k: v[b:b + 1] for k, v in proj.items()}, dv[b:b + 1],
+                                 ndepths=(8, 8, 8))
+            d = np.abs(to_np(out["depth"][b]).astype(np.float64) - ref["depth"][0].numpy()).mean()
+            assert d <= 1e-4, (b, d)
+            np.testing.assert_allclose(to_np(out["stage1"]["prob_volume"][b]), to_np(ref["stage1"]["prob_volume"][0]),
+                                       atol=1e-5)
+    assert out["depth"].shape == (2, H, W) and out["prob_volume"].shape == (2, 8, H, W)
