@@ -923,13 +923,15 @@ __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __re
         const int row = (2 * odl + kd) * LH + 2 * ohl + kh;
         b[r] = *reinterpret_cast<const float4*>(tile + ((row * 2 + (kw & 1)) * SW + col + (kw >> 1)) * 8 + 4 * half);
       }
+      // component-major: consecutive MFMAs alternate accumulators (no back-to-back dependence)
 #pragma unroll
-      for (int r = 0; r < NBW; ++r) {
-        acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[r].x, acc[r], 0, 0, 0);
-        acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[r].y, acc[r], 0, 0, 0);
-        acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[r].z, acc[r], 0, 0, 0);
-        acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[r].w, acc[r], 0, 0, 0);
-      }
+      for (int r = 0; r < NBW; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[r].x, acc[r], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < NBW; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[r].y, acc[r], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < NBW; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[r].z, acc[r], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < NBW; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[r].w, acc[r], 0, 0, 0);
     }
     const int ow = c.ow0 + col;
     const size_t out_n = (size_t)c.n * g.Do * g.Ho * g.Wo;
