@@ -6,4 +6,4 @@ tail -1 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --e2e-steps 0 > $O/bench.json 2>/dev/null || exit $?
 python -c "import json; d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1]); print(d['value'], d['kernel_ms_per_depth_map'])"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $O/trace -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --e2e-steps 0 > $O/trace.log 2>&1 || exit $?
-python scripts/trace_table.py $O/trace/run_kernel_trace.csv | grep -E "deconv|s2c8|total"
+python scripts/trace_table.py $O/trace/run_kernel_trace.csv | grep -E "${AB_REGEX:-deconv|s2c8|total}"

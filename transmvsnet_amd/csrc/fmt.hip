@@ -231,13 +231,13 @@ __device__ __forceinline__ void load_token_frag(const float* __restrict__ row, f
 
 constexpr int kTilesPerWave = 8;  // 16-token tiles per wave (kv): amortises the weight-fragment loads
 constexpr int kApplyTilesPerWave = 4;  // apply: weights come from LDS; more, shorter waves
-constexpr int kKvTilesPerWave = 8;     // kv: more tiles per wave keeps the partial slabs (and the combine) small
+constexpr int kKvTilesPerWave = 8;     // kv: at most this many tiles per wave (see kv_tiles_per_wave)
 
 // (KV, Ksum) partial sums: per wave, tiles of 16 source tokens; K, V by MFMA; per lane the
 // two heads it owns are accumulated over its tokens, then summed over the 16 token lanes.
 __global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __restrict__ src, int S,
                                                               const float* __restrict__ w,
-                                                              float* __restrict__ partial) {
+                                                              float* __restrict__ partial, int tpw) {
   __shared__ float red[4][kKV];
   __shared__ __attribute__((aligned(16))) float frag[2 * 32 * 32];  // Wk, Wv fragments (see stage_afrag)
   const int v = blockIdx.y;
@@ -263,9 +263,14 @@ __global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __rest
   }
   __syncthreads();
   const float* sv = src + (size_t)v * S * kD;
-  const int tile0 = (blockIdx.x * 4 + wv) * kKvTilesPerWave;
+  const int tile0 = (blockIdx.x * 4 + wv) * tpw;
+  floatx4 xnext[2];  // the next tile's tokens, loaded while this tile computes
+  if (tile0 * 16 < S) {
+    const int t = tile0 * 16 + (lane & 15);
+    load_token_frag(sv + (size_t)(t < S ? t : S - 1) * kD, xnext, lane);
+  }
 #pragma unroll 1
-  for (int it = 0; it < kKvTilesPerWave; ++it) {
+  for (int it = 0; it < tpw; ++it) {
     if ((tile0 + it) * 16 >= S) break;  // wave-uniform
     int salt = 0;  // opaque offset: fragment reads stay in the loop (not hoisted back into VGPRs)
     asm volatile("" : "+v"(salt));
@@ -275,7 +280,12 @@ __global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __rest
     {
       const int t = (tile0 + it) * 16 + (lane & 15);
       okp[0] = t < S;
-      load_token_frag(sv + (size_t)(okp[0] ? t : S - 1) * kD, xin[0], lane);
+      xin[0][0] = xnext[0];
+      xin[0][1] = xnext[1];
+      if (it + 1 < tpw && (tile0 + it + 1) * 16 < S) {
+        const int tn = t + 16;
+        load_token_frag(sv + (size_t)(tn < S ? tn : S - 1) * kD, xnext, lane);
+      }
     }
     mfma_linear_lds<32, 32, 1>(fr, xin, kk, lane);
     mfma_linear_lds<32, 32, 1>(fr + 1024, xin, vv, lane);
@@ -335,20 +345,21 @@ __global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __rest
 
 // grid (nv, 5): 8 groups x 32 entries; group g sums partial blocks g, g+8, ... with all
 // loads independent, then the 8 group sums are added in a fixed order (bitwise reproducible).
-__global__ __launch_bounds__(256) void fmt_kv_combine_kernel(const float* __restrict__ partial, int nblk,
-                                                             float* __restrict__ kv) {
-  __shared__ float red[8][32];
+__global__ __launch_bounds__(1024) void fmt_kv_combine_kernel(const float* __restrict__ partial, int nblk,
+                                                              float* __restrict__ kv) {
+  __shared__ float red[32][32];
   const int v = blockIdx.x;
   const int e = blockIdx.y * 32 + (threadIdx.x & 31);
   const int g = threadIdx.x >> 5;
   float s = 0.f;
-  for (int b = g; b < nblk; b += 8) s += partial[((size_t)v * nblk + b) * kKV + e];
+#pragma unroll 4
+  for (int b = g; b < nblk; b += 32) s += partial[((size_t)v * nblk + b) * kKV + e];
   red[g][threadIdx.x & 31] = s;
   __syncthreads();
   if (g == 0) {
     float t = red[0][threadIdx.x];
 #pragma unroll
-    for (int k = 1; k < 8; ++k) t += red[k][threadIdx.x];
+    for (int k = 1; k < 32; ++k) t += red[k][threadIdx.x];
     kv[(size_t)v * kKV + e] = t;
   }
 }
@@ -373,6 +384,12 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
   __syncthreads();
   float* xv = x + (size_t)v * L * kD;
   const int tile0 = (blockIdx.x * 4 + wv) * kApplyTilesPerWave;
+  static_assert(kApplyNT == 1, "the token prefetch below assumes one tile per iteration");
+  floatx4 xnext[2];  // the next tile's tokens, loaded while this tile computes
+  if (tile0 * 16 < L) {
+    const int t = tile0 * 16 + (lane & 15);
+    load_token_frag(xv + (size_t)(t < L ? t : L - 1) * kD, xnext, lane);
+  }
 #pragma unroll 1
   for (int it = 0; it < kApplyTilesPerWave; it += kApplyNT) {
     if ((tile0 + it) * 16 >= L) break;  // wave-uniform
@@ -383,12 +400,16 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
     float* row[NT];
     bool ok[NT];
     floatx4 xs[NT][2];
-#pragma unroll
-    for (int p = 0; p < NT; ++p) {
-      const int t = (tile0 + it + p) * 16 + (lane & 15);
-      ok[p] = t < L;
-      row[p] = xv + (size_t)(ok[p] ? t : L - 1) * kD;
-      load_token_frag(row[p], xs[p], lane);
+    {
+      const int t = (tile0 + it) * 16 + (lane & 15);
+      ok[0] = t < L;
+      row[0] = xv + (size_t)(ok[0] ? t : L - 1) * kD;
+      xs[0][0] = xnext[0];
+      xs[0][1] = xnext[1];
+      if (it + 1 < kApplyTilesPerWave && (tile0 + it + 1) * 16 < L) {
+        const int tn = t + 16;
+        load_token_frag(xv + (size_t)(tn < L ? tn : L - 1) * kD, xnext, lane);
+      }
     }
     floatx4 q[NT][2], msg[NT][2];
     mfma_linear_lds<32, 32, NT>(fr, xs, q, lane);
@@ -448,7 +469,18 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
   }
 }
 
-static int kv_nblk(int S) { return (S + 16 * 4 * kKvTilesPerWave - 1) / (16 * 4 * kKvTilesPerWave); }
+// Tiles per wave: as many as possible (small partial slabs, short combine) while the launch still
+// has >= 2048 waves (2 per SIMD); the one-view cross-attention K/V otherwise runs at 0.1 waves/SIMD.
+static int kv_tiles_per_wave(int nv, int S) {
+  const int tiles = (S + 15) / 16;
+  int tpw = kKvTilesPerWave;
+  while (tpw > 2 && (long)nv * ((tiles + tpw - 1) / tpw) < 2048) tpw >>= 1;
+  return tpw;
+}
+static int kv_nblk(int nv, int S) {
+  const int per = 16 * 4 * kv_tiles_per_wave(nv, S);
+  return (S + per - 1) / per;
+}
 static int apply_nblk(int L) { return (L + 16 * 4 * kApplyTilesPerWave - 1) / (16 * 4 * kApplyTilesPerWave); }
 
 }  // namespace tmvs
@@ -467,19 +499,19 @@ extern "C" int tmvs_fmt_embed(const float* feat, long feat_view_stride, const fl
 }
 
 extern "C" size_t tmvs_fmt_kv_workspace(int nv, int s_tokens) {
-  return (size_t)nv * kv_nblk(s_tokens) * kKV * sizeof(float);
+  return (size_t)nv * kv_nblk(nv, s_tokens) * kKV * sizeof(float);
 }
 
 extern "C" int tmvs_fmt_kv(const float* source, int nv, int s_tokens, const float* enc_w, void* workspace,
                            size_t workspace_bytes, float* kv, void* stream) {
   if (!source || !enc_w || !workspace || !kv || nv <= 0 || s_tokens <= 0) return TMVS_ERR_ARG;
   if (workspace_bytes < tmvs_fmt_kv_workspace(nv, s_tokens)) return TMVS_ERR_ARG;
-  const int nblk = kv_nblk(s_tokens);
+  const int nblk = kv_nblk(nv, s_tokens);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(fmt_kv_partial_kernel, dim3(nblk, nv), dim3(kKvBlock), 0, st, source, s_tokens, enc_w,
-                     (float*)workspace);
+                     (float*)workspace, kv_tiles_per_wave(nv, s_tokens));
   TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(fmt_kv_combine_kernel, dim3(nv, kKV / 32), dim3(256), 0, st, (const float*)workspace, nblk, kv);
+  hipLaunchKernelGGL(fmt_kv_combine_kernel, dim3(nv, kKV / 32), dim3(1024), 0, st, (const float*)workspace, nblk, kv);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }

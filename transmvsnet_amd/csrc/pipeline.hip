@@ -3,10 +3,14 @@
 #include "common.h"
 
 static size_t align_up256(size_t v) { return (v + 255) & ~(size_t)255; }
+static size_t fmt_kv_slab(int nv, int l_tokens) {  // self K/V runs on nv views, cross K/V on one
+  const size_t a = tmvs_fmt_kv_workspace(nv, l_tokens), b = tmvs_fmt_kv_workspace(1, l_tokens);
+  return align_up256(a > b ? a : b);
+}
 
 extern "C" size_t tmvs_fmt_forward_workspace(int nv, int l_tokens) {
   // kv slabs (one per layer application in flight) + 4 cross-layer kv + per-view kv
-  return align_up256(tmvs_fmt_kv_workspace(nv, l_tokens)) + align_up256((size_t)(4 + nv) * TMVS_KV_NFLOATS * 4);
+  return fmt_kv_slab(nv, l_tokens) + align_up256((size_t)(4 + nv) * TMVS_KV_NFLOATS * 4);
 }
 
 // FMT of FMT_with_pathway (models/FMT.py:147-177, 212-226), all views batched on the launch
@@ -20,7 +24,7 @@ extern "C" int tmvs_fmt_forward(const float* stage1, long view_stride, const flo
   const int L = height * width;
   if (workspace_bytes < tmvs_fmt_forward_workspace(nv, L)) return TMVS_ERR_ARG;
   char* ws = (char*)workspace;
-  const size_t slab = align_up256(tmvs_fmt_kv_workspace(nv, L));
+  const size_t slab = fmt_kv_slab(nv, L);
   void* kv_ws = ws;
   float* kv_cross = (float*)(ws + slab);
   float* kv_self = kv_cross + 4 * TMVS_KV_NFLOATS;
