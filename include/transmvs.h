@@ -276,6 +276,29 @@ int tmvs_conv2d_bn_relu(const float* x, int batch, int cin, int height, int widt
 int tmvs_fusibile(const float* rgbd, const float* cams, int n_views, int height, int width, int ref_view,
                   int consistent_threshold, float depth_threshold, float* coord, float* texture, void* stream);
 
+/* ------------------------------------------------------------------ training losses
+ * entropy_loss (models/module.py:495-529) of one stage, as trans_mvsnet_loss / focal_loss_bld
+ * (:532-588) call it, fused with the backward through the stage's softmax (:prob = softmax(logits)).
+ *   prob        [batch][ndepth][H][W]   softmax probability volume (outputs[stage]["prob_volume"])
+ *   depth_values [batch][ndepth][H][W] (dv_per_pixel = 1) or [batch][ndepth] (0, module.py:503-504)
+ *   depth_gt, mask [batch][H][W]        mask > 0.5 is valid (module.py:540)
+ *   out (device, 2 floats): out[0] = entropy loss (unweighted, :522), out[1] = smooth-L1 depth_loss of
+ *             the WTA depth over the masked pixels (:545; NaN for an empty mask, as torch)
+ *   wta_depth / photo_conf [batch][H][W] (nullable): WTA depth (:524-525) and max prob (:528)
+ *   grad_logits [batch][ndepth][H][W] (nullable): d(grad_scale * loss)/d(logits); grad_scale is the
+ *             caller's weight of this stage's loss (entropy_weight 2.0 x dlossw[stage], :547-553).
+ *   workspace: tmvs_entropy_loss_workspace(batch, H, W) bytes of device memory.                   */
+size_t tmvs_entropy_loss_workspace(int batch, int height, int width);
+int tmvs_entropy_loss(const float* prob, const float* depth_values, int dv_per_pixel, const float* depth_gt,
+                      const float* mask, int batch, int ndepth, int height, int width, float grad_scale,
+                      void* workspace, size_t workspace_bytes, float* out, float* wta_depth, float* photo_conf,
+                      float* grad_logits, void* stream);
+/* focal_loss_bld's metrics (module.py:581-587): err = |gt - depth| / (depth_interval * 192 / 128) over
+ * the n masked elements; out (device, 3 floats) = {epe, less1, less3}; NaN for an empty mask.      */
+size_t tmvs_depth_metrics_workspace(int n);
+int tmvs_depth_metrics(const float* depth, const float* depth_gt, const float* mask, int n, float depth_interval,
+                       void* workspace, size_t workspace_bytes, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

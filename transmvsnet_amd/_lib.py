@@ -49,6 +49,10 @@ SIGNATURES = {
     "tmvs_conv2d_pack": (I, [P, I, I, I, P]),
     "tmvs_conv2d_bn_relu": (I, [P, I, I, I, I, P, I, I, I, P, P, I, P, P]),
     "tmvs_fusibile": (I, [P, P, I, I, I, I, I, F, P, P, P]),
+    "tmvs_entropy_loss_workspace": (S, [I, I, I]),
+    "tmvs_entropy_loss": (I, [P, P, I, P, P, I, I, I, I, F, P, S, P, P, P, P, P]),
+    "tmvs_depth_metrics_workspace": (S, [I]),
+    "tmvs_depth_metrics": (I, [P, P, P, I, F, P, S, P, P]),
 }
 
 ABI_VERSION = 1

@@ -422,3 +422,51 @@ def conv2d_bn_relu(x, w_packed, cout, k, stride, bn=None, relu=True, nchw_input=
         _lib.check(_lib_h().tmvs_conv2d_bn_relu(_ptr(x), b, cin, h, w, _ptr(w_packed), cout, k, stride, _ptr(alpha),
                                                 _ptr(shift), int(relu), _ptr(out), _stream()), "tmvs_conv2d_bn_relu")
     return out
+
+
+def entropy_loss(prob, depth_values, depth_gt, mask, grad_scale=0.0, want_grad=False):
+    """One stage's entropy_loss (models/module.py:495-529) + smooth-L1 depth loss (:545), and with
+    want_grad the gradient of grad_scale * loss w.r.t. the stage's softmax logits.
+    Returns (loss [], depth_loss [], wta_depth [B,H,W], photo_conf [B,H,W], grad_logits or None)."""
+    for t, n in ((prob, "prob"), (depth_values, "depth_values"), (depth_gt, "depth_gt"), (mask, "mask")):
+        _dev(t, n)
+    b, d, h, w = prob.shape
+    if depth_values.dim() == 4:
+        if tuple(depth_values.shape) != (b, d, h, w):
+            raise ValueError("depth_values must be [B,D,H,W] or [B,D]")
+        per_pixel = 1
+    elif tuple(depth_values.shape) == (b, d):
+        per_pixel = 0
+    else:
+        raise ValueError("depth_values must be [B,D,H,W] or [B,D]")
+    if tuple(depth_gt.shape) != (b, h, w) or tuple(mask.shape) != (b, h, w):
+        raise ValueError("depth_gt and mask must be [B,H,W]")
+    nbytes = _lib_h().tmvs_entropy_loss_workspace(b, h, w)
+    ws = torch.empty(nbytes // 4 + 64, device=prob.device)
+    out = torch.empty(2, device=prob.device)
+    wta = torch.empty(b, h, w, device=prob.device)
+    conf = torch.empty_like(wta)
+    grad = torch.empty_like(prob) if want_grad else None
+    with _Span("tmvs_entropy_loss"):
+        _lib.check(_lib_h().tmvs_entropy_loss(_ptr(prob), _ptr(depth_values), per_pixel, _ptr(depth_gt), _ptr(mask), b,
+                                              d, h, w, ctypes.c_float(grad_scale), _ptr(ws), ws.numel() * 4,
+                                              _ptr(out), _ptr(wta), _ptr(conf), _ptr(grad), _stream()),
+                   "tmvs_entropy_loss")
+    return out[0], out[1], wta, conf, grad
+
+
+def depth_metrics(depth, depth_gt, mask, depth_interval):
+    """focal_loss_bld's epe / less1 / less3 (models/module.py:581-587) -> tensor [3]."""
+    for t, n in ((depth, "depth"), (depth_gt, "depth_gt"), (mask, "mask")):
+        _dev(t, n)
+    if depth.shape != depth_gt.shape or depth.shape != mask.shape:
+        raise ValueError("depth, depth_gt and mask must have one shape")
+    n = depth.numel()
+    nbytes = _lib_h().tmvs_depth_metrics_workspace(n)
+    ws = torch.empty(nbytes // 4 + 64, device=depth.device)
+    out = torch.empty(3, device=depth.device)
+    with _Span("tmvs_depth_metrics"):
+        _lib.check(_lib_h().tmvs_depth_metrics(_ptr(depth), _ptr(depth_gt), _ptr(mask), n,
+                                               ctypes.c_float(float(depth_interval)), _ptr(ws), ws.numel() * 4,
+                                               _ptr(out), _stream()), "tmvs_depth_metrics")
+    return out
