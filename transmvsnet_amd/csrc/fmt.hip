@@ -343,8 +343,8 @@ __global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __rest
   }
 }
 
-// grid (nv, 5): 8 groups x 32 entries; group g sums partial blocks g, g+8, ... with all
-// loads independent, then the 8 group sums are added in a fixed order (bitwise reproducible).
+// grid (nv, 5): 32 groups x 32 entries; group g sums partial blocks g, g+32, ... with all
+// loads independent, then the 32 group sums are added in a fixed order (bitwise reproducible).
 __global__ __launch_bounds__(1024) void fmt_kv_combine_kernel(const float* __restrict__ partial, int nblk,
                                                               float* __restrict__ kv) {
   __shared__ float red[32][32];
