@@ -4,6 +4,9 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+Without a launcher, --gpus N > 1 makes this (GPU-untouched) process spawn N fresh rank processes
+(rendezvous on 127.0.0.1, RCCL); under torchrun each process is one rank (WORLD_SIZE from the env).
+
 A step is one hot-path forward (TransMVSNet.forward_features: FMT + pathway + 3-stage
 stage glue / fused cost volume / CostRegNet / softmax-WTA) of one depth map from synthetic
 FeatureNet-shaped features already resident in HBM; random-init weights of the reference
@@ -40,7 +43,9 @@ def _args():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--mode", choices=("replica", "views"), default="replica")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="oracle threads for cpu_baseline; 0 = the cores this process may run on")
+    ap.add_argument("--cpu-runs", type=int, default=3, help="timed oracle runs (after 1 warm-up); median")
     ap.add_argument("--profile-steps", type=int, default=3)
     ap.add_argument("--no-overlap", action="store_true", help="run the FMT pathway on the main stream (A/B)")
     ap.add_argument("--e2e-steps", type=int, default=10,
@@ -88,22 +93,66 @@ def make_inputs(device, seed_feat=2):
     from transmvsnet_amd import synthetic
     proj = synthetic.synthetic_cameras(NVIEWS, H, W, seed=1)
     dv = synthetic.synthetic_depth_values(1)
-    g = torch.Generator(device="cpu").manual_seed(seed_feat)
-    feats = {}
-    for name, c, s in (("stage1", 32, 4), ("stage2", 16, 2), ("stage3", 8, 1)):
-        feats[name] = torch.randn(1, NVIEWS, c, H // s, W // s, generator=g)
-    return feats, proj, dv
+    return synthetic.stacked_features(NVIEWS, H, W, seed=seed_feat), proj, dv
+
+
+def resolve_launch(gpus, env):
+    """How this invocation maps onto ranks (no GPU call is made here).
+
+    -> ("spawn", N): no launcher env and --gpus N > 1: this parent spawns N fresh rank processes;
+       ("rank", world, rank, local_rank): run one rank (torchrun env, or a single process).
+    """
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if gpus not in (1, world):
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}")
+        return ("rank", world, int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", env.get("RANK", "0"))))
+    if gpus > 1:
+        return ("spawn", gpus)
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    return ("rank", 1, 0, 0)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(rank, world, port):
+    """Environment of spawned rank `rank` (torchrun's variables, rendezvous on 127.0.0.1)."""
+    return {"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_WORLD_SIZE": str(world),
+            "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)}
+
+
+def _spawned(rank, args, world, port):
+    os.environ.update(rank_env(rank, world, port))
+    run(args, world, rank, rank)
 
 
 def main():
     args = _args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    how = resolve_launch(args.gpus, os.environ)
+    if how[0] == "spawn":
+        # this parent has made no GPU call: start N fresh interpreters (spawn, not fork/exec of a
+        # GPU-initialised process), one per GPU; a failing rank raises here
+        import torch.multiprocessing as mp
+        mp.start_processes(_spawned, args=(args, how[1], _free_port()), nprocs=how[1], join=True,
+                           start_method="spawn")
+        return
+    _, world, rank, local = how
+    run(args, world, rank, local)
+
+
+def run(args, world, rank, local):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != world:
+            raise RuntimeError(f"process group has {dist.get_world_size()} ranks, expected {world}")
 
     from transmvsnet_amd import TransMVSNet, ops, synthetic
     model = TransMVSNet().eval()
@@ -136,18 +185,32 @@ def main():
         if world > 1:
             dist.barrier()
         elapsed = t1 - t0
+        ranks_ok = None
         if world > 1:
             t = torch.tensor([elapsed], device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
+            # every rank ran the same K steps on the same inputs: its final depth map must be
+            # bitwise identical to every other rank's (deterministic kernels), else the job failed
+            chk = torch.tensor([float(args.steps), float(out["depth"].double().sum())], device=dev, dtype=torch.float64)
+            allc = [torch.empty_like(chk) for _ in range(world)]
+            dist.all_gather(allc, chk)
+            allc = [c.cpu().tolist() for c in allc]
+            if any(c != allc[0] for c in allc):
+                raise RuntimeError(f"ranks disagree (steps, depth checksum): {allc}")
+            ranks_ok = {"ranks": world, "steps_each": args.steps, "depth_checksum": allc[0][1]}
 
         # instrumented steps (outside the timed region): per-launch HIP-event durations
         timer = EventTimer()
         model.decomposed = True   # same kernels, one C-ABI call each, so each gets its own event pair
         ops.set_timer(timer)
+        if shard is not None:
+            shard.timer = timer
         for _ in range(args.profile_steps):
             step()
         ops.set_timer(None)
+        if shard is not None:
+            shard.timer = None
         model.decomposed = False
         spans = timer.durations()
 
@@ -197,10 +260,19 @@ def main():
         except Exception:
             pass
 
+    comm = None
+    if shard is not None:
+        ar = per_kernel.get("rccl_all_reduce", [])
+        if ar:
+            per_launch = np.array(ar).reshape(steps_p, -1).mean(0)
+            comm = {"collective": "all_reduce(SUM) of packed [D+1,h,w] fp32 per stage",
+                    "bytes_per_stage": shard.comm_bytes[:3], "ms_per_stage": [round(float(x), 4) for x in per_launch],
+                    "busbw_GBs": [round(2 * (world - 1) / world * b / (ms * 1e-3) / 1e9, 1)
+                                  for b, ms in zip(shard.comm_bytes[:3], per_launch)]}
     cpu = None
     l1 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, l1 = cpu_baseline(args.cpu_threads, feats_cpu, proj, dv, out)
+        cpu, l1 = cpu_baseline(args.cpu_threads, args.cpu_runs, feats_cpu, proj, dv, out)
 
     if rank == 0:
         line = {
@@ -226,6 +298,10 @@ def main():
             "abs_depth_l1_vs_ref": l1,
             "end_to_end": e2e,
         }
+        if ranks_ok is not None:
+            line["ranks_check"] = ranks_ok
+        if comm is not None:
+            line["allreduce"] = comm
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -259,43 +335,81 @@ def end_to_end(model, steps, proj, dv_dev, dev):
                         "path above"}
 
 
-def cpu_baseline(threads, feats_cpu, proj, dv, gpu_out):
-    """The oracle (torch-CPU restatement of the reference forward) on the host cores.
-
-    Bounded sample: one full DTU depth map (same inputs/weights) after one untimed
-    repetition; also returns the mean |depth_gpu - depth_cpu| (the 'Abs depth L1 vs ref').
-    """
-    import platform
-
-    from oracle import transmvs_ref as oracle
-    from transmvsnet_amd import synthetic
-    torch.set_num_threads(threads)
-    from transmvsnet_amd import TransMVSNet
-    shapes = synthetic.state_dict_shapes(TransMVSNet())
-    sd = synthetic.synthetic_state_dict(shapes, seed=0, sharpen=100.0)
-    feats = [{k: v[:, i] for k, v in feats_cpu.items()} for i in range(NVIEWS)]
-    with torch.no_grad():
-        t0 = time.perf_counter()
-        ref = oracle.forward_from_features(sd, feats, proj, dv, (H, W))
-        t1 = time.perf_counter()
-    d_gpu = gpu_out["depth"].float().cpu().numpy().astype(np.float64)
-    d_ref = ref["depth"].numpy().astype(np.float64)
-    l1 = float(np.abs(d_gpu - d_ref).mean())
-    cpu_model = platform.processor() or "unknown"
+def host_cores():
+    """(cores this process may run on, cgroup CPU quota or None, CPU model)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    cpu_model = line.split(":", 1)[1].strip()
+                    model = line.split(":", 1)[1].strip()
                     break
     except OSError:
         pass
-    return ({"value": round(1.0 / (t1 - t0), 5), "unit": "depth_maps/s", "cores": threads, "kind": "port",
-             "sample": f"1 DTU depth map (864x1152, N=5, 48/32/8) through the oracle's hot path, "
-                       f"{t1 - t0:.2f} s, torch-CPU fp32, {threads} threads, {cpu_model}"},
-            {"stage3_mean_abs_mm": l1,
-             "stage3_max_abs_mm": float(np.abs(d_gpu - d_ref).max()),
-             "stage3_frac_pixels_differing": float((np.abs(d_gpu - d_ref) > 1e-3).mean())})
+    return n, quota, model
+
+
+def parity_report(gpu_out, ref, margin=1e-4):
+    """Abs depth L1 vs the reference restatement, per stage, with every differing pixel
+    classified: a near-tie has a top-2 log-prob margin < `margin` in the reference's prob volume
+    (SURVEY.md 8c); a flip elsewhere is a real mismatch."""
+    rep = {}
+    for s in (1, 2, 3):
+        g = gpu_out[f"stage{s}"]["depth"].float().cpu().numpy().astype(np.float64)
+        r = ref[f"stage{s}"]["depth"].numpy().astype(np.float64)
+        pr = ref[f"stage{s}"]["prob_volume"].numpy().astype(np.float64)
+        srt = np.sort(pr, axis=1)
+        near = (np.log(np.maximum(srt[:, -1], 1e-30)) - np.log(np.maximum(srt[:, -2], 1e-30))) < margin
+        diff = np.abs(g - r) > 1e-3
+        rep[f"stage{s}"] = {"mean_abs_mm": float(np.abs(g - r).mean()), "max_abs_mm": float(np.abs(g - r).max()),
+                            "pixels_differing": int(diff.sum()), "near_tie_flips": int((diff & near).sum()),
+                            "other_flips": int((diff & ~near).sum())}
+    d3 = rep["stage3"]
+    return {"stage3_mean_abs_mm": d3["mean_abs_mm"], "stage3_max_abs_mm": d3["max_abs_mm"],
+            "stage3_frac_pixels_differing": d3["pixels_differing"] / gpu_out["depth"].numel(),
+            "per_stage": rep, "near_tie_margin": margin}
+
+
+def cpu_baseline(threads, runs, feats_cpu, proj, dv, gpu_out):
+    """The oracle (torch-CPU restatement of the reference forward) on the host cores.
+
+    SURVEY.md 8d recipe: torch threads = the cores this process may run on (sched_getaffinity,
+    capped by a cgroup CPU quota when one is set), 1 untimed warm-up run, then `runs` timed runs of
+    one full DTU depth map (same inputs/weights as the GPU step); the median is reported. Also
+    returns the per-stage 'Abs depth L1 vs ref' of the GPU step against the last run's output.
+    """
+    from oracle import transmvs_ref as oracle
+    from transmvsnet_amd import TransMVSNet, synthetic
+    n_aff, quota, cpu_model = host_cores()
+    if threads <= 0:
+        threads = n_aff if quota is None else max(1, min(n_aff, int(quota)))
+    torch.set_num_threads(threads)
+    shapes = synthetic.state_dict_shapes(TransMVSNet())
+    sd = synthetic.synthetic_state_dict(shapes, seed=0, sharpen=100.0)
+    feats = [{k: v[:, i] for k, v in feats_cpu.items()} for i in range(NVIEWS)]
+    ts = []
+    with torch.no_grad():
+        for i in range(runs + 1):
+            t0 = time.perf_counter()
+            ref = oracle.forward_from_features(sd, feats, proj, dv, (H, W))
+            t1 = time.perf_counter()
+            if i > 0:
+                ts.append(t1 - t0)
+    med = float(np.median(ts))
+    quota_txt = f", cgroup quota {quota:g} CPUs" if quota is not None else ""
+    return ({"value": round(1.0 / med, 5), "unit": "depth_maps/s", "cores": threads, "kind": "port",
+             "sample": f"1 DTU depth map (864x1152, N=5, 48/32/8) through the oracle's hot path (torch-CPU fp32); "
+                       f"median of {runs} timed runs after 1 warm-up: {med:.2f} s (runs {', '.join(f'{t:.2f}' for t in ts)}); "
+                       f"{threads} threads = sched_getaffinity {n_aff}{quota_txt}; {cpu_model}"},
+            parity_report(gpu_out, ref))
 
 
 if __name__ == "__main__":

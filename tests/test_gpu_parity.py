@@ -360,3 +360,25 @@ def test_e2e_images_batch_of_two(sd, model):
             np.testing.assert_allclose(to_np(out["stage1"]["prob_volume"][b]), to_np(ref["stage1"]["prob_volume"][0]),
                                        atol=1e-5)
     assert out["depth"].shape == (2, H, W) and out["prob_volume"].shape == (2, 8, H, W)
+
+
+def test_e2e_images_batch_of_two_different_depth_ranges(sd, model):
+    """B=2 whose samples have different depth-range widths, against the oracle's BATCHED forward:
+    stage 1 samples each sample's own range, stages 2/3 take the hypothesis interval from
+    depth_values[0] for both samples (models/TransMVSNet.py:146-148, get_depth_samples)."""
+    from oracle import transmvs_ref as oracle
+    H, W, N = 64, 96, 3
+    imgs = torch.cat([synthetic.synthetic_images(N, H, W, seed=12), synthetic.synthetic_images(N, H, W, seed=13)], 0)
+    cams = [synthetic.synthetic_cameras(N, H, W, seed=22), synthetic.synthetic_cameras(N, H, W, seed=23)]
+    proj = {k: torch.cat([c[k] for c in cams], 0) for k in cams[0]}
+    dv0 = synthetic.synthetic_depth_values(1)
+    dv = torch.cat([dv0, 450.0 + (dv0 - 425.0) * 1.5], 0)   # sample 1: 450..1166 mm, 1.5x the interval
+    with torch.no_grad():
+        out = model(imgs.to(DEV), proj, dv.to(DEV))
+        ref = oracle.forward(sd, imgs, proj, dv, ndepths=(8, 8, 8))
+    for s in (1, 2, 3):
+        np.testing.assert_allclose(to_np(out[f"stage{s}"]["depth_values"]), to_np(ref[f"stage{s}"]["depth_values"]),
+                                   rtol=0, atol=0 if s == 1 else 1e-3)
+        mean_l1, near, flips = depth_parity(to_np(out[f"stage{s}"]["depth"]), to_np(ref[f"stage{s}"]["depth"]),
+                                            to_np(ref[f"stage{s}"]["prob_volume"]))
+        assert flips == 0, (s, mean_l1, near, flips)

@@ -50,6 +50,8 @@ class ViewShard:
         self.src_views = partition_views(n_src, world, rank)
         self._partial = partial_fn or _hip_partial
         self._finalize = finalize_fn or _hip_finalize
+        self.timer = None       # optional begin(name)/end(token) around each collective (bench.py)
+        self.comm_bytes = []    # bytes of each all-reduce issued, in order (3 per forward)
 
     @property
     def local_views(self) -> List[int]:
@@ -85,7 +87,12 @@ class ViewShard:
 
     def allreduce(self, buf: torch.Tensor) -> None:
         if self.world > 1:
+            tok = self.timer.begin("rccl_all_reduce") if self.timer is not None else None
             dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+            if tok is not None:
+                self.timer.end(tok)
+            if len(self.comm_bytes) < 3:
+                self.comm_bytes.append(buf.numel() * buf.element_size())
 
 
 def _hip_partial(fs, rows, hyp, stage, view_w, pw, sim_out, wsum_out):

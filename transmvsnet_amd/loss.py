@@ -63,8 +63,12 @@ def trans_mvsnet_loss(inputs, depth_gt_ms, mask_ms, dlossw=None, return_grad=Fal
 
 def focal_loss_bld(inputs, depth_gt_ms, mask_ms, depth_interval, dlossw=None, return_grad=False):
     """module.py:559: (total_loss, depth_loss, epe, less1, less3). depth_interval: a number or a
-    one-element tensor (the reference broadcasts a [B] tensor against [B,H,W] along W, which is
-    only meaningful for B == 1)."""
+    one-element tensor. The reference divides [B,H,W] errors by a [B] tensor, which broadcasts
+    along W (an error unless W == B, and then not a per-sample scaling): a depth_interval with more
+    than one element is refused here rather than silently reduced to sample 0's."""
+    if torch.is_tensor(depth_interval) and depth_interval.numel() != 1:
+        raise ValueError(f"focal_loss_bld: depth_interval must be a number or a one-element tensor, got shape "
+                         f"{tuple(depth_interval.shape)} (the reference's [B] broadcast is along W)")
     total, depth_loss, _, _, grads = _stage_losses(inputs, depth_gt_ms, mask_ms, dlossw, return_grad)
     di = float(depth_interval.reshape(-1)[0]) if torch.is_tensor(depth_interval) else float(depth_interval)
     m = ops.depth_metrics(_f32(inputs["stage3"]["depth"]), _f32(depth_gt_ms["stage3"]), _f32(mask_ms["stage3"]), di)

@@ -6,8 +6,10 @@ Its submodules are parameter containers with the reference names; the depth-infe
 path -- FMT linear attention, the FMT pathway, stage glue, the fused warp + correlation +
 view-aggregation cost volume, CostRegNet and softmax/WTA -- runs as hand-written HIP kernels
 through the C-ABI (include/transmvs.h). Weights are re-laid-out once per load_state_dict into
-the kernels' packed formats (BN folded exactly as the reference CPU kernel folds it).
-FeatureNet stays on PyTorch-ROCm for now (featurenet.py).
+the kernels' packed formats (BN folded exactly as the reference CPU kernel folds it), and
+re-packed whenever a parameter or buffer is replaced or updated in place. FeatureNet (SURVEY.md
+8f rank 1) runs natively too (featurenet.py: trunk conv, FPN merge, fused DCN kernels).
+Inference only: BatchNorm is folded with running statistics, so forward() refuses train mode.
 """
 from __future__ import annotations
 
@@ -219,6 +221,7 @@ class TransMVSNet(nn.Module):
         self.cost_regularization = nn.ModuleList([CostRegNet(1, self.cr_base_chs[i]) for i in range(self.num_stage)])
         self.DepthNet = DepthNet()
         self._prep = None
+        self._tracked = None
         self._pe = {}
         self.decomposed = False  # True: one C-ABI call per op (instrumentation); False: native stage calls
         # the FMT pathway (stage-2/3 features) depends only on the FMT output: run it on a side
@@ -227,19 +230,35 @@ class TransMVSNet(nn.Module):
         self._side = {}
         self.register_load_state_dict_post_hook(lambda m, k: m.invalidate())
 
+    def _apply(self, fn, *a, **kw):  # .to() / .cuda() / .float() replace tensors: re-track them
+        self._tracked = None
+        self._prep = None
+        return super()._apply(fn, *a, **kw)
+
     def invalidate(self):
         """Drop packed kernel weights (after any in-place parameter change)."""
         self._prep = None
 
+    def _param_key(self):
+        """Identity + in-place version of every parameter/buffer the packed weights derive from:
+        an optimizer step or a .copy_() bumps a version, a reassignment changes a data_ptr."""
+        ts = self._tracked
+        if ts is None:
+            ts = self._tracked = [t for t in list(self.parameters()) + list(self.buffers())]
+        return (len(ts), sum(t._version for t in ts), hash(tuple(t.data_ptr() for t in ts)))
+
     # --------------------------------------------------------- weight preparation
     def _prepared(self, device):
-        if self._prep is not None and self._prep["device"] == device:
+        key = self._param_key()
+        if self._prep is not None and self._prep["device"] == device and self._prep["key"] == key:
             return self._prep
+        self._prep = None
         fp = self.FMT_with_pathway
         enc = [layer.packed().to(device) for layer in fp.FMT.layers]
         cr = [c.packed(device) for c in self.cost_regularization]
         self._prep = {
             "device": device,
+            "key": key,
             "enc": enc,
             "red1": fp.dim_reduction_1.weight.detach().float().reshape(16, 32).t().contiguous().to(device),
             "red2": fp.dim_reduction_2.weight.detach().float().reshape(8, 16).t().contiguous().to(device),
@@ -260,10 +279,17 @@ class TransMVSNet(nn.Module):
     def forward(self, imgs, proj_matrix, depth_values):
         """models/TransMVSNet.py:141-226. FeatureNet runs once over all B*N views (the reference
         loops over views, :151-153; eval BatchNorm is per sample, so batching is exact)."""
+        self._check_eval()
         b, n = imgs.shape[:2]
-        f = self.feature(imgs.reshape(b * n, *imgs.shape[2:]))
+        with torch.cuda.device(imgs.device):
+            f = self.feature(imgs.reshape(b * n, *imgs.shape[2:]))
         feats = {k: v.reshape(b, n, *v.shape[1:]) for k, v in f.items()}
         return self.forward_features(feats, proj_matrix, depth_values, (imgs.shape[3], imgs.shape[4]))
+
+    def _check_eval(self):
+        if self.training:
+            raise RuntimeError("transmvsnet_amd.TransMVSNet runs inference only (BatchNorm folded with running "
+                               "statistics); call .eval() first")
 
     @staticmethod
     def stack_features(features):
@@ -279,12 +305,18 @@ class TransMVSNet(nn.Module):
         features: per-view list of FeatureNet dicts, or {stage: [B,N,C,h,w]} stacked.
         view_shard: optional transmvsnet_amd.distributed.ViewShard (source views split over ranks).
         """
+        self._check_eval()
         feats = self.stack_features(features)
         if view_shard is not None:  # reference view + this rank's source views only
             feats = view_shard.select_features(feats)
         dev = feats["stage1"].device
         if not feats["stage1"].is_cuda:
             raise RuntimeError("TransMVSNet (HIP) needs GPU features; the HIP path has no CPU fallback")
+        with torch.cuda.device(dev):  # kernels + current stream of the features' device
+            return self._forward_features(feats, proj_matrix, depth_values, img_hw, return_view_weights,
+                                          view_shard, dev)
+
+    def _forward_features(self, feats, proj_matrix, depth_values, img_hw, return_view_weights, view_shard, dev):
         prep = self._prepared(dev)
         dv = depth_values.to(dev, torch.float32).contiguous()
         rows = {k: ops.proj_rows(proj_matrix[k]) for k in ("stage1", "stage2", "stage3")}
@@ -293,9 +325,11 @@ class TransMVSNet(nn.Module):
         b = feats["stage1"].shape[0]
         per = []
         vws = []
+        # stage 1 samples each sample's own depth range; the stage-2/3 hypothesis interval comes
+        # from depth_values[0] for every sample (models/TransMVSNet.py:146-148)
         for i in range(b):
             o, vw = self._forward_one({k: v[i] for k, v in feats.items()}, {k: r[i:i + 1] for k, r in rows.items()},
-                                      dv[i:i + 1], img_hw, prep, view_shard)
+                                      dv[i:i + 1], dv[0:1], img_hw, prep, view_shard)
             per.append(o)
             vws.append(vw)
         outputs = {}
@@ -315,7 +349,7 @@ class TransMVSNet(nn.Module):
         n, c, h1, w1 = s1.shape
         return ops.fmt_forward(s1, self._pe_slice(h1, w1, s1.device), prep["enc"])
 
-    def _forward_one(self, f, rows, dv, img_hw, prep, view_shard):
+    def _forward_one(self, f, rows, dv, dv0, img_hw, prep, view_shard):
         s1, s2, s3 = f["stage1"], f["stage2"], f["stage3"]
         n, _, h1, w1 = s1.shape
         tokens = self._fmt(s1, prep)
@@ -359,12 +393,12 @@ class TransMVSNet(nn.Module):
                 torch.cuda.current_stream(s1.device).wait_event(lateral["done"])
             fs = (st1, lateral.get("st2"), lateral.get("st3"))[s]
             if view_shard is None and not self.decomposed and s > 0:
-                out, depth_raw = ops.depth_stage(dv, depth_raw, fs, self.ndepths[s], self.depth_interals_ratio[s],
+                out, depth_raw = ops.depth_stage(dv0, depth_raw, fs, self.ndepths[s], self.depth_interals_ratio[s],
                                                  img_hw, STAGE_SCALES[s], rows[name][0], None, view_w, s,
                                                  prep["cr"][s][0], DEPTH_CLAMP)
             else:  # per-op path: stage 1 (pathway launched between its cost volume and CostRegNet),
                 # view-sharded mode, or per-kernel instrumentation -- the same kernels
-                hyp = ops.stage_hypotheses(dv, depth_raw, self.ndepths[s], self.depth_interals_ratio[s], img_hw,
+                hyp = ops.stage_hypotheses(dv if s == 0 else dv0, depth_raw, self.ndepths[s], self.depth_interals_ratio[s], img_hw,
                                            STAGE_SCALES[s])
                 if view_shard is not None:
                     sim, vw_new = view_shard.cost_volume(fs, rows[name], hyp, s, view_w, prep["pw"])

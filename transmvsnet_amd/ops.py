@@ -46,7 +46,27 @@ def _ptr(t):
 
 
 def _stream():
+    """The current HIP stream of the current device. Every public op below runs under a device guard
+    set from its first GPU tensor argument (_on_tensor_device), so this is that tensor's device."""
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _on_tensor_device(fn):
+    """Run `fn` with the current device = the device of its first GPU tensor argument, so its kernels
+    launch on that device and on that device's current stream (a model on cuda:1 works without
+    torch.cuda.set_device(1))."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapped(*args, **kwargs):
+        for a in (*args, *kwargs.values()):
+            if isinstance(a, torch.Tensor) and a.is_cuda:
+                if a.device.index == torch.cuda.current_device():
+                    return fn(*args, **kwargs)
+                with torch.cuda.device(a.device):
+                    return fn(*args, **kwargs)
+        return fn(*args, **kwargs)
+    return wrapped
 
 
 def _dev(t, name):
@@ -470,3 +490,11 @@ def depth_metrics(depth, depth_gt, mask, depth_interval):
                                                ctypes.c_float(float(depth_interval)), _ptr(ws), ws.numel() * 4,
                                                _ptr(out), _stream()), "tmvs_depth_metrics")
     return out
+
+
+for _name in ("stage_hypotheses", "warp_corr", "aggregate_finalize", "homo_warping", "softmax_wta", "costregnet",
+              "conv3d_bn_relu", "deconv3d_bn_relu_add", "fmt_embed", "fmt_kv", "fmt_apply", "fmt_pathway",
+              "fmt_forward", "depth_stage", "deform_conv2d", "dcn_fused", "conv3x3_nhwc", "fpn_merge",
+              "conv2d_bn_relu", "entropy_loss", "depth_metrics"):
+    globals()[_name] = _on_tensor_device(globals()[_name])
+del _name

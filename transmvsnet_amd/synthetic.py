@@ -148,3 +148,11 @@ def synthetic_features(n_views: int, height: int, width: int, batch: int = 1, se
             f[name] = torch.from_numpy(rng.standard_normal((batch, c, height // s, width // s), dtype=np.float32))
         feats.append(f)
     return feats
+
+
+def stacked_features(n_views: int, height: int, width: int, seed: int = 2):
+    """FeatureNet-shaped pyramids already stacked as forward_features takes them:
+    {stage: [1, N, C, h, w]} ~N(0,1) from torch's CPU generator (bench.py's inputs)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return {name: torch.randn(1, n_views, c, height // s, width // s, generator=g)
+            for name, c, s in (("stage1", 32, 4), ("stage2", 16, 2), ("stage3", 8, 1))}
