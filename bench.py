@@ -43,6 +43,8 @@ def _args():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--mode", choices=("replica", "views"), default="replica")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="nccl = RCCL (the product path); gloo only to rehearse the launcher with more ranks than GPUs")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="oracle threads for cpu_baseline; 0 = the cores this process may run on")
     ap.add_argument("--cpu-runs", type=int, default=3, help="timed oracle runs (after 1 warm-up); median")
@@ -147,10 +149,17 @@ def main():
 
 
 def run(args, world, rank, local):
+    ndev = torch.cuda.device_count()
+    if local >= ndev and args.dist_backend == "nccl":
+        raise SystemExit(f"bench.py: rank {rank} needs GPU {local} but {ndev} are visible")
+    local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
         if dist.get_world_size() != world:
             raise RuntimeError(f"process group has {dist.get_world_size()} ranks, expected {world}")
 

