@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TMVS_ABI_VERSION 1
+#define TMVS_ABI_VERSION 2
 
 #define TMVS_OK 0
 #define TMVS_ERR_ARG (-1)    /* null pointer / non-positive size / bad enum        */
@@ -77,11 +77,16 @@ int tmvs_stage_hypotheses(const float* depth_values, int n_values, const float* 
  *   flags        : TMVS_WARP_PARTIAL -> write sim_out = Σ_v w_v·sim_v and wsum_out = Σ_v w_v
  *                  undivided (view-sharded mode; finish with tmvs_aggregate_finalize after the
  *                  all-reduce); 0 -> sim_out = the reference's normalised similarity.
+ *                  TMVS_WARP_ROT_PLAIN -> rot·(x,y,1) as (r0·x + r1·y) + r2, the rounding of the
+ *                  reference's torch.matmul (module.py:303) where the host BLAS does not contract
+ *                  it (MKL on AMD EPYC); without it fmaf(r1, y, r0·x) + r2 (MKL on AVX-512 Xeons).
+ *                  The two differ by up to 1.2e-4 px in the sample coordinate.
  *   sim_out      : [B][D][H][W]       wsum_out : [B][H][W] (PARTIAL only, else may be NULL)
  *   view_w_out   : [B][vw_total][H][W] written at vw_offset.. when view_w_in == NULL
  * Supported: C in {8,16,32}; D in {8,16,24,32,48,64}; 1 <= V <= TMVS_MAX_VIEWS;
  *            V*H*W*C*4 < 2^30 bytes per sample (32-bit buffer offsets); H, W <= 32766.      */
 #define TMVS_WARP_PARTIAL 1
+#define TMVS_WARP_ROT_PLAIN 2
 #define TMVS_PW_NPARAMS 201 /* w0[16] a0[16] s0[16] w1[8][16] a1[8] s1[8] w2[8] b2 */
 int tmvs_warp_corr(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,
                    const float* view_w_in, int vw_shift, int vw_offset, int vw_total, const float* pw_params,
@@ -93,9 +98,10 @@ int tmvs_aggregate_finalize(float* sim_sum, const float* w_sum, int batch, int n
                             void* stream);
 
 /* Materialising homo_warping (models/module.py:284-322) for the reference seam / tests:
- *   src_fea [B][C][H][W] (NCHW), proj HOST [B][12], hyp [B][D][H][W] -> out [B][C][D][H][W]. */
+ *   src_fea [B][C][H][W] (NCHW), proj HOST [B][12], hyp [B][D][H][W] -> out [B][C][D][H][W];
+ *   flags: TMVS_WARP_ROT_PLAIN as for tmvs_warp_corr. */
 int tmvs_homo_warping(const float* src_fea, const float* proj, const float* hyp, int batch, int channels,
-                      int ndepth, int height, int width, float* out, void* stream);
+                      int ndepth, int height, int width, int flags, float* out, void* stream);
 
 /* ------------------------------------------------------------------ CostRegNet
  * 3-D U-Net of models/module.py:425-456 on an NDHWC volume, eval-mode BN folded into a
@@ -202,12 +208,13 @@ int tmvs_fmt_forward(const float* stage1, long view_stride, const float* pe, int
  * tmvs_stage_hypotheses -> tmvs_warp_corr -> tmvs_costregnet -> tmvs_softmax_wta.
  *   feat [n_views][h][w][channels] NHWC, reference view first; proj HOST [n_views-1][12];
  *   pw_params HOST (stage 1: view_w [n_views-1][h][w] is written) or NULL (view_w is read at
- *   1/2^vw_shift resolution); outputs hyp/prob [ndepth][h][w], depth/depth_raw/conf [h][w]. */
+ *   1/2^vw_shift resolution); warp_flags: TMVS_WARP_ROT_PLAIN or 0 (tmvs_warp_corr);
+ *   outputs hyp/prob [ndepth][h][w], depth/depth_raw/conf [h][w]. */
 size_t tmvs_depth_stage_workspace(int ndepth, int height, int width, int base_ch);
 int tmvs_depth_stage(const float* depth_values, int n_values, const float* prev_depth, int prev_h, int prev_w,
                      const float* feat, int n_views, int channels, int ndepth, float ratio, int full_h, int full_w,
                      int stage_scale, const float* proj, const float* pw_params, float* view_w, int vw_shift,
-                     const TmvsCostRegWeights* cr, void* workspace, size_t workspace_bytes, float clamp_lo,
+                     int warp_flags, const TmvsCostRegWeights* cr, void* workspace, size_t workspace_bytes, float clamp_lo,
                      float clamp_hi, float* hyp_out, float* prob_out, float* depth_out, float* depth_raw_out,
                      float* conf_out, void* stream);
 

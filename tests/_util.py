@@ -10,6 +10,27 @@ from transmvsnet_amd import synthetic
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
+# The fixtures were generated (tests/golden/make_golden.py) by the reference on this build
+# container's AVX-512 Xeon, whose MKL rounds homo_warping's rot·(x, y, 1) as an FMA chain;
+# comparisons against them pin that rounding (ops.host_rot_order explains the two forms).
+GOLDEN_ROT_ORDER = "fma"
+
+
+class golden_rot:
+    """with golden_rot(model): forward passes reproduce the fixtures' host rounding."""
+
+    def __init__(self, model):
+        self.model = model
+
+    def __enter__(self):
+        self.prev = self.model.warp_rot_order
+        self.model.warp_rot_order = GOLDEN_ROT_ORDER
+        return self.model
+
+    def __exit__(self, *a):
+        self.model.warp_rot_order = self.prev
+
+
 def golden(name):
     return dict(np.load(os.path.join(GOLD, name)))
 

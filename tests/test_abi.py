@@ -56,6 +56,7 @@ def test_header_constants_match_binding():
     assert int(consts["TMVS_ENC_NPARAMS"]) == _lib.ENC_NPARAMS
     assert int(consts["TMVS_KV_NFLOATS"]) == _lib.KV_NFLOATS
     assert int(consts["TMVS_WARP_PARTIAL"]) == _lib.WARP_PARTIAL
+    assert int(consts["TMVS_WARP_ROT_PLAIN"]) == _lib.WARP_ROT_PLAIN
 
 
 def test_status_strings(lib):
@@ -144,3 +145,26 @@ def test_conv2d_pack_host(lib):
                             if c < ci:
                                 want = wn[c_o, c, tap // k, tap % k]
                         assert pk[((b * mt + m) * 64 + lane) * 4 + e] == want
+
+
+def test_host_rot_order_matches_torch_matmul():
+    """ops.host_rot_order names the rounding this host's torch.matmul gives rot·(x, y, 1) (the
+    reference's homo_warping grid, models/module.py:303); emulate it and compare bit for bit."""
+    import numpy as np
+    import torch
+    from transmvsnet_amd import ops
+    h, w = 216, 288
+    order = ops.host_rot_order(h * w)
+    assert order in ("fma", "plain")
+    assert ops.warp_flags("auto", h * w) == (_lib.WARP_ROT_PLAIN if order == "plain" else 0)
+    assert ops.warp_flags("fma", h * w) == 0 and ops.warp_flags("plain", h * w) == _lib.WARP_ROT_PLAIN
+    rot = np.float32([[0.99, -0.02, -3.1], [0.015, 1.01, 2.7], [1.2e-5, -3e-6, 1.0]])
+    y, x = np.meshgrid(np.arange(h, dtype=np.float32), np.arange(w, dtype=np.float32), indexing="ij")
+    x, y = x.reshape(-1), y.reshape(-1)
+    got = torch.matmul(torch.from_numpy(rot)[None], torch.from_numpy(np.stack([x, y, np.ones_like(x)]))[None])[0]
+    r0, r1, r2 = rot[:, 0:1], rot[:, 1:2], rot[:, 2:3]
+    if order == "fma":
+        emu = (r1.astype(np.float64) * y + (r0 * x)).astype(np.float32) + r2
+    else:
+        emu = (r0 * x + r1 * y) + r2
+    assert (emu == got.numpy()).mean() == 1.0

@@ -82,7 +82,7 @@ def _worker(rank, world, port, q):
         feats, proj, dv = _inputs()
         part = _oracle_partial(sd, feats, proj)
         shard = ViewShard(rank, world, N_VIEWS - 1, finalize_fn=_finalize)
-        shard._partial = lambda *a: part(*a, views=shard.src_views)
+        shard._partial = lambda *a, **k: part(*a, views=shard.src_views)
         sim, vw = shard.cost_volume(None, None, dv, 0, None, None)
         ref_sim, ref_vw = oracle.build_cost_volume(sd, feats, proj, dv)
         err = float((sim - ref_sim[:, 0]).abs().max())

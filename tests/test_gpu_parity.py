@@ -16,7 +16,7 @@ import torch.nn.functional as F
 
 from oracle import transmvs_ref as oracle
 from transmvsnet_amd import TransMVSNet, ops, synthetic
-from tests._util import depth_parity, golden, golden_state_dict, to_np
+from tests._util import GOLDEN_ROT_ORDER, depth_parity, golden, golden_rot, golden_state_dict, to_np
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -48,7 +48,8 @@ def test_homo_warping_seam():
     g = golden("ops.npz")
     p = torch.from_numpy(g["warp_proj"])
     out = ops.homo_warping(torch.from_numpy(g["warp_src"]).to(DEV), oracle.compose_proj(p[:, 1]),
-                           oracle.compose_proj(p[:, 0]), torch.from_numpy(g["warp_hyp"]).to(DEV))
+                           oracle.compose_proj(p[:, 0]), torch.from_numpy(g["warp_hyp"]).to(DEV),
+                           rot_order=GOLDEN_ROT_ORDER)
     np.testing.assert_allclose(to_np(out), g["warp_out"], rtol=0, atol=2e-5)
 
 
@@ -295,8 +296,9 @@ def test_e2e_c1_features(model):
     g = golden("e2e_c1_features.npz")
     H, W, N = 128, 160, 3
     feats = [{k: v.to(DEV) for k, v in f.items()} for f in synthetic.synthetic_features(N, H, W, seed=2)]
-    out, vw = model.forward_features(feats, synthetic.synthetic_cameras(N, H, W, seed=1),
-                                     synthetic.synthetic_depth_values(1).to(DEV), (H, W), return_view_weights=True)
+    with golden_rot(model):
+        out, vw = model.forward_features(feats, synthetic.synthetic_cameras(N, H, W, seed=1),
+                                         synthetic.synthetic_depth_values(1).to(DEV), (H, W), return_view_weights=True)
     rep = _e2e_check(out, vw, g)
     for s in (1, 2, 3):
         np.testing.assert_allclose(to_np(out[f"stage{s}"]["prob_volume"]), g[f"stage{s}_prob"], rtol=0, atol=1e-3)
@@ -308,6 +310,7 @@ def test_e2e_cascade_48_32_8(sd):
     m = TransMVSNet().eval()
     m.load_state_dict(sd, strict=True)
     m = m.to(DEV)
+    m.warp_rot_order = GOLDEN_ROT_ORDER
     H, W, N = 256, 320, 3
     feats = [{k: v.to(DEV) for k, v in f.items()} for f in synthetic.synthetic_features(N, H, W, seed=2)]
     out, vw = m.forward_features(feats, synthetic.synthetic_cameras(N, H, W, seed=1),
@@ -322,6 +325,7 @@ def test_e2e_cascade_view_sharded_path(sd):
     m = TransMVSNet().eval()
     m.load_state_dict(sd, strict=True)
     m = m.to(DEV)
+    m.warp_rot_order = GOLDEN_ROT_ORDER
     H, W, N = 256, 320, 3
     feats = [{k: v.to(DEV) for k, v in f.items()} for f in synthetic.synthetic_features(N, H, W, seed=2)]
     out, vw = m.forward_features(feats, synthetic.synthetic_cameras(N, H, W, seed=1),
@@ -333,7 +337,7 @@ def test_e2e_cascade_view_sharded_path(sd):
 def test_e2e_images_full_forward(model):
     g = golden("e2e_c1_imgs.npz")
     H, W, N = 128, 160, 3
-    with torch.no_grad():
+    with torch.no_grad(), golden_rot(model):
         out = model(synthetic.synthetic_images(N, H, W, seed=0).to(DEV), synthetic.synthetic_cameras(N, H, W, seed=1),
                     synthetic.synthetic_depth_values(1).to(DEV))
     l1 = float(np.abs(to_np(out["depth"]).astype(np.float64) - g["stage3_depth"]).mean())

@@ -24,7 +24,7 @@ SIGNATURES = {
     "tmvs_stage_hypotheses": (I, [P, I, P, I, I, I, I, F, I, I, I, P, P]),
     "tmvs_warp_corr": (I, [P, P, P, P, P, I, I, I, P, I, I, I, I, I, I, I, P, P, P, P]),
     "tmvs_aggregate_finalize": (I, [P, P, I, I, I, I, P]),
-    "tmvs_homo_warping": (I, [P, P, P, I, I, I, I, I, P, P]),
+    "tmvs_homo_warping": (I, [P, P, P, I, I, I, I, I, I, P, P]),
     "tmvs_costregnet_workspace": (S, [I, I, I, I, I]),
     "tmvs_costregnet": (I, [P, I, I, I, I, P, P, S, P, P]),
     "tmvs_conv3d_bn_relu": (I, [P, I, I, I, I, I, P, P, P, I, I, P, P]),
@@ -38,7 +38,7 @@ SIGNATURES = {
     "tmvs_fmt_forward_workspace": (S, [I, I]),
     "tmvs_fmt_forward": (I, [P, L, P, I, I, I, I, I, P, P, S, P, P]),
     "tmvs_depth_stage_workspace": (S, [I, I, I, I]),
-    "tmvs_depth_stage": (I, [P, I, P, I, I, P, I, I, I, F, I, I, I, P, P, P, I, P, P, S, F, F, P, P, P, P, P, P]),
+    "tmvs_depth_stage": (I, [P, I, P, I, I, P, I, I, I, F, I, I, I, P, P, P, I, I, P, P, S, F, F, P, P, P, P, P, P]),
     "tmvs_deform_conv2d_packed_floats": (S, [I]),
     "tmvs_deform_conv2d_pack": (I, [P, I, I, P]),
     "tmvs_deform_conv2d": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P, P, P]),
@@ -55,11 +55,12 @@ SIGNATURES = {
     "tmvs_depth_metrics": (I, [P, P, P, I, F, P, S, P, P]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 PW_NPARAMS = 201
 ENC_NPARAMS = 8544
 KV_NFLOATS = 160
 WARP_PARTIAL = 1
+WARP_ROT_PLAIN = 2
 
 
 class CostRegWeights(ctypes.Structure):

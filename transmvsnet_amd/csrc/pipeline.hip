@@ -55,7 +55,7 @@ extern "C" size_t tmvs_depth_stage_workspace(int ndepth, int height, int width, 
 extern "C" int tmvs_depth_stage(const float* depth_values, int n_values, const float* prev_depth, int prev_h,
                                 int prev_w, const float* feat, int n_views, int channels, int ndepth, float ratio,
                                 int full_h, int full_w, int stage_scale, const float* proj, const float* pw_params,
-                                float* view_w, int vw_shift, const TmvsCostRegWeights* cr, void* workspace,
+                                float* view_w, int vw_shift, int warp_flags, const TmvsCostRegWeights* cr, void* workspace,
                                 size_t workspace_bytes, float clamp_lo, float clamp_hi, float* hyp_out,
                                 float* prob_out, float* depth_out, float* depth_raw_out, float* conf_out,
                                 void* stream) {
@@ -76,11 +76,12 @@ extern "C" int tmvs_depth_stage(const float* depth_values, int n_values, const f
   const float* ref = feat;
   const float* src = feat + (size_t)h * w * channels;
   if (pw_params)
-    rc = tmvs_warp_corr(ref, src, proj, hyp_out, nullptr, 0, 0, V, pw_params, 1, V, channels, ndepth, h, w, 0, sim,
+    rc = tmvs_warp_corr(ref, src, proj, hyp_out, nullptr, 0, 0, V, pw_params, 1, V, channels, ndepth, h, w,
+                        warp_flags & TMVS_WARP_ROT_PLAIN, sim,
                         nullptr, view_w, stream);
   else
-    rc = tmvs_warp_corr(ref, src, proj, hyp_out, view_w, vw_shift, 0, V, nullptr, 1, V, channels, ndepth, h, w, 0,
-                        sim, nullptr, nullptr, stream);
+    rc = tmvs_warp_corr(ref, src, proj, hyp_out, view_w, vw_shift, 0, V, nullptr, 1, V, channels, ndepth, h, w,
+                        warp_flags & TMVS_WARP_ROT_PLAIN, sim, nullptr, nullptr, stream);
   if (rc) return rc;
   if ((rc = tmvs_costregnet(sim, 1, ndepth, h, w, cr, crws, crbytes, logits, stream))) return rc;
   return tmvs_softmax_wta(logits, hyp_out, 1, ndepth, h, w, clamp_lo, clamp_hi, prob_out, depth_out, depth_raw_out,

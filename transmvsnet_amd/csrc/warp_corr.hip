@@ -7,7 +7,8 @@
 // against the reference features held in registers; the warped [C,D,H,W] volume never exists.
 //
 // fp32 op order follows the reference's PyTorch-CPU kernels (DESIGN.md "Numerics"):
-//   rot·(x,y,1)   : fmaf(r1, y, r0*x) + r2            (bmm, FMA chain)
+//   rot·(x,y,1)   : fmaf(r1, y, r0*x) + r2            (bmm as MKL runs it on AVX-512 Xeons: FMA chain)
+//               or (r0*x + r1*y) + r2                  (bmm as MKL runs it on AMD EPYC: TMVS_WARP_ROT_PLAIN)
 //   X = rot_xyz*d + t ; px = X/Z ; xn = px/((W-1)/2) - 1 ; z < 1e-6 -> xn = yn = -99
 //   ix = (xn + 1) * ((W-1)/2)                          (grid_sample, align_corners=True)
 //   v  = fmaf(se_v,se, fmaf(sw_v,sw, fmaf(ne_v,ne, nw_v*nw)))  (zeros padding)
@@ -22,7 +23,15 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 struct WarpArgs {
   float proj[TMVS_MAX_VIEWS][12];
   float pw[TMVS_PW_NPARAMS];
+  int rot_plain;  // TMVS_WARP_ROT_PLAIN: the host BLAS's rounding of rot·(x, y, 1)
 };
+
+// One row of rot·(x, y, 1) (homo_warping's torch.matmul, models/module.py:303) in the op order of
+// the host BLAS the reference runs on: MKL contracts it into an FMA chain on AVX-512 Xeons and does
+// not on AMD EPYC (measured, scripts/diag/warp_bits.py); the coordinate then differs by up to 1.2e-4.
+__device__ __forceinline__ float rot_row(const float* R, float x, float y, int plain) {
+  return plain ? (R[0] * x + R[1] * y) + R[2] : fmaf(R[1], y, R[0] * x) + R[2];
+}
 
 __device__ __forceinline__ float pixelwise_logit(float s, const float* __restrict__ pw) {
   // PixelwiseNet (TransMVSNet.py:20-26): 1x1x1 convs 1->16 (BN,ReLU) ->8 (BN,ReLU) ->1 (+bias).
@@ -354,9 +363,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 
   for (int v = 0; v < V; ++v) {
     const float* R = args.proj[v];
-    const float rx = fmaf(R[1], fyp, R[0] * fxp) + R[2];
-    const float ry = fmaf(R[5], fyp, R[4] * fxp) + R[6];
-    const float rz = fmaf(R[9], fyp, R[8] * fxp) + R[10];
+    const float rx = rot_row(R, fxp, fyp, args.rot_plain);
+    const float ry = rot_row(R + 4, fxp, fyp, args.rot_plain);
+    const float rz = rot_row(R + 8, fxp, fyp, args.rot_plain);
     const unsigned vbase = (unsigned)(v * HW * C * 4 + 16 * k);
     float w = 0.f;
     if constexpr (!PW) w = vw_in[(size_t)(vw_offset + v) * Hs * Ws + (py >> vw_shift) * Ws + (px >> vw_shift)];
@@ -413,9 +422,9 @@ __global__ void homo_warping_kernel(const float* __restrict__ src, const float* 
   const int py = p / W, px = p - py * W;
   const float* R = args.proj[0];
   const float fx = (float)px, fy = (float)py;
-  const float rx = fmaf(R[1], fy, R[0] * fx) + R[2];
-  const float ry = fmaf(R[5], fy, R[4] * fx) + R[6];
-  const float rz = fmaf(R[9], fy, R[8] * fx) + R[10];
+  const float rx = rot_row(R, fx, fy, args.rot_plain);
+  const float ry = rot_row(R + 4, fx, fy, args.rot_plain);
+  const float rz = rot_row(R + 8, fx, fy, args.rot_plain);
   const float dep = hyp[idx];
   const float X = rx * dep + R[3], Y = ry * dep + R[7], Z = rz * dep + R[11];
   const float halfw = (float)(W - 1) / 2.f, halfh = (float)(H - 1) / 2.f;
@@ -570,9 +579,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const unsigned rowb = (unsigned)W * C * 4;
   for (int v = 0; v < V; ++v) {
     const float* R = args.proj[v];
-    const float rx = fmaf(R[1], fyp, R[0] * fxp) + R[2];
-    const float ry = fmaf(R[5], fyp, R[4] * fxp) + R[6];
-    const float rz = fmaf(R[9], fyp, R[8] * fxp) + R[10];
+    const float rx = rot_row(R, fxp, fyp, args.rot_plain);
+    const float ry = rot_row(R + 4, fxp, fyp, args.rot_plain);
+    const float rz = rot_row(R + 8, fxp, fyp, args.rot_plain);
     const unsigned vbase = (unsigned)(v * HW * C * 4 + 16 * q);
     const float w = wv[(size_t)v * Hs * Ws];
 #pragma unroll 1
@@ -678,6 +687,7 @@ extern "C" int tmvs_warp_corr(const float* ref_fea, const float* src_fea, const 
   const size_t HW = (size_t)height * width;
   for (int b = 0; b < batch; ++b) {
     WarpArgs a;
+    a.rot_plain = (flags & TMVS_WARP_ROT_PLAIN) ? 1 : 0;
     for (int v = 0; v < n_src; ++v)
       for (int k = 0; k < 12; ++k) a.proj[v][k] = proj[((size_t)b * n_src + v) * 12 + k];
     if (pw)
@@ -725,12 +735,13 @@ extern "C" int tmvs_aggregate_finalize(float* sim_sum, const float* w_sum, int b
 }
 
 extern "C" int tmvs_homo_warping(const float* src_fea, const float* proj, const float* hyp, int batch, int channels,
-                                 int ndepth, int height, int width, float* out, void* stream) {
+                                 int ndepth, int height, int width, int flags, float* out, void* stream) {
   if (!src_fea || !proj || !hyp || !out || batch <= 0 || channels <= 0 || ndepth <= 0 || height <= 0 || width <= 0)
     return TMVS_ERR_ARG;
   const size_t HW = (size_t)height * width;
   for (int b = 0; b < batch; ++b) {
     WarpArgs a = {};
+    a.rot_plain = (flags & TMVS_WARP_ROT_PLAIN) ? 1 : 0;
     for (int k = 0; k < 12; ++k) a.proj[0][k] = proj[(size_t)b * 12 + k];
     const int n = ndepth * (int)HW;
     hipLaunchKernelGGL(homo_warping_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,

@@ -69,7 +69,7 @@ class ViewShard:
         """proj rows [B,V,12] (source views) -> own source views."""
         return rows[:, self.src_views]
 
-    def cost_volume(self, fs, rows, hyp, stage, view_w, pw):
+    def cost_volume(self, fs, rows, hyp, stage, view_w, pw, rot_order="auto"):
         """Full aggregated similarity [1,D,h,w] on every rank + this rank's stage-1 view weights.
 
         fs: [1+n_local, h, w, C] NHWC (reference first); rows: [1, n_local, 12] host array.
@@ -79,7 +79,7 @@ class ViewShard:
         sim_sum, w_sum = buf[:, :d], buf[:, d]
         new_vw = view_w
         if self.src_views:
-            new_vw = self._partial(fs, rows, hyp, stage, view_w, pw, sim_sum, w_sum)
+            new_vw = self._partial(fs, rows, hyp, stage, view_w, pw, sim_sum, w_sum, rot_order=rot_order)
         self.allreduce(buf)
         sim = buf[:, :d]
         self._finalize(sim, buf[:, d])
@@ -95,15 +95,16 @@ class ViewShard:
                 self.comm_bytes.append(buf.numel() * buf.element_size())
 
 
-def _hip_partial(fs, rows, hyp, stage, view_w, pw, sim_out, wsum_out):
+def _hip_partial(fs, rows, hyp, stage, view_w, pw, sim_out, wsum_out, rot_order="auto"):
     from . import ops
     ref = fs[0:1]
     src = fs[1:].unsqueeze(0)
     if stage == 0:
-        _, _, vw = ops.warp_corr(ref, src, rows, hyp, pw_params=pw, partial=True, sim_out=sim_out, wsum_out=wsum_out)
+        _, _, vw = ops.warp_corr(ref, src, rows, hyp, pw_params=pw, partial=True, sim_out=sim_out, wsum_out=wsum_out,
+                                 rot_order=rot_order)
         return vw
     ops.warp_corr(ref, src, rows, hyp, view_w_in=view_w, vw_shift=stage, partial=True, sim_out=sim_out,
-                  wsum_out=wsum_out)
+                  wsum_out=wsum_out, rot_order=rot_order)
     return None
 
 

@@ -227,6 +227,9 @@ class TransMVSNet(nn.Module):
         # the FMT pathway (stage-2/3 features) depends only on the FMT output: run it on a side
         # stream, concurrently with stage 1 (whose small CostRegNet grids leave the GPU idle)
         self.overlap_pathway = True
+        # rounding of homo_warping's rot·(x, y, 1) to reproduce: 'auto' = the host torch's
+        # (ops.host_rot_order), or 'fma' / 'plain' to pin it (fixtures made on another machine)
+        self.warp_rot_order = "auto"
         self._side = {}
         self.register_load_state_dict_post_hook(lambda m, k: m.invalidate())
 
@@ -395,18 +398,20 @@ class TransMVSNet(nn.Module):
             if view_shard is None and not self.decomposed and s > 0:
                 out, depth_raw = ops.depth_stage(dv0, depth_raw, fs, self.ndepths[s], self.depth_interals_ratio[s],
                                                  img_hw, STAGE_SCALES[s], rows[name][0], None, view_w, s,
-                                                 prep["cr"][s][0], DEPTH_CLAMP)
+                                                 prep["cr"][s][0], DEPTH_CLAMP, rot_order=self.warp_rot_order)
             else:  # per-op path: stage 1 (pathway launched between its cost volume and CostRegNet),
                 # view-sharded mode, or per-kernel instrumentation -- the same kernels
                 hyp = ops.stage_hypotheses(dv if s == 0 else dv0, depth_raw, self.ndepths[s], self.depth_interals_ratio[s], img_hw,
                                            STAGE_SCALES[s])
                 if view_shard is not None:
-                    sim, vw_new = view_shard.cost_volume(fs, rows[name], hyp, s, view_w, prep["pw"])
+                    sim, vw_new = view_shard.cost_volume(fs, rows[name], hyp, s, view_w, prep["pw"],
+                                                         rot_order=self.warp_rot_order)
                 elif s == 0:
-                    sim, _, vw_new = ops.warp_corr(fs[0:1], fs[1:].unsqueeze(0), rows[name], hyp, pw_params=prep["pw"])
+                    sim, _, vw_new = ops.warp_corr(fs[0:1], fs[1:].unsqueeze(0), rows[name], hyp, pw_params=prep["pw"],
+                                                   rot_order=self.warp_rot_order)
                 else:
                     sim, _, _ = ops.warp_corr(fs[0:1], fs[1:].unsqueeze(0), rows[name], hyp, view_w_in=view_w,
-                                              vw_shift=s)
+                                              vw_shift=s, rot_order=self.warp_rot_order)
                 if s == 0:
                     view_w = vw_new
                     if overlap:

@@ -115,6 +115,42 @@ def proj_rows(proj_matrix_stage):
     return torch.stack(rows, 1).contiguous().numpy()
 
 
+_ROT_ORDER = {}
+
+
+def host_rot_order(n_pixels):
+    """'fma' or 'plain': how THIS host's torch.matmul rounds homo_warping's rot·(x, y, 1)
+    (models/module.py:303, a [3,3] x [3,H*W] bmm). The reference's sample coordinates depend on it:
+    MKL contracts the 3-term dot into fmaf(r1, y, r0·x) + r2 on AVX-512 Xeons and computes
+    (r0·x + r1·y) + r2 on AMD EPYC (scripts/diag/warp_bits.py). Probed once per size with the
+    reference's own call shape; the warp kernels then reproduce the host's coordinates bit for bit."""
+    order = _ROT_ORDER.get(n_pixels)
+    if order is None:
+        g = np.random.default_rng(12345)
+        w = 1 << max(1, int(np.ceil(np.log2(max(2.0, np.sqrt(n_pixels))))))
+        xs = (np.arange(n_pixels) % w).astype(np.float32)
+        ys = (np.arange(n_pixels) // w).astype(np.float32)
+        rot = g.uniform(-1.0, 1.0, (3, 3)).astype(np.float32)
+        rot[:, 2] *= 300.0
+        xyz = torch.from_numpy(np.stack([xs, ys, np.ones_like(xs)]))[None]
+        got = torch.matmul(torch.from_numpy(rot)[None], xyz)[0].numpy()
+        r0, r1, r2 = rot[:, 0:1], rot[:, 1:2], rot[:, 2:3]
+        fma = (r1.astype(np.float64) * ys + (r0 * xs)).astype(np.float32) + r2
+        plain = (r0 * xs + r1 * ys) + r2
+        order = "plain" if (plain == got).sum() > (fma == got).sum() else "fma"
+        _ROT_ORDER[n_pixels] = order
+    return order
+
+
+def warp_flags(rot_order, n_pixels):
+    """TMVS_WARP_ROT_PLAIN or 0 for rot_order 'fma' / 'plain' / 'auto' (= host_rot_order)."""
+    if rot_order == "auto":
+        rot_order = host_rot_order(n_pixels)
+    if rot_order not in ("fma", "plain"):
+        raise ValueError(f"rot_order must be 'auto', 'fma' or 'plain', got {rot_order!r}")
+    return _lib.WARP_ROT_PLAIN if rot_order == "plain" else 0
+
+
 # ----------------------------------------------------------------- ops
 def stage_hypotheses(depth_values, prev_depth, ndepth, ratio, full_hw, stage_scale):
     """Stage glue (models/TransMVSNet.py:174-204): -> [B, D, H/s, W/s]."""
@@ -132,10 +168,11 @@ def stage_hypotheses(depth_values, prev_depth, ndepth, ratio, full_hw, stage_sca
 
 
 def warp_corr(ref_nhwc, src_nhwc, proj12, hyp, view_w_in=None, vw_shift=0, vw_offset=0, vw_total=None,
-              pw_params=None, partial=False, view_w_out=None, sim_out=None, wsum_out=None):
+              pw_params=None, partial=False, view_w_out=None, sim_out=None, wsum_out=None, rot_order="auto"):
     """Fused cost volume (models/TransMVSNet.py:58-93). ref [B,H,W,C], src [B,V,H,W,C], proj12 HOST [B,V,12].
 
     Returns sim [B,D,H,W] (and w_sum [B,H,W] when partial) ; stage 1 writes view_w_out [B,vw_total,H,W].
+    rot_order: the reference's rounding of rot·(x, y, 1) ('auto' = this host's torch, host_rot_order).
     """
     for t, n in ((ref_nhwc, "ref"), (src_nhwc, "src"), (hyp, "hyp"), (view_w_in, "view_w_in"), (view_w_out, "view_w_out")):
         _dev(t, n)
@@ -160,7 +197,8 @@ def warp_corr(ref_nhwc, src_nhwc, proj12, hyp, view_w_in=None, vw_shift=0, vw_of
     with _Span("tmvs_warp_corr"):
         _lib.check(_lib_h().tmvs_warp_corr(_ptr(ref_nhwc), _ptr(src_nhwc), proj.ctypes.data, _ptr(hyp), _ptr(view_w_in),
                                            vw_shift, vw_offset, vw_total, pw_ptr, b, v, c, d, h, w,
-                                           _lib.WARP_PARTIAL if partial else 0, _ptr(sim), _ptr(wsum),
+                                           (_lib.WARP_PARTIAL if partial else 0) | warp_flags(rot_order, h * w),
+                                           _ptr(sim), _ptr(wsum),
                                            _ptr(view_w_out if view_w_in is None else None), _stream()), "tmvs_warp_corr")
     return sim, wsum, (view_w_out if view_w_in is None else None)
 
@@ -175,7 +213,7 @@ def aggregate_finalize(sim_sum, w_sum):
     return sim_sum
 
 
-def homo_warping(src_fea, src_proj, ref_proj, depth_values):
+def homo_warping(src_fea, src_proj, ref_proj, depth_values, rot_order="auto"):
     """Seam-compatible homo_warping (models/module.py:284-322): [B,C,H,W] -> [B,C,D,H,W]."""
     _dev(src_fea, "src_fea")
     _dev(depth_values, "depth_values")
@@ -186,7 +224,8 @@ def homo_warping(src_fea, src_proj, ref_proj, depth_values):
     out = torch.empty(b, c, d, h, w, device=src_fea.device)
     with _Span("tmvs_homo_warping"):
         _lib.check(_lib_h().tmvs_homo_warping(_ptr(src_fea), rows.ctypes.data, _ptr(depth_values.contiguous()), b, c, d,
-                                              h, w, _ptr(out), _stream()), "tmvs_homo_warping")
+                                              h, w, warp_flags(rot_order, h * w), _ptr(out), _stream()),
+                   "tmvs_homo_warping")
     return out
 
 
@@ -296,7 +335,7 @@ def fmt_forward(stage1_nchw, pe, enc_list, tokens=None):
 
 
 def depth_stage(depth_values, prev_depth, feat_nhwc, ndepth, ratio, full_hw, stage_scale, proj12, pw_params,
-                view_w, vw_shift, cr_weights, clamp=(425.0, 935.0)):
+                view_w, vw_shift, cr_weights, clamp=(425.0, 935.0), rot_order="auto"):
     """One cascade stage for one sample (models/TransMVSNet.py:174-221). feat [N,h,w,C] NHWC.
 
     Returns dict(depth, photo_confidence, prob_volume, depth_values) with a batch dim of 1, and depth_raw.
@@ -321,7 +360,7 @@ def depth_stage(depth_values, prev_depth, feat_nhwc, ndepth, ratio, full_hw, sta
         _lib.check(_lib_h().tmvs_depth_stage(_ptr(depth_values), depth_values.shape[-1], _ptr(prev_depth), ph, pwd,
                                              _ptr(feat_nhwc), n, c, ndepth, ctypes.c_float(ratio), full_hw[0], full_hw[1],
                                              stage_scale, proj.ctypes.data, None if pw is None else pw.ctypes.data,
-                                             _ptr(view_w), vw_shift, ctypes.byref(cr_weights), _ptr(ws), ws.numel() * 4,
+                                             _ptr(view_w), vw_shift, warp_flags(rot_order, h * w), ctypes.byref(cr_weights), _ptr(ws), ws.numel() * 4,
                                              ctypes.c_float(clamp[0]), ctypes.c_float(clamp[1]), _ptr(hyp), _ptr(prob),
                                              _ptr(depth), _ptr(raw), _ptr(conf), _stream()), "tmvs_depth_stage")
     return {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}, raw
