@@ -113,3 +113,51 @@ def test_load_sample_synthetic_scan():
     np.testing.assert_allclose(p1[0, 1, 0, 0], 2892.33 / 4 * 288 / 400, rtol=1e-6)
     np.testing.assert_allclose(p1[0, 1, 1, 1], 2883.18 / 4 * 192 / 300, rtol=1e-6)
     assert len(s["depth_values"]) == 192 and s["depth_values"][1] == np.float32(427.5)
+
+
+def _write_scan(td, scan, n_views, cams_dir, h=300, w=400, tnt=False, seed=3):
+    """A scan directory in the reference's layout: images/{:08}.jpg, <cams_dir>/{:08}_cam.txt
+    (per-view translated camera), pair.txt."""
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    os.makedirs(os.path.join(td, scan, "images"), exist_ok=True)
+    os.makedirs(os.path.join(td, scan, cams_dir), exist_ok=True)
+    for v in range(n_views):
+        Image.fromarray((rng.random((h, w, 3)) * 255).astype(np.uint8)).save(
+            os.path.join(td, scan, "images", "{:0>8}.jpg".format(v)))
+        lines = CAM_TXT.splitlines()
+        row = lines[1].split()
+        row[3] = "%.3f" % (float(row[3]) + 40.0 * v)
+        lines[1] = " ".join(row)
+        if tnt:
+            lines[11] = "425.0 935.0"
+        open(os.path.join(td, scan, cams_dir, "{:0>8}_cam.txt".format(v)), "w").write("\n".join(lines) + "\n")
+    with open(os.path.join(td, scan, "pair.txt"), "w") as f:
+        f.write(f"{n_views}\n")
+        for v in range(n_views):
+            src = [u for u in range(n_views) if u != v]
+            f.write(f"{v}\n{len(src)} " + " ".join(f"{u} {10.0 - u:.1f}" for u in src) + "\n")
+
+
+def test_read_pair_file_tnt_no_padding():
+    with tempfile.TemporaryDirectory() as td:
+        fn = os.path.join(td, "pair.txt")
+        open(fn, "w").write(PAIR_TXT)
+        metas = data.read_pair_file(fn, nviews=11, pad=False)
+    assert metas == [(0, [10, 1, 9, 12, 11, 13, 2, 8, 14, 27]), (1, [5, 6])]  # view 2 has no sources
+
+
+def test_load_sample_tnt_shrinks_views_and_ranges():
+    with tempfile.TemporaryDirectory() as td:
+        _write_scan(td, "Family", 4, "cams_1", tnt=True)
+        metas = data.read_pair_file(os.path.join(td, "Family", "pair.txt"), pad=False)
+        s = data.load_sample_tnt(td, "Family", metas[0][0], metas[0][1], nviews=11)
+        # an explicit cap for a scan outside the table, and the dataset-wide resolution carried over
+        s2 = data.load_sample_tnt(td, "Family", 1, [0, 2], image_size=(256, 192), fixed_hw=s["fixed_hw"])
+    assert s["imgs"].shape == (4, 3, 288, 384)  # 1 + 3 sources; 300x400 under 1920x1080 -> multiples of 32
+    assert s2["imgs"].shape == (3, 3, 288, 384)  # resized back to the fixed resolution
+    dint = (935.0 - 425.0) / 192
+    np.testing.assert_array_equal(s["depth_values"], np.arange(425.0, dint * 192 + 425.0, dint, dtype=np.float32))
+    p = s2["proj_matrix"]["stage1"]
+    # 400x300 -> capped at 256x192 (x0.64: 256x192) -> back to 384x288: intrinsics x0.64 x1.5 x(1/4)
+    np.testing.assert_allclose(p[0, 1, 0, 0], 2892.33 / 4 * (256 / 400) * (384 / 256), rtol=1e-6)

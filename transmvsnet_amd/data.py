@@ -8,6 +8,10 @@ scans can be fed to ``TransMVSNet.forward`` instead of synthetic tensors.
   read_img                     datasets/general_eval.py:99-103 (PIL, / 255)
   scale_mvs_input              datasets/general_eval.py:106-124 (resize to a multiple of 32)
   load_sample                  datasets/general_eval.py:126-210 (imgs, 3-stage proj_matrix, depth_values)
+  read_pair_file(pad=False)    datasets/tnt_eval.py:44-59 (no filling: the sample shrinks instead)
+  load_sample_tnt              datasets/tnt_eval.py:120-210 (cams_1/, per-scan image_sizes caps, nviews
+                               shrunk to 1 + #sources, np.arange(dmin, dint*nd + dmin, dint), optional
+                               inverse-depth hypotheses, the dataset-wide fixed resolution)
 
 Host-side, as in the reference (its DataLoader workers). The reference resizes with
 cv2.resize(INTER_LINEAR) -- absent here; ``resize_bilinear`` restates OpenCV's float path
@@ -64,9 +68,10 @@ def save_pfm(filename, image, scale=1):
 
 
 # ------------------------------------------------------------------ scan files (general_eval.py)
-def read_pair_file(filename, nviews=5):
+def read_pair_file(filename, nviews=5, pad=True):
     """general_eval.build_list for one scan: [(ref_view, [src views...])]; views without sources are
-    dropped, fewer than nviews sources are filled with the first source (:47-56)."""
+    dropped, fewer than nviews sources are filled with the first source (:47-56). pad=False is
+    tnt_eval.build_list (:44-59): no filling (load_sample_tnt shrinks the view count instead)."""
     metas = []
     with open(filename) as f:
         n = int(f.readline())
@@ -74,7 +79,7 @@ def read_pair_file(filename, nviews=5):
             ref = int(f.readline().rstrip())
             src = [int(x) for x in f.readline().rstrip().split()[1::2]]
             if len(src) > 0:
-                if len(src) < nviews:
+                if pad and len(src) < nviews:
                     src += [src[0]] * (nviews - len(src))
                 metas.append((ref, src))
     return metas
@@ -149,6 +154,69 @@ def scale_mvs_input(img, intrinsics, max_w, max_h, base=32):
     return resize_bilinear(img, int(new_w), int(new_h)), intrinsics
 
 
+def _stack_sample(imgs, projs, depth_values, scan, ref_view):
+    imgs = np.stack(imgs).transpose(0, 3, 1, 2)
+    proj = np.stack(projs)
+    s2, s3 = proj.copy(), proj.copy()
+    s2[:, 1, :2, :] = proj[:, 1, :2, :] * 2
+    s3[:, 1, :2, :] = proj[:, 1, :2, :] * 4
+    return {"imgs": imgs, "proj_matrix": {"stage1": proj, "stage2": s2, "stage3": s3},
+            "depth_values": depth_values, "filename": scan + "/{}/" + "{:0>8}".format(ref_view) + "{}"}
+
+
+# Tanks&Temples image sizes (datasets/tnt_eval.py:24-37): the per-scan (max_w, max_h) of scale_mvs_input
+TNT_IMAGE_SIZES = {"Family": (1920, 1080), "Francis": (1920, 1080), "Horse": (1920, 1080),
+                   "Lighthouse": (2048, 1080), "M60": (2048, 1080), "Panther": (2048, 1080),
+                   "Playground": (1920, 1080), "Train": (1920, 1080), "Auditorium": (1920, 1080),
+                   "Ballroom": (1920, 1080), "Courtroom": (1920, 1080), "Museum": (1920, 1080),
+                   "Palace": (1920, 1080), "Temple": (1920, 1080)}
+
+
+def load_sample_tnt(datapath, scan, ref_view, src_views, nviews=11, ndepths=192, interval_scale=1.0,
+                    inverse_depth=False, fixed_hw=None, image_size=None):
+    """tnt_eval.MVSDataset.__getitem__ (:120-210) for one (scan, ref, srcs).
+
+    nviews shrinks to 1 + len(src_views) when there are fewer sources (:125-126). Images come from
+    {scan}/images/, cameras from {scan}/cams_1/ (read_cam_file(tnt=True): depth_min, depth_max on line
+    11); each image is fitted into the scan's TNT_IMAGE_SIZES (or `image_size` = (max_w, max_h) for a
+    scan outside the table). The reference fixes ONE resolution for the whole dataset from the first
+    image it ever loads (fix_res, :137-141): pass that (h, w) as `fixed_hw` to reproduce it across
+    samples; by default this sample's reference image sets it. Returns the dict of load_sample plus
+    "fixed_hw"."""
+    nviews = min(nviews, len(src_views) + 1)
+    view_ids = [ref_view] + list(src_views[:nviews - 1])
+    max_w, max_h = image_size if image_size is not None else TNT_IMAGE_SIZES[scan]
+    imgs, projs, depth_values = [], [], None
+    s_h, s_w = fixed_hw if fixed_hw is not None else (None, None)
+    for i, vid in enumerate(view_ids):
+        img = read_img(os.path.join(datapath, "{}/images/{:0>8}.jpg".format(scan, vid)))
+        intr, extr, dmin, dint, dmax = read_cam_file(
+            os.path.join(datapath, "{}/cams_1/{:0>8}_cam.txt".format(scan, vid)), ndepths, tnt=True)
+        img, intr = scale_mvs_input(img, intr, max_w, max_h)
+        if s_h is None:
+            s_h, s_w = img.shape[:2]
+        c_h, c_w = img.shape[:2]
+        if (c_h, c_w) != (s_h, s_w):
+            img = resize_bilinear(img, s_w, s_h)
+            intr[0, :] *= 1.0 * s_w / c_w
+            intr[1, :] *= 1.0 * s_h / c_h
+        imgs.append(img)
+        p = np.zeros((2, 4, 4), np.float32)
+        p[0] = extr
+        p[1, :3, :3] = intr
+        projs.append(p)
+        if i == 0:
+            if not inverse_depth:
+                depth_values = np.arange(dmin, dint * ndepths + dmin, dint, dtype=np.float32)
+            else:  # tnt_eval.py:181-185
+                depth_end = dmax - dint / interval_scale
+                depth_values = (1.0 / np.linspace(1.0 / depth_end, 1.0 / dmin, ndepths, endpoint=False)).astype(
+                    np.float32)
+    out = _stack_sample(imgs, projs, depth_values, scan, ref_view)
+    out["fixed_hw"] = (s_h, s_w)
+    return out
+
+
 def load_sample(datapath, scan, ref_view, src_views, nviews=5, ndepths=192, interval_scale=1.0, max_h=864,
                 max_w=1152):
     """general_eval.MVSDataset.__getitem__ (:126-210) for one (scan, ref, srcs): imgs [N,3,H,W],
@@ -178,10 +246,4 @@ def load_sample(datapath, scan, ref_view, src_views, nviews=5, ndepths=192, inte
         projs.append(p)
         if i == 0:
             depth_values = np.arange(dmin, dint * (ndepths - 0.5) + dmin, dint, dtype=np.float32)
-    imgs = np.stack(imgs).transpose(0, 3, 1, 2)
-    proj = np.stack(projs)
-    s2, s3 = proj.copy(), proj.copy()
-    s2[:, 1, :2, :] = proj[:, 1, :2, :] * 2
-    s3[:, 1, :2, :] = proj[:, 1, :2, :] * 4
-    return {"imgs": imgs, "proj_matrix": {"stage1": proj, "stage2": s2, "stage3": s3},
-            "depth_values": depth_values, "filename": scan + "/{}/" + "{:0>8}".format(view_ids[0]) + "{}"}
+    return _stack_sample(imgs, projs, depth_values, scan, view_ids[0])
