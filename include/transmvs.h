@@ -218,6 +218,44 @@ int tmvs_depth_stage(const float* depth_values, int n_values, const float* prev_
                      float clamp_hi, float* hyp_out, float* prob_out, float* depth_out, float* depth_raw_out,
                      float* conf_out, void* stream);
 
+/* ------------------------------------------------------------------ CostRegNet training
+ * Train-mode forward and backward of CostRegNet (models/module.py:425-456, Conv3d :108-147,
+ * Deconv3d :150-191, nn.BatchNorm3d with batch statistics), the pieces torch.autograd needs.
+ * Activations NDHWC [B][D][H][W][C]; weights packed [27][Cout][Cin] (tap = kd*9+kh*3+kw) in the
+ * arrangement each use needs (transmvsnet_amd/train.py packs them). C in {1, 8, 16, 32, 64}.
+ *
+ * tmvs_conv3d_generic: y = conv of x, no bias. Without TMVS_CONV_TRANSPOSED: y[o] = sum W[k]
+ *   x[o*s - 1 + k] (Conv3d k3 p1 stride s; the dgrad of a ConvTranspose3d); with it: y[o] = sum
+ *   W[k] x[(o + 1 - k)/s] over the k with s | o + 1 - k (ConvTranspose3d k3 s2 p1 op1; the dgrad
+ *   of a Conv3d). TMVS_CONV_ACCUMULATE: y += the result. Output dims are explicit; taps outside
+ *   the input grid contribute nothing.                                                          */
+#define TMVS_CONV_TRANSPOSED 1
+#define TMVS_CONV_ACCUMULATE 2
+int tmvs_conv3d_generic(const float* x, int batch, int cin, int d_in, int h_in, int w_in, const float* w, int cout,
+                        int d_out, int h_out, int w_out, int stride, int flags, float* y, void* stream);
+
+/* dw[k][a][b] = sum_p direct[p][a] * gathered[p*stride - 1 + k][b] over every voxel p of direct
+ * [B][pd][ph][pw][a_ch] (taps outside gathered [B][gd][gh][gw][b_ch] are zero): the weight
+ * gradient of a Conv3d (direct = dz, gathered = x) or of a ConvTranspose3d (direct = x,
+ * gathered = dz, stride 2). Block partials + fixed-order combine (deterministic).            */
+size_t tmvs_conv3d_wgrad_workspace(int batch, int d, int h, int w, int a_ch, int b_ch);
+int tmvs_conv3d_wgrad(const float* direct, int a_ch, int batch, int pd, int ph, int pw, const float* gathered,
+                      int b_ch, int gd, int gh, int gw, int stride, void* workspace, size_t workspace_bytes,
+                      float* dw, void* stream);
+
+/* BatchNorm3d in train mode over z [nvox][C] (C divides 256): batch mean and biased variance
+ * (fp64 partials, fixed-order combine); y = relu(fmaf(z, a, b)) [+ skip] with a = gamma /
+ * sqrt(var + eps), b = beta - mean * a; the backward of that (incl. the ReLU mask) gives dz,
+ * dgamma = sum g * xhat, dbeta = sum g. The running-statistics update is the caller's.        */
+size_t tmvs_bn_train_workspace(long nvox, int channels);
+int tmvs_bn_stats(const float* z, long nvox, int channels, void* workspace, size_t workspace_bytes, float* mean,
+                  float* var, void* stream);
+int tmvs_bn_relu_train(const float* z, long nvox, int channels, const float* mean, const float* var,
+                       const float* gamma, const float* beta, float eps, const float* skip, float* out, void* stream);
+int tmvs_bn_relu_backward(const float* dy, const float* z, long nvox, int channels, const float* mean,
+                          const float* var, const float* gamma, const float* beta, float eps, void* workspace,
+                          size_t workspace_bytes, float* dz, float* dgamma, float* dbeta, void* stream);
+
 /* ------------------------------------------------------------------ FeatureNet heads
  * Modulated deformable convolution of DCN.forward (models/dcn.py:66-80; torchvision.ops.deform_conv2d,
  * torchvision 0.10.1): 3x3, stride 1, padding 1, dilation 1, one offset group, with the head's bias,

@@ -34,10 +34,11 @@ DEPTH_CLAMP = (425.0, 935.0)         # models/TransMVSNet.py:221
 
 
 # ----------------------------------------------------------------------------- helpers
-def _bn(x, sd, p):
-    """nn.BatchNorm{2,3}d in eval mode (models/module.py:132,173,218)."""
+def _bn(x, sd, p, training=False):
+    """nn.BatchNorm{2,3}d (models/module.py:132,173,218): eval mode, or train mode (batch statistics;
+    the running statistics in `sd` are updated in place with momentum 0.1, as the module does)."""
     return F.batch_norm(x, sd[p + "running_mean"], sd[p + "running_var"], sd[p + "weight"], sd[p + "bias"],
-                        False, 0.1, BN_EPS)
+                        training, 0.1, BN_EPS)
 
 
 def _lin(x, sd, p):
@@ -223,24 +224,26 @@ def build_cost_volume(sd, features, proj_matrix, depth_values, view_weights=None
 
 
 # ----------------------------------------------------------------------------- CostRegNet
-def _conv3d_bn_relu(sd, p, x, stride):
-    return F.relu(_bn(F.conv3d(x, sd[p + "conv.weight"], stride=stride, padding=1), sd, p + "bn."))
+def _conv3d_bn_relu(sd, p, x, stride, training=False):
+    return F.relu(_bn(F.conv3d(x, sd[p + "conv.weight"], stride=stride, padding=1), sd, p + "bn.", training))
 
 
-def _deconv3d_bn_relu(sd, p, x):
+def _deconv3d_bn_relu(sd, p, x, training=False):
     y = F.conv_transpose3d(x, sd[p + "conv.weight"], stride=2, padding=1, output_padding=1)
-    return F.relu(_bn(y, sd, p + "bn."))
+    return F.relu(_bn(y, sd, p + "bn.", training))
 
 
-def cost_reg_net(sd, p, x):
-    """CostRegNet.forward, models/module.py:447-456 (Conv3d :135-141, Deconv3d :179-185)."""
-    conv0 = _conv3d_bn_relu(sd, p + "conv0.", x, 1)
-    conv2 = _conv3d_bn_relu(sd, p + "conv2.", _conv3d_bn_relu(sd, p + "conv1.", conv0, 2), 1)
-    conv4 = _conv3d_bn_relu(sd, p + "conv4.", _conv3d_bn_relu(sd, p + "conv3.", conv2, 2), 1)
-    x = _conv3d_bn_relu(sd, p + "conv6.", _conv3d_bn_relu(sd, p + "conv5.", conv4, 2), 1)
-    x = conv4 + _deconv3d_bn_relu(sd, p + "conv7.", x)
-    x = conv2 + _deconv3d_bn_relu(sd, p + "conv9.", x)
-    x = conv0 + _deconv3d_bn_relu(sd, p + "conv11.", x)
+def cost_reg_net(sd, p, x, training=False):
+    """CostRegNet.forward, models/module.py:447-456 (Conv3d :135-141, Deconv3d :179-185); training=True
+    is the module in train mode (BatchNorm3d batch statistics, running statistics updated)."""
+    t = training
+    conv0 = _conv3d_bn_relu(sd, p + "conv0.", x, 1, t)
+    conv2 = _conv3d_bn_relu(sd, p + "conv2.", _conv3d_bn_relu(sd, p + "conv1.", conv0, 2, t), 1, t)
+    conv4 = _conv3d_bn_relu(sd, p + "conv4.", _conv3d_bn_relu(sd, p + "conv3.", conv2, 2, t), 1, t)
+    x = _conv3d_bn_relu(sd, p + "conv6.", _conv3d_bn_relu(sd, p + "conv5.", conv4, 2, t), 1, t)
+    x = conv4 + _deconv3d_bn_relu(sd, p + "conv7.", x, t)
+    x = conv2 + _deconv3d_bn_relu(sd, p + "conv9.", x, t)
+    x = conv0 + _deconv3d_bn_relu(sd, p + "conv11.", x, t)
     return F.conv3d(x, sd[p + "prob.weight"], stride=1, padding=1)
 
 

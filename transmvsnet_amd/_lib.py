@@ -53,6 +53,13 @@ SIGNATURES = {
     "tmvs_entropy_loss": (I, [P, P, I, P, P, I, I, I, I, F, P, S, P, P, P, P, P]),
     "tmvs_depth_metrics_workspace": (S, [I]),
     "tmvs_depth_metrics": (I, [P, P, P, I, F, P, S, P, P]),
+    "tmvs_conv3d_generic": (I, [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P]),
+    "tmvs_conv3d_wgrad_workspace": (S, [I, I, I, I, I, I]),
+    "tmvs_conv3d_wgrad": (I, [P, I, I, I, I, I, P, I, I, I, I, I, P, S, P, P]),
+    "tmvs_bn_train_workspace": (S, [L, I]),
+    "tmvs_bn_stats": (I, [P, L, I, P, S, P, P, P]),
+    "tmvs_bn_relu_train": (I, [P, L, I, P, P, P, P, F, P, P, P]),
+    "tmvs_bn_relu_backward": (I, [P, P, L, I, P, P, P, P, F, P, S, P, P, P, P]),
 }
 
 ABI_VERSION = 2
@@ -61,6 +68,8 @@ ENC_NPARAMS = 8544
 KV_NFLOATS = 160
 WARP_PARTIAL = 1
 WARP_ROT_PLAIN = 2
+CONV_TRANSPOSED = 1
+CONV_ACCUMULATE = 2
 
 
 class CostRegWeights(ctypes.Structure):

@@ -1,0 +1,486 @@
+// CostRegNet training: the train-mode forward and the backward of
+// models/module.py:425-456 (Conv3d :108-147, Deconv3d :150-191, nn.BatchNorm3d in train mode).
+//
+// Every convolution of the network and of its backward is one of two gathers over NDHWC
+// activations with weights packed [27][Cout][Cin] (tap = kd*9 + kh*3 + kw):
+//   strided    : y[o] = sum_{k,ci} W[k][co][ci] x[o*s - 1 + k]          (Conv3d k3 p1; dgrad of a
+//                                                                        ConvTranspose3d)
+//   transposed : y[o] = sum_{k,ci} W[k][co][ci] x[(o + 1 - k)/s]  if s | (o + 1 - k)
+//                                                                       (ConvTranspose3d k3 s2 p1 op1;
+//                                                                        dgrad of a Conv3d, s = 1 or 2)
+// and every weight gradient is one reduction
+//   dW[k][a][b] = sum_p direct[p][a] * gathered[p*s - 1 + k][b]         (conv: direct = dz, gathered
+//                                                                        = x; deconv: direct = x,
+//                                                                        gathered = dz)
+// The host packs the weights for each use (transposes / flips are index permutations of the
+// [27][Cout][Cin] block). BatchNorm3d in train mode: batch mean and biased variance per channel
+// over all B*D*H*W voxels (fp64 partial sums, combined in a fixed order: bitwise reproducible),
+// y = relu(fmaf(z, alpha, shift)) [+ skip] with alpha = gamma/sqrt(var+eps), shift = beta -
+// mean*alpha (the CPU kernel's form); backward dz = alpha/N * (N*g - sum g - xhat * sum g*xhat),
+// g = dy * [fmaf(z, alpha, shift) > 0]. No atomics anywhere: every reduction is block partials
+// plus a fixed-order combine.
+//
+// Bounds: the convolutions are fp32 FMA work (VALU; 3 x 3,456 MAC per voxel for forward + both
+// gradients), the BN passes HBM (2-3 reads of z per pass).
+#include "common.h"
+
+namespace tmvs {
+
+constexpr int kTrainBlock = 256;
+
+// ---------------------------------------------------------------- generic direct conv (VALU)
+// One thread = one output voxel x COB output channels; the co-block's weights [27][COB][CIN]
+// sit in LDS and are read as wave-uniform broadcasts. Each tap's CIN input channels are one
+// contiguous NDHWC row (float4 loads).
+template <int CIN, int COB>
+__global__ __launch_bounds__(kTrainBlock) void conv3d_generic_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, int cout, int B, int Di, int Hi, int Wi, int Do, int Ho,
+    int Wo, int stride, int transposed, int accumulate, float* __restrict__ y) {
+  __shared__ __attribute__((aligned(16))) float wl[27 * COB * CIN];
+  const int cob = blockIdx.y;
+  for (int i = threadIdx.x; i < 27 * COB * CIN; i += kTrainBlock) {
+    const int ci = i % CIN, co = (i / CIN) % COB, k = i / (CIN * COB);
+    wl[i] = w[((size_t)k * cout + cob * COB + co) * CIN + ci];
+  }
+  __syncthreads();
+  const long nvox = (long)B * Do * Ho * Wo;
+  const long v = (long)blockIdx.x * kTrainBlock + threadIdx.x;
+  if (v >= nvox) return;
+  const int ow = (int)(v % Wo);
+  long t = v / Wo;
+  const int oh = (int)(t % Ho);
+  t /= Ho;
+  const int od = (int)(t % Do);
+  const int b = (int)(t / Do);
+  float acc[COB];
+#pragma unroll
+  for (int c = 0; c < COB; ++c) acc[c] = 0.f;
+  const float* xb = x + (size_t)b * Di * Hi * Wi * CIN;
+#pragma unroll 1
+  for (int k = 0; k < 27; ++k) {
+    const int kd = k / 9, kh = (k / 3) % 3, kw = k % 3;
+    int id, ih, iw;
+    if (transposed) {
+      const int td = od + 1 - kd, th = oh + 1 - kh, tw = ow + 1 - kw;
+      if (td < 0 || th < 0 || tw < 0 || td % stride || th % stride || tw % stride) continue;
+      id = td / stride;
+      ih = th / stride;
+      iw = tw / stride;
+    } else {
+      id = od * stride - 1 + kd;
+      ih = oh * stride - 1 + kh;
+      iw = ow * stride - 1 + kw;
+      if (id < 0 || ih < 0 || iw < 0) continue;
+    }
+    if (id >= Di || ih >= Hi || iw >= Wi) continue;
+    const float* xp = xb + (((size_t)id * Hi + ih) * Wi + iw) * CIN;
+    const float* wk = wl + k * COB * CIN;
+    if constexpr (CIN % 4 == 0) {
+#pragma unroll 4
+      for (int c4 = 0; c4 < CIN / 4; ++c4) {
+        const float4 xv = *reinterpret_cast<const float4*>(xp + 4 * c4);
+#pragma unroll
+        for (int co = 0; co < COB; ++co) {
+          const float4 wv = *reinterpret_cast<const float4*>(wk + co * CIN + 4 * c4);
+          acc[co] = fmaf(wv.x, xv.x, acc[co]);
+          acc[co] = fmaf(wv.y, xv.y, acc[co]);
+          acc[co] = fmaf(wv.z, xv.z, acc[co]);
+          acc[co] = fmaf(wv.w, xv.w, acc[co]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int ci = 0; ci < CIN; ++ci) {
+        const float xv = xp[ci];
+#pragma unroll
+        for (int co = 0; co < COB; ++co) acc[co] = fmaf(wk[co * CIN + ci], xv, acc[co]);
+      }
+    }
+  }
+  float* yp = y + (size_t)v * cout + cob * COB;
+  if (accumulate) {  // y += conv (a gradient reaching a tensor along two paths)
+#pragma unroll
+    for (int c = 0; c < COB; ++c) acc[c] = yp[c] + acc[c];
+  }
+  if constexpr (COB % 4 == 0) {
+#pragma unroll
+    for (int c4 = 0; c4 < COB / 4; ++c4)
+      *reinterpret_cast<float4*>(yp + 4 * c4) = make_float4(acc[4 * c4], acc[4 * c4 + 1], acc[4 * c4 + 2], acc[4 * c4 + 3]);
+  } else {
+#pragma unroll
+    for (int c = 0; c < COB; ++c) yp[c] = acc[c];
+  }
+}
+
+// ---------------------------------------------------------------- weight gradient
+// grid (nblk, 27): block (j, k) reduces voxels [j*vpb, (j+1)*vpb) of `direct` for tap k into
+// partial[j][k][A][BC]; thread q owns pairs q, q+256, ... of the A x BC block. Rows of both
+// operands are staged 32 voxels at a time in LDS (a zero row where the tap falls outside).
+template <int A, int BC>
+__global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_kernel(
+    const float* __restrict__ direct, const float* __restrict__ gath, int B, int Pd, int Ph, int Pw, int Gd, int Gh,
+    int Gw, int stride, long vpb, float* __restrict__ partial) {
+  constexpr int NP = (A * BC + kTrainBlock - 1) / kTrainBlock;
+  constexpr int CH = 32;
+  __shared__ __attribute__((aligned(16))) float sd[CH][A];
+  __shared__ __attribute__((aligned(16))) float sg[CH][BC];
+  const int k = blockIdx.y;
+  const int kd = k / 9, kh = (k / 3) % 3, kw = k % 3;
+  const long nvox = (long)B * Pd * Ph * Pw;
+  const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
+  float acc[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) acc[j] = 0.f;
+#pragma unroll 1
+  for (long vb = v0; vb < v1; vb += CH) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < CH * A; i += kTrainBlock) {
+      const int r = i / A, a = i % A;
+      const long v = vb + r;
+      sd[r][a] = v < v1 ? direct[v * A + a] : 0.f;
+    }
+    for (int i = threadIdx.x; i < CH * BC; i += kTrainBlock) {
+      const int r = i / BC, c = i % BC;
+      const long v = vb + r;
+      float val = 0.f;
+      if (v < v1) {
+        const int pw = (int)(v % Pw);
+        long t = v / Pw;
+        const int ph = (int)(t % Ph);
+        t /= Ph;
+        const int pd = (int)(t % Pd);
+        const int b = (int)(t / Pd);
+        const int gd = pd * stride - 1 + kd, gh = ph * stride - 1 + kh, gw = pw * stride - 1 + kw;
+        if (gd >= 0 && gh >= 0 && gw >= 0 && gd < Gd && gh < Gh && gw < Gw)
+          val = gath[((((size_t)b * Gd + gd) * Gh + gh) * Gw + gw) * BC + c];
+      }
+      sg[r][c] = val;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int q = threadIdx.x + j * kTrainBlock;
+      if (q < A * BC) {
+        const int a = q / BC, c = q % BC;
+        float s = acc[j];
+#pragma unroll 8
+        for (int r = 0; r < CH; ++r) s = fmaf(sd[r][a], sg[r][c], s);
+        acc[j] = s;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int q = threadIdx.x + j * kTrainBlock;
+    if (q < A * BC) partial[((size_t)blockIdx.x * 27 + k) * A * BC + q] = acc[j];
+  }
+}
+
+// dw[i] = sum_j partial[j][i], j = 0..nblk-1 in order (fp64 accumulation)
+__global__ __launch_bounds__(kTrainBlock) void sum_partials_kernel(const float* __restrict__ partial, int nblk, long n,
+                                                                   float* __restrict__ out) {
+  const long i = (long)blockIdx.x * kTrainBlock + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.0;
+  for (int j = 0; j < nblk; ++j) s += (double)partial[(size_t)j * n + i];
+  out[i] = (float)s;
+}
+
+// ---------------------------------------------------------------- BatchNorm3d, train mode
+// Per-block fp64 partials of (sum z, sum z^2) per channel: thread t handles channel t % C of
+// rows t / C, t / C + 256/C, ... (C divides 256).
+__global__ __launch_bounds__(kTrainBlock) void bn_stats_partial_kernel(const float* __restrict__ z, long nvox, int C,
+                                                                       long vpb, double* __restrict__ partial) {
+  __shared__ double red[2][kTrainBlock];
+  const int c = threadIdx.x % C, r0 = threadIdx.x / C, rs = kTrainBlock / C;
+  const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
+  double s = 0.0, q = 0.0;
+  for (long v = v0 + r0; v < v1; v += rs) {
+    const double x = (double)z[v * C + c];
+    s += x;
+    q += x * x;
+  }
+  red[0][threadIdx.x] = s;
+  red[1][threadIdx.x] = q;
+  __syncthreads();
+  if (threadIdx.x < C) {
+    double ts = 0.0, tq = 0.0;
+    for (int r = 0; r < rs; ++r) {
+      ts += red[0][r * C + threadIdx.x];
+      tq += red[1][r * C + threadIdx.x];
+    }
+    partial[((size_t)blockIdx.x * 2 + 0) * C + threadIdx.x] = ts;
+    partial[((size_t)blockIdx.x * 2 + 1) * C + threadIdx.x] = tq;
+  }
+}
+
+// mean, biased var (fp32) from the partials, fixed order
+__global__ void bn_stats_combine_kernel(const double* __restrict__ partial, int nblk, int C, long nvox,
+                                        float* __restrict__ mean, float* __restrict__ var) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int j = 0; j < nblk; ++j) {
+    s += partial[((size_t)j * 2 + 0) * C + c];
+    q += partial[((size_t)j * 2 + 1) * C + c];
+  }
+  const double m = s / (double)nvox;
+  double v = q / (double)nvox - m * m;
+  mean[c] = (float)m;
+  var[c] = (float)(v > 0.0 ? v : 0.0);
+}
+
+__device__ __forceinline__ void bn_affine(float mean, float var, float g, float bt, float eps, float& al, float& sh) {
+  al = (1.f / sqrtf(var + eps)) * g;
+  sh = fmaf(-mean, al, bt);
+}
+
+// out = relu(fmaf(z, alpha, shift)) [+ skip]
+__global__ __launch_bounds__(kTrainBlock) void bn_relu_apply_kernel(const float* __restrict__ z, long n, int C,
+                                                                    const float* __restrict__ mean,
+                                                                    const float* __restrict__ var,
+                                                                    const float* __restrict__ gamma,
+                                                                    const float* __restrict__ beta, float eps,
+                                                                    const float* __restrict__ skip,
+                                                                    float* __restrict__ out) {
+  const long i = (long)blockIdx.x * kTrainBlock + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i % C);
+  float al, sh;
+  bn_affine(mean[c], var[c], gamma[c], beta[c], eps, al, sh);
+  float y = relu(fmaf(z[i], al, sh));
+  if (skip) y = skip[i] + y;
+  out[i] = y;
+}
+
+// backward pass 1: per-block fp64 partials of (sum g, sum g*xhat), g = dy * [fmaf(z, alpha, shift) > 0]
+__global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_partial_kernel(
+    const float* __restrict__ dy, const float* __restrict__ z, long nvox, int C, const float* __restrict__ mean,
+    const float* __restrict__ var, const float* __restrict__ gamma, const float* __restrict__ beta, float eps, long vpb,
+    double* __restrict__ partial) {
+  __shared__ double red[2][kTrainBlock];
+  const int c = threadIdx.x % C, r0 = threadIdx.x / C, rs = kTrainBlock / C;
+  float al, sh;
+  bn_affine(mean[c], var[c], gamma[c], beta[c], eps, al, sh);
+  const float m = mean[c], rstd = 1.f / sqrtf(var[c] + eps);
+  const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
+  double sg = 0.0, sgx = 0.0;
+  for (long v = v0 + r0; v < v1; v += rs) {
+    const float zz = z[v * C + c];
+    const float g = fmaf(zz, al, sh) > 0.f ? dy[v * C + c] : 0.f;
+    sg += (double)g;
+    sgx += (double)g * (double)((zz - m) * rstd);
+  }
+  red[0][threadIdx.x] = sg;
+  red[1][threadIdx.x] = sgx;
+  __syncthreads();
+  if (threadIdx.x < C) {
+    double a = 0.0, b = 0.0;
+    for (int r = 0; r < rs; ++r) {
+      a += red[0][r * C + threadIdx.x];
+      b += red[1][r * C + threadIdx.x];
+    }
+    partial[((size_t)blockIdx.x * 2 + 0) * C + threadIdx.x] = a;
+    partial[((size_t)blockIdx.x * 2 + 1) * C + threadIdx.x] = b;
+  }
+}
+
+// combine: dbeta = sum g, dgamma = sum g*xhat (fp32 out), and the fp64 sums for pass 2
+__global__ void bn_relu_bwd_combine_kernel(const double* __restrict__ partial, int nblk, int C,
+                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                           double* __restrict__ sums) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, b = 0.0;
+  for (int j = 0; j < nblk; ++j) {
+    a += partial[((size_t)j * 2 + 0) * C + c];
+    b += partial[((size_t)j * 2 + 1) * C + c];
+  }
+  dbeta[c] = (float)a;
+  dgamma[c] = (float)b;
+  sums[c] = a;
+  sums[C + c] = b;
+}
+
+// pass 2: dz = gamma*rstd/N * (N*g - sum g - xhat * sum g*xhat)
+__global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_apply_kernel(
+    const float* __restrict__ dy, const float* __restrict__ z, long n, int C, long nvox, const float* __restrict__ mean,
+    const float* __restrict__ var, const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+    const double* __restrict__ sums, float* __restrict__ dz) {
+  const long i = (long)blockIdx.x * kTrainBlock + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i % C);
+  float al, sh;
+  bn_affine(mean[c], var[c], gamma[c], beta[c], eps, al, sh);
+  const float zz = z[i];
+  const float rstd = 1.f / sqrtf(var[c] + eps);
+  const float xhat = (zz - mean[c]) * rstd;
+  const float g = fmaf(zz, al, sh) > 0.f ? dy[i] : 0.f;
+  const double inv_n = 1.0 / (double)nvox;
+  const float mg = (float)(sums[c] * inv_n), mgx = (float)(sums[C + c] * inv_n);
+  dz[i] = (gamma[c] * rstd) * ((g - mg) - xhat * mgx);
+}
+
+// ---------------------------------------------------------------- dispatch helpers
+template <int CIN, int COB>
+static int launch_generic(const float* x, const float* w, int cout, int B, int Di, int Hi, int Wi, int Do, int Ho,
+                          int Wo, int stride, int transposed, int accumulate, float* y, hipStream_t st) {
+  const long nvox = (long)B * Do * Ho * Wo;
+  hipLaunchKernelGGL((conv3d_generic_kernel<CIN, COB>), dim3((unsigned)((nvox + kTrainBlock - 1) / kTrainBlock),
+                                                             cout / COB),
+                     dim3(kTrainBlock), 0, st, x, w, cout, B, Di, Hi, Wi, Do, Ho, Wo, stride, transposed, accumulate, y);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+static long wgrad_vpb(long nvox) {
+  long vpb = 2048;
+  while ((nvox + vpb - 1) / vpb > 512) vpb *= 2;
+  return vpb;
+}
+
+template <int A, int BC>
+static int launch_wgrad(const float* direct, const float* gath, int B, int Pd, int Ph, int Pw, int Gd, int Gh, int Gw,
+                        int stride, float* ws, float* dw, hipStream_t st) {
+  const long nvox = (long)B * Pd * Ph * Pw;
+  const long vpb = wgrad_vpb(nvox);
+  const int nblk = (int)((nvox + vpb - 1) / vpb);
+  hipLaunchKernelGGL((conv3d_wgrad_kernel<A, BC>), dim3(nblk, 27), dim3(kTrainBlock), 0, st, direct, gath, B, Pd, Ph,
+                     Pw, Gd, Gh, Gw, stride, vpb, ws);
+  TMVS_CHECK_LAUNCH();
+  const long n = 27L * A * BC;
+  hipLaunchKernelGGL(sum_partials_kernel, dim3((unsigned)((n + kTrainBlock - 1) / kTrainBlock)), dim3(kTrainBlock), 0,
+                     st, ws, nblk, n, dw);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+static bool valid_ch(int c) { return c == 1 || c == 8 || c == 16 || c == 32 || c == 64; }
+
+static long bn_vpb(long nvox) {
+  long vpb = 4096;
+  while ((nvox + vpb - 1) / vpb > 1024) vpb *= 2;
+  return vpb;
+}
+
+}  // namespace tmvs
+
+using namespace tmvs;
+
+extern "C" int tmvs_conv3d_generic(const float* x, int batch, int cin, int d_in, int h_in, int w_in, const float* w,
+                                   int cout, int d_out, int h_out, int w_out, int stride, int flags, float* y,
+                                   void* stream) {
+  const int transposed = (flags & TMVS_CONV_TRANSPOSED) ? 1 : 0, accumulate = (flags & TMVS_CONV_ACCUMULATE) ? 1 : 0;
+  if (!x || !w || !y || batch <= 0 || d_in <= 0 || h_in <= 0 || w_in <= 0 || d_out <= 0 || h_out <= 0 || w_out <= 0)
+    return TMVS_ERR_ARG;
+  if (!valid_ch(cin) || !valid_ch(cout) || (stride != 1 && stride != 2)) return TMVS_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+#define TMVS_GEN(CI, CB) \
+  return launch_generic<CI, CB>(x, w, cout, batch, d_in, h_in, w_in, d_out, h_out, w_out, stride, transposed, \
+                                accumulate, y, st)
+  if (cout == 1) {
+    switch (cin) {
+      case 1: TMVS_GEN(1, 1);
+      case 8: TMVS_GEN(8, 1);
+      case 16: TMVS_GEN(16, 1);
+      case 32: TMVS_GEN(32, 1);
+      case 64: TMVS_GEN(64, 1);
+    }
+  } else if (cin == 64) {
+    TMVS_GEN(64, 4);
+  } else {
+    switch (cin) {
+      case 1: TMVS_GEN(1, 8);
+      case 8: TMVS_GEN(8, 8);
+      case 16: TMVS_GEN(16, 8);
+      case 32: TMVS_GEN(32, 8);
+    }
+  }
+#undef TMVS_GEN
+  return TMVS_ERR_SHAPE;
+}
+
+extern "C" size_t tmvs_conv3d_wgrad_workspace(int batch, int d, int h, int w, int a_ch, int b_ch) {
+  const long nvox = (long)batch * d * h * w;
+  const long vpb = wgrad_vpb(nvox);
+  return (size_t)((nvox + vpb - 1) / vpb) * 27 * a_ch * b_ch * sizeof(float);
+}
+
+extern "C" int tmvs_conv3d_wgrad(const float* direct, int a_ch, int batch, int pd, int ph, int pw, const float* gathered,
+                                 int b_ch, int gd, int gh, int gw, int stride, void* workspace, size_t workspace_bytes,
+                                 float* dw, void* stream) {
+  if (!direct || !gathered || !workspace || !dw || batch <= 0 || pd <= 0 || ph <= 0 || pw <= 0 || gd <= 0 ||
+      gh <= 0 || gw <= 0)
+    return TMVS_ERR_ARG;
+  if (stride != 1 && stride != 2) return TMVS_ERR_SHAPE;
+  if (workspace_bytes < tmvs_conv3d_wgrad_workspace(batch, pd, ph, pw, a_ch, b_ch)) return TMVS_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  float* ws = (float*)workspace;
+#define TMVS_WG(AA, BB)                                                                                             \
+  if (a_ch == AA && b_ch == BB)                                                                                     \
+    return launch_wgrad<AA, BB>(direct, gathered, batch, pd, ph, pw, gd, gh, gw, stride, ws, dw, st);
+  // (direct, gathered) channel pairs of CostRegNet's layers: conv (dz, x) and deconv (x, dz)
+  TMVS_WG(8, 1) TMVS_WG(16, 8) TMVS_WG(16, 16) TMVS_WG(32, 16) TMVS_WG(32, 32) TMVS_WG(64, 32) TMVS_WG(64, 64)
+  TMVS_WG(1, 8) TMVS_WG(8, 16) TMVS_WG(16, 32) TMVS_WG(32, 64)
+#undef TMVS_WG
+  return TMVS_ERR_SHAPE;
+}
+
+extern "C" size_t tmvs_bn_train_workspace(long nvox, int channels) {
+  const long vpb = bn_vpb(nvox);
+  return (size_t)((nvox + vpb - 1) / vpb) * 2 * channels * sizeof(double) + 2 * channels * sizeof(double);
+}
+
+extern "C" int tmvs_bn_stats(const float* z, long nvox, int channels, void* workspace, size_t workspace_bytes,
+                             float* mean, float* var, void* stream) {
+  if (!z || !workspace || !mean || !var || nvox <= 0) return TMVS_ERR_ARG;
+  if (channels <= 0 || kTrainBlock % channels) return TMVS_ERR_SHAPE;
+  if (workspace_bytes < tmvs_bn_train_workspace(nvox, channels)) return TMVS_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const long vpb = bn_vpb(nvox);
+  const int nblk = (int)((nvox + vpb - 1) / vpb);
+  double* part = (double*)workspace;
+  hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(nblk), dim3(kTrainBlock), 0, st, z, nvox, channels, vpb, part);
+  TMVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_stats_combine_kernel, dim3(1), dim3(64), 0, st, (const double*)part, nblk, channels, nvox,
+                     mean, var);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+extern "C" int tmvs_bn_relu_train(const float* z, long nvox, int channels, const float* mean, const float* var,
+                                  const float* gamma, const float* beta, float eps, const float* skip, float* out,
+                                  void* stream) {
+  if (!z || !mean || !var || !gamma || !beta || !out || nvox <= 0 || channels <= 0) return TMVS_ERR_ARG;
+  const long n = nvox * channels;
+  hipLaunchKernelGGL(bn_relu_apply_kernel, dim3((unsigned)((n + kTrainBlock - 1) / kTrainBlock)), dim3(kTrainBlock), 0,
+                     (hipStream_t)stream, z, n, channels, mean, var, gamma, beta, eps, skip, out);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+extern "C" int tmvs_bn_relu_backward(const float* dy, const float* z, long nvox, int channels, const float* mean,
+                                     const float* var, const float* gamma, const float* beta, float eps,
+                                     void* workspace, size_t workspace_bytes, float* dz, float* dgamma, float* dbeta,
+                                     void* stream) {
+  if (!dy || !z || !mean || !var || !gamma || !beta || !workspace || !dz || !dgamma || !dbeta || nvox <= 0)
+    return TMVS_ERR_ARG;
+  if (channels <= 0 || kTrainBlock % channels) return TMVS_ERR_SHAPE;
+  if (workspace_bytes < tmvs_bn_train_workspace(nvox, channels)) return TMVS_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const long vpb = bn_vpb(nvox);
+  const int nblk = (int)((nvox + vpb - 1) / vpb);
+  double* part = (double*)workspace;
+  double* sums = part + (size_t)nblk * 2 * channels;
+  hipLaunchKernelGGL(bn_relu_bwd_partial_kernel, dim3(nblk), dim3(kTrainBlock), 0, st, dy, z, nvox, channels, mean, var,
+                     gamma, beta, eps, vpb, part);
+  TMVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_relu_bwd_combine_kernel, dim3(1), dim3(64), 0, st, (const double*)part, nblk, channels, dgamma,
+                     dbeta, sums);
+  TMVS_CHECK_LAUNCH();
+  const long n = nvox * channels;
+  hipLaunchKernelGGL(bn_relu_bwd_apply_kernel, dim3((unsigned)((n + kTrainBlock - 1) / kTrainBlock)), dim3(kTrainBlock),
+                     0, st, dy, z, n, channels, nvox, mean, var, gamma, beta, eps, (const double*)sums, dz);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}

@@ -537,3 +537,88 @@ for _name in ("stage_hypotheses", "warp_corr", "aggregate_finalize", "homo_warpi
               "conv2d_bn_relu", "entropy_loss", "depth_metrics"):
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name
+
+
+# ----------------------------------------------------------------- CostRegNet training (train.py)
+def conv3d_generic(x, w_packed, cout, out_dhw, stride, transposed=False, out=None):
+    """tmvs_conv3d_generic: x NDHWC [B,D,H,W,Cin], w_packed [27][cout][Cin] -> y [B,*out_dhw,cout]
+    (accumulated into `out` when given)."""
+    _dev(x, "x")
+    _dev(w_packed, "w_packed")
+    b, d, h, w, cin = x.shape
+    flags = (_lib.CONV_TRANSPOSED if transposed else 0) | (_lib.CONV_ACCUMULATE if out is not None else 0)
+    y = torch.empty(b, *out_dhw, cout, device=x.device) if out is None else out
+    if tuple(y.shape) != (b, *out_dhw, cout) or not y.is_contiguous():
+        raise ValueError("conv3d_generic: out must be a contiguous [B, D, H, W, cout] tensor")
+    with _Span("tmvs_conv3d_generic"):
+        _lib.check(_lib_h().tmvs_conv3d_generic(_ptr(x), b, cin, d, h, w, _ptr(w_packed), cout, out_dhw[0], out_dhw[1],
+                                                out_dhw[2], stride, flags, _ptr(y), _stream()), "tmvs_conv3d_generic")
+    return y
+
+
+def conv3d_wgrad(direct, gathered, stride):
+    """tmvs_conv3d_wgrad: direct [B,pd,ph,pw,A], gathered [B,gd,gh,gw,BC] -> dw [27][A][BC]."""
+    _dev(direct, "direct")
+    _dev(gathered, "gathered")
+    b, pd, ph, pw, a = direct.shape
+    _, gd, gh, gw, bc = gathered.shape
+    nbytes = _lib_h().tmvs_conv3d_wgrad_workspace(b, pd, ph, pw, a, bc)
+    ws = torch.empty(nbytes // 4 + 64, device=direct.device)
+    dw = torch.empty(27, a, bc, device=direct.device)
+    with _Span("tmvs_conv3d_wgrad"):
+        _lib.check(_lib_h().tmvs_conv3d_wgrad(_ptr(direct), a, b, pd, ph, pw, _ptr(gathered), bc, gd, gh, gw, stride,
+                                              _ptr(ws), ws.numel() * 4, _ptr(dw), _stream()), "tmvs_conv3d_wgrad")
+    return dw
+
+
+def _bn_ws(nvox, c, device):
+    return torch.empty(_lib_h().tmvs_bn_train_workspace(nvox, c) // 4 + 64, device=device)
+
+
+def bn_stats(z):
+    """tmvs_bn_stats: z [..., C] -> (batch mean [C], biased variance [C])."""
+    _dev(z, "z")
+    c = z.shape[-1]
+    nvox = z.numel() // c
+    ws = _bn_ws(nvox, c, z.device)
+    mean = torch.empty(c, device=z.device)
+    var = torch.empty(c, device=z.device)
+    with _Span("tmvs_bn_stats"):
+        _lib.check(_lib_h().tmvs_bn_stats(_ptr(z), nvox, c, _ptr(ws), ws.numel() * 4, _ptr(mean), _ptr(var), _stream()),
+                   "tmvs_bn_stats")
+    return mean, var
+
+
+def bn_relu_train(z, mean, var, gamma, beta, eps, skip=None):
+    """tmvs_bn_relu_train: relu(BN_batch(z)) [+ skip], z [..., C]."""
+    for t, n in ((z, "z"), (mean, "mean"), (var, "var"), (gamma, "gamma"), (beta, "beta"), (skip, "skip")):
+        _dev(t, n)
+    c = z.shape[-1]
+    out = torch.empty_like(z)
+    with _Span("tmvs_bn_relu_train"):
+        _lib.check(_lib_h().tmvs_bn_relu_train(_ptr(z), z.numel() // c, c, _ptr(mean), _ptr(var), _ptr(gamma),
+                                               _ptr(beta), ctypes.c_float(eps), _ptr(skip), _ptr(out), _stream()),
+                   "tmvs_bn_relu_train")
+    return out
+
+
+def bn_relu_backward(dy, z, mean, var, gamma, beta, eps):
+    """tmvs_bn_relu_backward -> (dz, dgamma, dbeta)."""
+    for t, n in ((dy, "dy"), (z, "z"), (mean, "mean"), (var, "var"), (gamma, "gamma"), (beta, "beta")):
+        _dev(t, n)
+    c = z.shape[-1]
+    nvox = z.numel() // c
+    ws = _bn_ws(nvox, c, z.device)
+    dz = torch.empty_like(z)
+    dg = torch.empty(c, device=z.device)
+    db = torch.empty(c, device=z.device)
+    with _Span("tmvs_bn_relu_backward"):
+        _lib.check(_lib_h().tmvs_bn_relu_backward(_ptr(dy), _ptr(z), nvox, c, _ptr(mean), _ptr(var), _ptr(gamma),
+                                                  _ptr(beta), ctypes.c_float(eps), _ptr(ws), ws.numel() * 4, _ptr(dz),
+                                                  _ptr(dg), _ptr(db), _stream()), "tmvs_bn_relu_backward")
+    return dz, dg, db
+
+
+for _name in ("conv3d_generic", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn_relu_backward"):
+    globals()[_name] = _on_tensor_device(globals()[_name])
+del _name
