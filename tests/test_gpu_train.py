@@ -3,9 +3,15 @@ train-mode forward + HIP backward against torch autograd through the oracle's Co
 mode (models/module.py:447-456 with BatchNorm3d batch statistics), at a small shape and the three
 C5 stage shapes (BlendedMVS 768x576: 48 x 144x192, 32 x 288x384, 8 x 576x768).
 
-Tolerances (fp32; the GPU sums in a different order than mkldnn / the CPU batch_norm):
-  logits: 1e-4 of max|logits|;  every gradient: 1e-3 of its max magnitude;  running statistics:
-  1e-5 of their max magnitude (batch variance from fp64 partial sums here).
+The reference is evaluated twice on the CPU: in fp32 (what the reference computes) and in fp64
+(the exact value). At the C5 sizes the fp32 reference's own gradients are 0.5-1.2 % (of their max
+magnitude) away from the fp64 ones (BatchNorm's backward subtracts batch means of 1e5-1e6 terms;
+measured: dx 4.7e-3 at 48x144x192, 1.2e-2 at 8x576x768), so the gradients are judged against fp64:
+  logits: 1e-4 of max|logits| against the fp32 reference;
+  every gradient (dx, each weight / gamma / beta): error against fp64 <= max(1e-4, twice the fp32
+  reference's own error against fp64), all relative to the quantity's max magnitude (measured:
+  the GPU's error is the reference's to within +-30 %, profiles/r05e/pytest_train.log);
+  running statistics: 1e-5 of their max magnitude.
 """
 import numpy as np
 import pytest
@@ -41,23 +47,32 @@ def test_costregnet_train_forward_backward(shape):
     out = costregnet_train(cr, xg)
     out.backward(gout.to(DEV))
     torch.cuda.synchronize()
-    # reference: torch autograd through the oracle in train mode (CPU)
-    ref_sd = {k: (v.clone().requires_grad_() if v.is_floating_point() and "running" not in k else v.clone())
-              for k, v in sd.items()}
-    xc = x.clone().requires_grad_()
-    ref = oracle.cost_reg_net(ref_sd, "", xc.unsqueeze(1), training=True)[:, 0]
-    ref.backward(gout)
-    rep = {"logits": _rel(out, ref), "dx": _rel(xg.grad, xc.grad)}
+    # reference: torch autograd through the oracle in train mode (CPU), fp32 and fp64
+    refs = {}
+    for dt in (torch.float32, torch.float64):
+        r_sd = {k: (v.to(dt).clone().requires_grad_() if v.is_floating_point() and "running" not in k
+                    else (v.to(dt).clone() if v.is_floating_point() else v.clone())) for k, v in sd.items()}
+        xc = x.to(dt).clone().requires_grad_()
+        r = oracle.cost_reg_net(r_sd, "", xc.unsqueeze(1), training=True)[:, 0]
+        r.backward(gout.to(dt))
+        refs[dt] = (r, xc.grad, r_sd)
+    ref, ref_dx, ref_sd = refs[torch.float32]
+    ex, ex_dx, ex_sd = refs[torch.float64]
+    rep = {"logits": _rel(out, ref)}
     assert rep["logits"] < 1e-4, rep
-    assert rep["dx"] < 1e-3, rep
     names = [n for n in sd if n.endswith(("conv.weight", "bn.weight", "bn.bias"))] + ["prob.weight"]
     params = dict(zip([f"{n}.{s}" for n in ("conv0", "conv1", "conv2", "conv3", "conv4", "conv5", "conv6", "conv7",
                                              "conv9", "conv11") for s in ("conv.weight", "bn.weight", "bn.bias")]
                       + ["prob.weight"], costregnet_params(cr)))
     assert set(params) == set(names)
-    worst = max((_rel(params[n].grad, ref_sd[n].grad), n) for n in names)
-    rep["worst_param_grad"] = worst
-    assert worst[0] < 1e-3, rep
+    checks = [("dx", xg.grad, ref_dx, ex_dx)] + [(n, params[n].grad, ref_sd[n].grad, ex_sd[n].grad) for n in names]
+    worst = (0.0, None, 0.0)
+    for n, got, r32, r64 in checks:
+        e_gpu, e_ref = _rel(got, r64), _rel(r32, r64)
+        assert e_gpu <= max(1e-4, 2.0 * e_ref), (n, e_gpu, e_ref)
+        worst = max(worst, (e_gpu, n, e_ref))
+    rep["worst_grad_vs_fp64 (gpu, name, fp32 reference)"] = worst
+    rep["dx_vs_fp64 (gpu, fp32 reference)"] = (_rel(xg.grad, ex_dx), _rel(ref_dx, ex_dx))
     for n in sd:
         if "running" in n:
             r = _rel(dict(cr.named_buffers())[n], ref_sd[n])
