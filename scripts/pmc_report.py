@@ -44,8 +44,8 @@ for (name, grid), d in sorted(vals.items(), key=lambda x: (x[0][0], x[0][1])):
         line.append(f"L1miss={m['TCP_TCC_READ_REQ_sum'] / max(m['TCP_TOTAL_CACHE_ACCESSES_sum'], 1):4.2f}")
     if cyc and "SQ_WAIT_ANY" in m and "SQ_WAVE_CYCLES" in m:
         line.append(f"parked={m['SQ_WAIT_ANY'] / max(m['SQ_WAVE_CYCLES'], 1):4.2f}")
-    if "SQ_WAVE_CYCLES" in m and cyc:
-        line.append(f"waves/SIMD={m['SQ_WAVE_CYCLES'] / 1024 / cyc:4.1f}")
+    if "SQ_WAVE_CYCLES" in m and cyc:  # SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md)
+        line.append(f"waves/SIMD={4 * m['SQ_WAVE_CYCLES'] / 1024 / cyc:4.1f}")
     if cyc and "SQ_WAIT_INST_ANY" in m and "SQ_WAVE_CYCLES" in m:
         line.append(f"wait={m['SQ_WAIT_INST_ANY'] / max(m['SQ_WAVE_CYCLES'], 1):4.2f}")
     print(" ".join(x for x in line if x))
