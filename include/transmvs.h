@@ -243,6 +243,18 @@ int tmvs_conv3d_wgrad(const float* direct, int a_ch, int batch, int pd, int ph, 
                       int b_ch, int gd, int gh, int gw, int stride, void* workspace, size_t workspace_bytes,
                       float* dw, void* stream);
 
+/* Backward of the per-view similarity (homo_warping + (warped*ref).mean(1), module.py:284-322,
+ * TransMVSNet.py:80) for the training path: given dsim [V][D][H][W] (d loss / d sim_v), writes
+ *   dref [H][W][C] = sum_v sum_d dsim/C * bilinear(src_v)          (NHWC, overwritten)
+ *   dsrc [V][H][W][C] = the bilinear scatter of dsim/C * ref          (NHWC, overwritten)
+ * ref/src/hyp/proj/flags as tmvs_warp_corr (one sample, C in {8,16,32}). The scatter is summed
+ * in 2^-40 fixed point with 64-bit integer atomics: deterministic; |a single contribution| must
+ * stay below 2^22 (checked: the workspace's int after the buffer is set to 1 otherwise).       */
+size_t tmvs_warp_corr_backward_workspace(int n_src, int channels, int height, int width);
+int tmvs_warp_corr_backward(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,
+                            const float* dsim, int n_src, int channels, int ndepth, int height, int width, int flags,
+                            void* workspace, size_t workspace_bytes, float* dref, float* dsrc, void* stream);
+
 /* BatchNorm3d in train mode over z [nvox][C] (C divides 256): batch mean and biased variance
  * (fp64 partials, fixed-order combine); y = relu(fmaf(z, a, b)) [+ skip] with a = gamma /
  * sqrt(var + eps), b = beta - mean * a; the backward of that (incl. the ReLU mask) gives dz,

@@ -189,15 +189,15 @@ def homo_warping(src_fea, src_proj, ref_proj, depth_values):
     return out.view(b, c, d, h, w)
 
 
-def pixelwise_net(sd, sim, p="DepthNet.pixel_wise_net."):
-    """PixelwiseNet.forward, models/TransMVSNet.py:20-30 -> [B,1,H,W]."""
-    x = F.relu(_bn(F.conv3d(sim, sd[p + "conv0.conv.weight"]), sd, p + "conv0.bn."))
-    x = F.relu(_bn(F.conv3d(x, sd[p + "conv1.conv.weight"]), sd, p + "conv1.bn."))
+def pixelwise_net(sd, sim, p="DepthNet.pixel_wise_net.", training=False):
+    """PixelwiseNet.forward, models/TransMVSNet.py:20-30 -> [B,1,H,W] (training: BN batch statistics)."""
+    x = F.relu(_bn(F.conv3d(sim, sd[p + "conv0.conv.weight"]), sd, p + "conv0.bn.", training))
+    x = F.relu(_bn(F.conv3d(x, sd[p + "conv1.conv.weight"]), sd, p + "conv1.bn.", training))
     x = F.conv3d(x, sd[p + "conv2.weight"], sd[p + "conv2.bias"]).squeeze(1)
     return torch.max(torch.sigmoid(x), dim=1, keepdim=True)[0]
 
 
-def build_cost_volume(sd, features, proj_matrix, depth_values, view_weights=None):
+def build_cost_volume(sd, features, proj_matrix, depth_values, view_weights=None, training=False):
     """Steps 1-2 of DepthNet.forward, models/TransMVSNet.py:58-93.
 
     Returns (similarity [B,1,D,H,W], view_weights [B,V,H,W] or None).
@@ -212,7 +212,7 @@ def build_cost_volume(sd, features, proj_matrix, depth_values, view_weights=None
         warped = homo_warping(src_fea, compose_proj(src_proj), compose_proj(ref_proj), depth_values)
         sim = (warped * ref_fea.unsqueeze(2)).mean(1, keepdim=True)
         if view_weights is None:
-            vw = pixelwise_net(sd, sim)
+            vw = pixelwise_net(sd, sim, training=training)
             weights_out.append(vw)
         else:
             vw = view_weights[:, i:i + 1]

@@ -79,3 +79,106 @@ def test_costregnet_train_forward_backward(shape):
             assert r < 1e-5, (n, r)
     assert int(cr.conv0.bn.num_batches_tracked) == 1 + int(sd["conv0.bn.num_batches_tracked"])
     print(shape, rep)
+
+
+@pytest.mark.parametrize("c,d,h,w,nv", [(8, 8, 24, 32, 3), (32, 48, 144, 192, 3), (16, 32, 288, 384, 3),
+                                        (8, 8, 576, 768, 3)])
+def test_warp_corr_views_forward_backward(c, d, h, w, nv):
+    """Per-view similarity volumes + their backward into the reference and source features against
+    torch autograd through the oracle's homo_warping + mean (CPU fp32). The source-feature gradient is
+    a bilinear scatter: the GPU sums it in 2^-40 fixed point (deterministic), the CPU in fp32."""
+    from transmvsnet_amd import ops, synthetic
+    from transmvsnet_amd.train import warp_corr_views
+    g = torch.Generator().manual_seed(c + d + h)
+    feats = [torch.randn(1, c, h, w, generator=g) for _ in range(nv + 1)]
+    proj = synthetic.synthetic_cameras(nv + 1, h * (4 if c == 32 else 2 if c == 16 else 1),
+                                       w * (4 if c == 32 else 2 if c == 16 else 1), seed=3)
+    proj = proj["stage1" if c == 32 else "stage2" if c == 16 else "stage3"]
+    hyp = (560.0 + 120.0 * torch.rand(1, d, h, w, generator=g)).contiguous()
+    dsim = torch.randn(nv, d, h, w, generator=g)
+    rows = ops.proj_rows(proj)[0]
+    ref_g = feats[0][0].permute(1, 2, 0).contiguous().to(DEV).requires_grad_()
+    src_g = torch.stack([f[0].permute(1, 2, 0) for f in feats[1:]]).contiguous().to(DEV).requires_grad_()
+    sims = warp_corr_views(ref_g, src_g, hyp[0].to(DEV), rows)
+    sims.backward(dsim.to(DEV))
+    torch.cuda.synchronize()
+    xs = [f.clone().requires_grad_() for f in feats]
+    projs = torch.unbind(proj, 1)
+    ref_sims = []
+    for i in range(nv):
+        warped = oracle.homo_warping(xs[1 + i], oracle.compose_proj(projs[1 + i]), oracle.compose_proj(projs[0]), hyp)
+        ref_sims.append((warped * xs[0].unsqueeze(2)).mean(1))
+    ref_sims = torch.cat(ref_sims, 0)
+    ref_sims.backward(dsim)
+    rep = {"sim": float((sims.cpu() - ref_sims).abs().max()),
+           "dref": _rel(ref_g.grad.permute(2, 0, 1), xs[0].grad[0]),
+           "dsrc": max(_rel(src_g.grad[i].permute(2, 0, 1), xs[1 + i].grad[0]) for i in range(nv))}
+    print((c, d, h, w, nv), rep)
+    assert rep["sim"] < 2e-5 and rep["dref"] < 1e-5 and rep["dsrc"] < 1e-5, rep
+
+
+def test_depth_stages_training_step():
+    """A training step's three DepthNet stages (hypotheses, cost volume + its backward, view aggregation,
+    train-mode PixelwiseNet and CostRegNets, softmax/WTA, trans_mvsnet_loss and d loss / d logits)
+    against torch autograd through the oracle + oracle/loss_ref.py on the CPU (fp32), 64x80, N=3,
+    8/8/8 hypotheses: loss value, d loss / d stage features, every CostRegNet and PixelwiseNet
+    parameter gradient (1e-3 of each quantity's max magnitude), identical WTA depths."""
+    import torch.nn.functional as F
+    from oracle import loss_ref
+    from transmvsnet_amd import TransMVSNet, synthetic
+    from transmvsnet_amd.train import depth_stages_train
+    H, W, N, ND = 64, 80, 3, (8, 8, 8)
+    sd = golden_state_dict()
+    model = TransMVSNet(ndepths=list(ND))
+    model.load_state_dict(sd, strict=True)
+    model = model.to(DEV)
+    g = torch.Generator().manual_seed(9)
+    feats = [{k: torch.randn(1, c, H // s, W // s, generator=g) for k, c, s in
+              (("stage1", 32, 4), ("stage2", 16, 2), ("stage3", 8, 1))} for _ in range(N)]
+    proj = synthetic.synthetic_cameras(N, H, W, seed=1)
+    dv = synthetic.synthetic_depth_values(1)
+    gt = {f"stage{s + 1}": 425.0 + 500.0 * torch.rand(1, H >> (2 - s), W >> (2 - s), generator=g) for s in range(3)}
+    gt = {"stage1": gt["stage1"][:, :H // 4, :W // 4], "stage2": gt["stage2"][:, :H // 2, :W // 2], "stage3": gt["stage3"]}
+    mask = {k: (torch.rand(v.shape, generator=g) > 0.3).float() for k, v in gt.items()}
+    # GPU
+    leaves = {k: torch.stack([f[k][0].permute(1, 2, 0) for f in feats]).contiguous().to(DEV).requires_grad_()
+              for k in ("stage1", "stage2", "stage3")}
+    total, outs = depth_stages_train(model, leaves, proj, dv.to(DEV), {k: v.to(DEV) for k, v in gt.items()},
+                                     {k: v.to(DEV) for k, v in mask.items()}, (H, W))
+    torch.cuda.synchronize()
+    # CPU reference: the oracle in train mode, autograd
+    rsd = {k: (v.clone().requires_grad_() if v.is_floating_point() and "running" not in k else v.clone())
+           for k, v in sd.items()}
+    rfe = [{k: v.clone().requires_grad_() for k, v in f.items()} for f in feats]
+    outputs, depth, vw = {}, None, None
+    for s in range(3):
+        name = f"stage{s + 1}"
+        hyp = oracle.stage_hypotheses(depth, dv, s, (H, W), ND)
+        if s > 0:
+            vw = F.interpolate(vw, scale_factor=2, mode="nearest")
+        sim, vw_new = oracle.build_cost_volume(rsd, [f[name] for f in rfe], proj[name], hyp, vw if s else None,
+                                               training=True)
+        if s == 0:
+            vw = vw_new.detach()
+        logits = oracle.cost_reg_net(rsd, f"cost_regularization.{s}.", sim, training=True)[:, 0]
+        prob = torch.exp(F.log_softmax(logits, dim=1))
+        depth = torch.gather(hyp, 1, prob.argmax(1, keepdim=True)).squeeze(1)
+        outputs[name] = {"prob_volume": prob, "depth_values": hyp}
+        np.testing.assert_array_equal(outs[name]["depth_values"].cpu().numpy(), hyp.detach().numpy())
+        assert torch.equal(outs[name]["depth"].cpu(), depth.clamp(425.0, 935.0).detach()), name
+    ref_total = loss_ref.trans_mvsnet_loss(outputs, gt, mask, dlossw=(0.5, 1.0, 2.0))[0]
+    ref_total.backward()
+    rep = {"loss": abs(float(total) - float(ref_total)) / abs(float(ref_total))}
+    assert rep["loss"] < 1e-5, rep
+    worst = (0.0, None)
+    for k in ("stage1", "stage2", "stage3"):
+        for v in range(N):
+            worst = max(worst, (_rel(leaves[k].grad[v].permute(2, 0, 1), rfe[v][k].grad[0]), f"d{k}[{v}]"))
+    params = dict(model.named_parameters())
+    for n, t in rsd.items():
+        if t.requires_grad and (n.startswith("cost_regularization.") or n.startswith("DepthNet.")):
+            assert params[n].grad is not None, n
+            worst = max(worst, (_rel(params[n].grad, t.grad), n))
+    rep["worst_grad"] = worst
+    print(rep)
+    assert worst[0] < 1e-3, rep

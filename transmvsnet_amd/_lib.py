@@ -53,6 +53,8 @@ SIGNATURES = {
     "tmvs_entropy_loss": (I, [P, P, I, P, P, I, I, I, I, F, P, S, P, P, P, P, P]),
     "tmvs_depth_metrics_workspace": (S, [I]),
     "tmvs_depth_metrics": (I, [P, P, P, I, F, P, S, P, P]),
+    "tmvs_warp_corr_backward_workspace": (S, [I, I, I, I]),
+    "tmvs_warp_corr_backward": (I, [P, P, P, P, P, I, I, I, I, I, I, P, S, P, P, P]),
     "tmvs_conv3d_generic": (I, [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P]),
     "tmvs_conv3d_wgrad_workspace": (S, [I, I, I, I, I, I]),
     "tmvs_conv3d_wgrad": (I, [P, I, I, I, I, I, P, I, I, I, I, I, P, S, P, P]),

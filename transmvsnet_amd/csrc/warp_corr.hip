@@ -663,6 +663,103 @@ static int dispatch_mode(bool pw, bool partial, int D, const float* ref, const f
                                          vw_total, a, st);
 }
 
+
+// ---------------------------------------------------------------- backward (training, C5)
+// Adjoint of the per-view similarity sim_v[d][p] = (1/C) sum_c ref[p][c] * bilinear(src_v, X(v,d,p))[c]
+// (homo_warping + (warped * ref).mean(1), models/module.py:284-322, TransMVSNet.py:80), given
+// dsim_v [V][D][H][W]:
+//   dref[p][c]   = sum_v sum_d (dsim_v[d][p] / C) * bilinear_c         (gather: registers, no atomics)
+//   dsrc_v[q][c] += w_tap * (dsim_v[d][p] / C) * ref[p][c]              (scatter to the 4 taps)
+// The scatter is deterministic: contributions are rounded to fixed point (2^kFixShift units) and
+// summed with 64-bit integer atomics (order-independent), then converted once. One thread per
+// reference pixel walks the views and planes; coordinates come from project() (same rounding as
+// the forward, incl. TMVS_WARP_ROT_PLAIN).
+constexpr int kFixShift = 40;
+
+template <int C>
+__global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restrict__ ref,
+                                                            const float* __restrict__ src,
+                                                            const float* __restrict__ hyp,
+                                                            const float* __restrict__ dsim, int V, int D, int H, int W,
+                                                            WarpArgs args, float* __restrict__ dref,
+                                                            unsigned long long* __restrict__ dsrc_fix,
+                                                            int* __restrict__ overflow) {
+  const int HW = H * W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= HW) return;
+  const int py = p / W, px = p - py * W;
+  const float fxp = (float)px, fyp = (float)py;
+  float r[C], dr[C];
+#pragma unroll
+  for (int c4 = 0; c4 < C / 4; ++c4) {
+    const float4 t = *reinterpret_cast<const float4*>(ref + (size_t)p * C + 4 * c4);
+    r[4 * c4] = t.x;
+    r[4 * c4 + 1] = t.y;
+    r[4 * c4 + 2] = t.z;
+    r[4 * c4 + 3] = t.w;
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) dr[c] = 0.f;
+  const float halfw = (float)(W - 1) / 2.f, halfh = (float)(H - 1) / 2.f;
+  const float fscale = (float)(1ULL << kFixShift);
+  bool ovf = false;
+  for (int v = 0; v < V; ++v) {
+    const float* R = args.proj[v];
+    const float rx = rot_row(R, fxp, fyp, args.rot_plain);
+    const float ry = rot_row(R + 4, fxp, fyp, args.rot_plain);
+    const float rz = rot_row(R + 8, fxp, fyp, args.rot_plain);
+    const float* sv = src + (size_t)v * HW * C;
+    unsigned long long* dv = dsrc_fix + (size_t)v * HW * C;
+#pragma unroll 1
+    for (int d = 0; d < D; ++d) {
+      const float g = dsim[((size_t)v * D + d) * HW + p] * (1.f / (float)C);  // C = 2^n: exact
+      int x0, y0;
+      float fx, fy;
+      project(rx, ry, rz, R[3], R[7], R[11], hyp[(size_t)d * HW + p], halfw, halfh, x0, y0, fx, fy);
+      const float ea = 1.f - fx, s = 1.f - fy;
+      const float wt[4] = {s * ea, s * fx, fy * ea, fy * fx};  // nw, ne, sw, se (grid_sample)
+      const int tx[4] = {x0, x0 + 1, x0, x0 + 1}, ty[4] = {y0, y0, y0 + 1, y0 + 1};
+      bool in[4];
+      const float* tp[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        in[t] = (unsigned)tx[t] < (unsigned)W && (unsigned)ty[t] < (unsigned)H;
+        tp[t] = sv + ((size_t)(in[t] ? ty[t] : 0) * W + (in[t] ? tx[t] : 0)) * C;
+      }
+      if (g == 0.f) continue;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float a = in[0] ? tp[0][c] : 0.f, b = in[1] ? tp[1][c] : 0.f;
+        const float cc = in[2] ? tp[2][c] : 0.f, dd = in[3] ? tp[3][c] : 0.f;
+        const float val = fmaf(dd, wt[3], fmaf(cc, wt[2], fmaf(b, wt[1], a * wt[0])));
+        dr[c] = fmaf(g, val, dr[c]);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (!in[t] || wt[t] == 0.f) continue;
+        unsigned long long* q = dv + ((size_t)ty[t] * W + tx[t]) * C;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const float contrib = wt[t] * (g * r[c]);
+          const float sc = contrib * fscale;
+          ovf |= fabsf(contrib) >= 4194304.f;  // 2^22: keeps every partial sum inside int64
+          if (sc != 0.f) atomicAdd(q + c, (unsigned long long)(long long)llrintf(sc));
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int c4 = 0; c4 < C / 4; ++c4)
+    *reinterpret_cast<float4*>(dref + (size_t)p * C + 4 * c4) =
+        make_float4(dr[4 * c4], dr[4 * c4 + 1], dr[4 * c4 + 2], dr[4 * c4 + 3]);
+  if (ovf) atomicOr(overflow, 1);
+}
+
+__global__ void fix_to_float_kernel(const unsigned long long* __restrict__ in, long n, float* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = (float)((double)(long long)in[i] * (1.0 / (double)(1ULL << kFixShift)));
+}
 }  // namespace tmvs
 
 using namespace tmvs;
@@ -749,5 +846,52 @@ extern "C" int tmvs_homo_warping(const float* src_fea, const float* proj, const 
                        out + (size_t)b * channels * ndepth * HW, channels, ndepth, height, width, a);
     TMVS_CHECK_LAUNCH();
   }
+  return TMVS_OK;
+}
+
+extern "C" size_t tmvs_warp_corr_backward_workspace(int n_src, int channels, int height, int width) {
+  return (size_t)n_src * height * width * channels * sizeof(unsigned long long) + 256;
+}
+
+extern "C" int tmvs_warp_corr_backward(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,
+                                       const float* dsim, int n_src, int channels, int ndepth, int height, int width,
+                                       int flags, void* workspace, size_t workspace_bytes, float* dref, float* dsrc,
+                                       void* stream) {
+  if (!ref_fea || !src_fea || !proj || !hyp || !dsim || !workspace || !dref || !dsrc) return TMVS_ERR_ARG;
+  if (n_src <= 0 || n_src > TMVS_MAX_VIEWS || ndepth <= 0 || height <= 0 || width <= 0) return TMVS_ERR_ARG;
+  if (width > 32766 || height > 32766) return TMVS_ERR_SHAPE;
+  if (workspace_bytes < tmvs_warp_corr_backward_workspace(n_src, channels, height, width)) return TMVS_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  WarpArgs a = {};
+  a.rot_plain = (flags & TMVS_WARP_ROT_PLAIN) ? 1 : 0;
+  for (int v = 0; v < n_src; ++v)
+    for (int k = 0; k < 12; ++k) a.proj[v][k] = proj[(size_t)v * 12 + k];
+  const long n = (long)n_src * height * width * channels;
+  unsigned long long* fix = (unsigned long long*)workspace;
+  int* ovf = (int*)((char*)workspace + (size_t)n * sizeof(unsigned long long));
+  if (hipMemsetAsync(workspace, 0, (size_t)n * sizeof(unsigned long long) + sizeof(int), st) != hipSuccess)
+    return TMVS_ERR_HIP;
+  const int HW = height * width;
+  const dim3 grid((HW + 255) / 256);
+  switch (channels) {
+    case 8:
+      hipLaunchKernelGGL(warp_corr_bwd_kernel<8>, grid, dim3(256), 0, st, ref_fea, src_fea, hyp, dsim, n_src, ndepth,
+                         height, width, a, dref, fix, ovf);
+      break;
+    case 16:
+      hipLaunchKernelGGL(warp_corr_bwd_kernel<16>, grid, dim3(256), 0, st, ref_fea, src_fea, hyp, dsim, n_src, ndepth,
+                         height, width, a, dref, fix, ovf);
+      break;
+    case 32:
+      hipLaunchKernelGGL(warp_corr_bwd_kernel<32>, grid, dim3(256), 0, st, ref_fea, src_fea, hyp, dsim, n_src, ndepth,
+                         height, width, a, dref, fix, ovf);
+      break;
+    default:
+      return TMVS_ERR_SHAPE;
+  }
+  TMVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(fix_to_float_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (const unsigned long long*)fix,
+                     n, dsrc);
+  TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }

@@ -619,6 +619,29 @@ def bn_relu_backward(dy, z, mean, var, gamma, beta, eps):
     return dz, dg, db
 
 
-for _name in ("conv3d_generic", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn_relu_backward"):
+def warp_corr_backward(ref_nhwc, src_nhwc, proj12, hyp, dsim, rot_order="auto"):
+    """tmvs_warp_corr_backward: one sample, ref [H,W,C], src [V,H,W,C] NHWC, proj12 HOST [V,12],
+    hyp [D,H,W], dsim [V,D,H,W] -> (dref [H,W,C], dsrc [V,H,W,C], overflow flag tensor [1] int32)."""
+    for t, n in ((ref_nhwc, "ref"), (src_nhwc, "src"), (hyp, "hyp"), (dsim, "dsim")):
+        _dev(t, n)
+    v, h, w, c = src_nhwc.shape
+    d = hyp.shape[0]
+    if tuple(dsim.shape) != (v, d, h, w) or tuple(ref_nhwc.shape) != (h, w, c):
+        raise ValueError("warp_corr_backward: shapes must be ref [H,W,C], src [V,H,W,C], hyp [D,H,W], dsim [V,D,H,W]")
+    proj = np.ascontiguousarray(proj12, np.float32).reshape(v, 12)
+    nbytes = _lib_h().tmvs_warp_corr_backward_workspace(v, c, h, w)
+    ws = torch.empty(nbytes // 4 + 64, device=hyp.device)
+    dref = torch.empty_like(ref_nhwc)
+    dsrc = torch.empty_like(src_nhwc)
+    with _Span("tmvs_warp_corr_backward"):
+        _lib.check(_lib_h().tmvs_warp_corr_backward(_ptr(ref_nhwc), _ptr(src_nhwc), proj.ctypes.data, _ptr(hyp), _ptr(dsim),
+                                                    v, c, d, h, w, warp_flags(rot_order, h * w), _ptr(ws),
+                                                    ws.numel() * 4, _ptr(dref), _ptr(dsrc), _stream()),
+                   "tmvs_warp_corr_backward")
+    flag = ws.view(torch.int32)[2 * v * h * w * c: 2 * v * h * w * c + 1]
+    return dref, dsrc, flag
+
+
+for _name in ("conv3d_generic", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn_relu_backward", "warp_corr_backward"):
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name

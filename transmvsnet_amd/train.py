@@ -1,5 +1,17 @@
-"""Training path, first differentiable block: CostRegNet in train
-mode with its backward on the HIP kernels of csrc/costreg_train.hip.
+"""Training path: the differentiable blocks that run on HIP.
+
+* ``warp_corr_views``: the per-view similarity volumes of DepthNet (homo_warping + (warped *
+  ref).mean(1), models/module.py:284-322, TransMVSNet.py:80) with the backward into the reference
+  and source features (tmvs_warp_corr_backward: gather for the reference, deterministic
+  fixed-point scatter for the sources). The view aggregation and the stage-1 PixelwiseNet that
+  consume these volumes are small elementwise / 1x1 work left to torch autograd.
+* ``costregnet_train``: CostRegNet in train mode with its backward on csrc/costreg_train.hip.
+* ``depth_stages_train``: the three DepthNet stages of a training step (models/TransMVSNet.py:38-109,
+  174-221) from the FMT/pathway features to trans_mvsnet_loss (module.py:532-556) and its backward:
+  hypotheses (tmvs_stage_hypotheses), per-view cost volumes (above), the view aggregation and the
+  stage-1 PixelwiseNet in train mode (torch), CostRegNet (above), softmax/WTA (tmvs_softmax_wta) and
+  the loss with d loss / d logits (tmvs_entropy_loss); gradients reach the stage features, the
+  CostRegNet and PixelwiseNet parameters.
 
 ``costregnet_train(module, x)`` is CostRegNet.forward (models/module.py:447-456) of a
 ``transmvsnet_amd.model.CostRegNet`` whose BatchNorm3d layers run in train mode, as in the
@@ -22,6 +34,7 @@ Tensor layout is NDHWC throughout; weight re-layouts are index permutations (pac
 from __future__ import annotations
 
 import torch
+import torch.nn.functional as F
 
 from . import ops
 
@@ -31,6 +44,38 @@ _LAYERS = (("conv0", 1, False, None), ("conv1", 2, False, None), ("conv2", 1, Fa
            ("conv6", 1, False, None), ("conv7", 2, True, "conv4"), ("conv9", 2, True, "conv2"),
            ("conv11", 2, True, "conv0"))
 BN_MOMENTUM = 0.1
+
+
+class _WarpCorrViews(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ref, src, hyp, proj12, rot_order):
+        v, h, w, c = src.shape
+        d = hyp.shape[0]
+        sims = torch.empty(v, d, h, w, device=src.device)
+        ones = torch.ones(1, 1, h, w, device=src.device)
+        wsum = torch.empty(1, h, w, device=src.device)
+        for i in range(v):  # one view per launch, weight 1, partial: sim_out = 1 * sim_v exactly
+            ops.warp_corr(ref[None], src[i:i + 1][None], proj12[None, i:i + 1], hyp[None], view_w_in=ones, vw_shift=0,
+                          vw_total=1, partial=True, sim_out=sims[i:i + 1], wsum_out=wsum, rot_order=rot_order)
+        ctx.save_for_backward(ref, src, hyp)
+        ctx.proj12, ctx.rot_order = proj12, rot_order
+        return sims
+
+    @staticmethod
+    def backward(ctx, dsims):
+        ref, src, hyp = ctx.saved_tensors
+        dref, dsrc, flag = ops.warp_corr_backward(ref, src, ctx.proj12, hyp, dsims.contiguous(), ctx.rot_order)
+        if int(flag.item()):
+            raise RuntimeError("warp_corr_backward: a gradient contribution exceeded the fixed-point range (2^22)")
+        return dref, dsrc, None, None, None
+
+
+def warp_corr_views(ref_nhwc, src_nhwc, hyp, proj12, rot_order="auto"):
+    """Per-view similarity volumes sim_v [V, D, H, W] for ONE sample (ref [H,W,C], src [V,H,W,C] NHWC,
+    hyp [D,H,W], proj12 HOST [V,12] from ops.proj_rows), differentiable w.r.t. ref and src."""
+    if not src_nhwc.is_cuda:
+        raise RuntimeError("warp_corr_views runs on the GPU only (no CPU fallback)")
+    return _WarpCorrViews.apply(ref_nhwc.contiguous(), src_nhwc.contiguous(), hyp.contiguous(), proj12, rot_order)
 
 
 def _pack_fwd(w, transposed):
@@ -157,3 +202,72 @@ def costregnet_train(module, x):
                 bn.running_var.mul_(1.0 - BN_MOMENTUM).add_(var * (n / max(n - 1, 1)), alpha=BN_MOMENTUM)
                 bn.num_batches_tracked.add_(1)
     return logits
+
+
+def pixelwise_net_train(pw, sim_v):
+    """PixelwiseNet.forward (models/TransMVSNet.py:20-30) in train mode on one view's similarity volume
+    sim_v [D, H, W] -> view weight [H, W]: 1x1x1 convs 1->16->8 (BatchNorm3d with batch statistics,
+    running statistics updated), ->1 (+bias), sigmoid, max over D. Channels-last torch ops."""
+    x = sim_v.unsqueeze(-1) * pw.conv0.conv.weight.reshape(1, 1, 1, -1)            # [D,H,W,16]
+    x = F.relu(_bn_last(x, pw.conv0.bn))
+    x = torch.matmul(x, pw.conv1.conv.weight.reshape(8, 16).t())                       # [D,H,W,8]
+    x = F.relu(_bn_last(x, pw.conv1.bn))
+    x = torch.matmul(x, pw.conv2.weight.reshape(1, 8).t()).squeeze(-1) + pw.conv2.bias  # [D,H,W]
+    return torch.sigmoid(x).max(dim=0)[0]
+
+
+def _bn_last(x, bn):
+    c = x.shape[-1]
+    y = F.batch_norm(x.reshape(1, -1, c).permute(0, 2, 1), bn.running_mean, bn.running_var, bn.weight, bn.bias,
+                     True, bn.momentum, bn.eps)
+    if bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    return y.permute(0, 2, 1).reshape(x.shape)
+
+
+def depth_stages_train(model, stage_features, proj_matrix, depth_values, depth_gt_ms, mask_ms, img_hw,
+                       dlossw=(0.5, 1.0, 2.0)):
+    """One training step's DepthNet stages for ONE sample (B = 1), forward and backward.
+
+    stage_features: {stage: [N, h, w, C]} NHWC FMT/pathway outputs, reference view first (leaf tensors
+    that require grad collect d loss / d features); proj_matrix {stage: [1, N, 2, 4, 4]}; depth_values
+    [1, 192]; depth_gt_ms / mask_ms {stage: [1, h, w]}. The CostRegNets and the PixelwiseNet run in train
+    mode (their BatchNorm running statistics are updated). Calls backward of trans_mvsnet_loss (dlossw:
+    train.py's default) and returns (total_loss, outputs) with outputs as TransMVSNet.forward's stage
+    dicts.
+    """
+    from . import loss as loss_mod
+    from .model import DEPTH_CLAMP, STAGE_SCALES
+    dev = stage_features["stage1"].device
+    with torch.cuda.device(dev):
+        dv = depth_values.to(dev, torch.float32).contiguous()
+        outputs, logits_all, prev_raw, vw_det = {}, [], None, None
+        for s in range(3):
+            name = f"stage{s + 1}"
+            f = stage_features[name]
+            hyp = ops.stage_hypotheses(dv, prev_raw, model.ndepths[s], model.depth_interals_ratio[s], img_hw,
+                                       STAGE_SCALES[s])
+            rows = ops.proj_rows(proj_matrix[name])[0]
+            sims = warp_corr_views(f[0], f[1:], hyp[0], rows, rot_order=model.warp_rot_order)  # [V,D,h,w]
+            if s == 0:
+                vws = [pixelwise_net_train(model.DepthNet.pixel_wise_net, sims[v]) for v in range(sims.shape[0])]
+                vw_det = torch.stack(vws).detach()  # TransMVSNet.py:107 returns view_weights.detach()
+            else:
+                up = vw_det
+                for _ in range(s):
+                    up = F.interpolate(up[None], scale_factor=2, mode="nearest")[0]
+                vws = list(up)
+            sim_sum, w_sum = 0, 1e-5
+            for v in range(sims.shape[0]):  # TransMVSNet.py:88-93, view order
+                sim_sum = sim_sum + sims[v] * vws[v].unsqueeze(0)
+                w_sum = w_sum + vws[v].unsqueeze(0)
+            sim = sim_sum / w_sum
+            logits = costregnet_train(model.cost_regularization[s].train(), sim.unsqueeze(0))
+            prob, depth, raw, conf = ops.softmax_wta(logits.detach(), hyp, DEPTH_CLAMP)
+            outputs[name] = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}
+            logits_all.append(logits)
+            prev_raw = raw
+        total, depth_loss, _, _, grads = loss_mod.trans_mvsnet_loss(outputs, depth_gt_ms, mask_ms, dlossw=dlossw,
+                                                                    return_grad=True)
+        torch.autograd.backward(logits_all, [grads[f"stage{s + 1}"] for s in range(3)])
+    return total, outputs
