@@ -52,6 +52,8 @@ def _args():
     ap.add_argument("--no-overlap", action="store_true", help="run the FMT pathway on the main stream (A/B)")
     ap.add_argument("--e2e-steps", type=int, default=10,
                     help="timed full forward() passes (images -> depth, FeatureNet included); 0 = skip")
+    ap.add_argument("--train-steps", type=int, default=3,
+                    help="timed C5 training steps of the DepthNet stages (transmvsnet_amd.train); 0 = skip")
     return ap.parse_args()
 
 
@@ -224,6 +226,7 @@ def run(args, world, rank, local):
         spans = timer.durations()
 
         e2e = end_to_end(model, args.e2e_steps, proj, dv_dev, dev) if args.e2e_steps > 0 and shard is None else None
+    train = train_timing(args.train_steps, dev, world) if args.train_steps > 0 and shard is None else None
 
     maps_per_step = 1 if args.mode == "views" else world
     value = maps_per_step * args.steps / elapsed
@@ -306,6 +309,7 @@ def run(args, world, rank, local):
             "cpu_baseline": cpu,
             "abs_depth_l1_vs_ref": l1,
             "end_to_end": e2e,
+            "train_depth_stages": train,
         }
         if ranks_ok is not None:
             line["ranks_check"] = ranks_ok
@@ -342,6 +346,52 @@ def end_to_end(model, steps, proj, dv_dev, dev):
             "workload": "TransMVSNet.forward(imgs [1,5,3,864,1152], proj, depth_values): FeatureNet (HIP: "
                         "tmvs_conv2d_bn_relu trunk, tmvs_fpn_merge, tmvs_conv3x3_nhwc, tmvs_dcn_fused) + the hot "
                         "path above"}
+
+
+def train_timing(steps, dev, world):
+    """C5 training step of the DepthNet stages (BlendedMVS 768x576, N=4, 48/32/8, one sample per rank),
+    forward + backward through transmvsnet_amd.train.depth_stages_train from synthetic FMT/pathway
+    features (leaf tensors) to trans_mvsnet_loss, plus DDP's gradient all-reduce when world > 1. HIP
+    events, median of `steps` after 1 warm-up; max over ranks."""
+    from transmvsnet_amd import TransMVSNet, synthetic
+    from transmvsnet_amd.train import allreduce_gradients, depth_stages_train
+    h5, w5, n5 = 576, 768, 4
+    m = TransMVSNet()
+    m.load_state_dict(synthetic.synthetic_state_dict(synthetic.state_dict_shapes(m), seed=0, sharpen=100.0))
+    m = m.to(dev)
+    feats = synthetic.stacked_features(n5, h5, w5, seed=5)
+    leaves = {k: v[0].permute(0, 2, 3, 1).contiguous().to(dev).requires_grad_() for k, v in feats.items()}
+    proj = synthetic.synthetic_cameras(n5, h5, w5, seed=6)
+    dv = synthetic.synthetic_depth_values(1).to(dev)
+    g = torch.Generator().manual_seed(7)
+    gt = {f"stage{s + 1}": (425.0 + 500.0 * torch.rand(1, h5 >> (2 - s), w5 >> (2 - s), generator=g)).to(dev)
+          for s in range(3)}
+    mask = {k: torch.ones_like(v) for k, v in gt.items()}
+    params = [p for n, p in m.named_parameters() if n.startswith(("cost_regularization.", "DepthNet."))]
+    ts = []
+    for i in range(steps + 1):
+        for p in params + list(leaves.values()):
+            p.grad = None
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        depth_stages_train(m, leaves, proj, dv, gt, mask, (h5, w5))
+        allreduce_gradients(params)
+        e1.record()
+        torch.cuda.synchronize()
+        if i > 0:
+            ts.append(e0.elapsed_time(e1))
+    ms = float(np.median(ts))
+    if world > 1:
+        t = torch.tensor([ms], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+    nbytes = sum(p.numel() for p in params) * 4
+    return {"ms_per_sample": round(ms, 3), "samples_per_s": round(world * 1e3 / ms, 3), "ranks": world,
+            "grad_allreduce_bytes": nbytes if world > 1 else 0,
+            "workload": "BlendedMVS 768x576, N=4, 48/32/8, 1 sample per rank: DepthNet stages forward + backward "
+                        "(HIP: hypotheses, per-view cost volumes + backward, CostRegNet train fwd/bwd, softmax/WTA, "
+                        "trans_mvsnet_loss + d/dlogits; torch: view aggregation, PixelwiseNet) + DDP gradient "
+                        "all-reduce; FMT / pathway / FeatureNet backward not included (not native yet)"}
 
 
 def host_cores():

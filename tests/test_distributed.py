@@ -116,3 +116,43 @@ def test_view_sharded_cost_volume_gloo(world):
         assert scale > 1e-3
         assert err <= 1e-6, (rank, err)
         assert vw_err == 0.0, (rank, vw_err)
+
+
+def _grad_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from transmvsnet_amd.train import allreduce_gradients
+        g = torch.Generator().manual_seed(100 + rank)
+        params = [torch.nn.Parameter(torch.zeros(n)) for n in (5, 300, 7)]
+        for p in params:
+            p.grad = torch.randn(p.shape, generator=g)
+        allreduce_gradients(params, bucket_bytes=1024)  # forces several buckets
+        q.put((rank, [p.grad.clone() for p in params]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_gradients_is_the_rank_mean():
+    """train.allreduce_gradients (DDP's gradient sync) over gloo, world 2, multiple buckets."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    expect = []
+    for n_i, n in enumerate((5, 300, 7)):
+        acc = 0
+        for r in range(world):
+            gg = torch.Generator().manual_seed(100 + r)
+            grads = [torch.randn(m, generator=gg) for m in (5, 300, 7)]
+            acc = acc + grads[n_i]
+        expect.append(acc / world)
+    for r in range(world):
+        for got, exp in zip(res[r], expect):
+            torch.testing.assert_close(got, exp, rtol=1e-6, atol=1e-6)

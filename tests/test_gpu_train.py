@@ -120,14 +120,14 @@ def test_warp_corr_views_forward_backward(c, d, h, w, nv):
 def test_depth_stages_training_step():
     """A training step's three DepthNet stages (hypotheses, cost volume + its backward, view aggregation,
     train-mode PixelwiseNet and CostRegNets, softmax/WTA, trans_mvsnet_loss and d loss / d logits)
-    against torch autograd through the oracle + oracle/loss_ref.py on the CPU (fp32), 64x80, N=3,
+    against torch autograd through the oracle + oracle/loss_ref.py on the CPU (fp32), 128x160, N=3,
     8/8/8 hypotheses: loss value, d loss / d stage features, every CostRegNet and PixelwiseNet
     parameter gradient (1e-3 of each quantity's max magnitude), identical WTA depths."""
     import torch.nn.functional as F
     from oracle import loss_ref
     from transmvsnet_amd import TransMVSNet, synthetic
     from transmvsnet_amd.train import depth_stages_train
-    H, W, N, ND = 64, 80, 3, (8, 8, 8)
+    H, W, N, ND = 128, 160, 3, (8, 8, 8)
     sd = golden_state_dict()
     model = TransMVSNet(ndepths=list(ND))
     model.load_state_dict(sd, strict=True)

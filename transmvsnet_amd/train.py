@@ -271,3 +271,31 @@ def depth_stages_train(model, stage_features, proj_matrix, depth_values, depth_g
                                                                     return_grad=True)
         torch.autograd.backward(logits_all, [grads[f"stage{s + 1}"] for s in range(3)])
     return total, outputs
+
+
+def allreduce_gradients(params, group=None, bucket_bytes=64 << 20):
+    """DDP's gradient synchronisation (train.py:363-366 wraps the model in DistributedDataParallel):
+    the mean over ranks of every parameter gradient, as few flat buckets (one at this model's
+    4.6 MB) reduced with one all_reduce(SUM) each over RCCL, then scaled by 1/world."""
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized():
+        return
+    world = dist.get_world_size(group)
+    grads = [p.grad for p in params if p.grad is not None]
+    if world == 1 or not grads:
+        return
+    bucket, size = [], 0
+    for g in grads + [None]:
+        if g is not None and size + g.numel() * 4 <= bucket_bytes or (g is not None and not bucket):
+            bucket.append(g)
+            size += g.numel() * 4
+            continue
+        flat = torch.cat([b.reshape(-1) for b in bucket])
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+        flat.div_(world)
+        off = 0
+        for b in bucket:
+            b.copy_(flat[off:off + b.numel()].view_as(b))
+            off += b.numel()
+        if g is not None:
+            bucket, size = [g], g.numel() * 4
