@@ -195,6 +195,7 @@ __global__ __launch_bounds__(kTrainBlock) void bn_stats_partial_kernel(const flo
   const int c = threadIdx.x % C, r0 = threadIdx.x / C, rs = kTrainBlock / C;
   const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
   double s = 0.0, q = 0.0;
+#pragma unroll 8
   for (long v = v0 + r0; v < v1; v += rs) {
     const double x = (double)z[v * C + c];
     s += x;
@@ -265,6 +266,7 @@ __global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_partial_kernel(
   const float m = mean[c], rstd = 1.f / sqrtf(var[c] + eps);
   const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
   double sg = 0.0, sgx = 0.0;
+#pragma unroll 8
   for (long v = v0 + r0; v < v1; v += rs) {
     const float zz = z[v * C + c];
     const float g = fmaf(zz, al, sh) > 0.f ? dy[v * C + c] : 0.f;

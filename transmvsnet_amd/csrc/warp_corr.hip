@@ -671,7 +671,9 @@ static int dispatch_mode(bool pw, bool partial, int D, const float* ref, const f
 //   dref[p][c]   = sum_v sum_d (dsim_v[d][p] / C) * bilinear_c         (gather: registers, no atomics)
 //   dsrc_v[q][c] += w_tap * (dsim_v[d][p] / C) * ref[p][c]              (scatter to the 4 taps)
 // The scatter is deterministic: contributions are rounded to fixed point (2^kFixShift units) and
-// summed with 64-bit integer atomics (order-independent), then converted once. One thread per
+// summed with 64-bit integer atomics (order-independent), then converted once. Before that, the
+// coefficients w_tap * g of a source pixel are summed in registers across the consecutive planes
+// that hit it (one slot per tap parity class), so a pixel-view issues C atomics per UNIQUE tap. One thread per
 // reference pixel walks the views and planes; coordinates come from project() (same rounding as
 // the forward, incl. TMVS_WARP_ROT_PLAIN).
 constexpr int kFixShift = 40;
@@ -703,13 +705,27 @@ __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restr
   const float halfw = (float)(W - 1) / 2.f, halfh = (float)(H - 1) / 2.f;
   const float fscale = (float)(1ULL << kFixShift);
   bool ovf = false;
+  unsigned skey[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  float scoef[4] = {0.f, 0.f, 0.f, 0.f};
+  unsigned long long* dv = dsrc_fix;
+  auto flush = [&](int sl) {
+    if (skey[sl] == 0xFFFFFFFFu || scoef[sl] == 0.f) return;
+    unsigned long long* q = dv + ((size_t)(skey[sl] >> 16) * W + (skey[sl] & 0xFFFFu)) * C;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float contrib = scoef[sl] * r[c];
+      ovf |= fabsf(contrib) >= 4194304.f;  // 2^22: keeps every partial sum inside int64
+      const float sc = contrib * fscale;
+      if (sc != 0.f) atomicAdd(q + c, (unsigned long long)(long long)llrintf(sc));
+    }
+  };
   for (int v = 0; v < V; ++v) {
     const float* R = args.proj[v];
     const float rx = rot_row(R, fxp, fyp, args.rot_plain);
     const float ry = rot_row(R + 4, fxp, fyp, args.rot_plain);
     const float rz = rot_row(R + 8, fxp, fyp, args.rot_plain);
     const float* sv = src + (size_t)v * HW * C;
-    unsigned long long* dv = dsrc_fix + (size_t)v * HW * C;
+    dv = dsrc_fix + (size_t)v * HW * C;
 #pragma unroll 1
     for (int d = 0; d < D; ++d) {
       const float g = dsim[((size_t)v * D + d) * HW + p] * (1.f / (float)C);  // C = 2^n: exact
@@ -734,18 +750,27 @@ __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restr
         const float val = fmaf(dd, wt[3], fmaf(cc, wt[2], fmaf(b, wt[1], a * wt[0])));
         dr[c] = fmaf(g, val, dr[c]);
       }
+      // scatter coefficients w_tap * g, summed per source pixel across consecutive planes: the 4 taps
+      // of a plane occupy the 4 (x, y) parity classes, so slot (X&1, Y&1) holds the latest tap of its
+      // class and its running coefficient; a slot is flushed (C atomics) only when its tap changes
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (!in[t] || wt[t] == 0.f) continue;
-        unsigned long long* q = dv + ((size_t)ty[t] * W + tx[t]) * C;
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-          const float contrib = wt[t] * (g * r[c]);
-          const float sc = contrib * fscale;
-          ovf |= fabsf(contrib) >= 4194304.f;  // 2^22: keeps every partial sum inside int64
-          if (sc != 0.f) atomicAdd(q + c, (unsigned long long)(long long)llrintf(sc));
+      for (int sl = 0; sl < 4; ++sl) {
+        const int X = x0 + ((x0 ^ sl) & 1), Y = y0 + ((y0 ^ (sl >> 1)) & 1);
+        const bool inside = (unsigned)X < (unsigned)W && (unsigned)Y < (unsigned)H;
+        const float wgt = ((Y == y0) ? s : fy) * ((X == x0) ? ea : fx);
+        const unsigned key = inside ? ((unsigned)Y << 16) | (unsigned)X : 0xFFFFFFFFu;
+        if (key != skey[sl]) {
+          flush(sl);
+          skey[sl] = key;
+          scoef[sl] = 0.f;
         }
+        if (inside) scoef[sl] = fmaf(wgt, g, scoef[sl]);
       }
+    }
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) {
+      flush(sl);
+      skey[sl] = 0xFFFFFFFFu;
     }
   }
 #pragma unroll
