@@ -176,6 +176,54 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_kernel(
   }
 }
 
+// Few (a, b) pairs (conv0: 8 x 1, prob: 1 x 8): voxel-parallel instead -- thread t takes voxels
+// t, t+256, ... of the block's range straight from global memory and accumulates all A*BC pairs, then
+// a fixed LDS tree per pair.
+template <int A, int BC>
+__global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_small_kernel(
+    const float* __restrict__ direct, const float* __restrict__ gath, int B, int Pd, int Ph, int Pw, int Gd, int Gh,
+    int Gw, int stride, long vpb, float* __restrict__ partial) {
+  constexpr int NPR = A * BC;
+  __shared__ float red[NPR][kTrainBlock];
+  const int k = blockIdx.y;
+  const int kd = k / 9, kh = (k / 3) % 3, kw = k % 3;
+  const long nvox = (long)B * Pd * Ph * Pw;
+  const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
+  float acc[NPR];
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) acc[q] = 0.f;
+  for (long v = v0 + threadIdx.x; v < v1; v += kTrainBlock) {
+    const int pw = (int)(v % Pw);
+    long t = v / Pw;
+    const int ph = (int)(t % Ph);
+    t /= Ph;
+    const int pd = (int)(t % Pd);
+    const int b = (int)(t / Pd);
+    const int gd = pd * stride - 1 + kd, gh = ph * stride - 1 + kh, gw = pw * stride - 1 + kw;
+    if (gd < 0 || gh < 0 || gw < 0 || gd >= Gd || gh >= Gh || gw >= Gw) continue;
+    const float* gp = gath + ((((size_t)b * Gd + gd) * Gh + gh) * Gw + gw) * BC;
+    float dv[A], gv[BC];
+#pragma unroll
+    for (int a = 0; a < A; ++a) dv[a] = direct[v * A + a];
+#pragma unroll
+    for (int c = 0; c < BC; ++c) gv[c] = gp[c];
+#pragma unroll
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+      for (int c = 0; c < BC; ++c) acc[a * BC + c] = fmaf(dv[a], gv[c], acc[a * BC + c]);
+  }
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) red[q][threadIdx.x] = acc[q];
+  __syncthreads();
+  for (int st = kTrainBlock / 2; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st)
+#pragma unroll
+      for (int q = 0; q < NPR; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + st];
+    __syncthreads();
+  }
+  if ((int)threadIdx.x < NPR) partial[((size_t)blockIdx.x * 27 + k) * NPR + threadIdx.x] = red[threadIdx.x][0];
+}
+
 // dw[i] = sum_j partial[j][i], j = 0..nblk-1 in order (fp64 accumulation)
 __global__ __launch_bounds__(kTrainBlock) void sum_partials_kernel(const float* __restrict__ partial, int nblk, long n,
                                                                    float* __restrict__ out) {
@@ -194,15 +242,25 @@ __global__ __launch_bounds__(kTrainBlock) void bn_stats_partial_kernel(const flo
   __shared__ double red[2][kTrainBlock];
   const int c = threadIdx.x % C, r0 = threadIdx.x / C, rs = kTrainBlock / C;
   const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
-  double s = 0.0, q = 0.0;
-#pragma unroll 8
-  for (long v = v0 + r0; v < v1; v += rs) {
-    const double x = (double)z[v * C + c];
-    s += x;
-    q += x * x;
+  double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};  // 4 independent chains
+  long v = v0 + r0;
+  for (; v + 3L * rs < v1; v += 4L * rs) {
+    float x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = z[(v + (long)j * rs) * C + c];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s[j] += (double)x[j];
+      q[j] += (double)x[j] * (double)x[j];
+    }
   }
-  red[0][threadIdx.x] = s;
-  red[1][threadIdx.x] = q;
+  for (; v < v1; v += rs) {
+    const double x = (double)z[v * C + c];
+    s[0] += x;
+    q[0] += x * x;
+  }
+  red[0][threadIdx.x] = (s[0] + s[1]) + (s[2] + s[3]);
+  red[1][threadIdx.x] = (q[0] + q[1]) + (q[2] + q[3]);
   __syncthreads();
   if (threadIdx.x < C) {
     double ts = 0.0, tq = 0.0;
@@ -215,18 +273,30 @@ __global__ __launch_bounds__(kTrainBlock) void bn_stats_partial_kernel(const flo
   }
 }
 
-// mean, biased var (fp32) from the partials, fixed order
-__global__ void bn_stats_combine_kernel(const double* __restrict__ partial, int nblk, int C, long nvox,
-                                        float* __restrict__ mean, float* __restrict__ var) {
+// out[k] = sum_j partial[j][k] (K values per block row): block k, threads stride j, then a fixed
+// LDS tree -- deterministic, and parallel over the (up to 4096) partial rows
+__global__ __launch_bounds__(kTrainBlock) void sum_double_partials_kernel(const double* __restrict__ partial, int nblk,
+                                                                          int K, double* __restrict__ out) {
+  __shared__ double red[kTrainBlock];
+  const int k = blockIdx.x;
+  double a = 0.0;
+  for (int j = threadIdx.x; j < nblk; j += kTrainBlock) a += partial[(size_t)j * K + k];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int st = kTrainBlock / 2; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[k] = red[0];
+}
+
+// mean, biased var (fp32) from the summed (sum z, sum z^2)
+__global__ void bn_stats_finalize_kernel(const double* __restrict__ sums, int C, long nvox, float* __restrict__ mean,
+                                         float* __restrict__ var) {
   const int c = threadIdx.x;
   if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int j = 0; j < nblk; ++j) {
-    s += partial[((size_t)j * 2 + 0) * C + c];
-    q += partial[((size_t)j * 2 + 1) * C + c];
-  }
-  const double m = s / (double)nvox;
-  double v = q / (double)nvox - m * m;
+  const double m = sums[c] / (double)nvox;
+  const double v = sums[C + c] / (double)nvox - m * m;
   mean[c] = (float)m;
   var[c] = (float)(v > 0.0 ? v : 0.0);
 }
@@ -265,16 +335,30 @@ __global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_partial_kernel(
   bn_affine(mean[c], var[c], gamma[c], beta[c], eps, al, sh);
   const float m = mean[c], rstd = 1.f / sqrtf(var[c] + eps);
   const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
-  double sg = 0.0, sgx = 0.0;
-#pragma unroll 8
-  for (long v = v0 + r0; v < v1; v += rs) {
+  double sg[4] = {0.0, 0.0, 0.0, 0.0}, sgx[4] = {0.0, 0.0, 0.0, 0.0};
+  long v = v0 + r0;
+  for (; v + 3L * rs < v1; v += 4L * rs) {
+    float zz[4], gg[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      zz[j] = z[(v + (long)j * rs) * C + c];
+      gg[j] = dy[(v + (long)j * rs) * C + c];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float g = fmaf(zz[j], al, sh) > 0.f ? gg[j] : 0.f;
+      sg[j] += (double)g;
+      sgx[j] += (double)g * (double)((zz[j] - m) * rstd);
+    }
+  }
+  for (; v < v1; v += rs) {
     const float zz = z[v * C + c];
     const float g = fmaf(zz, al, sh) > 0.f ? dy[v * C + c] : 0.f;
-    sg += (double)g;
-    sgx += (double)g * (double)((zz - m) * rstd);
+    sg[0] += (double)g;
+    sgx[0] += (double)g * (double)((zz - m) * rstd);
   }
-  red[0][threadIdx.x] = sg;
-  red[1][threadIdx.x] = sgx;
+  red[0][threadIdx.x] = (sg[0] + sg[1]) + (sg[2] + sg[3]);
+  red[1][threadIdx.x] = (sgx[0] + sgx[1]) + (sgx[2] + sgx[3]);
   __syncthreads();
   if (threadIdx.x < C) {
     double a = 0.0, b = 0.0;
@@ -287,21 +371,13 @@ __global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_partial_kernel(
   }
 }
 
-// combine: dbeta = sum g, dgamma = sum g*xhat (fp32 out), and the fp64 sums for pass 2
-__global__ void bn_relu_bwd_combine_kernel(const double* __restrict__ partial, int nblk, int C,
-                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                           double* __restrict__ sums) {
+// dbeta = sum g, dgamma = sum g*xhat (fp32) from the summed partials
+__global__ void bn_relu_bwd_finalize_kernel(const double* __restrict__ sums, int C, float* __restrict__ dgamma,
+                                            float* __restrict__ dbeta) {
   const int c = threadIdx.x;
   if (c >= C) return;
-  double a = 0.0, b = 0.0;
-  for (int j = 0; j < nblk; ++j) {
-    a += partial[((size_t)j * 2 + 0) * C + c];
-    b += partial[((size_t)j * 2 + 1) * C + c];
-  }
-  dbeta[c] = (float)a;
-  dgamma[c] = (float)b;
-  sums[c] = a;
-  sums[C + c] = b;
+  dbeta[c] = (float)sums[c];
+  dgamma[c] = (float)sums[C + c];
 }
 
 // pass 2: dz = gamma*rstd/N * (N*g - sum g - xhat * sum g*xhat)
@@ -347,8 +423,12 @@ static int launch_wgrad(const float* direct, const float* gath, int B, int Pd, i
   const long nvox = (long)B * Pd * Ph * Pw;
   const long vpb = wgrad_vpb(nvox);
   const int nblk = (int)((nvox + vpb - 1) / vpb);
-  hipLaunchKernelGGL((conv3d_wgrad_kernel<A, BC>), dim3(nblk, 27), dim3(kTrainBlock), 0, st, direct, gath, B, Pd, Ph,
-                     Pw, Gd, Gh, Gw, stride, vpb, ws);
+  if constexpr (A * BC <= 16)
+    hipLaunchKernelGGL((conv3d_wgrad_small_kernel<A, BC>), dim3(nblk, 27), dim3(kTrainBlock), 0, st, direct, gath, B,
+                       Pd, Ph, Pw, Gd, Gh, Gw, stride, vpb, ws);
+  else
+    hipLaunchKernelGGL((conv3d_wgrad_kernel<A, BC>), dim3(nblk, 27), dim3(kTrainBlock), 0, st, direct, gath, B, Pd,
+                       Ph, Pw, Gd, Gh, Gw, stride, vpb, ws);
   TMVS_CHECK_LAUNCH();
   const long n = 27L * A * BC;
   hipLaunchKernelGGL(sum_partials_kernel, dim3((unsigned)((n + kTrainBlock - 1) / kTrainBlock)), dim3(kTrainBlock), 0,
@@ -360,8 +440,8 @@ static int launch_wgrad(const float* direct, const float* gath, int B, int Pd, i
 static bool valid_ch(int c) { return c == 1 || c == 8 || c == 16 || c == 32 || c == 64; }
 
 static long bn_vpb(long nvox) {
-  long vpb = 4096;
-  while ((nvox + vpb - 1) / vpb > 1024) vpb *= 2;
+  long vpb = 1024;
+  while ((nvox + vpb - 1) / vpb > 4096) vpb *= 2;
   return vpb;
 }
 
@@ -444,8 +524,12 @@ extern "C" int tmvs_bn_stats(const float* z, long nvox, int channels, void* work
   double* part = (double*)workspace;
   hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(nblk), dim3(kTrainBlock), 0, st, z, nvox, channels, vpb, part);
   TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_stats_combine_kernel, dim3(1), dim3(64), 0, st, (const double*)part, nblk, channels, nvox,
-                     mean, var);
+  double* sums = part + (size_t)nblk * 2 * channels;
+  hipLaunchKernelGGL(sum_double_partials_kernel, dim3(2 * channels), dim3(kTrainBlock), 0, st, (const double*)part,
+                     nblk, 2 * channels, sums);
+  TMVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(1), dim3(64), 0, st, (const double*)sums, channels, nvox, mean,
+                     var);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -477,8 +561,11 @@ extern "C" int tmvs_bn_relu_backward(const float* dy, const float* z, long nvox,
   hipLaunchKernelGGL(bn_relu_bwd_partial_kernel, dim3(nblk), dim3(kTrainBlock), 0, st, dy, z, nvox, channels, mean, var,
                      gamma, beta, eps, vpb, part);
   TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_relu_bwd_combine_kernel, dim3(1), dim3(64), 0, st, (const double*)part, nblk, channels, dgamma,
-                     dbeta, sums);
+  hipLaunchKernelGGL(sum_double_partials_kernel, dim3(2 * channels), dim3(kTrainBlock), 0, st, (const double*)part,
+                     nblk, 2 * channels, sums);
+  TMVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_relu_bwd_finalize_kernel, dim3(1), dim3(64), 0, st, (const double*)sums, channels, dgamma,
+                     dbeta);
   TMVS_CHECK_LAUNCH();
   const long n = nvox * channels;
   hipLaunchKernelGGL(bn_relu_bwd_apply_kernel, dim3((unsigned)((n + kTrainBlock - 1) / kTrainBlock)), dim3(kTrainBlock),
