@@ -119,7 +119,7 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_generic_kernel(
 template <int A, int BC>
 __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_kernel(
     const float* __restrict__ direct, const float* __restrict__ gath, int B, int Pd, int Ph, int Pw, int Gd, int Gh,
-    int Gw, int stride, long vpb, float* __restrict__ partial) {
+    int Gw, int stride, long vpb, double* __restrict__ partial) {
   constexpr int NP = (A * BC + kTrainBlock - 1) / kTrainBlock;
   constexpr int CH = 32;
   __shared__ __attribute__((aligned(16))) float sd[CH][A];
@@ -128,9 +128,9 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_kernel(
   const int kd = k / 9, kh = (k / 3) % 3, kw = k % 3;
   const long nvox = (long)B * Pd * Ph * Pw;
   const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
-  float acc[NP];
+  double acc[NP];  // a 32-voxel chunk sums in fp32, chunks in fp64 (BN-normalised gradients cancel)
 #pragma unroll
-  for (int j = 0; j < NP; ++j) acc[j] = 0.f;
+  for (int j = 0; j < NP; ++j) acc[j] = 0.0;
 #pragma unroll 1
   for (long vb = v0; vb < v1; vb += CH) {
     __syncthreads();
@@ -162,10 +162,10 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_kernel(
       const int q = threadIdx.x + j * kTrainBlock;
       if (q < A * BC) {
         const int a = q / BC, c = q % BC;
-        float s = acc[j];
+        float s = 0.f;
 #pragma unroll 8
         for (int r = 0; r < CH; ++r) s = fmaf(sd[r][a], sg[r][c], s);
-        acc[j] = s;
+        acc[j] += (double)s;
       }
     }
   }
@@ -182,16 +182,16 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_kernel(
 template <int A, int BC>
 __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_small_kernel(
     const float* __restrict__ direct, const float* __restrict__ gath, int B, int Pd, int Ph, int Pw, int Gd, int Gh,
-    int Gw, int stride, long vpb, float* __restrict__ partial) {
+    int Gw, int stride, long vpb, double* __restrict__ partial) {
   constexpr int NPR = A * BC;
-  __shared__ float red[NPR][kTrainBlock];
+  __shared__ double red[NPR][kTrainBlock];
   const int k = blockIdx.y;
   const int kd = k / 9, kh = (k / 3) % 3, kw = k % 3;
   const long nvox = (long)B * Pd * Ph * Pw;
   const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
-  float acc[NPR];
+  double acc[NPR];
 #pragma unroll
-  for (int q = 0; q < NPR; ++q) acc[q] = 0.f;
+  for (int q = 0; q < NPR; ++q) acc[q] = 0.0;
   for (long v = v0 + threadIdx.x; v < v1; v += kTrainBlock) {
     const int pw = (int)(v % Pw);
     long t = v / Pw;
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_small_kernel(
 #pragma unroll
     for (int a = 0; a < A; ++a)
 #pragma unroll
-      for (int c = 0; c < BC; ++c) acc[a * BC + c] = fmaf(dv[a], gv[c], acc[a * BC + c]);
+      for (int c = 0; c < BC; ++c) acc[a * BC + c] += (double)(dv[a] * gv[c]);
   }
 #pragma unroll
   for (int q = 0; q < NPR; ++q) red[q][threadIdx.x] = acc[q];
@@ -225,12 +225,12 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_small_kernel(
 }
 
 // dw[i] = sum_j partial[j][i], j = 0..nblk-1 in order (fp64 accumulation)
-__global__ __launch_bounds__(kTrainBlock) void sum_partials_kernel(const float* __restrict__ partial, int nblk, long n,
+__global__ __launch_bounds__(kTrainBlock) void sum_partials_kernel(const double* __restrict__ partial, int nblk, long n,
                                                                    float* __restrict__ out) {
   const long i = (long)blockIdx.x * kTrainBlock + threadIdx.x;
   if (i >= n) return;
   double s = 0.0;
-  for (int j = 0; j < nblk; ++j) s += (double)partial[(size_t)j * n + i];
+  for (int j = 0; j < nblk; ++j) s += partial[(size_t)j * n + i];
   out[i] = (float)s;
 }
 
@@ -419,7 +419,7 @@ static long wgrad_vpb(long nvox) {
 
 template <int A, int BC>
 static int launch_wgrad(const float* direct, const float* gath, int B, int Pd, int Ph, int Pw, int Gd, int Gh, int Gw,
-                        int stride, float* ws, float* dw, hipStream_t st) {
+                        int stride, double* ws, float* dw, hipStream_t st) {
   const long nvox = (long)B * Pd * Ph * Pw;
   const long vpb = wgrad_vpb(nvox);
   const int nblk = (int)((nvox + vpb - 1) / vpb);
@@ -485,7 +485,7 @@ extern "C" int tmvs_conv3d_generic(const float* x, int batch, int cin, int d_in,
 extern "C" size_t tmvs_conv3d_wgrad_workspace(int batch, int d, int h, int w, int a_ch, int b_ch) {
   const long nvox = (long)batch * d * h * w;
   const long vpb = wgrad_vpb(nvox);
-  return (size_t)((nvox + vpb - 1) / vpb) * 27 * a_ch * b_ch * sizeof(float);
+  return (size_t)((nvox + vpb - 1) / vpb) * 27 * a_ch * b_ch * sizeof(double);
 }
 
 extern "C" int tmvs_conv3d_wgrad(const float* direct, int a_ch, int batch, int pd, int ph, int pw, const float* gathered,
@@ -497,7 +497,7 @@ extern "C" int tmvs_conv3d_wgrad(const float* direct, int a_ch, int batch, int p
   if (stride != 1 && stride != 2) return TMVS_ERR_SHAPE;
   if (workspace_bytes < tmvs_conv3d_wgrad_workspace(batch, pd, ph, pw, a_ch, b_ch)) return TMVS_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  float* ws = (float*)workspace;
+  double* ws = (double*)workspace;
 #define TMVS_WG(AA, BB)                                                                                             \
   if (a_ch == AA && b_ch == BB)                                                                                     \
     return launch_wgrad<AA, BB>(direct, gathered, batch, pd, ph, pw, gd, gh, gw, stride, ws, dw, st);
