@@ -230,7 +230,10 @@ __device__ __forceinline__ void load_token_frag(const float* __restrict__ row, f
 }
 
 constexpr int kTilesPerWave = 8;  // 16-token tiles per wave (kv): amortises the weight-fragment loads
-constexpr int kApplyTilesPerWave = 4;  // apply: weights come from LDS; more, shorter waves
+#ifndef TMVS_APPLY_TPW
+#define TMVS_APPLY_TPW 4
+#endif
+constexpr int kApplyTilesPerWave = TMVS_APPLY_TPW;  // apply: weights come from LDS; more, shorter waves
 constexpr int kKvTilesPerWave = 8;     // kv: at most this many tiles per wave (see kv_tiles_per_wave)
 
 // (KV, Ksum) partial sums: per wave, tiles of 16 source tokens; K, V by MFMA; per lane the
