@@ -1,10 +1,15 @@
 """HIP path vs the CPU oracle / golden vectors (needs an MI355X; run with -m gpu).
 
-Tolerances (fp32 throughout; stated per check):
-  * cost volume similarity, PixelwiseNet view weights, pathway features: 2e-5 abs
-    (same op order as the reference except the channel-sum order of the correlation mean)
+Tolerances (fp32 throughout; stated per check, each with the deviation measured on the MI355X in
+profiles/r05n/pytest_parity.log):
+  * homo_warping seam: bit-exact (same op order, the fixtures' host rounding pinned)
+  * cost volume similarity, PixelwiseNet view weights: 5e-7 abs (measured <= 1.5e-7: the channel-
+    sum order of the correlation mean is the only difference, a few ulps)
+  * pathway features: 3e-6 (measured 9.5e-7); FMT EncoderLayer tokens: 2e-6 (measured 7.2e-7;
+    LayerNorm'd, O(1) values)
   * CostRegNet logits: 2e-5 relative to the volume's max |logit| (MFMA k-order vs mkldnn order)
-  * probabilities: 1e-5 abs;  FMT tokens: 1e-4 abs (LayerNorm'd, O(1) values)
+  * probabilities: 1e-5 abs for a softmax of given logits; 2e-4 end to end (measured 8.4e-5: the
+    sharpened logits, up to ~700, carry the CostRegNet deviation into the softmax)
   * hypotheses of the stage glue: bit-exact (same fp32 op sequence)
   * depth: identical argmax except at near-ties (top-2 log-prob margin < 1e-4),
     and mean |Δdepth| <= 1e-4 mm (the north-star bar)
@@ -38,6 +43,13 @@ def _nhwc(t):
     return t.permute(0, 2, 3, 1).contiguous()
 
 
+def _close(got, ref, atol, what):
+    """assert max |got - ref| <= atol, printing the measured deviation (GPU logs keep the numbers)."""
+    err = float(np.abs(np.asarray(got, np.float64) - np.asarray(ref, np.float64)).max())
+    print(f"{what}: max abs err {err:.2e} (bound {atol:.0e})")
+    assert err <= atol, (what, err, atol)
+
+
 def test_library_loads_on_gpu():
     from transmvsnet_amd import _lib
     assert _lib.load().tmvs_abi_version() == _lib.ABI_VERSION
@@ -50,7 +62,7 @@ def test_homo_warping_seam():
     out = ops.homo_warping(torch.from_numpy(g["warp_src"]).to(DEV), oracle.compose_proj(p[:, 1]),
                            oracle.compose_proj(p[:, 0]), torch.from_numpy(g["warp_hyp"]).to(DEV),
                            rot_order=GOLDEN_ROT_ORDER)
-    np.testing.assert_allclose(to_np(out), g["warp_out"], rtol=0, atol=2e-5)
+    _close(to_np(out), g["warp_out"], 0.0, "homo_warping seam vs golden")
 
 
 @pytest.mark.parametrize("c,d", [(8, 8), (16, 32), (32, 48)])
@@ -66,8 +78,8 @@ def test_warp_corr_stage1_mode(sd, c, d):
     nh = [_nhwc(f).to(DEV) for f in feats]
     src = torch.stack([x[0] for x in nh[1:]], 0).unsqueeze(0).contiguous()
     sim, _, vw = ops.warp_corr(nh[0], src, ops.proj_rows(proj), hyp.to(DEV), pw_params=_pw_params(sd))
-    np.testing.assert_allclose(to_np(sim)[:, None], to_np(sim_ref), rtol=0, atol=2e-5)
-    np.testing.assert_allclose(to_np(vw), to_np(vw_ref), rtol=0, atol=2e-5)
+    _close(to_np(sim)[:, None], to_np(sim_ref), 5e-7, f"stage1-mode sim c{c} d{d}")
+    _close(to_np(vw), to_np(vw_ref), 5e-7, f"stage1-mode view weights c{c} d{d}")
 
 
 @pytest.mark.parametrize("c,d,stage1", [(32, 48, True), (16, 32, False), (8, 8, False)])
@@ -84,19 +96,20 @@ def test_warp_corr_ten_source_views(sd, c, d, stage1):
     if stage1:
         sim_ref, vw_ref = oracle.build_cost_volume(sd, feats, proj, hyp)
         sim, _, vw = ops.warp_corr(nh[0], src, rows, hyp.to(DEV), pw_params=_pw_params(sd))
-        np.testing.assert_allclose(to_np(vw), to_np(vw_ref), rtol=0, atol=2e-5)
+        _close(to_np(vw), to_np(vw_ref), 5e-7, f"N=11 view weights c{c}")
     else:
         vw = torch.rand(1, n - 1, h, w)
         sim_ref, _ = oracle.build_cost_volume({}, feats, proj, hyp, view_weights=vw)
         sim, _, _ = ops.warp_corr(nh[0], src, rows, hyp.to(DEV), view_w_in=vw.to(DEV), vw_shift=0)
-    np.testing.assert_allclose(to_np(sim)[:, None], to_np(sim_ref), rtol=0, atol=2e-5)
+    _close(to_np(sim)[:, None], to_np(sim_ref), 5e-7, f"N=11 sim c{c}")
 
 
 @pytest.mark.parametrize("given", [False, True])
 def test_warp_corr_dtu_stage1_size(sd, given):
     """Fused cost volume at the DTU stage-1 size (216x288, C=32, D=48, 4 src views) with the
     forward's uniform fronto-parallel planes, against the oracle. 3M outputs: the channel-sum order
-    leaves 5 of them between 2e-5 and 2.7e-5 in given-weight mode, hence 3e-5 here."""
+    left 5 of them between 2e-5 and 2.7e-5 in round 1, before the host-BLAS rounding of the sample
+    coordinates was reproduced; now within 1.1e-7."""
     torch.manual_seed(7)
     n, h, w, c, d = 5, 216, 288, 32, 48
     feats = [torch.randn(1, c, h, w) for _ in range(n)]
@@ -113,8 +126,8 @@ def test_warp_corr_dtu_stage1_size(sd, given):
     else:
         sim_ref, vw_ref = oracle.build_cost_volume(sd, feats, proj, hyp)
         sim, _, vw_out = ops.warp_corr(nh[0], src, rows, hyp.to(DEV), pw_params=_pw_params(sd))
-        np.testing.assert_allclose(to_np(vw_out), to_np(vw_ref), rtol=0, atol=2e-5)
-    np.testing.assert_allclose(to_np(sim)[:, None], to_np(sim_ref), rtol=0, atol=3e-5)
+        _close(to_np(vw_out), to_np(vw_ref), 5e-7, "DTU stage-1 view weights")
+    _close(to_np(sim)[:, None], to_np(sim_ref), 5e-7, f"DTU stage-1 sim (given={given})")
 
 
 def test_warp_corr_incoherent_depth_and_degenerate_planes(sd):
@@ -131,8 +144,8 @@ def test_warp_corr_incoherent_depth_and_degenerate_planes(sd):
     src = torch.stack([x[0] for x in nh[1:]], 0).unsqueeze(0).contiguous()
     sim_ref, vw_ref = oracle.build_cost_volume(sd, feats, proj, hyp)
     sim, _, vw = ops.warp_corr(nh[0], src, ops.proj_rows(proj), hyp.to(DEV), pw_params=_pw_params(sd))
-    np.testing.assert_allclose(to_np(sim)[:, None], to_np(sim_ref), rtol=0, atol=2e-5)
-    np.testing.assert_allclose(to_np(vw), to_np(vw_ref), rtol=0, atol=2e-5)
+    _close(to_np(sim)[:, None], to_np(sim_ref), 5e-7, "incoherent sim")
+    _close(to_np(vw), to_np(vw_ref), 5e-7, "incoherent view weights")
 
 
 def test_e2e_eleven_views_tnt_aspect(sd):
@@ -177,7 +190,7 @@ def test_warp_corr_given_weights_and_partial(shift):
     src = torch.stack([x[0] for x in nh[1:]], 0).unsqueeze(0).contiguous()
     rows = ops.proj_rows(proj)
     sim, _, _ = ops.warp_corr(nh[0], src, rows, hyp.to(DEV), view_w_in=vw.to(DEV), vw_shift=shift)
-    np.testing.assert_allclose(to_np(sim)[:, None], to_np(sim_ref), rtol=0, atol=2e-5)
+    _close(to_np(sim)[:, None], to_np(sim_ref), 5e-7, f"given weights shift{shift}")
     # view-sharded form: two partial sums (views 0-1 and 2-3) + finalize == unsharded
     s_a, w_a, _ = ops.warp_corr(nh[0], src[:, :2].contiguous(), rows[:, :2], hyp.to(DEV), view_w_in=vw.to(DEV),
                                 vw_shift=shift, vw_offset=0, vw_total=4, partial=True)
@@ -259,7 +272,7 @@ def test_fmt_encoder_layer(model):
     src = torch.from_numpy(g["enc_src"]).to(DEV).contiguous()
     kv = ops.fmt_kv(src, enc)
     ops.fmt_apply(x, kv, enc)
-    np.testing.assert_allclose(to_np(x), g["enc_out"], rtol=0, atol=1e-4)
+    _close(to_np(x), g["enc_out"], 2e-6, "EncoderLayer vs golden")
 
 
 def test_fmt_pathway(sd, model):
@@ -270,7 +283,7 @@ def test_fmt_pathway(sd, model):
                                  mode="bilinear") + lat, sd["FMT_with_pathway.smooth_1.weight"], padding=1)
     prep = model._prepared(torch.device(DEV))
     out = ops.fmt_pathway(coarse.permute(0, 2, 3, 1).contiguous().to(DEV), lat.to(DEV), prep["red1"], prep["sm1"])
-    np.testing.assert_allclose(to_np(out), ref.permute(0, 2, 3, 1).numpy(), rtol=0, atol=2e-5)
+    _close(to_np(out), ref.permute(0, 2, 3, 1).numpy(), 3e-6, "pathway")
 
 
 def _e2e_check(out, vw, g, stages=(1, 2, 3)):
@@ -288,7 +301,7 @@ def _e2e_check(out, vw, g, stages=(1, 2, 3)):
         report[f"l1_{s}"] = mean_l1
     assert report["l1_3"] <= 1e-4, report
     if vw is not None:
-        np.testing.assert_allclose(to_np(vw), g["view_weights"], rtol=0, atol=1e-4)
+        _close(to_np(vw), g["view_weights"], 5e-7, "e2e view weights vs golden")
     return report
 
 
@@ -301,7 +314,7 @@ def test_e2e_c1_features(model):
                                          synthetic.synthetic_depth_values(1).to(DEV), (H, W), return_view_weights=True)
     rep = _e2e_check(out, vw, g)
     for s in (1, 2, 3):
-        np.testing.assert_allclose(to_np(out[f"stage{s}"]["prob_volume"]), g[f"stage{s}_prob"], rtol=0, atol=1e-3)
+        _close(to_np(out[f"stage{s}"]["prob_volume"]), g[f"stage{s}_prob"], 2e-4, f"e2e C1 prob stage{s}")
     print("e2e c1", rep)
 
 
