@@ -255,6 +255,32 @@ int tmvs_warp_corr_backward(const float* ref_fea, const float* src_fea, const fl
                             const float* dsim, int n_src, int channels, int ndepth, int height, int width, int flags,
                             void* workspace, size_t workspace_bytes, float* dref, float* dsrc, void* stream);
 
+/* DepthNet view aggregation + stage-1 PixelwiseNet in train mode (TransMVSNet.py:10-30, 71-93),
+ * one sample, per-view similarity volumes sims [V][D][H][W] (tmvs_warp_corr per view):
+ *   pwp [201] (device): w0[16] gamma0[16] beta0[16] W1[8][16] gamma1[8] beta1[8] w2[8] b2.
+ *   tmvs_pixelwise_train_forward: per view, BatchNorm batch statistics (stats [V][48]: mean0[16]
+ *     var0[16] mean1[8] var1[8], biased) and the view weight view_w [V][H][W] = max over D of the
+ *     sigmoid output, with its first argmax dstar [V][H][W] (int32).
+ *   tmvs_aggregate_train: sim [D][H][W] = sum_v sims_v w_v / (1e-5 + sum_v w_v) (views in order),
+ *     wsum [H][W]; view_w read at (y >> vw_shift, x >> vw_shift) of [V][H>>s][W>>s].
+ *   tmvs_aggregate_train_backward: dsims = dsim / wsum * w_v, and (dview_w non-NULL)
+ *     dview_w = sum_d dsim / wsum * (sims_v - sim).
+ *   tmvs_pixelwise_train_backward: adds the PixelwiseNet path to dsims and its parameter gradients
+ *     to dpwp [201] (accumulated: zero it first).
+ * All reductions: fp64 block partials + fixed-order combines (deterministic).                  */
+size_t tmvs_pixelwise_train_workspace(void);
+int tmvs_pixelwise_train_forward(const float* sims, int n_views, int ndepth, int height, int width, const float* pwp,
+                                 void* workspace, size_t workspace_bytes, float* stats, float* view_w, int* dstar,
+                                 void* stream);
+int tmvs_aggregate_train(const float* sims, const float* view_w, int n_views, int ndepth, int height, int width,
+                         int vw_shift, float* sim, float* wsum, void* stream);
+int tmvs_aggregate_train_backward(const float* dsim, const float* sims, const float* sim, const float* wsum,
+                                  const float* view_w, int n_views, int ndepth, int height, int width, int vw_shift,
+                                  float* dsims, float* dview_w, void* stream);
+int tmvs_pixelwise_train_backward(const float* sims, int n_views, int ndepth, int height, int width, const float* pwp,
+                                  const float* stats, const float* view_w, const int* dstar, const float* dview_w,
+                                  void* workspace, size_t workspace_bytes, float* dsims, float* dpwp, void* stream);
+
 /* BatchNorm3d in train mode over z [nvox][C] (C divides 256): batch mean and biased variance
  * (fp64 partials, fixed-order combine); y = relu(fmaf(z, a, b)) [+ skip] with a = gamma /
  * sqrt(var + eps), b = beta - mean * a; the backward of that (incl. the ReLU mask) gives dz,

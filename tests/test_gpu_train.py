@@ -185,3 +185,59 @@ def test_depth_stages_training_step():
     rep["worst_grad"] = worst
     print(rep)
     assert worst[0] < 1e-3, rep
+
+
+@pytest.mark.parametrize("stage", [1, 2])
+def test_aggregate_and_pixelwise_train(stage):
+    """View aggregation + (stage 1) train-mode PixelwiseNet on csrc/pw_train.hip against torch autograd
+    through the oracle's build_cost_volume pieces (pixelwise_net with batch statistics, the view-ordered
+    weighted mean), C5 stage-1 size (48 x 144 x 192, 3 source views) / stage-2 size with given weights:
+    sim, view weights, d sims, every PixelwiseNet gradient (1e-4 of max magnitude), running stats."""
+    import torch.nn.functional as F
+    from transmvsnet_amd import TransMVSNet
+    from transmvsnet_amd.train import aggregate_train
+    sd = golden_state_dict()
+    model = TransMVSNet()
+    model.load_state_dict(sd, strict=True)
+    model = model.to(DEV)
+    v, d, h, w = (3, 48, 144, 192) if stage == 1 else (3, 32, 288, 384)
+    g = torch.Generator().manual_seed(31 + stage)
+    sims = (torch.randn(v, d, h, w, generator=g) * 0.3).contiguous()
+    dsim = torch.randn(d, h, w, generator=g)
+    vw_small = torch.rand(v, h // 2, w // 2, generator=g) if stage == 2 else None
+    sg = sims.to(DEV).requires_grad_()
+    sim, vw = aggregate_train(sg, model, None if stage == 1 else vw_small.to(DEV), 0 if stage == 1 else 1)
+    sim.backward(dsim.to(DEV))
+    torch.cuda.synchronize()
+    P = "DepthNet.pixel_wise_net."
+    rsd = {k: (t.clone().requires_grad_() if t.is_floating_point() and "running" not in k else t.clone())
+           for k, t in sd.items() if k.startswith(P)}
+    sc = sims.clone().requires_grad_()
+    sim_sum, w_sum, vws = 0, 1e-5, []
+    for i in range(v):
+        s_v = sc[i][None, None]
+        if stage == 1:
+            vw_i = oracle.pixelwise_net(rsd, s_v, training=True)[:, 0]
+        else:
+            vw_i = F.interpolate(vw_small[i][None, None], scale_factor=2, mode="nearest")[0]
+        vws.append(vw_i)
+        sim_sum = sim_sum + s_v[0] * vw_i.unsqueeze(1)
+        w_sum = w_sum + vw_i.unsqueeze(1)
+    ref = (sim_sum / w_sum)[0]
+    ref.backward(dsim)
+    rep = {"sim": _rel(sim, ref), "dsims": _rel(sg.grad, sc.grad)}
+    if stage == 1:
+        rep["view_w"] = _rel(vw, torch.cat(vws, 0))
+        pw = model.DepthNet.pixel_wise_net
+        for name, t in (("conv0.conv.weight", pw.conv0.conv.weight), ("conv0.bn.weight", pw.conv0.bn.weight),
+                        ("conv0.bn.bias", pw.conv0.bn.bias), ("conv1.conv.weight", pw.conv1.conv.weight),
+                        ("conv1.bn.weight", pw.conv1.bn.weight), ("conv1.bn.bias", pw.conv1.bn.bias),
+                        ("conv2.weight", pw.conv2.weight), ("conv2.bias", pw.conv2.bias)):
+            rep[name] = _rel(t.grad, rsd[P + name].grad)
+        for name, t in (("conv0.bn.running_mean", pw.conv0.bn.running_mean),
+                        ("conv0.bn.running_var", pw.conv0.bn.running_var),
+                        ("conv1.bn.running_mean", pw.conv1.bn.running_mean),
+                        ("conv1.bn.running_var", pw.conv1.bn.running_var)):
+            rep[name] = _rel(t, rsd[P + name])
+    print(stage, rep)
+    assert all(val < 1e-4 for val in rep.values()), rep

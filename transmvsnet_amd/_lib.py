@@ -55,6 +55,11 @@ SIGNATURES = {
     "tmvs_depth_metrics": (I, [P, P, P, I, F, P, S, P, P]),
     "tmvs_warp_corr_backward_workspace": (S, [I, I, I, I]),
     "tmvs_warp_corr_backward": (I, [P, P, P, P, P, I, I, I, I, I, I, P, S, P, P, P]),
+    "tmvs_pixelwise_train_workspace": (S, []),
+    "tmvs_pixelwise_train_forward": (I, [P, I, I, I, I, P, P, S, P, P, P, P]),
+    "tmvs_aggregate_train": (I, [P, P, I, I, I, I, I, P, P, P]),
+    "tmvs_aggregate_train_backward": (I, [P, P, P, P, P, I, I, I, I, I, P, P, P]),
+    "tmvs_pixelwise_train_backward": (I, [P, I, I, I, I, P, P, P, P, P, P, S, P, P, P]),
     "tmvs_conv3d_generic": (I, [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P]),
     "tmvs_conv3d_wgrad_workspace": (S, [I, I, I, I, I, I]),
     "tmvs_conv3d_wgrad": (I, [P, I, I, I, I, I, P, I, I, I, I, I, P, S, P, P]),

@@ -642,6 +642,66 @@ def warp_corr_backward(ref_nhwc, src_nhwc, proj12, hyp, dsim, rot_order="auto"):
     return dref, dsrc, flag
 
 
-for _name in ("conv3d_generic", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn_relu_backward", "warp_corr_backward"):
+def pixelwise_train_forward(sims, pwp):
+    """tmvs_pixelwise_train_forward: sims [V,D,H,W], pwp [201] -> (stats [V,48], view_w [V,H,W], dstar int32)."""
+    _dev(sims, "sims")
+    _dev(pwp, "pwp")
+    v, d, h, w = sims.shape
+    ws = torch.empty(_lib_h().tmvs_pixelwise_train_workspace() // 4 + 64, device=sims.device)
+    stats = torch.empty(v, 48, device=sims.device)
+    vw = torch.empty(v, h, w, device=sims.device)
+    dstar = torch.empty(v, h, w, device=sims.device, dtype=torch.int32)
+    with _Span("tmvs_pixelwise_train_forward"):
+        _lib.check(_lib_h().tmvs_pixelwise_train_forward(_ptr(sims), v, d, h, w, _ptr(pwp), _ptr(ws), ws.numel() * 4,
+                                                         _ptr(stats), _ptr(vw), _ptr(dstar), _stream()),
+                   "tmvs_pixelwise_train_forward")
+    return stats, vw, dstar
+
+
+def aggregate_train(sims, view_w, vw_shift):
+    """tmvs_aggregate_train: sims [V,D,H,W], view_w [V,H>>s,W>>s] -> (sim [D,H,W], wsum [H,W])."""
+    _dev(sims, "sims")
+    _dev(view_w, "view_w")
+    v, d, h, w = sims.shape
+    sim = torch.empty(d, h, w, device=sims.device)
+    wsum = torch.empty(h, w, device=sims.device)
+    with _Span("tmvs_aggregate_train"):
+        _lib.check(_lib_h().tmvs_aggregate_train(_ptr(sims), _ptr(view_w), v, d, h, w, vw_shift, _ptr(sim), _ptr(wsum),
+                                                 _stream()), "tmvs_aggregate_train")
+    return sim, wsum
+
+
+def aggregate_train_backward(dsim, sims, sim, wsum, view_w, vw_shift, want_dview_w):
+    """tmvs_aggregate_train_backward -> (dsims [V,D,H,W], dview_w [V,H,W] or None)."""
+    for t, n in ((dsim, "dsim"), (sims, "sims"), (sim, "sim"), (wsum, "wsum"), (view_w, "view_w")):
+        _dev(t, n)
+    v, d, h, w = sims.shape
+    dsims = torch.empty_like(sims)
+    dvw = torch.empty(v, h, w, device=sims.device) if want_dview_w else None
+    with _Span("tmvs_aggregate_train_backward"):
+        _lib.check(_lib_h().tmvs_aggregate_train_backward(_ptr(dsim), _ptr(sims), _ptr(sim), _ptr(wsum), _ptr(view_w), v,
+                                                          d, h, w, vw_shift, _ptr(dsims), _ptr(dvw), _stream()),
+                   "tmvs_aggregate_train_backward")
+    return dsims, dvw
+
+
+def pixelwise_train_backward(sims, pwp, stats, view_w, dstar, dview_w, dsims):
+    """tmvs_pixelwise_train_backward: adds the PixelwiseNet path into dsims (in place) -> dpwp [201]."""
+    for t, n in ((sims, "sims"), (pwp, "pwp"), (stats, "stats"), (view_w, "view_w"), (dview_w, "dview_w"),
+                 (dsims, "dsims")):
+        _dev(t, n)
+    v, d, h, w = sims.shape
+    ws = torch.empty(_lib_h().tmvs_pixelwise_train_workspace() // 4 + 64, device=sims.device)
+    dpwp = torch.zeros(201, device=sims.device)
+    with _Span("tmvs_pixelwise_train_backward"):
+        _lib.check(_lib_h().tmvs_pixelwise_train_backward(_ptr(sims), v, d, h, w, _ptr(pwp), _ptr(stats), _ptr(view_w),
+                                                          _ptr(dstar), _ptr(dview_w), _ptr(ws), ws.numel() * 4,
+                                                          _ptr(dsims), _ptr(dpwp), _stream()),
+                   "tmvs_pixelwise_train_backward")
+    return dpwp
+
+
+for _name in ("conv3d_generic", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn_relu_backward", "warp_corr_backward",
+              "pixelwise_train_forward", "aggregate_train", "aggregate_train_backward", "pixelwise_train_backward"):
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name

@@ -9,9 +9,10 @@
 * ``depth_stages_train``: the three DepthNet stages of a training step (models/TransMVSNet.py:38-109,
   174-221) from the FMT/pathway features to trans_mvsnet_loss (module.py:532-556) and its backward:
   hypotheses (tmvs_stage_hypotheses), per-view cost volumes (above), the view aggregation and the
-  stage-1 PixelwiseNet in train mode (torch), CostRegNet (above), softmax/WTA (tmvs_softmax_wta) and
-  the loss with d loss / d logits (tmvs_entropy_loss); gradients reach the stage features, the
-  CostRegNet and PixelwiseNet parameters.
+  stage-1 PixelwiseNet in train mode (``aggregate_train``: csrc/pw_train.hip), CostRegNet (above),
+  softmax/WTA (tmvs_softmax_wta) and the loss with d loss / d logits (tmvs_entropy_loss); gradients
+  reach the stage features, the CostRegNet and PixelwiseNet parameters. Torch only packs
+  parameters and sums gradients that meet.
 
 ``costregnet_train(module, x)`` is CostRegNet.forward (models/module.py:447-456) of a
 ``transmvsnet_amd.model.CostRegNet`` whose BatchNorm3d layers run in train mode, as in the
@@ -204,25 +205,62 @@ def costregnet_train(module, x):
     return logits
 
 
-def pixelwise_net_train(pw, sim_v):
-    """PixelwiseNet.forward (models/TransMVSNet.py:20-30) in train mode on one view's similarity volume
-    sim_v [D, H, W] -> view weight [H, W]: 1x1x1 convs 1->16->8 (BatchNorm3d with batch statistics,
-    running statistics updated), ->1 (+bias), sigmoid, max over D. Channels-last torch ops."""
-    x = sim_v.unsqueeze(-1) * pw.conv0.conv.weight.reshape(1, 1, 1, -1)            # [D,H,W,16]
-    x = F.relu(_bn_last(x, pw.conv0.bn))
-    x = torch.matmul(x, pw.conv1.conv.weight.reshape(8, 16).t())                       # [D,H,W,8]
-    x = F.relu(_bn_last(x, pw.conv1.bn))
-    x = torch.matmul(x, pw.conv2.weight.reshape(1, 8).t()).squeeze(-1) + pw.conv2.bias  # [D,H,W]
-    return torch.sigmoid(x).max(dim=0)[0]
+class _AggregateTrain(torch.autograd.Function):
+    """View aggregation (TransMVSNet.py:71-93) with, at stage 1, the train-mode PixelwiseNet weights
+    (TransMVSNet.py:10-30), forward and backward on csrc/pw_train.hip. Outputs (sim [D,H,W], the
+    view weights used [V,H',W'], non-differentiable as the reference returns them detached)."""
+
+    @staticmethod
+    def forward(ctx, sims, pwp, vw_given, vw_shift, stats_out):
+        sims = sims.contiguous()
+        if vw_given is None:
+            stats, vw, dstar = ops.pixelwise_train_forward(sims, pwp.detach().contiguous())
+            stats_out.append(stats)
+            ctx.pw = (stats, dstar)
+        else:
+            vw = vw_given.contiguous()
+            ctx.pw = None
+        sim, wsum = ops.aggregate_train(sims, vw, vw_shift)
+        ctx.vw_shift = vw_shift
+        ctx.save_for_backward(sims, sim, wsum, vw, pwp)
+        ctx.mark_non_differentiable(vw)
+        return sim, vw
+
+    @staticmethod
+    def backward(ctx, dsim, _dvw):
+        sims, sim, wsum, vw, pwp = ctx.saved_tensors
+        stage1 = ctx.pw is not None
+        dsims, dvw = ops.aggregate_train_backward(dsim.contiguous(), sims, sim, wsum, vw, ctx.vw_shift, stage1)
+        dpwp = None
+        if stage1:
+            stats, dstar = ctx.pw
+            dpwp = ops.pixelwise_train_backward(sims, pwp.detach().contiguous(), stats, vw, dstar, dvw, dsims)
+        return dsims, dpwp, None, None, None
 
 
-def _bn_last(x, bn):
-    c = x.shape[-1]
-    y = F.batch_norm(x.reshape(1, -1, c).permute(0, 2, 1), bn.running_mean, bn.running_var, bn.weight, bn.bias,
-                     True, bn.momentum, bn.eps)
-    if bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
-    return y.permute(0, 2, 1).reshape(x.shape)
+def _pw_params(pw):
+    """The 201-float device parameter block of tmvs_pixelwise_train_* (differentiable torch.cat)."""
+    return torch.cat([pw.conv0.conv.weight.reshape(16), pw.conv0.bn.weight, pw.conv0.bn.bias,
+                      pw.conv1.conv.weight.reshape(128), pw.conv1.bn.weight, pw.conv1.bn.bias,
+                      pw.conv2.weight.reshape(8), pw.conv2.bias.reshape(1)]).float()
+
+
+def aggregate_train(sims, model, vw_given=None, vw_shift=0):
+    """DepthNet's view aggregation for training; at stage 1 (vw_given None) the view weights come
+    from PixelwiseNet in train mode, whose BatchNorm running statistics are updated once per view
+    (the reference calls it per view). Returns (sim [D,H,W], view weights)."""
+    pw = model.DepthNet.pixel_wise_net
+    stats = []
+    sim, vw = _AggregateTrain.apply(sims, _pw_params(pw), vw_given, vw_shift, stats)
+    if stats:
+        n = sims.shape[1] * sims.shape[2] * sims.shape[3]
+        with torch.no_grad():
+            for st in stats[0]:  # views in order
+                for bn, m, v in ((pw.conv0.bn, st[0:16], st[16:32]), (pw.conv1.bn, st[32:40], st[40:48])):
+                    bn.running_mean.mul_(1.0 - bn.momentum).add_(m, alpha=bn.momentum)
+                    bn.running_var.mul_(1.0 - bn.momentum).add_(v * (n / max(n - 1, 1)), alpha=bn.momentum)
+                    bn.num_batches_tracked.add_(1)
+    return sim, vw
 
 
 def depth_stages_train(model, stage_features, proj_matrix, depth_values, depth_gt_ms, mask_ms, img_hw,
@@ -249,19 +287,10 @@ def depth_stages_train(model, stage_features, proj_matrix, depth_values, depth_g
                                        STAGE_SCALES[s])
             rows = ops.proj_rows(proj_matrix[name])[0]
             sims = warp_corr_views(f[0], f[1:], hyp[0], rows, rot_order=model.warp_rot_order)  # [V,D,h,w]
-            if s == 0:
-                vws = [pixelwise_net_train(model.DepthNet.pixel_wise_net, sims[v]) for v in range(sims.shape[0])]
-                vw_det = torch.stack(vws).detach()  # TransMVSNet.py:107 returns view_weights.detach()
-            else:
-                up = vw_det
-                for _ in range(s):
-                    up = F.interpolate(up[None], scale_factor=2, mode="nearest")[0]
-                vws = list(up)
-            sim_sum, w_sum = 0, 1e-5
-            for v in range(sims.shape[0]):  # TransMVSNet.py:88-93, view order
-                sim_sum = sim_sum + sims[v] * vws[v].unsqueeze(0)
-                w_sum = w_sum + vws[v].unsqueeze(0)
-            sim = sim_sum / w_sum
+            if s == 0:  # TransMVSNet.py:107 returns the stage-1 view weights detached
+                sim, vw_det = aggregate_train(sims, model)
+            else:       # nearest x2 per stage (:194) = reading the stage-1 map at (y >> s, x >> s)
+                sim, _ = aggregate_train(sims, model, vw_det, s)
             logits = costregnet_train(model.cost_regularization[s].train(), sim.unsqueeze(0))
             prob, depth, raw, conf = ops.softmax_wta(logits.detach(), hyp, DEPTH_CLAMP)
             outputs[name] = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}
