@@ -389,9 +389,10 @@ def train_timing(steps, dev, world):
     return {"ms_per_sample": round(ms, 3), "samples_per_s": round(world * 1e3 / ms, 3), "ranks": world,
             "grad_allreduce_bytes": nbytes if world > 1 else 0,
             "workload": "BlendedMVS 768x576, N=4, 48/32/8, 1 sample per rank: DepthNet stages forward + backward "
-                        "(HIP: hypotheses, per-view cost volumes + backward, CostRegNet train fwd/bwd, softmax/WTA, "
-                        "trans_mvsnet_loss + d/dlogits; torch: view aggregation, PixelwiseNet) + DDP gradient "
-                        "all-reduce; FMT / pathway / FeatureNet backward not included (not native yet)"}
+                        "on HIP (hypotheses, per-view cost volumes + backward, view aggregation + train-mode "
+                        "PixelwiseNet + backward, CostRegNet train fwd/bwd, softmax/WTA, trans_mvsnet_loss + "
+                        "d/dlogits) + DDP gradient all-reduce; FMT / pathway / FeatureNet backward not included "
+                        "(not native yet)"}
 
 
 def host_cores():

@@ -190,9 +190,12 @@ def test_depth_stages_training_step():
 @pytest.mark.parametrize("stage", [1, 2])
 def test_aggregate_and_pixelwise_train(stage):
     """View aggregation + (stage 1) train-mode PixelwiseNet on csrc/pw_train.hip against torch autograd
-    through the oracle's build_cost_volume pieces (pixelwise_net with batch statistics, the view-ordered
-    weighted mean), C5 stage-1 size (48 x 144 x 192, 3 source views) / stage-2 size with given weights:
-    sim, view weights, d sims, every PixelwiseNet gradient (1e-4 of max magnitude), running stats."""
+    through the oracle's pieces (pixelwise_net with batch statistics, the view-ordered weighted mean),
+    C5 stage-1 size (48 x 144 x 192, 3 source views) / stage-2 size with given weights. The reference
+    runs in fp32 and fp64: sim, view weights, d sims within 1e-4 of the fp32 reference; PixelwiseNet
+    gradients within max(1e-4, 2 x the fp32 reference's own error) of fp64 (the BatchNorm backward
+    sums cancel: conv0.conv.weight's gradient exists only through BatchNorm's eps, since BN removes
+    the scale of a single-input 1x1 conv -- the fp32 reference gets it badly wrong, see the log)."""
     import torch.nn.functional as F
     from transmvsnet_amd import TransMVSNet
     from transmvsnet_amd.train import aggregate_train
@@ -210,34 +213,44 @@ def test_aggregate_and_pixelwise_train(stage):
     sim.backward(dsim.to(DEV))
     torch.cuda.synchronize()
     P = "DepthNet.pixel_wise_net."
-    rsd = {k: (t.clone().requires_grad_() if t.is_floating_point() and "running" not in k else t.clone())
-           for k, t in sd.items() if k.startswith(P)}
-    sc = sims.clone().requires_grad_()
-    sim_sum, w_sum, vws = 0, 1e-5, []
-    for i in range(v):
-        s_v = sc[i][None, None]
-        if stage == 1:
-            vw_i = oracle.pixelwise_net(rsd, s_v, training=True)[:, 0]
-        else:
-            vw_i = F.interpolate(vw_small[i][None, None], scale_factor=2, mode="nearest")[0]
-        vws.append(vw_i)
-        sim_sum = sim_sum + s_v[0] * vw_i.unsqueeze(1)
-        w_sum = w_sum + vw_i.unsqueeze(1)
-    ref = (sim_sum / w_sum)[0]
-    ref.backward(dsim)
-    rep = {"sim": _rel(sim, ref), "dsims": _rel(sg.grad, sc.grad)}
+    refs = {}
+    for dt in (torch.float32, torch.float64):
+        rsd = {k: (t.to(dt).clone().requires_grad_() if t.is_floating_point() and "running" not in k
+                   else (t.to(dt).clone() if t.is_floating_point() else t.clone())) for k, t in sd.items()
+               if k.startswith(P)}
+        sc = sims.to(dt).clone().requires_grad_()
+        sim_sum, w_sum, vws = 0, 1e-5, []
+        for i in range(v):
+            s_v = sc[i][None, None]
+            if stage == 1:
+                vw_i = oracle.pixelwise_net(rsd, s_v, training=True)[:, 0]
+            else:
+                vw_i = F.interpolate(vw_small.to(dt)[i][None, None], scale_factor=2, mode="nearest")[0]
+            vws.append(vw_i)
+            sim_sum = sim_sum + s_v[0] * vw_i.unsqueeze(1)
+            w_sum = w_sum + vw_i.unsqueeze(1)
+        ref = (sim_sum / w_sum)[0]
+        ref.backward(dsim.to(dt))
+        refs[dt] = (ref, sc.grad, torch.cat(vws, 0), rsd)
+    ref, ref_ds, ref_vw, rsd = refs[torch.float32]
+    ex, ex_ds, ex_vw, esd = refs[torch.float64]
+    rep = {"sim": _rel(sim, ref), "dsims": _rel(sg.grad, ref_ds)}
+    assert rep["sim"] < 1e-4 and rep["dsims"] < 1e-4, rep
     if stage == 1:
-        rep["view_w"] = _rel(vw, torch.cat(vws, 0))
+        rep["view_w"] = _rel(vw, ref_vw)
+        assert rep["view_w"] < 1e-4, rep
         pw = model.DepthNet.pixel_wise_net
-        for name, t in (("conv0.conv.weight", pw.conv0.conv.weight), ("conv0.bn.weight", pw.conv0.bn.weight),
-                        ("conv0.bn.bias", pw.conv0.bn.bias), ("conv1.conv.weight", pw.conv1.conv.weight),
-                        ("conv1.bn.weight", pw.conv1.bn.weight), ("conv1.bn.bias", pw.conv1.bn.bias),
-                        ("conv2.weight", pw.conv2.weight), ("conv2.bias", pw.conv2.bias)):
-            rep[name] = _rel(t.grad, rsd[P + name].grad)
+        grads = {"conv0.conv.weight": pw.conv0.conv.weight, "conv0.bn.weight": pw.conv0.bn.weight, "conv0.bn.bias": pw.conv0.bn.bias,
+                 "conv1.conv.weight": pw.conv1.conv.weight, "conv1.bn.weight": pw.conv1.bn.weight,
+                 "conv1.bn.bias": pw.conv1.bn.bias, "conv2.weight": pw.conv2.weight, "conv2.bias": pw.conv2.bias}
+        for name, t in grads.items():
+            e_gpu, e_ref = _rel(t.grad, esd[P + name].grad), _rel(rsd[P + name].grad, esd[P + name].grad)
+            rep[name] = (e_gpu, e_ref)
+            assert e_gpu <= max(1e-4, 2.0 * e_ref), (name, rep)
         for name, t in (("conv0.bn.running_mean", pw.conv0.bn.running_mean),
                         ("conv0.bn.running_var", pw.conv0.bn.running_var),
                         ("conv1.bn.running_mean", pw.conv1.bn.running_mean),
                         ("conv1.bn.running_var", pw.conv1.bn.running_var)):
             rep[name] = _rel(t, rsd[P + name])
+            assert rep[name] < 1e-5, rep
     print(stage, rep)
-    assert all(val < 1e-4 for val in rep.values()), rep
