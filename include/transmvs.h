@@ -281,6 +281,16 @@ int tmvs_pixelwise_train_backward(const float* sims, int n_views, int ndepth, in
                                   const float* stats, const float* view_w, const int* dstar, const float* dview_w,
                                   void* workspace, size_t workspace_bytes, float* dsims, float* dpwp, void* stream);
 
+/* FMT_with_pathway lateral step for training (FMT.py:201-209, 221-228), NHWC, C in {8, 16}:
+ *   tmvs_upsample2_add_nhwc: u [n][2h][2w][C] = bilinear x2 (align_corners=False) of r [n][h][w][C]
+ *     + lateral [n][C][2h][2w] (NCHW);  tmvs_upsample2_backward_nhwc: dr [n][h][w][C] = the adjoint
+ *     of the interpolation applied to du [n][2h][2w][C] (gather, deterministic).
+ * The 1x1 reduction and the 3x3 smoothing run on tmvs_conv3d_generic / tmvs_conv3d_wgrad with
+ * depth 1 (kd = 1 taps).                                                                       */
+int tmvs_upsample2_add_nhwc(const float* r, const float* lateral, int n, int h, int w, int channels, float* u,
+                            void* stream);
+int tmvs_upsample2_backward_nhwc(const float* du, int n, int h, int w, int channels, float* dr, void* stream);
+
 /* BatchNorm3d in train mode over z [nvox][C] (C divides 256): batch mean and biased variance
  * (fp64 partials, fixed-order combine); y = relu(fmaf(z, a, b)) [+ skip] with a = gamma /
  * sqrt(var + eps), b = beta - mean * a; the backward of that (incl. the ReLU mask) gives dz,

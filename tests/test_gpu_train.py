@@ -254,3 +254,49 @@ def test_aggregate_and_pixelwise_train(stage):
             rep[name] = _rel(t, rsd[P + name])
             assert rep[name] < 1e-5, rep
     print(stage, rep)
+
+
+def test_pathway_train_forward_backward():
+    """FMT_with_pathway's lateral steps (models/FMT.py:201-209, 221-228) with their backward, C5 sizes
+    (stage-1 FMT output 144x192x32, N=4 views), against torch autograd through the same ops on the CPU
+    (fp32): stage-2/3 features, d FMT output, d FeatureNet stage-2/3 features, the four conv weight
+    gradients -- 1e-4 of each quantity's max magnitude (the weight gradients sum ~1e5-1e6 terms)."""
+    import torch.nn.functional as F
+    from transmvsnet_amd import TransMVSNet
+    from transmvsnet_amd.train import pathway_train
+    sd = golden_state_dict()
+    model = TransMVSNet()
+    model.load_state_dict(sd, strict=True)
+    model = model.to(DEV)
+    n, h, w = 4, 144, 192
+    g = torch.Generator().manual_seed(41)
+    s1 = torch.randn(n, 32, h, w, generator=g)
+    s2 = torch.randn(n, 16, 2 * h, 2 * w, generator=g)
+    s3 = torch.randn(n, 8, 4 * h, 4 * w, generator=g)
+    d2 = torch.randn(n, 16, 2 * h, 2 * w, generator=g)
+    d3 = torch.randn(n, 8, 4 * h, 4 * w, generator=g)
+    a1 = s1.permute(0, 2, 3, 1).contiguous().to(DEV).requires_grad_()
+    a2, a3 = s2.to(DEV).requires_grad_(), s3.to(DEV).requires_grad_()
+    o2, o3 = pathway_train(model, a1, a2, a3)
+    torch.autograd.backward([o2, o3], [d2.permute(0, 2, 3, 1).contiguous().to(DEV),
+                                       d3.permute(0, 2, 3, 1).contiguous().to(DEV)])
+    torch.cuda.synchronize()
+    P = "FMT_with_pathway."
+    W = {k: sd[P + k].clone().requires_grad_() for k in ("dim_reduction_1.weight", "smooth_1.weight",
+                                                         "dim_reduction_2.weight", "smooth_2.weight")}
+    c1, c2, c3 = s1.clone().requires_grad_(), s2.clone().requires_grad_(), s3.clone().requires_grad_()
+    r2 = F.conv2d(F.interpolate(F.conv2d(c1, W["dim_reduction_1.weight"]), size=(2 * h, 2 * w), mode="bilinear") + c2,
+                  W["smooth_1.weight"], padding=1)
+    r3 = F.conv2d(F.interpolate(F.conv2d(r2, W["dim_reduction_2.weight"]), size=(4 * h, 4 * w), mode="bilinear") + c3,
+                  W["smooth_2.weight"], padding=1)
+    torch.autograd.backward([r2, r3], [d2, d3])
+    fp = model.FMT_with_pathway
+    rep = {"stage2": _rel(o2.permute(0, 3, 1, 2), r2), "stage3": _rel(o3.permute(0, 3, 1, 2), r3),
+           "d_fmt_out": _rel(a1.grad.permute(0, 3, 1, 2), c1.grad), "d_stage2": _rel(a2.grad, c2.grad),
+           "d_stage3": _rel(a3.grad, c3.grad),
+           "dim_reduction_1": _rel(fp.dim_reduction_1.weight.grad, W["dim_reduction_1.weight"].grad),
+           "smooth_1": _rel(fp.smooth_1.weight.grad, W["smooth_1.weight"].grad),
+           "dim_reduction_2": _rel(fp.dim_reduction_2.weight.grad, W["dim_reduction_2.weight"].grad),
+           "smooth_2": _rel(fp.smooth_2.weight.grad, W["smooth_2.weight"].grad)}
+    print(rep)
+    assert all(v < 1e-4 for v in rep.values()), rep

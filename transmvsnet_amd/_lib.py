@@ -60,6 +60,8 @@ SIGNATURES = {
     "tmvs_aggregate_train": (I, [P, P, I, I, I, I, I, P, P, P]),
     "tmvs_aggregate_train_backward": (I, [P, P, P, P, P, I, I, I, I, I, P, P, P]),
     "tmvs_pixelwise_train_backward": (I, [P, I, I, I, I, P, P, P, P, P, P, S, P, P, P]),
+    "tmvs_upsample2_add_nhwc": (I, [P, P, I, I, I, I, P, P]),
+    "tmvs_upsample2_backward_nhwc": (I, [P, I, I, I, I, P, P]),
     "tmvs_conv3d_generic": (I, [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P]),
     "tmvs_conv3d_wgrad_workspace": (S, [I, I, I, I, I, I]),
     "tmvs_conv3d_wgrad": (I, [P, I, I, I, I, I, P, I, I, I, I, I, P, S, P, P]),

@@ -503,7 +503,7 @@ extern "C" int tmvs_conv3d_wgrad(const float* direct, int a_ch, int batch, int p
     return launch_wgrad<AA, BB>(direct, gathered, batch, pd, ph, pw, gd, gh, gw, stride, ws, dw, st);
   // (direct, gathered) channel pairs of CostRegNet's layers: conv (dz, x) and deconv (x, dz)
   TMVS_WG(8, 1) TMVS_WG(16, 8) TMVS_WG(16, 16) TMVS_WG(32, 16) TMVS_WG(32, 32) TMVS_WG(64, 32) TMVS_WG(64, 64)
-  TMVS_WG(1, 8) TMVS_WG(8, 16) TMVS_WG(16, 32) TMVS_WG(32, 64)
+  TMVS_WG(1, 8) TMVS_WG(8, 16) TMVS_WG(16, 32) TMVS_WG(32, 64) TMVS_WG(8, 8)
 #undef TMVS_WG
   return TMVS_ERR_SHAPE;
 }

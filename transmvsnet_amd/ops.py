@@ -701,7 +701,32 @@ def pixelwise_train_backward(sims, pwp, stats, view_w, dstar, dview_w, dsims):
     return dpwp
 
 
+def upsample2_add_nhwc(r, lateral_nchw):
+    """tmvs_upsample2_add_nhwc: r [N,h,w,C] -> bilinear x2 + lateral [N,C,2h,2w] -> [N,2h,2w,C]."""
+    _dev(r, "r")
+    _dev(lateral_nchw, "lateral")
+    n, h, w, c = r.shape
+    if tuple(lateral_nchw.shape) != (n, c, 2 * h, 2 * w):
+        raise ValueError("upsample2_add_nhwc: lateral must be [N, C, 2h, 2w]")
+    u = torch.empty(n, 2 * h, 2 * w, c, device=r.device)
+    with _Span("tmvs_upsample2_add_nhwc"):
+        _lib.check(_lib_h().tmvs_upsample2_add_nhwc(_ptr(r), _ptr(lateral_nchw), n, h, w, c, _ptr(u), _stream()),
+                   "tmvs_upsample2_add_nhwc")
+    return u
+
+
+def upsample2_backward_nhwc(du):
+    """tmvs_upsample2_backward_nhwc: du [N,2h,2w,C] -> dr [N,h,w,C]."""
+    _dev(du, "du")
+    n, hh, ww, c = du.shape
+    dr = torch.empty(n, hh // 2, ww // 2, c, device=du.device)
+    with _Span("tmvs_upsample2_backward_nhwc"):
+        _lib.check(_lib_h().tmvs_upsample2_backward_nhwc(_ptr(du), n, hh // 2, ww // 2, c, _ptr(dr), _stream()),
+                   "tmvs_upsample2_backward_nhwc")
+    return dr
+
+
 for _name in ("conv3d_generic", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn_relu_backward", "warp_corr_backward",
-              "pixelwise_train_forward", "aggregate_train", "aggregate_train_backward", "pixelwise_train_backward"):
+              "upsample2_add_nhwc", "upsample2_backward_nhwc", "pixelwise_train_forward", "aggregate_train", "aggregate_train_backward", "pixelwise_train_backward"):
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name
