@@ -300,3 +300,67 @@ def test_pathway_train_forward_backward():
            "smooth_2": _rel(fp.smooth_2.weight.grad, W["smooth_2.weight"].grad)}
     print(rep)
     assert all(v < 1e-4 for v in rep.values()), rep
+
+
+def test_training_step_from_fmt_output():
+    """The training step from the FMT output and FeatureNet's stage-2/3 features on: FMT_with_pathway's
+    lateral steps, then the three DepthNet stages and trans_mvsnet_loss (all HIP), against torch
+    autograd through the same chain on the CPU (128x160, N=3, 8/8/8): loss, d FMT output, d FeatureNet
+    stage-2/3 features, the pathway weight gradients (1e-3 of max magnitude)."""
+    import torch.nn.functional as F
+    from oracle import loss_ref
+    from transmvsnet_amd import TransMVSNet, synthetic
+    from transmvsnet_amd.train import depth_stages_train, pathway_train
+    H, W, N, ND = 128, 160, 3, (8, 8, 8)
+    sd = golden_state_dict()
+    model = TransMVSNet(ndepths=list(ND))
+    model.load_state_dict(sd, strict=True)
+    model = model.to(DEV)
+    g = torch.Generator().manual_seed(19)
+    s1 = torch.randn(N, 32, H // 4, W // 4, generator=g)
+    s2 = torch.randn(N, 16, H // 2, W // 2, generator=g)
+    s3 = torch.randn(N, 8, H, W, generator=g)
+    proj = synthetic.synthetic_cameras(N, H, W, seed=1)
+    dv = synthetic.synthetic_depth_values(1)
+    gt = {f"stage{s + 1}": 425.0 + 500.0 * torch.rand(1, H >> (2 - s), W >> (2 - s), generator=g) for s in range(3)}
+    mask = {k: (torch.rand(v.shape, generator=g) > 0.3).float() for k, v in gt.items()}
+    a1 = s1.permute(0, 2, 3, 1).contiguous().to(DEV).requires_grad_()
+    a2, a3 = s2.to(DEV).requires_grad_(), s3.to(DEV).requires_grad_()
+    st2, st3 = pathway_train(model, a1, a2, a3)
+    total, _ = depth_stages_train(model, {"stage1": a1, "stage2": st2, "stage3": st3}, proj, dv.to(DEV),
+                                  {k: v.to(DEV) for k, v in gt.items()}, {k: v.to(DEV) for k, v in mask.items()},
+                                  (H, W))
+    torch.cuda.synchronize()
+    rsd = {k: (v.clone().requires_grad_() if v.is_floating_point() and "running" not in k else v.clone())
+           for k, v in sd.items()}
+    c1, c2, c3 = s1.clone().requires_grad_(), s2.clone().requires_grad_(), s3.clone().requires_grad_()
+    P = "FMT_with_pathway."
+    r2 = F.conv2d(F.interpolate(F.conv2d(c1, rsd[P + "dim_reduction_1.weight"]), size=(H // 2, W // 2),
+                                mode="bilinear") + c2, rsd[P + "smooth_1.weight"], padding=1)
+    r3 = F.conv2d(F.interpolate(F.conv2d(r2, rsd[P + "dim_reduction_2.weight"]), size=(H, W), mode="bilinear") + c3,
+                  rsd[P + "smooth_2.weight"], padding=1)
+    feats = {"stage1": c1, "stage2": r2, "stage3": r3}
+    outputs, depth, vw = {}, None, None
+    for s in range(3):
+        name = f"stage{s + 1}"
+        hyp = oracle.stage_hypotheses(depth, dv, s, (H, W), ND)
+        if s > 0:
+            vw = F.interpolate(vw, scale_factor=2, mode="nearest")
+        sim, vw_new = oracle.build_cost_volume(rsd, [feats[name][i:i + 1] for i in range(N)], proj[name], hyp,
+                                               vw if s else None, training=True)
+        if s == 0:
+            vw = vw_new.detach()
+        logits = oracle.cost_reg_net(rsd, f"cost_regularization.{s}.", sim, training=True)[:, 0]
+        prob = torch.exp(F.log_softmax(logits, dim=1))
+        depth = torch.gather(hyp, 1, prob.argmax(1, keepdim=True)).squeeze(1)
+        outputs[name] = {"prob_volume": prob, "depth_values": hyp}
+    ref_total = loss_ref.trans_mvsnet_loss(outputs, gt, mask, dlossw=(0.5, 1.0, 2.0))[0]
+    ref_total.backward()
+    params = dict(model.named_parameters())
+    rep = {"loss": abs(float(total) - float(ref_total)) / abs(float(ref_total)),
+           "d_fmt_out": _rel(a1.grad.permute(0, 3, 1, 2), c1.grad), "d_stage2": _rel(a2.grad, c2.grad),
+           "d_stage3": _rel(a3.grad, c3.grad)}
+    for k in ("dim_reduction_1.weight", "smooth_1.weight", "dim_reduction_2.weight", "smooth_2.weight"):
+        rep[k] = _rel(params[P + k].grad, rsd[P + k].grad)
+    print(rep)
+    assert rep["loss"] < 1e-5 and all(v < 1e-3 for v in rep.values()), rep
