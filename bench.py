@@ -349,19 +349,19 @@ def end_to_end(model, steps, proj, dv_dev, dev):
 
 
 def train_timing(steps, dev, world):
-    """C5 training step (BlendedMVS 768x576, N=4, 48/32/8, one sample per rank) from the FMT output and
-    FeatureNet's stage-2/3 features (synthetic leaf tensors): FMT_with_pathway's lateral steps, the three
-    DepthNet stages and trans_mvsnet_loss, forward + backward (transmvsnet_amd.train.pathway_train +
-    depth_stages_train), plus DDP's gradient all-reduce when world > 1. HIP events, median of `steps`
-    after 1 warm-up; max over ranks."""
+    """C5 training step (BlendedMVS 768x576, N=4, 48/32/8, one sample per rank) from FeatureNet's
+    stage-1/2/3 features (synthetic leaf tensors): the FMT (8 encoder layers), FMT_with_pathway's
+    lateral steps, the three DepthNet stages and trans_mvsnet_loss, forward + backward
+    (transmvsnet_amd.train.fmt_train + pathway_train + depth_stages_train), plus DDP's gradient
+    all-reduce when world > 1. HIP events, median of `steps` after 1 warm-up; max over ranks."""
     from transmvsnet_amd import TransMVSNet, synthetic
-    from transmvsnet_amd.train import allreduce_gradients, depth_stages_train, pathway_train
+    from transmvsnet_amd.train import allreduce_gradients, depth_stages_train, fmt_train, pathway_train
     h5, w5, n5 = 576, 768, 4
     m = TransMVSNet()
     m.load_state_dict(synthetic.synthetic_state_dict(synthetic.state_dict_shapes(m), seed=0, sharpen=100.0))
     m = m.to(dev)
     feats = synthetic.stacked_features(n5, h5, w5, seed=5)
-    leaves = {"stage1": feats["stage1"][0].permute(0, 2, 3, 1).contiguous().to(dev).requires_grad_(),
+    leaves = {"stage1": feats["stage1"][0].contiguous().to(dev).requires_grad_(),
               "stage2": feats["stage2"][0].contiguous().to(dev).requires_grad_(),
               "stage3": feats["stage3"][0].contiguous().to(dev).requires_grad_()}
     proj = synthetic.synthetic_cameras(n5, h5, w5, seed=6)
@@ -371,15 +371,16 @@ def train_timing(steps, dev, world):
           for s in range(3)}
     mask = {k: torch.ones_like(v) for k, v in gt.items()}
     params = [p for n, p in m.named_parameters()
-              if n.startswith(("cost_regularization.", "DepthNet.", "FMT_with_pathway.")) and ".FMT." not in n]
+              if n.startswith(("cost_regularization.", "DepthNet.", "FMT_with_pathway."))]
     ts = []
     for i in range(steps + 1):
         for p in params + list(leaves.values()):
             p.grad = None
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        st2, st3 = pathway_train(m, leaves["stage1"], leaves["stage2"], leaves["stage3"])
-        depth_stages_train(m, {"stage1": leaves["stage1"], "stage2": st2, "stage3": st3}, proj, dv, gt, mask, (h5, w5))
+        st1 = fmt_train(m, leaves["stage1"])
+        st2, st3 = pathway_train(m, st1, leaves["stage2"], leaves["stage3"])
+        depth_stages_train(m, {"stage1": st1, "stage2": st2, "stage3": st3}, proj, dv, gt, mask, (h5, w5))
         allreduce_gradients(params)
         e1.record()
         torch.cuda.synchronize()
@@ -393,12 +394,13 @@ def train_timing(steps, dev, world):
     nbytes = sum(p.numel() for p in params) * 4
     return {"ms_per_sample": round(ms, 3), "samples_per_s": round(world * 1e3 / ms, 3), "ranks": world,
             "grad_allreduce_bytes": nbytes if world > 1 else 0,
-            "workload": "BlendedMVS 768x576, N=4, 48/32/8, 1 sample per rank: from the FMT output and FeatureNet "
-                        "stage-2/3 features, forward + backward on HIP of FMT_with_pathway's lateral steps and the "
+            "workload": "BlendedMVS 768x576, N=4, 48/32/8, 1 sample per rank: from FeatureNet's stage-1/2/3 "
+                        "features, forward + backward on HIP of the FMT (8 encoder layers), FMT_with_pathway's "
+                        "lateral steps and the "
                         "DepthNet stages (hypotheses, per-view cost volumes + backward, view aggregation + train-mode "
                         "PixelwiseNet + backward, CostRegNet train fwd/bwd, softmax/WTA, trans_mvsnet_loss + "
-                        "d/dlogits) + DDP gradient all-reduce; the FMT and FeatureNet backward are not included "
-                        "(not native yet)"}
+                        "d/dlogits) + DDP gradient all-reduce; FeatureNet's backward is not included (not native "
+                        "yet)"}
 
 
 def host_cores():

@@ -291,6 +291,38 @@ int tmvs_upsample2_add_nhwc(const float* r, const float* lateral, int n, int h, 
                             void* stream);
 int tmvs_upsample2_backward_nhwc(const float* du, int n, int h, int w, int channels, float* dr, void* stream);
 
+/* FMT EncoderLayer backward for training (FMT.py:96-111, 56-75, 22-37), tokens [T][C] fp32,
+ * C in {32, 64}; every cross-token sum is fp64 with a fixed combine order (no atomics).
+ *   tmvs_token_linear:   y = x W^T + b (W [out][in], torch Linear), or with transpose_w y = x W
+ *     (W [in'][out'] = the Linear's weight: the data gradient); relu_of (nullable, [T][out])
+ *     zeroes y where relu_of <= 0; accumulate adds into y. (in, out) in {(32,32), (32,64), (64,32)}.
+ *   tmvs_token_wgrad:    dw [a][b] = sum_t dy[t][a] x[t][b], db [a] = sum_t dy[t][a].
+ *   tmvs_layer_norm_fwd / _bwd: LayerNorm(32, eps 1e-5); the backward takes the LN input x,
+ *     gives dx and dgb = {dgamma[32], dbeta[32]} (statistics recomputed per token).
+ *   tmvs_linattn_fwd:    msg = linear attention of q (pre-elu) against kv [groups][TMVS_KV_NFLOATS]
+ *     (token t uses group t / tokens_per_group; kv_stride 0 shares one group).
+ *   tmvs_linattn_bwd_q:  dq through the elu and dkv [groups][TMVS_KV_NFLOATS] = dKV, dKsum summed
+ *     over each group's query tokens (tokens % tokens_per_group == 0).
+ *   tmvs_linattn_bwd_kv: dk (through the elu), dv of the source tokens from k (pre-elu), v, dkv. */
+int tmvs_token_linear(const float* x, long tokens, int in_features, int out_features, const float* w,
+                      const float* b, int transpose_w, const float* relu_of, int accumulate, float* y,
+                      void* stream);
+size_t tmvs_token_wgrad_workspace(long tokens, int a, int b);
+int tmvs_token_wgrad(const float* dy, int a, const float* x, int b, long tokens, void* workspace,
+                     size_t workspace_bytes, float* dw, float* db, int accumulate, void* stream);
+int tmvs_layer_norm_fwd(const float* x, long tokens, const float* g, const float* b, float* y, void* stream);
+size_t tmvs_layer_norm_bwd_workspace(long tokens);
+int tmvs_layer_norm_bwd(const float* dy, const float* x, long tokens, const float* g, void* workspace,
+                        size_t workspace_bytes, float* dx, float* dgb, int accumulate, void* stream);
+int tmvs_linattn_fwd(const float* q, long tokens, long tokens_per_group, const float* kv, long kv_stride,
+                     float* msg, void* stream);
+size_t tmvs_linattn_bwd_workspace(long tokens, long tokens_per_group);
+int tmvs_linattn_bwd_q(const float* q, const float* dmsg, long tokens, long tokens_per_group, const float* kv,
+                       long kv_stride, void* workspace, size_t workspace_bytes, float* dq, float* dkv,
+                       void* stream);
+int tmvs_linattn_bwd_kv(const float* k, const float* v, long tokens, long tokens_per_group, const float* dkv,
+                        float* dk, float* dv, void* stream);
+
 /* BatchNorm3d in train mode over z [nvox][C] (C divides 256): batch mean and biased variance
  * (fp64 partials, fixed-order combine); y = relu(fmaf(z, a, b)) [+ skip] with a = gamma /
  * sqrt(var + eps), b = beta - mean * a; the backward of that (incl. the ReLU mask) gives dz,

@@ -302,15 +302,17 @@ def test_pathway_train_forward_backward():
     assert all(v < 1e-4 for v in rep.values()), rep
 
 
-def test_training_step_from_fmt_output():
-    """The training step from the FMT output and FeatureNet's stage-2/3 features on: FMT_with_pathway's
-    lateral steps, then the three DepthNet stages and trans_mvsnet_loss (all HIP), against torch
-    autograd through the same chain on the CPU (128x160, N=3, 8/8/8): loss, d FMT output, d FeatureNet
-    stage-2/3 features, the pathway weight gradients (1e-3 of max magnitude)."""
+@pytest.mark.parametrize("with_fmt", [False, True])
+def test_training_step_from_fmt_output(with_fmt):
+    """The training step from the FMT output (with_fmt: from FeatureNet's stage-1 output, the FMT's 8
+    encoder layers included) and FeatureNet's stage-2/3 features on: FMT_with_pathway's lateral steps,
+    then the three DepthNet stages and trans_mvsnet_loss (all HIP), against torch autograd through the
+    same chain on the CPU (128x160, N=3, 8/8/8): loss, d stage-1 input, d FeatureNet stage-2/3
+    features, the pathway (and FMT) weight gradients (1e-3 of max magnitude)."""
     import torch.nn.functional as F
     from oracle import loss_ref
     from transmvsnet_amd import TransMVSNet, synthetic
-    from transmvsnet_amd.train import depth_stages_train, pathway_train
+    from transmvsnet_amd.train import depth_stages_train, fmt_train, pathway_train
     H, W, N, ND = 128, 160, 3, (8, 8, 8)
     sd = golden_state_dict()
     model = TransMVSNet(ndepths=list(ND))
@@ -324,10 +326,11 @@ def test_training_step_from_fmt_output():
     dv = synthetic.synthetic_depth_values(1)
     gt = {f"stage{s + 1}": 425.0 + 500.0 * torch.rand(1, H >> (2 - s), W >> (2 - s), generator=g) for s in range(3)}
     mask = {k: (torch.rand(v.shape, generator=g) > 0.3).float() for k, v in gt.items()}
-    a1 = s1.permute(0, 2, 3, 1).contiguous().to(DEV).requires_grad_()
+    a1 = (s1 if with_fmt else s1.permute(0, 2, 3, 1)).contiguous().to(DEV).requires_grad_()
     a2, a3 = s2.to(DEV).requires_grad_(), s3.to(DEV).requires_grad_()
-    st2, st3 = pathway_train(model, a1, a2, a3)
-    total, _ = depth_stages_train(model, {"stage1": a1, "stage2": st2, "stage3": st3}, proj, dv.to(DEV),
+    st1 = fmt_train(model, a1) if with_fmt else a1
+    st2, st3 = pathway_train(model, st1, a2, a3)
+    total, _ = depth_stages_train(model, {"stage1": st1, "stage2": st2, "stage3": st3}, proj, dv.to(DEV),
                                   {k: v.to(DEV) for k, v in gt.items()}, {k: v.to(DEV) for k, v in mask.items()},
                                   (H, W))
     torch.cuda.synchronize()
@@ -335,11 +338,15 @@ def test_training_step_from_fmt_output():
            for k, v in sd.items()}
     c1, c2, c3 = s1.clone().requires_grad_(), s2.clone().requires_grad_(), s3.clone().requires_grad_()
     P = "FMT_with_pathway."
-    r2 = F.conv2d(F.interpolate(F.conv2d(c1, rsd[P + "dim_reduction_1.weight"]), size=(H // 2, W // 2),
+    f1 = c1
+    if with_fmt:
+        ref_list = oracle.fmt_ref(rsd, c1[:1])
+        f1 = torch.cat([ref_list[-1]] + [oracle.fmt_src(rsd, ref_list, c1[i:i + 1]) for i in range(1, N)])
+    r2 = F.conv2d(F.interpolate(F.conv2d(f1, rsd[P + "dim_reduction_1.weight"]), size=(H // 2, W // 2),
                                 mode="bilinear") + c2, rsd[P + "smooth_1.weight"], padding=1)
     r3 = F.conv2d(F.interpolate(F.conv2d(r2, rsd[P + "dim_reduction_2.weight"]), size=(H, W), mode="bilinear") + c3,
                   rsd[P + "smooth_2.weight"], padding=1)
-    feats = {"stage1": c1, "stage2": r2, "stage3": r3}
+    feats = {"stage1": f1, "stage2": r2, "stage3": r3}
     outputs, depth, vw = {}, None, None
     for s in range(3):
         name = f"stage{s + 1}"
@@ -358,9 +365,105 @@ def test_training_step_from_fmt_output():
     ref_total.backward()
     params = dict(model.named_parameters())
     rep = {"loss": abs(float(total) - float(ref_total)) / abs(float(ref_total)),
-           "d_fmt_out": _rel(a1.grad.permute(0, 3, 1, 2), c1.grad), "d_stage2": _rel(a2.grad, c2.grad),
-           "d_stage3": _rel(a3.grad, c3.grad)}
+           "d_stage1_input": _rel(a1.grad if with_fmt else a1.grad.permute(0, 3, 1, 2), c1.grad),
+           "d_stage2": _rel(a2.grad, c2.grad), "d_stage3": _rel(a3.grad, c3.grad)}
     for k in ("dim_reduction_1.weight", "smooth_1.weight", "dim_reduction_2.weight", "smooth_2.weight"):
         rep[k] = _rel(params[P + k].grad, rsd[P + k].grad)
+    if with_fmt:
+        names = [n for n in params if ".FMT." in n]
+        rep["fmt_worst"] = max(_rel(params[n].grad, rsd[n].grad) for n in names)
     print(rep)
     assert rep["loss"] < 1e-5 and all(v < 1e-3 for v in rep.values()), rep
+
+
+def _fmt_ref_sd(sd, dt):
+    return {k: v.to(dt).clone().requires_grad_() for k, v in sd.items() if k.startswith("FMT_with_pathway.FMT.")}
+
+
+@pytest.mark.parametrize("self_attn,L", [(True, 320), (False, 320), (True, 27648), (False, 27648)])
+def test_encoder_layer_backward(self_attn, L):
+    """One EncoderLayer's backward on the HIP token kernels (models/FMT.py:96-111; 3 views x 320
+    tokens; a cross layer's queries are the 2 source views, its K/V the reference tokens) against
+    torch autograd through oracle.encoder_layer in fp64: dx, d source, all 16 parameter gradients
+    within max(1e-4, 2 x the fp32 reference's own error) of each quantity's max magnitude."""
+    from transmvsnet_amd.train import _ENC_PARAMS, _encoder_layer_backward, _pack_enc
+    sd = golden_state_dict()
+    i = 0 if self_attn else 1
+    P = f"FMT_with_pathway.FMT.layers.{i}."
+    g = torch.Generator().manual_seed(5 + i)
+    nv = 3
+    x = torch.randn(nv, L, 32, generator=g)
+    dy = torch.randn(nv, L, 32, generator=g)
+    refs = {}
+    for dt in (torch.float32, torch.float64):
+        rsd = _fmt_ref_sd(sd, dt)
+        xc = x.to(dt).clone().requires_grad_()
+        if self_attn:
+            out = oracle.encoder_layer(rsd, P, xc, xc)
+            out.backward(dy.to(dt))
+            refs[dt] = (out, xc.grad, None, rsd)
+        else:
+            out = oracle.encoder_layer(rsd, P, xc[1:], xc[:1].expand(nv - 1, L, 32))
+            out.backward(dy[1:].to(dt))
+            refs[dt] = (out, xc.grad[1:], xc.grad[0], rsd)
+    p = [sd[P + n].to(DEV).contiguous() for n in _ENC_PARAMS]
+    xd = x.to(DEV)
+    if self_attn:
+        dx, dsrc, grads = _encoder_layer_backward(p, _pack_enc(p), xd.view(-1, 32), xd.view(-1, 32),
+                                                  dy.to(DEV).view(-1, 32), L, L, True)
+    else:
+        dx, dsrc, grads = _encoder_layer_backward(p, _pack_enc(p), xd[1:].reshape(-1, 32), xd[0].contiguous(),
+                                                  dy[1:].to(DEV).reshape(-1, 32), (nv - 1) * L, L, False)
+    torch.cuda.synchronize()
+    (_, r_dx, r_ds, rsd32), (_, e_dx, e_ds, rsd64) = refs[torch.float32], refs[torch.float64]
+    checks = [("dx", dx.view_as(e_dx), r_dx, e_dx)]
+    if not self_attn:
+        checks.append(("dsrc", dsrc.view_as(e_ds), r_ds, e_ds))
+    checks += [(n, gr, rsd32[P + n].grad, rsd64[P + n].grad) for n, gr in zip(_ENC_PARAMS, grads)]
+    errs = [(n, _rel(got.reshape(r64.shape), r64), _rel(r32, r64)) for n, got, r32, r64 in checks]
+    print("self" if self_attn else "cross", L, [(n, f"{a:.1e}", f"{b:.1e}") for n, a, b in errs])
+    for n, e_gpu, e_ref in errs:
+        assert e_gpu <= max(1e-4, 2.0 * e_ref), (n, e_gpu, e_ref)
+
+
+@pytest.mark.parametrize("nv,h,w", [(3, 16, 20), (4, 144, 192)])
+def test_fmt_train_forward_backward(nv, h, w):
+    """The whole FMT for training (models/FMT.py:147-177: 4 self + 4 cross layers, reference view first)
+    at a small shape and the C5 stage-1 shape (BlendedMVS 768x576 -> 144x192, N=4): HIP forward against
+    the fp32 oracle (1e-4 of max magnitude), d stage-1 features and all 128 parameter gradients against
+    fp64 torch autograd through the oracle, within max(1e-4, 2 x the fp32 reference's own error, the
+    fp32 reference's worst error over all gradients) of each quantity's max magnitude."""
+    from transmvsnet_amd import TransMVSNet
+    from transmvsnet_amd.train import _ENC_PARAMS, fmt_params, fmt_train
+    sd = golden_state_dict()
+    model = TransMVSNet()
+    model.load_state_dict(sd, strict=True)
+    model = model.to(DEV)
+    g = torch.Generator().manual_seed(nv + h)
+    s1 = torch.randn(nv, 32, h, w, generator=g)
+    gout = torch.randn(nv, 32, h, w, generator=g)
+    a1 = s1.to(DEV).requires_grad_()
+    out = fmt_train(model, a1)
+    out.backward(gout.permute(0, 2, 3, 1).contiguous().to(DEV))
+    torch.cuda.synchronize()
+    refs = {}
+    for dt in (torch.float32, torch.float64):
+        rsd = _fmt_ref_sd(sd, dt)
+        xc = s1.to(dt).clone().requires_grad_()
+        ref_list = oracle.fmt_ref(rsd, xc[:1])
+        r = torch.cat([ref_list[-1]] + [oracle.fmt_src(rsd, ref_list, xc[i:i + 1]) for i in range(1, nv)])
+        r.backward(gout.to(dt))
+        refs[dt] = (r, xc.grad, rsd)
+    (r32, dx32, rsd32), (_, dx64, rsd64) = refs[torch.float32], refs[torch.float64]
+    fwd = _rel(out.permute(0, 3, 1, 2), r32)
+    assert fwd < 1e-4, fwd
+    names = [f"FMT_with_pathway.FMT.layers.{i}.{n}" for i in range(8) for n in _ENC_PARAMS]
+    checks = [("d_stage1", a1.grad, dx32, dx64)] + [(n, p.grad, rsd32[n].grad, rsd64[n].grad)
+                                                    for n, p in zip(names, fmt_params(model))]
+    errs = [(n, _rel(got, e64), _rel(e32, e64)) for n, got, e32, e64 in checks]
+    ref_worst = max(e for _, _, e in errs)
+    worst = max((a, n, b) for n, a, b in errs)
+    print((nv, h, w), {"forward": fwd, "d_stage1 (gpu, fp32 ref)": errs[0][1:], "worst (gpu, name, fp32 ref)": worst,
+                       "fp32 ref worst": ref_worst})
+    for n, e_gpu, e_ref in errs:
+        assert e_gpu <= max(1e-4, 2.0 * e_ref, ref_worst), (n, e_gpu, e_ref, ref_worst)

@@ -62,6 +62,16 @@ SIGNATURES = {
     "tmvs_pixelwise_train_backward": (I, [P, I, I, I, I, P, P, P, P, P, P, S, P, P, P]),
     "tmvs_upsample2_add_nhwc": (I, [P, P, I, I, I, I, P, P]),
     "tmvs_upsample2_backward_nhwc": (I, [P, I, I, I, I, P, P]),
+    "tmvs_token_linear": (I, [P, L, I, I, P, P, I, P, I, P, P]),
+    "tmvs_token_wgrad_workspace": (S, [L, I, I]),
+    "tmvs_token_wgrad": (I, [P, I, P, I, L, P, S, P, P, I, P]),
+    "tmvs_layer_norm_fwd": (I, [P, L, P, P, P, P]),
+    "tmvs_layer_norm_bwd_workspace": (S, [L]),
+    "tmvs_layer_norm_bwd": (I, [P, P, L, P, P, S, P, P, I, P]),
+    "tmvs_linattn_fwd": (I, [P, L, L, P, L, P, P]),
+    "tmvs_linattn_bwd_workspace": (S, [L, L]),
+    "tmvs_linattn_bwd_q": (I, [P, P, L, L, P, L, P, S, P, P, P]),
+    "tmvs_linattn_bwd_kv": (I, [P, P, L, L, P, P, P, P]),
     "tmvs_conv3d_generic": (I, [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P]),
     "tmvs_conv3d_wgrad_workspace": (S, [I, I, I, I, I, I]),
     "tmvs_conv3d_wgrad": (I, [P, I, I, I, I, I, P, I, I, I, I, I, P, S, P, P]),

@@ -1,0 +1,462 @@
+// FMT backward for training: the pieces of EncoderLayer.forward
+// (models/FMT.py:96-111; AttentionLayer :56-75; LinearAttention :22-37) that autograd needs, as
+// token-wise kernels over [T][C] token matrices (C = 32, hidden 64, 8 heads x 4):
+//   tmvs_token_linear      y = x W^T (+ b) or y = x W (the data gradient), optionally accumulated
+//   tmvs_token_wgrad       dW = dy^T x and db = column sums of dy (fp64 block partials, fixed combine)
+//   tmvs_layer_norm_fwd    LayerNorm(32) forward (the backward recomputes its statistics)
+//   tmvs_layer_norm_bwd    dx, and dgamma / dbeta (deterministic reductions)
+//   tmvs_linattn_fwd       msg = (Q KV) / (Q Ksum + 1e-6) per head, Q = elu(q) + 1
+//   tmvs_linattn_bwd_q     dq (through the elu), and dKV / dKsum reduced over the queries of each
+//                          K/V group (per view for self layers, all views for cross layers)
+//   tmvs_linattn_bwd_kv    dk (through the elu), dv of the source tokens
+// KV layout as the forward (csrc/fmt.hip): kv[h*16 + m*4 + d] = sum_s K[s,h,d] V[s,h,m], Ksum at
+// 128 + h*4 + d. fp32 per token, fp64 in every cross-token reduction, no atomics.
+#include "common.h"
+
+namespace tmvs {
+
+constexpr int kTB = 256;
+constexpr float kLnEps = 1e-5f;
+constexpr float kAttnEps = 1e-6f;
+
+__device__ __forceinline__ float elu1f(float x) { return (x > 0.f ? x : expm1f(x)) + 1.f; }
+__device__ __forceinline__ float elu1_grad(float x) { return x > 0.f ? 1.f : expf(x); }
+
+// y[t][o] = sum_i W[o][i] x[t][i] + b[o] for a torch Linear weight W [OUT][IN]; TRANS: y[t][o] = sum_i W[i][o] x[t][i]
+// for W [IN][OUT] (the data gradient dx = dy W of a Linear with weight W); relu_of masks y where relu_of <= 0
+template <int IN, int OUT, bool TRANS>
+__global__ __launch_bounds__(kTB) void token_linear_kernel(const float* __restrict__ x, long T,
+                                                           const float* __restrict__ W, const float* __restrict__ b,
+                                                           const float* __restrict__ relu_of, int accumulate,
+                                                           float* __restrict__ y) {
+  __shared__ float ws[IN * OUT];
+  for (int i = threadIdx.x; i < IN * OUT; i += kTB) ws[i] = W[i];
+  __syncthreads();
+  const long t = (long)blockIdx.x * kTB + threadIdx.x;
+  if (t >= T) return;
+  float xv[IN];
+#pragma unroll
+  for (int i = 0; i < IN; ++i) xv[i] = x[t * IN + i];
+#pragma unroll 4
+  for (int o = 0; o < OUT; ++o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < IN; ++i) acc = fmaf(TRANS ? ws[i * OUT + o] : ws[o * IN + i], xv[i], acc);
+    if (b) acc = acc + b[o];
+    if (relu_of && !(relu_of[t * OUT + o] > 0.f)) acc = 0.f;  // relu backward mask (the forward's pre-activation)
+    if (accumulate) acc = y[t * OUT + o] + acc;
+    y[t * OUT + o] = acc;
+  }
+}
+
+// partial[blk][a][b] = sum_t dy[t][a] x[t][b] over the block's token range; partial[blk][A*B + a] = sum_t dy[t][a]
+template <int A, int B>
+__global__ __launch_bounds__(kTB) void token_wgrad_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                          long T, long tpb, double* __restrict__ partial) {
+  constexpr int CH = 32;
+  constexpr int NP = (A * B + A + kTB - 1) / kTB;
+  __shared__ float sd[CH][A];
+  __shared__ float sx[CH][B];
+  const long t0 = (long)blockIdx.x * tpb, t1 = t0 + tpb < T ? t0 + tpb : T;
+  double acc[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) acc[j] = 0.0;
+  for (long tb = t0; tb < t1; tb += CH) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < CH * A; i += kTB) {
+      const long t = tb + i / A;
+      sd[i / A][i % A] = t < t1 ? dy[t * A + i % A] : 0.f;
+    }
+    for (int i = threadIdx.x; i < CH * B; i += kTB) {
+      const long t = tb + i / B;
+      sx[i / B][i % B] = t < t1 ? x[t * B + i % B] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int q = threadIdx.x + j * kTB;
+      if (q < A * B) {
+        const int a = q / B, c = q % B;
+        float s = 0.f;
+#pragma unroll 8
+        for (int r = 0; r < CH; ++r) s = fmaf(sd[r][a], sx[r][c], s);
+        acc[j] += (double)s;
+      } else if (q < A * B + A) {
+        const int a = q - A * B;
+        float s = 0.f;
+        for (int r = 0; r < CH; ++r) s += sd[r][a];
+        acc[j] += (double)s;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int q = threadIdx.x + j * kTB;
+    if (q < A * B + A) partial[(size_t)blockIdx.x * (A * B + A) + q] = acc[j];
+  }
+}
+
+// out0[i] (i < n0) / out1[i - n0] = sum over the block partials in block order
+__global__ __launch_bounds__(kTB) void fmt_sum_partials_kernel(const double* __restrict__ partial, int nblk, long n,
+                                                               long n0, float* __restrict__ out0,
+                                                               float* __restrict__ out1, int accumulate) {
+  const long i = (long)blockIdx.x * kTB + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.0;
+  for (int j = 0; j < nblk; ++j) s += partial[(size_t)j * n + i];
+  float* o = i < n0 ? out0 + i : out1 + (i - n0);
+  *o = accumulate ? *o + (float)s : (float)s;
+}
+
+// LayerNorm over 32 features, the reference CPU op order: mean, biased variance, (x - mean) * rstd * g + b
+__device__ __forceinline__ void ln_stats(const float (&x)[32], float& mean, float& rstd) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) s += x[i];
+  mean = s / 32.f;
+  float v = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const float d = x[i] - mean;
+    v = fmaf(d, d, v);
+  }
+  rstd = 1.f / sqrtf(v / 32.f + kLnEps);
+}
+
+__global__ __launch_bounds__(kTB) void layer_norm_fwd_kernel(const float* __restrict__ x, long T,
+                                                             const float* __restrict__ g, const float* __restrict__ b,
+                                                             float* __restrict__ y) {
+  const long t = (long)blockIdx.x * kTB + threadIdx.x;
+  if (t >= T) return;
+  float v[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) v[i] = x[t * 32 + i];
+  float mean, rstd;
+  ln_stats(v, mean, rstd);
+#pragma unroll
+  for (int i = 0; i < 32; ++i) y[t * 32 + i] = fmaf((v[i] - mean) * rstd, g[i], b[i]);
+}
+
+// dx = rstd/32 * (32*gy - sum gy - xhat * sum gy*xhat), gy = dy * g; partial[blk] = {sum dy*xhat (32), sum dy (32)}
+__global__ __launch_bounds__(kTB) void layer_norm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                             long T, const float* __restrict__ g, long tpb,
+                                                             float* __restrict__ dx, double* __restrict__ partial) {
+  __shared__ double red[64][kTB / 64];
+  const long t0 = (long)blockIdx.x * tpb, t1 = t0 + tpb < T ? t0 + tpb : T;
+  float pg[32], pb[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) pg[i] = pb[i] = 0.f;
+  for (long t = t0 + threadIdx.x; t < t1; t += kTB) {
+    float v[32], d[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      v[i] = x[t * 32 + i];
+      d[i] = dy[t * 32 + i];
+    }
+    float mean, rstd;
+    ln_stats(v, mean, rstd);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const float xh = (v[i] - mean) * rstd;
+      const float gy = d[i] * g[i];
+      s1 += gy;
+      s2 = fmaf(gy, xh, s2);
+      pg[i] = fmaf(d[i], xh, pg[i]);
+      pb[i] += d[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const float xh = (v[i] - mean) * rstd;
+      dx[t * 32 + i] = (rstd / 32.f) * ((32.f * (d[i] * g[i]) - s1) - xh * s2);
+    }
+  }
+  // fp64 block reduction of the 64 per-thread sums (fixed butterfly per wave, then the 4 waves in order)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    double val = (double)(i < 32 ? pg[i] : pb[i - 32]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off, 64);
+    if (lane == 0) red[i][wv] = val;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64)
+    partial[(size_t)blockIdx.x * 64 + threadIdx.x] =
+        (red[threadIdx.x][0] + red[threadIdx.x][1]) + (red[threadIdx.x][2] + red[threadIdx.x][3]);
+}
+
+// msg[t][h*4+m] = (sum_d Q[h,d] KV[h][m][d]) / (sum_d Q[h,d] Ks[h][d] + eps); tokens of group gi use kv[gi*kvs]
+__global__ __launch_bounds__(kTB) void linattn_fwd_kernel(const float* __restrict__ q, long T, long tpg,
+                                                          const float* __restrict__ kv, long kv_stride,
+                                                          float* __restrict__ msg) {
+  const long t = (long)blockIdx.x * kTB + threadIdx.x;
+  if (t >= T) return;
+  const float* K = kv + (t / tpg) * kv_stride;
+#pragma unroll
+  for (int h = 0; h < 8; ++h) {
+    float Q[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) Q[d] = elu1f(q[t * 32 + h * 4 + d]);
+    float den = 0.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) den = fmaf(Q[d], K[128 + h * 4 + d], den);
+    const float z = 1.f / (den + kAttnEps);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      float num = 0.f;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) num = fmaf(Q[d], K[h * 16 + m * 4 + d], num);
+      msg[t * 32 + h * 4 + m] = num * z;
+    }
+  }
+}
+
+// query side: dq, and per block partial dKV (128) + dKs (32) -- blocks never straddle a K/V group.
+// One head at a time (20 accumulators per thread, then an fp64 block reduction of those 20).
+__global__ __launch_bounds__(kTB) void linattn_bwd_q_kernel(const float* __restrict__ q, const float* __restrict__ dmsg,
+                                                            long T, long tpg, long tpb, const float* __restrict__ kv,
+                                                            long kv_stride, float* __restrict__ dq,
+                                                            double* __restrict__ partial) {
+  __shared__ double red[20][kTB / 64];
+  const long t0 = (long)blockIdx.x * tpb, t1 = t0 + tpb < T ? t0 + tpb : T;
+  const float* K = kv + (t0 / tpg) * kv_stride;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll 1
+  for (int h = 0; h < 8; ++h) {
+    float kvh[16], ksh[4];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) kvh[i] = K[h * 16 + i];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) ksh[d] = K[128 + h * 4 + d];
+    float acc[20];
+#pragma unroll
+    for (int i = 0; i < 20; ++i) acc[i] = 0.f;
+    for (long t = t0 + threadIdx.x; t < t1; t += kTB) {
+      float qr[4], Q[4], dm[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        qr[d] = q[t * 32 + h * 4 + d];
+        Q[d] = elu1f(qr[d]);
+        dm[d] = dmsg[t * 32 + h * 4 + d];
+      }
+      float den = 0.f;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) den = fmaf(Q[d], ksh[d], den);
+      const float z = 1.f / (den + kAttnEps);
+      float dz = 0.f;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        float nm = 0.f;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) nm = fmaf(Q[d], kvh[m * 4 + d], nm);
+        dz = fmaf(dm[m], nm, dz);
+      }
+      const float dden = -dz * z * z;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        float dQ = dden * ksh[d];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const float dn = dm[m] * z;
+          dQ = fmaf(dn, kvh[m * 4 + d], dQ);
+          acc[m * 4 + d] = fmaf(dn, Q[d], acc[m * 4 + d]);
+        }
+        acc[16 + d] = fmaf(dden, Q[d], acc[16 + d]);
+        dq[t * 32 + h * 4 + d] = dQ * elu1_grad(qr[d]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 20; ++i) {
+      double val = (double)acc[i];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off, 64);
+      if (lane == 0) red[i][wv] = val;
+    }
+    __syncthreads();
+    if (threadIdx.x < 20) {
+      const int i = threadIdx.x;
+      const double v = (red[i][0] + red[i][1]) + (red[i][2] + red[i][3]);
+      partial[(size_t)blockIdx.x * 160 + (i < 16 ? h * 16 + i : 128 + h * 4 + (i - 16))] = v;
+    }
+    __syncthreads();
+  }
+}
+
+// dkv[g][i] = sum over the blocks of group g (in order) of partial[blk][i]
+__global__ void linattn_group_combine_kernel(const double* __restrict__ partial, int blocks_per_group,
+                                             float* __restrict__ dkv) {
+  const int g = blockIdx.x, i = threadIdx.x;
+  if (i >= 160) return;
+  double s = 0.0;
+  for (int j = 0; j < blocks_per_group; ++j) s += partial[((size_t)g * blocks_per_group + j) * 160 + i];
+  dkv[(size_t)g * 160 + i] = (float)s;
+}
+
+// source side: dK[s,h,d] = sum_m dKV[h][m][d] V[s,h,m] + dKs[h][d]; dV[s,h,m] = sum_d dKV[h][m][d] K[s,h,d]
+__global__ __launch_bounds__(kTB) void linattn_bwd_kv_kernel(const float* __restrict__ k, const float* __restrict__ v,
+                                                             long S, long spg, const float* __restrict__ dkv,
+                                                             float* __restrict__ dk, float* __restrict__ dv) {
+  const long s = (long)blockIdx.x * kTB + threadIdx.x;
+  if (s >= S) return;
+  const float* G = dkv + (s / spg) * 160;
+#pragma unroll
+  for (int h = 0; h < 8; ++h) {
+    float kr[4], Kf[4], V[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      kr[d] = k[s * 32 + h * 4 + d];
+      Kf[d] = elu1f(kr[d]);
+      V[d] = v[s * 32 + h * 4 + d];
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      float g = G[128 + h * 4 + d];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) g = fmaf(G[h * 16 + m * 4 + d], V[m], g);
+      dk[s * 32 + h * 4 + d] = g * elu1_grad(kr[d]);
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      float g = 0.f;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) g = fmaf(G[h * 16 + m * 4 + d], Kf[d], g);
+      dv[s * 32 + h * 4 + m] = g;
+    }
+  }
+}
+
+static long tok_chunk(long T, long maxblk) {
+  long c = 1024;
+  while ((T + c - 1) / c > maxblk) c *= 2;
+  return c;
+}
+
+}  // namespace tmvs
+
+using namespace tmvs;
+
+extern "C" int tmvs_token_linear(const float* x, long tokens, int in_features, int out_features, const float* w,
+                                 const float* b, int transpose_w, const float* relu_of, int accumulate, float* y,
+                                 void* stream) {
+  if (!x || !w || !y || tokens <= 0) return TMVS_ERR_ARG;
+  const dim3 grid((unsigned)((tokens + kTB - 1) / kTB));
+  hipStream_t st = (hipStream_t)stream;
+#define TMVS_TL(I, O)                                                                                             \
+  if (in_features == I && out_features == O) {                                                                    \
+    if (transpose_w)                                                                                              \
+      hipLaunchKernelGGL((token_linear_kernel<I, O, true>), grid, dim3(kTB), 0, st, x, tokens, w, b, relu_of,     \
+                         accumulate, y);                                                                          \
+    else                                                                                                          \
+      hipLaunchKernelGGL((token_linear_kernel<I, O, false>), grid, dim3(kTB), 0, st, x, tokens, w, b, relu_of,    \
+                         accumulate, y);                                                                          \
+    TMVS_CHECK_LAUNCH();                                                                                          \
+    return TMVS_OK;                                                                                               \
+  }
+  TMVS_TL(32, 32) TMVS_TL(32, 64) TMVS_TL(64, 32)
+#undef TMVS_TL
+  return TMVS_ERR_SHAPE;
+}
+
+extern "C" size_t tmvs_token_wgrad_workspace(long tokens, int a, int b) {
+  const long c = tok_chunk(tokens, 1024);
+  return (size_t)((tokens + c - 1) / c) * (a * b + a) * sizeof(double);
+}
+
+extern "C" int tmvs_token_wgrad(const float* dy, int a, const float* x, int b, long tokens, void* workspace,
+                                size_t workspace_bytes, float* dw, float* db, int accumulate, void* stream) {
+  if (!dy || !x || !workspace || !dw || !db || tokens <= 0) return TMVS_ERR_ARG;
+  if (workspace_bytes < tmvs_token_wgrad_workspace(tokens, a, b)) return TMVS_ERR_ARG;
+  const long c = tok_chunk(tokens, 1024);
+  const int nblk = (int)((tokens + c - 1) / c);
+  hipStream_t st = (hipStream_t)stream;
+  double* part = (double*)workspace;
+#define TMVS_TW(A, B)                                                                                           \
+  if (a == A && b == B) {                                                                                       \
+    hipLaunchKernelGGL((token_wgrad_kernel<A, B>), dim3(nblk), dim3(kTB), 0, st, dy, x, tokens, c, part);       \
+    TMVS_CHECK_LAUNCH();                                                                                        \
+    hipLaunchKernelGGL(fmt_sum_partials_kernel, dim3((A * B + A + kTB - 1) / kTB), dim3(kTB), 0, st,           \
+                       (const double*)part, nblk, (long)(A * B + A), (long)(A * B), dw, db, accumulate);        \
+    TMVS_CHECK_LAUNCH();                                                                                        \
+    return TMVS_OK;                                                                                             \
+  }
+  TMVS_TW(32, 32) TMVS_TW(64, 32) TMVS_TW(32, 64)
+#undef TMVS_TW
+  return TMVS_ERR_SHAPE;
+}
+
+extern "C" int tmvs_layer_norm_fwd(const float* x, long tokens, const float* g, const float* b, float* y, void* stream) {
+  if (!x || !g || !b || !y || tokens <= 0) return TMVS_ERR_ARG;
+  hipLaunchKernelGGL(layer_norm_fwd_kernel, dim3((unsigned)((tokens + kTB - 1) / kTB)), dim3(kTB), 0,
+                     (hipStream_t)stream, x, tokens, g, b, y);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+extern "C" size_t tmvs_layer_norm_bwd_workspace(long tokens) {
+  const long c = tok_chunk(tokens, 1024);
+  return (size_t)((tokens + c - 1) / c) * 64 * sizeof(double);
+}
+
+extern "C" int tmvs_layer_norm_bwd(const float* dy, const float* x, long tokens, const float* g, void* workspace,
+                                   size_t workspace_bytes, float* dx, float* dgb, int accumulate, void* stream) {
+  if (!dy || !x || !g || !workspace || !dx || !dgb || tokens <= 0) return TMVS_ERR_ARG;
+  if (workspace_bytes < tmvs_layer_norm_bwd_workspace(tokens)) return TMVS_ERR_ARG;
+  const long c = tok_chunk(tokens, 1024);
+  const int nblk = (int)((tokens + c - 1) / c);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(layer_norm_bwd_kernel, dim3(nblk), dim3(kTB), 0, st, dy, x, tokens, g, c, dx, (double*)workspace);
+  TMVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(fmt_sum_partials_kernel, dim3(1), dim3(kTB), 0, st, (const double*)workspace, nblk, 64L, 64L, dgb,
+                     dgb, accumulate);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+extern "C" int tmvs_linattn_fwd(const float* q, long tokens, long tokens_per_group, const float* kv, long kv_stride,
+                                float* msg, void* stream) {
+  if (!q || !kv || !msg || tokens <= 0 || tokens_per_group <= 0) return TMVS_ERR_ARG;
+  hipLaunchKernelGGL(linattn_fwd_kernel, dim3((unsigned)((tokens + kTB - 1) / kTB)), dim3(kTB), 0,
+                     (hipStream_t)stream, q, tokens, tokens_per_group, kv, kv_stride, msg);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+// blocks of tpb tokens that never straddle a group: tpb divides tokens_per_group
+static long group_chunk(long tpg) {
+  long c = 1024;
+  while (c > 1 && tpg % c) c >>= 1;
+  while (tpg / c > 512 && tpg % (2 * c) == 0) c *= 2;
+  return c;
+}
+
+extern "C" size_t tmvs_linattn_bwd_workspace(long tokens, long tokens_per_group) {
+  return (size_t)(tokens / group_chunk(tokens_per_group)) * 160 * sizeof(double);
+}
+
+extern "C" int tmvs_linattn_bwd_q(const float* q, const float* dmsg, long tokens, long tokens_per_group,
+                                  const float* kv, long kv_stride, void* workspace, size_t workspace_bytes, float* dq,
+                                  float* dkv, void* stream) {
+  if (!q || !dmsg || !kv || !workspace || !dq || !dkv || tokens <= 0 || tokens_per_group <= 0) return TMVS_ERR_ARG;
+  if (tokens % tokens_per_group) return TMVS_ERR_SHAPE;
+  if (workspace_bytes < tmvs_linattn_bwd_workspace(tokens, tokens_per_group)) return TMVS_ERR_ARG;
+  const long c = group_chunk(tokens_per_group);
+  const int nblk = (int)(tokens / c);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(linattn_bwd_q_kernel, dim3(nblk), dim3(kTB), 0, st, q, dmsg, tokens, tokens_per_group, c, kv,
+                     kv_stride, dq, (double*)workspace);
+  TMVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(linattn_group_combine_kernel, dim3((unsigned)(tokens / tokens_per_group)), dim3(256), 0, st,
+                     (const double*)workspace, (int)(tokens_per_group / c), dkv);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+extern "C" int tmvs_linattn_bwd_kv(const float* k, const float* v, long tokens, long tokens_per_group,
+                                   const float* dkv, float* dk, float* dv, void* stream) {
+  if (!k || !v || !dkv || !dk || !dv || tokens <= 0 || tokens_per_group <= 0) return TMVS_ERR_ARG;
+  hipLaunchKernelGGL(linattn_bwd_kv_kernel, dim3((unsigned)((tokens + kTB - 1) / kTB)), dim3(kTB), 0,
+                     (hipStream_t)stream, k, v, tokens, tokens_per_group, dkv, dk, dv);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}

@@ -726,7 +726,135 @@ def upsample2_backward_nhwc(du):
     return dr
 
 
+def _tokens(x, name, c=None):
+    _dev(x, name)
+    if x.dim() != 2 or (c is not None and x.shape[1] != c):
+        raise ValueError(f"{name}: expected a [T, {c or 'C'}] token matrix, got {tuple(x.shape)}")
+    return x.shape[0]
+
+
+def token_linear(x, w, b=None, transpose_w=False, relu_of=None, out=None):
+    """tmvs_token_linear: x [T,in] -> x w^T + b (w [out,in]) or, transpose_w, x w (w [in',out'] -> out = in').
+
+    relu_of [T,out] masks the result where relu_of <= 0; out (given) is accumulated into."""
+    t = _tokens(x, "x")
+    for a, n in ((w, "w"), (b, "b"), (relu_of, "relu_of"), (out, "out")):
+        _dev(a, n)
+    o_f = w.shape[0] if not transpose_w else w.shape[1]
+    if x.shape[1] != (w.shape[1] if not transpose_w else w.shape[0]):
+        raise ValueError("token_linear: x / w feature mismatch")
+    acc = out is not None
+    for a, n in ((relu_of, "relu_of"), (out, "out")):
+        if a is not None and tuple(a.shape) != (t, o_f):
+            raise ValueError(f"token_linear: {n} must be [{t}, {o_f}]")
+    y = out if acc else torch.empty(t, o_f, device=x.device)
+    with _Span("tmvs_token_linear"):
+        _lib.check(_lib_h().tmvs_token_linear(_ptr(x), t, x.shape[1], o_f, _ptr(w), _ptr(b) if b is not None else None,
+                                              int(transpose_w), _ptr(relu_of) if relu_of is not None else None, int(acc),
+                                              _ptr(y), _stream()), "tmvs_token_linear")
+    return y
+
+
+def token_wgrad(dy, x, dw=None, db=None):
+    """tmvs_token_wgrad: dy [T,a], x [T,b] -> (dw [a,b] = dy^T x, db [a] = column sums of dy); accumulates into
+    dw/db when both are given."""
+    t = _tokens(dy, "dy")
+    if _tokens(x, "x") != t:
+        raise ValueError("token_wgrad: token counts differ")
+    a, b = dy.shape[1], x.shape[1]
+    acc = dw is not None
+    if acc != (db is not None):
+        raise ValueError("token_wgrad: give both dw and db or neither")
+    if not acc:
+        dw, db = torch.empty(a, b, device=dy.device), torch.empty(a, device=dy.device)
+    for z, n, shp in ((dw, "dw", (a, b)), (db, "db", (a,))):
+        _dev(z, n)
+        if tuple(z.shape) != shp:
+            raise ValueError(f"token_wgrad: {n} must be {shp}")
+    ws = torch.empty(_lib_h().tmvs_token_wgrad_workspace(t, a, b) // 4 + 64, device=dy.device)
+    with _Span("tmvs_token_wgrad"):
+        _lib.check(_lib_h().tmvs_token_wgrad(_ptr(dy), a, _ptr(x), b, t, _ptr(ws), ws.numel() * 4, _ptr(dw), _ptr(db),
+                                             int(acc), _stream()), "tmvs_token_wgrad")
+    return dw, db
+
+
+def layer_norm_fwd(x, g, b):
+    """tmvs_layer_norm_fwd: LayerNorm(32) of x [T,32]."""
+    t = _tokens(x, "x", 32)
+    _dev(g, "g")
+    _dev(b, "b")
+    y = torch.empty_like(x)
+    with _Span("tmvs_layer_norm_fwd"):
+        _lib.check(_lib_h().tmvs_layer_norm_fwd(_ptr(x), t, _ptr(g), _ptr(b), _ptr(y), _stream()), "tmvs_layer_norm_fwd")
+    return y
+
+
+def layer_norm_bwd(dy, x, g, dgb=None):
+    """tmvs_layer_norm_bwd: -> (dx [T,32], dgb [64] = dgamma | dbeta); accumulates into dgb when given."""
+    t = _tokens(dy, "dy", 32)
+    if _tokens(x, "x", 32) != t:
+        raise ValueError("layer_norm_bwd: token counts differ")
+    _dev(g, "g")
+    _dev(dgb, "dgb")
+    acc = dgb is not None
+    dgb = dgb if acc else torch.empty(64, device=dy.device)
+    dx = torch.empty_like(dy)
+    ws = torch.empty(_lib_h().tmvs_layer_norm_bwd_workspace(t) // 4 + 64, device=dy.device)
+    with _Span("tmvs_layer_norm_bwd"):
+        _lib.check(_lib_h().tmvs_layer_norm_bwd(_ptr(dy), _ptr(x), t, _ptr(g), _ptr(ws), ws.numel() * 4, _ptr(dx),
+                                                _ptr(dgb), int(acc), _stream()), "tmvs_layer_norm_bwd")
+    return dx, dgb
+
+
+def linattn_fwd(q, kv, tokens_per_group):
+    """tmvs_linattn_fwd: q [T,32] (pre-elu), kv [G,160] (G == 1: shared) -> msg [T,32]."""
+    t = _tokens(q, "q", 32)
+    _dev(kv, "kv")
+    msg = torch.empty_like(q)
+    stride = 0 if kv.shape[0] == 1 else _lib.KV_NFLOATS
+    with _Span("tmvs_linattn_fwd"):
+        _lib.check(_lib_h().tmvs_linattn_fwd(_ptr(q), t, tokens_per_group, _ptr(kv), stride, _ptr(msg), _stream()),
+                   "tmvs_linattn_fwd")
+    return msg
+
+
+def linattn_bwd_q(q, dmsg, kv, tokens_per_group):
+    """tmvs_linattn_bwd_q: -> (dq [T,32], dkv [T / tokens_per_group, 160])."""
+    t = _tokens(q, "q", 32)
+    if _tokens(dmsg, "dmsg", 32) != t:
+        raise ValueError("linattn_bwd_q: token counts differ")
+    if t % tokens_per_group:
+        raise ValueError("linattn_bwd_q: tokens must be a multiple of tokens_per_group")
+    _dev(kv, "kv")
+    groups = t // tokens_per_group
+    stride = 0 if kv.shape[0] == 1 else _lib.KV_NFLOATS
+    if stride and kv.shape[0] != groups:
+        raise ValueError("linattn_bwd_q: kv must have one row per group (or one shared row)")
+    dq = torch.empty_like(q)
+    dkv = torch.empty(groups, _lib.KV_NFLOATS, device=q.device)
+    ws = torch.empty(_lib_h().tmvs_linattn_bwd_workspace(t, tokens_per_group) // 4 + 64, device=q.device)
+    with _Span("tmvs_linattn_bwd_q"):
+        _lib.check(_lib_h().tmvs_linattn_bwd_q(_ptr(q), _ptr(dmsg), t, tokens_per_group, _ptr(kv), stride, _ptr(ws),
+                                               ws.numel() * 4, _ptr(dq), _ptr(dkv), _stream()), "tmvs_linattn_bwd_q")
+    return dq, dkv
+
+
+def linattn_bwd_kv(k, v, dkv, tokens_per_group):
+    """tmvs_linattn_bwd_kv: k (pre-elu), v [S,32], dkv [S / tokens_per_group, 160] -> (dk, dv)."""
+    s = _tokens(k, "k", 32)
+    if _tokens(v, "v", 32) != s or dkv.shape[0] * tokens_per_group != s:
+        raise ValueError("linattn_bwd_kv: shape mismatch")
+    _dev(dkv, "dkv")
+    dk, dv = torch.empty_like(k), torch.empty_like(v)
+    with _Span("tmvs_linattn_bwd_kv"):
+        _lib.check(_lib_h().tmvs_linattn_bwd_kv(_ptr(k), _ptr(v), s, tokens_per_group, _ptr(dkv), _ptr(dk), _ptr(dv),
+                                                _stream()), "tmvs_linattn_bwd_kv")
+    return dk, dv
+
+
 for _name in ("conv3d_generic", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn_relu_backward", "warp_corr_backward",
-              "upsample2_add_nhwc", "upsample2_backward_nhwc", "pixelwise_train_forward", "aggregate_train", "aggregate_train_backward", "pixelwise_train_backward"):
+              "upsample2_add_nhwc", "upsample2_backward_nhwc", "pixelwise_train_forward", "aggregate_train", "aggregate_train_backward", "pixelwise_train_backward",
+              "token_linear", "token_wgrad", "layer_norm_fwd", "layer_norm_bwd", "linattn_fwd", "linattn_bwd_q",
+              "linattn_bwd_kv"):
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name

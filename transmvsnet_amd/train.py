@@ -142,6 +142,131 @@ def pathway_train(model, stage1_nhwc, stage2_nchw, stage3_nchw):
     return st2, st3
 
 
+_ENC_PARAMS = ("attention.query_projection.weight", "attention.query_projection.bias",
+               "attention.key_projection.weight", "attention.key_projection.bias",
+               "attention.value_projection.weight", "attention.value_projection.bias",
+               "attention.out_projection.weight", "attention.out_projection.bias", "linear1.weight", "linear1.bias",
+               "linear2.weight", "linear2.bias", "norm1.weight", "norm1.bias", "norm2.weight", "norm2.bias")
+
+
+def _encoder_layer_backward(p, enc_w, x, src, dy, tpg, spg, self_attn):
+    """EncoderLayer backward (models/FMT.py:96-111): x [T,32] the layer input, src [S,32] its attention
+    source (x itself for a self layer), dy [T,32] -> (dx [T,32], dsrc [S,32] or None, 16 parameter grads).
+    The token-wise forward is recomputed from x (HIP token kernels; K/V sums by the forward's own
+    tmvs_fmt_kv); tpg / spg = query / source tokens per K/V group (a view for self layers; all views
+    share the reference view's K/V in cross layers)."""
+    wq, bq, wk, bk, wv, bv, wo, bo, w1, b1, w2, b2, g1, n1, g2, n2 = p
+    groups = src.shape[0] // spg
+    q = ops.token_linear(x, wq, bq)
+    k = ops.token_linear(src, wk, bk)
+    v = ops.token_linear(src, wv, bv)
+    kv = ops.fmt_kv(src.view(groups, spg, 32), enc_w)
+    msg = ops.linattn_fwd(q, kv, tpg)
+    xp1 = ops.token_linear(msg, wo, bo, out=x.clone())                     # x + out_projection(msg)
+    x1 = ops.layer_norm_fwd(xp1, g1, n1)
+    hp = ops.token_linear(x1, w1, b1)
+    hdn = ops.token_linear(x1, w1, b1, relu_of=hp)                         # relu(linear1(x1))
+    xp2 = ops.token_linear(hdn, w2, b2, out=x1.clone())                    # x1 + linear2(hdn)
+    dxp2, dgb2 = ops.layer_norm_bwd(dy, xp2, g2)
+    dw2, db2 = ops.token_wgrad(dxp2, hdn)
+    dhp = ops.token_linear(dxp2, w2, transpose_w=True, relu_of=hp)
+    dw1, db1 = ops.token_wgrad(dhp, x1)
+    dx1 = ops.token_linear(dhp, w1, transpose_w=True, out=dxp2.clone())
+    dxp1, dgb1 = ops.layer_norm_bwd(dx1, xp1, g1)
+    dwo, dbo = ops.token_wgrad(dxp1, msg)
+    dmsg = ops.token_linear(dxp1, wo, transpose_w=True)
+    dq, dkv = ops.linattn_bwd_q(q, dmsg, kv, tpg)
+    dwq, dbq = ops.token_wgrad(dq, x)
+    dx = ops.token_linear(dq, wq, transpose_w=True, out=dxp1)
+    dk, dv = ops.linattn_bwd_kv(k, v, dkv, spg)
+    dwk, dbk = ops.token_wgrad(dk, src)
+    dwv, dbv = ops.token_wgrad(dv, src)
+    dsrc = dx if self_attn else None
+    dsrc = ops.token_linear(dk, wk, transpose_w=True, out=dsrc)
+    ops.token_linear(dv, wv, transpose_w=True, out=dsrc)
+    grads = (dwq, dbq, dwk, dbk, dwv, dbv, dwo, dbo, dw1, db1, dw2, db2, dgb1[:32], dgb1[32:], dgb2[:32], dgb2[32:])
+    return dx, (None if self_attn else dsrc), grads
+
+
+def _pack_enc(p):
+    """The tmvs_fmt_* weight block of one layer from its 16 _ENC_PARAMS (as EncoderLayer.packed: key,
+    value and linear2 weights transposed)."""
+    parts = list(p)
+    for i in (2, 4, 10):
+        parts[i] = parts[i].t()
+    return torch.cat([t.detach().float().contiguous().reshape(-1) for t in parts])
+
+
+class _FMTTrain(torch.autograd.Function):
+    """FMT (models/FMT.py:147-177, 212-220) for training: stage-1 features [nv,32,h,w] (reference view
+    first) -> tokens [nv,h*w,32]. Forward: the inference kernels layer by layer (tmvs_fmt_embed,
+    tmvs_fmt_kv, tmvs_fmt_apply), keeping each layer's input; backward: _encoder_layer_backward in
+    reverse, the cross layers' source gradient summed into the reference view's tokens."""
+
+    @staticmethod
+    def forward(ctx, s1, pe, *params):
+        nv, c, h, w = s1.shape
+        L = h * w
+        enc = [_pack_enc(params[16 * i:16 * i + 16]) for i in range(8)]
+        tokens = torch.empty(nv, L, c, device=s1.device)
+        ops.fmt_embed(s1.contiguous(), pe, tokens)
+        saved = []
+        for j in range(4):
+            xs = tokens.clone()
+            ops.fmt_apply(tokens, ops.fmt_kv(tokens, enc[2 * j]), enc[2 * j])
+            ref = tokens[0].clone()
+            xc = tokens[1:].clone()
+            ops.fmt_apply(tokens[1:], ops.fmt_kv(tokens[:1], enc[2 * j + 1]), enc[2 * j + 1], shared_kv=True)
+            saved += [xs, ref, xc]
+        ctx.save_for_backward(*saved, *params)
+        ctx.enc, ctx.shape = enc, (nv, c, h, w)
+        return tokens
+
+    @staticmethod
+    def backward(ctx, dtokens):
+        nv, c, h, w = ctx.shape
+        L = h * w
+        t = ctx.saved_tensors
+        saved, params = t[:12], [p.detach().float().contiguous() for p in t[12:]]
+        grads = [None] * 128
+        dt = dtokens.contiguous().clone()
+        for j in reversed(range(4)):
+            xs, ref, xc = saved[3 * j:3 * j + 3]
+            i = 2 * j + 1
+            dxc, dref, gi = _encoder_layer_backward(params[16 * i:16 * i + 16], ctx.enc[i], xc.view(-1, c), ref,
+                                                    dt[1:].reshape(-1, c), (nv - 1) * L, L, False)
+            dt[1:] = dxc.view(nv - 1, L, c)
+            dt[0] += dref
+            grads[16 * i:16 * i + 16] = gi
+            i = 2 * j
+            dxs, _, gi = _encoder_layer_backward(params[16 * i:16 * i + 16], ctx.enc[i], xs.view(-1, c), xs.view(-1, c),
+                                                 dt.view(-1, c), L, L, True)
+            dt = dxs.view(nv, L, c)
+            grads[16 * i:16 * i + 16] = gi
+        ds1 = dt.view(nv, h, w, c).permute(0, 3, 1, 2).contiguous()
+        return (ds1, None, *grads)
+
+
+def fmt_params(model):
+    """The 128 FMT parameters (8 EncoderLayers x _ENC_PARAMS) in _FMTTrain's order."""
+    layers = model.FMT_with_pathway.FMT.layers
+    return [dict(layer.named_parameters())[n] for layer in layers for n in _ENC_PARAMS]
+
+
+def fmt_train(model, stage1_nchw):
+    """FMT_with_pathway's FMT part (models/FMT.py:212-220) for training: FeatureNet stage-1 features
+    [nv,32,h,w] (reference view first) -> FMT output [nv,h,w,32] NHWC, differentiable w.r.t. the input
+    and every FMT parameter (HIP forward and backward)."""
+    if not stage1_nchw.is_cuda:
+        raise RuntimeError("fmt_train runs on the GPU only (no CPU fallback)")
+    nv, c, h, w = stage1_nchw.shape
+    if nv < 2 or c != 32:
+        raise ValueError("fmt_train: stage1 must be [nv >= 2, 32, h, w]")
+    pe = model._pe_slice(h, w, stage1_nchw.device)
+    tokens = _FMTTrain.apply(stage1_nchw, pe, *fmt_params(model))
+    return tokens.view(nv, h, w, c)
+
+
 def _pack_fwd(w, transposed):
     """Conv3d [Co][Ci][27] / ConvTranspose3d [Ci][Co][27] -> [27][Co][Ci]."""
     if transposed:
