@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TMVS_ABI_VERSION 2
+#define TMVS_ABI_VERSION 3
 
 #define TMVS_OK 0
 #define TMVS_ERR_ARG (-1)    /* null pointer / non-positive size / bad enum        */
@@ -249,8 +249,10 @@ int tmvs_conv3d_wgrad(const float* direct, int a_ch, int batch, int pd, int ph, 
  *   dsrc [V][H][W][C] = the bilinear scatter of dsim/C * ref          (NHWC, overwritten)
  * ref/src/hyp/proj/flags as tmvs_warp_corr (one sample, C in {8,16,32}). The scatter is summed
  * in 2^-40 fixed point with 64-bit integer atomics: deterministic; |a single contribution| must
- * stay below 2^22 (checked: the workspace's int after the buffer is set to 1 otherwise).       */
-size_t tmvs_warp_corr_backward_workspace(int n_src, int channels, int height, int width);
+ * stay below 2^22 (checked: the workspace's int after the buffer is set to 1 otherwise). One
+ * thread per (pixel, view, chunk of 8 planes); dref is the fixed-order sum of those partials.
+ * ABI 3: the workspace size takes ndepth (the d ref partials live in it).                      */
+size_t tmvs_warp_corr_backward_workspace(int n_src, int channels, int height, int width, int ndepth);
 int tmvs_warp_corr_backward(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,
                             const float* dsim, int n_src, int channels, int ndepth, int height, int width, int flags,
                             void* workspace, size_t workspace_bytes, float* dref, float* dsrc, void* stream);

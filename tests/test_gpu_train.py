@@ -334,46 +334,66 @@ def test_training_step_from_fmt_output(with_fmt):
                                   {k: v.to(DEV) for k, v in gt.items()}, {k: v.to(DEV) for k, v in mask.items()},
                                   (H, W))
     torch.cuda.synchronize()
-    rsd = {k: (v.clone().requires_grad_() if v.is_floating_point() and "running" not in k else v.clone())
-           for k, v in sd.items()}
-    c1, c2, c3 = s1.clone().requires_grad_(), s2.clone().requires_grad_(), s3.clone().requires_grad_()
     P = "FMT_with_pathway."
-    f1 = c1
-    if with_fmt:
-        ref_list = oracle.fmt_ref(rsd, c1[:1])
-        f1 = torch.cat([ref_list[-1]] + [oracle.fmt_src(rsd, ref_list, c1[i:i + 1]) for i in range(1, N)])
-    r2 = F.conv2d(F.interpolate(F.conv2d(f1, rsd[P + "dim_reduction_1.weight"]), size=(H // 2, W // 2),
-                                mode="bilinear") + c2, rsd[P + "smooth_1.weight"], padding=1)
-    r3 = F.conv2d(F.interpolate(F.conv2d(r2, rsd[P + "dim_reduction_2.weight"]), size=(H, W), mode="bilinear") + c3,
-                  rsd[P + "smooth_2.weight"], padding=1)
-    feats = {"stage1": f1, "stage2": r2, "stage3": r3}
-    outputs, depth, vw = {}, None, None
-    for s in range(3):
-        name = f"stage{s + 1}"
-        hyp = oracle.stage_hypotheses(depth, dv, s, (H, W), ND)
-        if s > 0:
-            vw = F.interpolate(vw, scale_factor=2, mode="nearest")
-        sim, vw_new = oracle.build_cost_volume(rsd, [feats[name][i:i + 1] for i in range(N)], proj[name], hyp,
-                                               vw if s else None, training=True)
-        if s == 0:
-            vw = vw_new.detach()
-        logits = oracle.cost_reg_net(rsd, f"cost_regularization.{s}.", sim, training=True)[:, 0]
-        prob = torch.exp(F.log_softmax(logits, dim=1))
-        depth = torch.gather(hyp, 1, prob.argmax(1, keepdim=True)).squeeze(1)
-        outputs[name] = {"prob_volume": prob, "depth_values": hyp}
-    ref_total = loss_ref.trans_mvsnet_loss(outputs, gt, mask, dlossw=(0.5, 1.0, 2.0))[0]
-    ref_total.backward()
+
+    def reference(dt):
+        rsd = {k: (v.to(dt).clone().requires_grad_() if v.is_floating_point() and "running" not in k
+                   else (v.to(dt).clone() if v.is_floating_point() else v.clone())) for k, v in sd.items()}
+        c1, c2, c3 = (x.to(dt).clone().requires_grad_() for x in (s1, s2, s3))
+        f1 = c1
+        if with_fmt:
+            ref_list = oracle.fmt_ref(rsd, c1[:1])
+            f1 = torch.cat([ref_list[-1]] + [oracle.fmt_src(rsd, ref_list, c1[i:i + 1]) for i in range(1, N)])
+        r2 = F.conv2d(F.interpolate(F.conv2d(f1, rsd[P + "dim_reduction_1.weight"]), size=(H // 2, W // 2),
+                                    mode="bilinear") + c2, rsd[P + "smooth_1.weight"], padding=1)
+        r3 = F.conv2d(F.interpolate(F.conv2d(r2, rsd[P + "dim_reduction_2.weight"]), size=(H, W), mode="bilinear")
+                      + c3, rsd[P + "smooth_2.weight"], padding=1)
+        feats = {"stage1": f1, "stage2": r2, "stage3": r3}
+        outputs, depth, vw = {}, None, None
+        for s in range(3):
+            name = f"stage{s + 1}"
+            hyp = oracle.stage_hypotheses(depth, dv.to(dt), s, (H, W), ND)
+            if s > 0:
+                vw = F.interpolate(vw, scale_factor=2, mode="nearest")
+            sim, vw_new = oracle.build_cost_volume(rsd, [feats[name][i:i + 1] for i in range(N)], proj[name].to(dt),
+                                                   hyp, vw if s else None, training=True)
+            if s == 0:
+                vw = vw_new.detach()
+            logits = oracle.cost_reg_net(rsd, f"cost_regularization.{s}.", sim, training=True)[:, 0]
+            prob = torch.exp(F.log_softmax(logits, dim=1))
+            depth = torch.gather(hyp, 1, prob.argmax(1, keepdim=True)).squeeze(1)
+            outputs[name] = {"prob_volume": prob, "depth_values": hyp}
+        tot = loss_ref.trans_mvsnet_loss(outputs, {k: v.to(dt) for k, v in gt.items()},
+                                         {k: v.to(dt) for k, v in mask.items()}, dlossw=(0.5, 1.0, 2.0))[0]
+        tot.backward()
+        grads = {"d_stage1_input": c1.grad, "d_stage2": c2.grad, "d_stage3": c3.grad}
+        grads.update({n: rsd[n].grad for n in sd if n.startswith(P) and rsd[n].grad is not None})
+        return float(tot), grads
+
     params = dict(model.named_parameters())
-    rep = {"loss": abs(float(total) - float(ref_total)) / abs(float(ref_total)),
-           "d_stage1_input": _rel(a1.grad if with_fmt else a1.grad.permute(0, 3, 1, 2), c1.grad),
-           "d_stage2": _rel(a2.grad, c2.grad), "d_stage3": _rel(a3.grad, c3.grad)}
-    for k in ("dim_reduction_1.weight", "smooth_1.weight", "dim_reduction_2.weight", "smooth_2.weight"):
-        rep[k] = _rel(params[P + k].grad, rsd[P + k].grad)
+    got = {"d_stage1_input": a1.grad if with_fmt else a1.grad.permute(0, 3, 1, 2), "d_stage2": a2.grad,
+           "d_stage3": a3.grad}
+    ref_total, r32 = reference(torch.float32)
+    names = ["d_stage1_input", "d_stage2", "d_stage3"] + [P + k for k in ("dim_reduction_1.weight", "smooth_1.weight",
+                                                                          "dim_reduction_2.weight", "smooth_2.weight")]
     if with_fmt:
-        names = [n for n in params if ".FMT." in n]
-        rep["fmt_worst"] = max(_rel(params[n].grad, rsd[n].grad) for n in names)
-    print(rep)
-    assert rep["loss"] < 1e-5 and all(v < 1e-3 for v in rep.values()), rep
+        names += [n for n in r32 if ".FMT." in n]
+    got.update({n: params[n].grad for n in names if n.startswith(P)})
+    rep = {"loss": abs(float(total) - ref_total) / abs(ref_total)}
+    assert rep["loss"] < 1e-5, rep
+    if not with_fmt:
+        rep.update({n: _rel(got[n], r32[n]) for n in names})
+        print(rep)
+        assert all(v < 1e-3 for v in rep.values()), rep
+        return
+    # with the FMT in the chain the fp32 reference's own gradients drift 1e-3..1e-2 from exact: judge vs fp64
+    _, r64 = reference(torch.float64)
+    errs = {n: (_rel(got[n], r64[n]), _rel(r32[n], r64[n])) for n in names}
+    ref_worst = max(e for _, e in errs.values())
+    print(rep, {n: (f"{a:.1e}", f"{b:.1e}") for n, (a, b) in errs.items() if ".FMT." not in n},
+          "FMT worst (gpu, fp32 ref):", max(errs[n] for n in names if ".FMT." in n), "fp32 ref worst:", ref_worst)
+    for n, (e_gpu, e_ref) in errs.items():
+        assert e_gpu <= max(1e-3, 2.0 * e_ref, ref_worst), (n, e_gpu, e_ref, ref_worst)
 
 
 def _fmt_ref_sd(sd, dt):

@@ -53,7 +53,7 @@ SIGNATURES = {
     "tmvs_entropy_loss": (I, [P, P, I, P, P, I, I, I, I, F, P, S, P, P, P, P, P]),
     "tmvs_depth_metrics_workspace": (S, [I]),
     "tmvs_depth_metrics": (I, [P, P, P, I, F, P, S, P, P]),
-    "tmvs_warp_corr_backward_workspace": (S, [I, I, I, I]),
+    "tmvs_warp_corr_backward_workspace": (S, [I, I, I, I, I]),
     "tmvs_warp_corr_backward": (I, [P, P, P, P, P, I, I, I, I, I, I, P, S, P, P, P]),
     "tmvs_pixelwise_train_workspace": (S, []),
     "tmvs_pixelwise_train_forward": (I, [P, I, I, I, I, P, P, S, P, P, P, P]),
@@ -81,7 +81,7 @@ SIGNATURES = {
     "tmvs_bn_relu_backward": (I, [P, P, L, I, P, P, P, P, F, P, S, P, P, P, P]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 PW_NPARAMS = 201
 ENC_NPARAMS = 8544
 KV_NFLOATS = 160

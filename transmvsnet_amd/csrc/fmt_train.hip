@@ -23,89 +23,178 @@ __device__ __forceinline__ float elu1f(float x) { return (x > 0.f ? x : expm1f(x
 __device__ __forceinline__ float elu1_grad(float x) { return x > 0.f ? 1.f : expf(x); }
 
 // y[t][o] = sum_i W[o][i] x[t][i] + b[o] for a torch Linear weight W [OUT][IN]; TRANS: y[t][o] = sum_i W[i][o] x[t][i]
-// for W [IN][OUT] (the data gradient dx = dy W of a Linear with weight W); relu_of masks y where relu_of <= 0
+// for W [IN][OUT] (the data gradient dx = dy W of a Linear with weight W); relu_of masks y where relu_of <= 0.
+// One token per lane; the weights are wave-uniform (scalar loads, SGPR operands of v_fma_f32); rows move as float4.
 template <int IN, int OUT, bool TRANS>
 __global__ __launch_bounds__(kTB) void token_linear_kernel(const float* __restrict__ x, long T,
                                                            const float* __restrict__ W, const float* __restrict__ b,
                                                            const float* __restrict__ relu_of, int accumulate,
                                                            float* __restrict__ y) {
-  __shared__ float ws[IN * OUT];
-  for (int i = threadIdx.x; i < IN * OUT; i += kTB) ws[i] = W[i];
-  __syncthreads();
   const long t = (long)blockIdx.x * kTB + threadIdx.x;
   if (t >= T) return;
-  float xv[IN];
+  float xv[IN], acc[OUT];
 #pragma unroll
-  for (int i = 0; i < IN; ++i) xv[i] = x[t * IN + i];
-#pragma unroll 4
+  for (int i = 0; i < IN; i += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(x + t * IN + i);
+    xv[i] = v.x;
+    xv[i + 1] = v.y;
+    xv[i + 2] = v.z;
+    xv[i + 3] = v.w;
+  }
+#pragma unroll
   for (int o = 0; o < OUT; ++o) {
-    float acc = 0.f;
+    float a = 0.f;
 #pragma unroll
-    for (int i = 0; i < IN; ++i) acc = fmaf(TRANS ? ws[i * OUT + o] : ws[o * IN + i], xv[i], acc);
-    if (b) acc = acc + b[o];
-    if (relu_of && !(relu_of[t * OUT + o] > 0.f)) acc = 0.f;  // relu backward mask (the forward's pre-activation)
-    if (accumulate) acc = y[t * OUT + o] + acc;
-    y[t * OUT + o] = acc;
+    for (int i = 0; i < IN; ++i) a = fmaf(TRANS ? W[i * OUT + o] : W[o * IN + i], xv[i], a);
+    acc[o] = b ? a + b[o] : a;
+  }
+#pragma unroll
+  for (int o = 0; o < OUT; o += 4) {
+    float4 v = make_float4(acc[o], acc[o + 1], acc[o + 2], acc[o + 3]);
+    if (relu_of) {  // relu backward mask (the forward's pre-activation)
+      const float4 m = *reinterpret_cast<const float4*>(relu_of + t * OUT + o);
+      v.x = m.x > 0.f ? v.x : 0.f;
+      v.y = m.y > 0.f ? v.y : 0.f;
+      v.z = m.z > 0.f ? v.z : 0.f;
+      v.w = m.w > 0.f ? v.w : 0.f;
+    }
+    if (accumulate) {
+      const float4 p = *reinterpret_cast<const float4*>(y + t * OUT + o);
+      v.x = p.x + v.x;
+      v.y = p.y + v.y;
+      v.z = p.z + v.z;
+      v.w = p.w + v.w;
+    }
+    *reinterpret_cast<float4*>(y + t * OUT + o) = v;
   }
 }
 
-// partial[blk][a][b] = sum_t dy[t][a] x[t][b] over the block's token range; partial[blk][A*B + a] = sum_t dy[t][a]
-template <int A, int B>
+// partial[blk][a][b] = sum_t dy[t][a] x[t][b] over the block's token range; partial[blk][A*B + a] = sum_t dy[t][a].
+// Chunks of 64 tokens are staged in LDS; wave w takes rows w, w+4, ...; each lane owns a TA x TB output tile
+// ((A/TA)(B/TB) = 64), fp32 over a chunk's 16 rows then fp64; the 4 waves combine in a fixed order in LDS.
+template <int A, int B, int TA, int TB>
 __global__ __launch_bounds__(kTB) void token_wgrad_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                           long T, long tpb, double* __restrict__ partial) {
-  constexpr int CH = 32;
-  constexpr int NP = (A * B + A + kTB - 1) / kTB;
-  __shared__ float sd[CH][A];
-  __shared__ float sx[CH][B];
+  static_assert((A / TA) * (B / TB) == 64, "one tile per lane");
+  constexpr int CH = 64, NO = A * B + A;
+  __shared__ __attribute__((aligned(16))) float sd[CH][A + 4];
+  __shared__ __attribute__((aligned(16))) float sx[CH][B + 4];
+  __shared__ double cmb[2][NO];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ci = lane % (B / TB), ai = lane / (B / TB);
   const long t0 = (long)blockIdx.x * tpb, t1 = t0 + tpb < T ? t0 + tpb : T;
-  double acc[NP];
+  double acc[TA][TB], accb[TA];
 #pragma unroll
-  for (int j = 0; j < NP; ++j) acc[j] = 0.0;
+  for (int i = 0; i < TA; ++i) {
+    accb[i] = 0.0;
+#pragma unroll
+    for (int j = 0; j < TB; ++j) acc[i][j] = 0.0;
+  }
   for (long tb = t0; tb < t1; tb += CH) {
     __syncthreads();
-    for (int i = threadIdx.x; i < CH * A; i += kTB) {
-      const long t = tb + i / A;
-      sd[i / A][i % A] = t < t1 ? dy[t * A + i % A] : 0.f;
+    for (int i = threadIdx.x; i < CH * A / 4; i += kTB) {
+      const int r = i / (A / 4), c = (i % (A / 4)) * 4;
+      const long t = tb + r;
+      *reinterpret_cast<float4*>(&sd[r][c]) =
+          t < t1 ? *reinterpret_cast<const float4*>(dy + t * A + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    for (int i = threadIdx.x; i < CH * B; i += kTB) {
-      const long t = tb + i / B;
-      sx[i / B][i % B] = t < t1 ? x[t * B + i % B] : 0.f;
+    for (int i = threadIdx.x; i < CH * B / 4; i += kTB) {
+      const int r = i / (B / 4), c = (i % (B / 4)) * 4;
+      const long t = tb + r;
+      *reinterpret_cast<float4*>(&sx[r][c]) =
+          t < t1 ? *reinterpret_cast<const float4*>(x + t * B + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
+    float s[TA][TB], sb[TA];
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int q = threadIdx.x + j * kTB;
-      if (q < A * B) {
-        const int a = q / B, c = q % B;
-        float s = 0.f;
-#pragma unroll 8
-        for (int r = 0; r < CH; ++r) s = fmaf(sd[r][a], sx[r][c], s);
-        acc[j] += (double)s;
-      } else if (q < A * B + A) {
-        const int a = q - A * B;
-        float s = 0.f;
-        for (int r = 0; r < CH; ++r) s += sd[r][a];
-        acc[j] += (double)s;
+    for (int i = 0; i < TA; ++i) {
+      sb[i] = 0.f;
+#pragma unroll
+      for (int j = 0; j < TB; ++j) s[i][j] = 0.f;
+    }
+#pragma unroll 4
+    for (int r = wv; r < CH; r += 4) {
+      float av[TA], bv[TB];
+#pragma unroll
+      for (int i = 0; i < TA; i += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(&sd[r][ai * TA + i]);
+        av[i] = v.x;
+        av[i + 1] = v.y;
+        av[i + 2] = v.z;
+        av[i + 3] = v.w;
+      }
+#pragma unroll
+      for (int j = 0; j < TB; j += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(&sx[r][ci * TB + j]);
+        bv[j] = v.x;
+        bv[j + 1] = v.y;
+        bv[j + 2] = v.z;
+        bv[j + 3] = v.w;
+      }
+#pragma unroll
+      for (int i = 0; i < TA; ++i) {
+        sb[i] += av[i];
+#pragma unroll
+        for (int j = 0; j < TB; ++j) s[i][j] = fmaf(av[i], bv[j], s[i][j]);
       }
     }
-  }
 #pragma unroll
-  for (int j = 0; j < NP; ++j) {
-    const int q = threadIdx.x + j * kTB;
-    if (q < A * B + A) partial[(size_t)blockIdx.x * (A * B + A) + q] = acc[j];
+    for (int i = 0; i < TA; ++i) {
+      accb[i] += (double)sb[i];
+#pragma unroll
+      for (int j = 0; j < TB; ++j) acc[i][j] += (double)s[i][j];
+    }
+  }
+  // fixed-order wave combine: (w0 + w2) + (w1 + w3)
+  auto put = [&](double* dst) {
+#pragma unroll
+    for (int i = 0; i < TA; ++i) {
+#pragma unroll
+      for (int j = 0; j < TB; ++j) dst[(ai * TA + i) * B + ci * TB + j] = acc[i][j];
+      if (ci == 0) dst[A * B + ai * TA + i] = accb[i];
+    }
+  };
+  auto add = [&](const double* src) {
+#pragma unroll
+    for (int i = 0; i < TA; ++i) {
+#pragma unroll
+      for (int j = 0; j < TB; ++j) acc[i][j] += src[(ai * TA + i) * B + ci * TB + j];
+      if (ci == 0) accb[i] += src[A * B + ai * TA + i];
+    }
+  };
+  __syncthreads();
+  if (wv >= 2) put(cmb[wv - 2]);
+  __syncthreads();
+  if (wv < 2) add(cmb[wv]);
+  __syncthreads();
+  if (wv == 1) put(cmb[0]);
+  __syncthreads();
+  if (wv == 0) {
+    add(cmb[0]);
+    put(partial + (size_t)blockIdx.x * NO);
   }
 }
 
-// out0[i] (i < n0) / out1[i - n0] = sum over the block partials in block order
+// out0[i] (i < n0) / out1[i - n0] = sum over the block partials: 8 interleaved chains (block j in chain j % 8),
+// then the 8 chain sums in order -- a fixed order, bitwise reproducible
 __global__ __launch_bounds__(kTB) void fmt_sum_partials_kernel(const double* __restrict__ partial, int nblk, long n,
                                                                long n0, float* __restrict__ out0,
                                                                float* __restrict__ out1, int accumulate) {
-  const long i = (long)blockIdx.x * kTB + threadIdx.x;
-  if (i >= n) return;
+  __shared__ double red[8][32];
+  const int g = threadIdx.x >> 5, k = threadIdx.x & 31;
+  const long i = (long)blockIdx.x * 32 + k;
   double s = 0.0;
-  for (int j = 0; j < nblk; ++j) s += partial[(size_t)j * n + i];
-  float* o = i < n0 ? out0 + i : out1 + (i - n0);
-  *o = accumulate ? *o + (float)s : (float)s;
+  if (i < n)
+    for (int j = g; j < nblk; j += 8) s += partial[(size_t)j * n + i];
+  red[g][k] = s;
+  __syncthreads();
+  if (g == 0 && i < n) {
+    double t = red[0][k];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) t += red[q][k];
+    float* o = i < n0 ? out0 + i : out1 + (i - n0);
+    *o = accumulate ? *o + (float)t : (float)t;
+  }
 }
 
 // LayerNorm over 32 features, the reference CPU op order: mean, biased variance, (x - mean) * rstd * g + b
@@ -326,8 +415,7 @@ __global__ __launch_bounds__(kTB) void linattn_bwd_kv_kernel(const float* __rest
   }
 }
 
-static long tok_chunk(long T, long maxblk) {
-  long c = 1024;
+static long tok_chunk(long T, long maxblk, long c = 1024) {
   while ((T + c - 1) / c > maxblk) c *= 2;
   return c;
 }
@@ -359,7 +447,7 @@ extern "C" int tmvs_token_linear(const float* x, long tokens, int in_features, i
 }
 
 extern "C" size_t tmvs_token_wgrad_workspace(long tokens, int a, int b) {
-  const long c = tok_chunk(tokens, 1024);
+  const long c = tok_chunk(tokens, 512, 256);
   return (size_t)((tokens + c - 1) / c) * (a * b + a) * sizeof(double);
 }
 
@@ -367,20 +455,20 @@ extern "C" int tmvs_token_wgrad(const float* dy, int a, const float* x, int b, l
                                 size_t workspace_bytes, float* dw, float* db, int accumulate, void* stream) {
   if (!dy || !x || !workspace || !dw || !db || tokens <= 0) return TMVS_ERR_ARG;
   if (workspace_bytes < tmvs_token_wgrad_workspace(tokens, a, b)) return TMVS_ERR_ARG;
-  const long c = tok_chunk(tokens, 1024);
+  const long c = tok_chunk(tokens, 512, 256);
   const int nblk = (int)((tokens + c - 1) / c);
   hipStream_t st = (hipStream_t)stream;
   double* part = (double*)workspace;
-#define TMVS_TW(A, B)                                                                                           \
+#define TMVS_TW(A, B, TA, TB)                                                                                   \
   if (a == A && b == B) {                                                                                       \
-    hipLaunchKernelGGL((token_wgrad_kernel<A, B>), dim3(nblk), dim3(kTB), 0, st, dy, x, tokens, c, part);       \
+    hipLaunchKernelGGL((token_wgrad_kernel<A, B, TA, TB>), dim3(nblk), dim3(kTB), 0, st, dy, x, tokens, c, part); \
     TMVS_CHECK_LAUNCH();                                                                                        \
-    hipLaunchKernelGGL(fmt_sum_partials_kernel, dim3((A * B + A + kTB - 1) / kTB), dim3(kTB), 0, st,           \
+    hipLaunchKernelGGL(fmt_sum_partials_kernel, dim3((A * B + A + 31) / 32), dim3(kTB), 0, st,                 \
                        (const double*)part, nblk, (long)(A * B + A), (long)(A * B), dw, db, accumulate);        \
     TMVS_CHECK_LAUNCH();                                                                                        \
     return TMVS_OK;                                                                                             \
   }
-  TMVS_TW(32, 32) TMVS_TW(64, 32) TMVS_TW(32, 64)
+  TMVS_TW(32, 32, 4, 4) TMVS_TW(64, 32, 8, 4) TMVS_TW(32, 64, 4, 8)
 #undef TMVS_TW
   return TMVS_ERR_SHAPE;
 }
@@ -407,7 +495,7 @@ extern "C" int tmvs_layer_norm_bwd(const float* dy, const float* x, long tokens,
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(layer_norm_bwd_kernel, dim3(nblk), dim3(kTB), 0, st, dy, x, tokens, g, c, dx, (double*)workspace);
   TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(fmt_sum_partials_kernel, dim3(1), dim3(kTB), 0, st, (const double*)workspace, nblk, 64L, 64L, dgb,
+  hipLaunchKernelGGL(fmt_sum_partials_kernel, dim3(2), dim3(kTB), 0, st, (const double*)workspace, nblk, 64L, 64L, dgb,
                      dgb, accumulate);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;

@@ -629,7 +629,7 @@ def warp_corr_backward(ref_nhwc, src_nhwc, proj12, hyp, dsim, rot_order="auto"):
     if tuple(dsim.shape) != (v, d, h, w) or tuple(ref_nhwc.shape) != (h, w, c):
         raise ValueError("warp_corr_backward: shapes must be ref [H,W,C], src [V,H,W,C], hyp [D,H,W], dsim [V,D,H,W]")
     proj = np.ascontiguousarray(proj12, np.float32).reshape(v, 12)
-    nbytes = _lib_h().tmvs_warp_corr_backward_workspace(v, c, h, w)
+    nbytes = _lib_h().tmvs_warp_corr_backward_workspace(v, c, h, w, hyp.shape[0])
     ws = torch.empty(nbytes // 4 + 64, device=hyp.device)
     dref = torch.empty_like(ref_nhwc)
     dsrc = torch.empty_like(src_nhwc)
