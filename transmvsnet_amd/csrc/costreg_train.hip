@@ -176,6 +176,106 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_kernel(
   }
 }
 
+// Register-tiled form for A, BC >= 8 (the CostRegNet / pathway layers): chunks of 64 voxel rows are
+// staged in LDS (float4, the tap's gather computed once per row quad); wave w takes rows w, w+4, ...;
+// lane (ai, ci) owns the TA x TB block a in [ai*TA, +TA), c in [ci*TB, +TB) (TA = A/8, TB = BC/8), fp32
+// over a chunk's 16 rows then fp64; the 4 waves combine in a fixed order ((w0 + w1) + w2) + w3 through
+// the (then idle) staging LDS.
+template <int A, int BC>
+__global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_tile_kernel(
+    const float* __restrict__ direct, const float* __restrict__ gath, int B, int Pd, int Ph, int Pw, int Gd, int Gh,
+    int Gw, int stride, long vpb, double* __restrict__ partial) {
+  constexpr int CH = 64, TA = A / 8, TB = BC / 8, SA = A + 4, SB = BC + 4;
+  static_assert(A >= 8 && BC >= 8, "tile kernel needs 8 x 8 lanes");
+  static_assert(CH * (SA + SB) * 4 >= A * BC * 8, "combine buffer fits the staging LDS");
+  __shared__ __attribute__((aligned(16))) float lds[CH * (SA + SB)];
+  float* sd = lds;
+  float* sg = lds + CH * SA;
+  const int k = blockIdx.y;
+  const int kd = k / 9, kh = (k / 3) % 3, kw = k % 3;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ci = lane & 7, ai = lane >> 3;
+  const long nvox = (long)B * Pd * Ph * Pw;
+  const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
+  double acc[TA][TB];
+#pragma unroll
+  for (int i = 0; i < TA; ++i)
+#pragma unroll
+    for (int j = 0; j < TB; ++j) acc[i][j] = 0.0;
+#pragma unroll 1
+  for (long vb = v0; vb < v1; vb += CH) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < CH * A / 4; i += kTrainBlock) {
+      const int r = i / (A / 4), c = (i % (A / 4)) * 4;
+      const long v = vb + r;
+      *reinterpret_cast<float4*>(sd + r * SA + c) =
+          v < v1 ? *reinterpret_cast<const float4*>(direct + v * A + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    for (int i = threadIdx.x; i < CH * BC / 4; i += kTrainBlock) {
+      const int r = i / (BC / 4), c = (i % (BC / 4)) * 4;
+      const long v = vb + r;
+      float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (v < v1) {
+        const int pw = (int)(v % Pw);
+        long t = v / Pw;
+        const int ph = (int)(t % Ph);
+        t /= Ph;
+        const int pd = (int)(t % Pd);
+        const int b = (int)(t / Pd);
+        const int gd = pd * stride - 1 + kd, gh = ph * stride - 1 + kh, gw = pw * stride - 1 + kw;
+        if (gd >= 0 && gh >= 0 && gw >= 0 && gd < Gd && gh < Gh && gw < Gw)
+          val = *reinterpret_cast<const float4*>(gath + ((((size_t)b * Gd + gd) * Gh + gh) * Gw + gw) * BC + c);
+      }
+      *reinterpret_cast<float4*>(sg + r * SB + c) = val;
+    }
+    __syncthreads();
+    float s[TA][TB];
+#pragma unroll
+    for (int i = 0; i < TA; ++i)
+#pragma unroll
+      for (int j = 0; j < TB; ++j) s[i][j] = 0.f;
+#pragma unroll 4
+    for (int r = wv; r < CH; r += 4) {
+      float av[TA], bv[TB];
+#pragma unroll
+      for (int i = 0; i < TA; ++i) av[i] = sd[r * SA + ai * TA + i];
+#pragma unroll
+      for (int j = 0; j < TB; ++j) bv[j] = sg[r * SB + ci * TB + j];
+#pragma unroll
+      for (int i = 0; i < TA; ++i)
+#pragma unroll
+        for (int j = 0; j < TB; ++j) s[i][j] = fmaf(av[i], bv[j], s[i][j]);
+    }
+#pragma unroll
+    for (int i = 0; i < TA; ++i)
+#pragma unroll
+      for (int j = 0; j < TB; ++j) acc[i][j] += (double)s[i][j];
+  }
+  double* cmb = reinterpret_cast<double*>(lds);
+#pragma unroll 1
+  for (int w = 1; w < 4; ++w) {
+    __syncthreads();
+    if (wv == w)
+#pragma unroll
+      for (int i = 0; i < TA; ++i)
+#pragma unroll
+        for (int j = 0; j < TB; ++j) cmb[(ai * TA + i) * BC + ci * TB + j] = acc[i][j];
+    __syncthreads();
+    if (wv == 0)
+#pragma unroll
+      for (int i = 0; i < TA; ++i)
+#pragma unroll
+        for (int j = 0; j < TB; ++j) acc[i][j] += cmb[(ai * TA + i) * BC + ci * TB + j];
+  }
+  if (wv == 0) {
+    double* out = partial + ((size_t)blockIdx.x * 27 + k) * A * BC;
+#pragma unroll
+    for (int i = 0; i < TA; ++i)
+#pragma unroll
+      for (int j = 0; j < TB; ++j) out[(ai * TA + i) * BC + ci * TB + j] = acc[i][j];
+  }
+}
+
 // Few (a, b) pairs (conv0: 8 x 1, prob: 1 x 8): voxel-parallel instead -- thread t takes voxels
 // t, t+256, ... of the block's range straight from global memory and accumulates all A*BC pairs, then
 // a fixed LDS tree per pair.
@@ -425,6 +525,9 @@ static int launch_wgrad(const float* direct, const float* gath, int B, int Pd, i
   const int nblk = (int)((nvox + vpb - 1) / vpb);
   if constexpr (A * BC <= 16)
     hipLaunchKernelGGL((conv3d_wgrad_small_kernel<A, BC>), dim3(nblk, 27), dim3(kTrainBlock), 0, st, direct, gath, B,
+                       Pd, Ph, Pw, Gd, Gh, Gw, stride, vpb, ws);
+  else if constexpr (A >= 8 && BC >= 8)
+    hipLaunchKernelGGL((conv3d_wgrad_tile_kernel<A, BC>), dim3(nblk, 27), dim3(kTrainBlock), 0, st, direct, gath, B,
                        Pd, Ph, Pw, Gd, Gh, Gw, stride, vpb, ws);
   else
     hipLaunchKernelGGL((conv3d_wgrad_kernel<A, BC>), dim3(nblk, 27), dim3(kTrainBlock), 0, st, direct, gath, B, Pd,
