@@ -29,20 +29,14 @@ namespace tmvs {
 constexpr int kTrainBlock = 256;
 
 // ---------------------------------------------------------------- generic direct conv (VALU)
-// One thread = one output voxel x COB output channels; the co-block's weights [27][COB][CIN]
-// sit in LDS and are read as wave-uniform broadcasts. Each tap's CIN input channels are one
-// contiguous NDHWC row (float4 loads).
+// One thread = one output voxel x COB output channels; the co-block's weights [27][COB][CIN] are
+// wave-uniform (scalar loads feeding v_fma_f32 as SGPR operands: no LDS staging per block). Each
+// tap's CIN input channels are one contiguous NDHWC row (float4 loads).
 template <int CIN, int COB>
 __global__ __launch_bounds__(kTrainBlock) void conv3d_generic_kernel(
     const float* __restrict__ x, const float* __restrict__ w, int cout, int B, int Di, int Hi, int Wi, int Do, int Ho,
     int Wo, int stride, int transposed, int accumulate, float* __restrict__ y) {
-  __shared__ __attribute__((aligned(16))) float wl[27 * COB * CIN];
   const int cob = blockIdx.y;
-  for (int i = threadIdx.x; i < 27 * COB * CIN; i += kTrainBlock) {
-    const int ci = i % CIN, co = (i / CIN) % COB, k = i / (CIN * COB);
-    wl[i] = w[((size_t)k * cout + cob * COB + co) * CIN + ci];
-  }
-  __syncthreads();
   const long nvox = (long)B * Do * Ho * Wo;
   const long v = (long)blockIdx.x * kTrainBlock + threadIdx.x;
   if (v >= nvox) return;
@@ -74,7 +68,7 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_generic_kernel(
     }
     if (id >= Di || ih >= Hi || iw >= Wi) continue;
     const float* xp = xb + (((size_t)id * Hi + ih) * Wi + iw) * CIN;
-    const float* wk = wl + k * COB * CIN;
+    const float* wk = w + ((size_t)k * cout + cob * COB) * CIN;  // wave-uniform: scalar loads, SGPR operands
     if constexpr (CIN % 4 == 0) {
 #pragma unroll 4
       for (int c4 = 0; c4 < CIN / 4; ++c4) {
@@ -211,17 +205,26 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_tile_kernel(
       *reinterpret_cast<float4*>(sd + r * SA + c) =
           v < v1 ? *reinterpret_cast<const float4*>(direct + v * A + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    // the chunk's first voxel once (wave-uniform), then each row by carrying from it
+    const int pw0 = (int)(vb % Pw);
+    const long t0 = vb / Pw;
+    const int ph0 = (int)(t0 % Ph), pd0 = (int)((t0 / Ph) % Pd), b0 = (int)(t0 / ((long)Ph * Pd));
     for (int i = threadIdx.x; i < CH * BC / 4; i += kTrainBlock) {
       const int r = i / (BC / 4), c = (i % (BC / 4)) * 4;
       const long v = vb + r;
       float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
       if (v < v1) {
-        const int pw = (int)(v % Pw);
-        long t = v / Pw;
-        const int ph = (int)(t % Ph);
-        t /= Ph;
-        const int pd = (int)(t % Pd);
-        const int b = (int)(t / Pd);
+        int pw = pw0 + r, ph = ph0, pd = pd0, b = b0;
+        while (pw >= Pw) {
+          pw -= Pw;
+          if (++ph == Ph) {
+            ph = 0;
+            if (++pd == Pd) {
+              pd = 0;
+              ++b;
+            }
+          }
+        }
         const int gd = pd * stride - 1 + kd, gh = ph * stride - 1 + kh, gw = pw * stride - 1 + kw;
         if (gd >= 0 && gh >= 0 && gw >= 0 && gd < Gd && gh < Gh && gw < Gw)
           val = *reinterpret_cast<const float4*>(gath + ((((size_t)b * Gd + gd) * Gh + gh) * Gw + gw) * BC + c);
@@ -292,19 +295,35 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_small_kernel(
   double acc[NPR];
 #pragma unroll
   for (int q = 0; q < NPR; ++q) acc[q] = 0.0;
-  for (long v = v0 + threadIdx.x; v < v1; v += kTrainBlock) {
-    const int pw = (int)(v % Pw);
-    long t = v / Pw;
-    const int ph = (int)(t % Ph);
-    t /= Ph;
-    const int pd = (int)(t % Pd);
-    const int b = (int)(t / Pd);
+  // voxel coordinates advance incrementally (one division per thread, not three per voxel)
+  long v = v0 + threadIdx.x;
+  int pw = (int)(v % Pw), ph, pd, b;
+  {
+    const long t = v / Pw;
+    ph = (int)(t % Ph);
+    pd = (int)((t / Ph) % Pd);
+    b = (int)(t / ((long)Ph * Pd));
+  }
+  for (; v < v1; v += kTrainBlock) {
     const int gd = pd * stride - 1 + kd, gh = ph * stride - 1 + kh, gw = pw * stride - 1 + kw;
-    if (gd < 0 || gh < 0 || gw < 0 || gd >= Gd || gh >= Gh || gw >= Gw) continue;
-    const float* gp = gath + ((((size_t)b * Gd + gd) * Gh + gh) * Gw + gw) * BC;
+    const bool ok = gd >= 0 && gh >= 0 && gw >= 0 && gd < Gd && gh < Gh && gw < Gw;
+    const long vv = v;
+    const float* gp = gath + ((((size_t)b * Gd + gd) * Gh + gh) * Gw + gw) * BC;  // used only when ok
+    pw += kTrainBlock;
+    while (pw >= Pw) {
+      pw -= Pw;
+      if (++ph == Ph) {
+        ph = 0;
+        if (++pd == Pd) {
+          pd = 0;
+          ++b;
+        }
+      }
+    }
+    if (!ok) continue;
     float dv[A], gv[BC];
 #pragma unroll
-    for (int a = 0; a < A; ++a) dv[a] = direct[v * A + a];
+    for (int a = 0; a < A; ++a) dv[a] = direct[vv * A + a];
 #pragma unroll
     for (int c = 0; c < BC; ++c) gv[c] = gp[c];
 #pragma unroll
@@ -327,11 +346,22 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_small_kernel(
 // dw[i] = sum_j partial[j][i], j = 0..nblk-1 in order (fp64 accumulation)
 __global__ __launch_bounds__(kTrainBlock) void sum_partials_kernel(const double* __restrict__ partial, int nblk, long n,
                                                                    float* __restrict__ out) {
-  const long i = (long)blockIdx.x * kTrainBlock + threadIdx.x;
-  if (i >= n) return;
+  // 32 outputs per block; 8 interleaved chains (partial j in chain j % 8), then the chains in order:
+  // a fixed order (bitwise reproducible) with 8x the loads in flight of one serial chain
+  __shared__ double red[8][32];
+  const int g = threadIdx.x >> 5, q = threadIdx.x & 31;
+  const long i = (long)blockIdx.x * 32 + q;
   double s = 0.0;
-  for (int j = 0; j < nblk; ++j) s += partial[(size_t)j * n + i];
-  out[i] = (float)s;
+  if (i < n)
+    for (int j = g; j < nblk; j += 8) s += partial[(size_t)j * n + i];
+  red[g][q] = s;
+  __syncthreads();
+  if (g == 0 && i < n) {
+    double t = red[0][q];
+#pragma unroll
+    for (int c = 1; c < 8; ++c) t += red[c][q];
+    out[i] = (float)t;
+  }
 }
 
 // ---------------------------------------------------------------- BatchNorm3d, train mode
@@ -534,7 +564,7 @@ static int launch_wgrad(const float* direct, const float* gath, int B, int Pd, i
                        Ph, Pw, Gd, Gh, Gw, stride, vpb, ws);
   TMVS_CHECK_LAUNCH();
   const long n = 27L * A * BC;
-  hipLaunchKernelGGL(sum_partials_kernel, dim3((unsigned)((n + kTrainBlock - 1) / kTrainBlock)), dim3(kTrainBlock), 0,
+  hipLaunchKernelGGL(sum_partials_kernel, dim3((unsigned)((n + 31) / 32)), dim3(kTrainBlock), 0,
                      st, ws, nblk, n, dw);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;

@@ -175,23 +175,23 @@ __global__ __launch_bounds__(kTB) void token_wgrad_kernel(const float* __restric
   }
 }
 
-// out0[i] (i < n0) / out1[i - n0] = sum over the block partials: 8 interleaved chains (block j in chain j % 8),
-// then the 8 chain sums in order -- a fixed order, bitwise reproducible
+// out0[i] (i < n0) / out1[i - n0] = sum over the block partials: 16 interleaved chains (block j in chain
+// j % 16), then the 16 chain sums in order -- a fixed order, bitwise reproducible
 __global__ __launch_bounds__(kTB) void fmt_sum_partials_kernel(const double* __restrict__ partial, int nblk, long n,
                                                                long n0, float* __restrict__ out0,
                                                                float* __restrict__ out1, int accumulate) {
-  __shared__ double red[8][32];
-  const int g = threadIdx.x >> 5, k = threadIdx.x & 31;
-  const long i = (long)blockIdx.x * 32 + k;
+  __shared__ double red[16][16];
+  const int g = threadIdx.x >> 4, k = threadIdx.x & 15;
+  const long i = (long)blockIdx.x * 16 + k;
   double s = 0.0;
   if (i < n)
-    for (int j = g; j < nblk; j += 8) s += partial[(size_t)j * n + i];
+    for (int j = g; j < nblk; j += 16) s += partial[(size_t)j * n + i];
   red[g][k] = s;
   __syncthreads();
   if (g == 0 && i < n) {
     double t = red[0][k];
 #pragma unroll
-    for (int q = 1; q < 8; ++q) t += red[q][k];
+    for (int q = 1; q < 16; ++q) t += red[q][k];
     float* o = i < n0 ? out0 + i : out1 + (i - n0);
     *o = accumulate ? *o + (float)t : (float)t;
   }
@@ -463,7 +463,7 @@ extern "C" int tmvs_token_wgrad(const float* dy, int a, const float* x, int b, l
   if (a == A && b == B) {                                                                                       \
     hipLaunchKernelGGL((token_wgrad_kernel<A, B, TA, TB>), dim3(nblk), dim3(kTB), 0, st, dy, x, tokens, c, part); \
     TMVS_CHECK_LAUNCH();                                                                                        \
-    hipLaunchKernelGGL(fmt_sum_partials_kernel, dim3((A * B + A + 31) / 32), dim3(kTB), 0, st,                 \
+    hipLaunchKernelGGL(fmt_sum_partials_kernel, dim3((A * B + A + 15) / 16), dim3(kTB), 0, st,                 \
                        (const double*)part, nblk, (long)(A * B + A), (long)(A * B), dw, db, accumulate);        \
     TMVS_CHECK_LAUNCH();                                                                                        \
     return TMVS_OK;                                                                                             \
@@ -495,7 +495,7 @@ extern "C" int tmvs_layer_norm_bwd(const float* dy, const float* x, long tokens,
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(layer_norm_bwd_kernel, dim3(nblk), dim3(kTB), 0, st, dy, x, tokens, g, c, dx, (double*)workspace);
   TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(fmt_sum_partials_kernel, dim3(2), dim3(kTB), 0, st, (const double*)workspace, nblk, 64L, 64L, dgb,
+  hipLaunchKernelGGL(fmt_sum_partials_kernel, dim3(4), dim3(kTB), 0, st, (const double*)workspace, nblk, 64L, 64L, dgb,
                      dgb, accumulate);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
