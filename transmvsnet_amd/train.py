@@ -1,10 +1,12 @@
 """Training path: the differentiable blocks that run on HIP.
 
+* ``fmt_train``: the FMT (models/FMT.py:96-177, 8 EncoderLayers) with its backward on the token
+  kernels of csrc/fmt_train.hip (``_encoder_layer_backward``); ``pathway_train``: FMT_with_pathway's
+  lateral steps (FMT.py:201-228) with their backward (csrc/pathway_train.hip + the generic convs).
 * ``warp_corr_views``: the per-view similarity volumes of DepthNet (homo_warping + (warped *
   ref).mean(1), models/module.py:284-322, TransMVSNet.py:80) with the backward into the reference
   and source features (tmvs_warp_corr_backward: gather for the reference, deterministic
-  fixed-point scatter for the sources). The view aggregation and the stage-1 PixelwiseNet that
-  consume these volumes are small elementwise / 1x1 work left to torch autograd.
+  fixed-point scatter for the sources, flushed wave-cooperatively).
 * ``costregnet_train``: CostRegNet in train mode with its backward on csrc/costreg_train.hip.
 * ``depth_stages_train``: the three DepthNet stages of a training step (models/TransMVSNet.py:38-109,
   174-221) from the FMT/pathway features to trans_mvsnet_loss (module.py:532-556) and its backward:
