@@ -18,5 +18,5 @@ tail -1 $OUT/bench.json | cut -c1-400
 timeout -k 10 300 python bench.py --gpus 2 --dist-backend gloo --mode views --steps 5 --warmup 2 --e2e-steps 0 \
     > $OUT/bench_views2_gloo.json 2> $OUT/bench_views2_gloo.err || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --e2e-steps 0 > $OUT/trace.log 2>&1 || exit $?
+    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --e2e-steps 0 --train-steps 0 > $OUT/trace.log 2>&1 || exit $?
 exit $rc

@@ -68,9 +68,19 @@ class _WarpCorrViews(torch.autograd.Function):
     def backward(ctx, dsims):
         ref, src, hyp = ctx.saved_tensors
         dref, dsrc, flag = ops.warp_corr_backward(ref, src, ctx.proj12, hyp, dsims.contiguous(), ctx.rot_order)
-        if int(flag.item()):
-            raise RuntimeError("warp_corr_backward: a gradient contribution exceeded the fixed-point range (2^22)")
+        if _DEFERRED_FLAGS is not None:  # inside depth_stages_train: one host sync after the whole backward
+            _DEFERRED_FLAGS.append(flag.clone())
+        else:
+            _check_overflow([flag])
         return dref, dsrc, None, None, None
+
+
+_DEFERRED_FLAGS = None
+
+
+def _check_overflow(flags):
+    if flags and int(torch.stack([f.reshape(()) for f in flags]).sum().item()):
+        raise RuntimeError("warp_corr_backward: a gradient contribution exceeded the fixed-point range (2^22)")
 
 
 def warp_corr_views(ref_nhwc, src_nhwc, hyp, proj12, rot_order="auto"):
@@ -488,7 +498,14 @@ def depth_stages_train(model, stage_features, proj_matrix, depth_values, depth_g
             prev_raw = raw
         total, depth_loss, _, _, grads = loss_mod.trans_mvsnet_loss(outputs, depth_gt_ms, mask_ms, dlossw=dlossw,
                                                                     return_grad=True)
-        torch.autograd.backward(logits_all, [grads[f"stage{s + 1}"] for s in range(3)])
+        global _DEFERRED_FLAGS
+        _DEFERRED_FLAGS = []
+        try:
+            torch.autograd.backward(logits_all, [grads[f"stage{s + 1}"] for s in range(3)])
+            flags = _DEFERRED_FLAGS
+        finally:
+            _DEFERRED_FLAGS = None
+        _check_overflow(flags)
     return total, outputs
 
 
