@@ -168,3 +168,30 @@ def test_host_rot_order_matches_torch_matmul():
     else:
         emu = (r0 * x + r1 * y) + r2
     assert (emu == got.numpy()).mean() == 1.0
+
+
+def test_training_host_logic():
+    """Training-path host logic (no GPU): the FMT weight block _FMTTrain packs from the 16 layer
+    parameters is exactly EncoderLayer.packed() (the tmvs_fmt_* layout, include/transmvs.h
+    TMVS_ENC_*); fmt_params walks the 8 layers in _ENC_PARAMS order; every training entry point
+    refuses CPU tensors instead of falling back."""
+    import torch
+    from transmvsnet_amd import TransMVSNet
+    from transmvsnet_amd.train import (_ENC_PARAMS, _pack_enc, costregnet_train, fmt_params, fmt_train,
+                                       pathway_train, warp_corr_views)
+    m = TransMVSNet()
+    layers = m.FMT_with_pathway.FMT.layers
+    ps = fmt_params(m)
+    assert len(ps) == 8 * len(_ENC_PARAMS) == 128
+    for i, layer in enumerate(layers):
+        named = dict(layer.named_parameters())
+        assert all(ps[16 * i + j] is named[n] for j, n in enumerate(_ENC_PARAMS))
+        assert torch.equal(_pack_enc(ps[16 * i:16 * i + 16]), layer.packed())
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        fmt_train(m, torch.zeros(3, 32, 8, 10))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        warp_corr_views(torch.zeros(8, 10, 32), torch.zeros(2, 8, 10, 32), torch.zeros(4, 8, 10), None)
+    with pytest.raises(RuntimeError):
+        costregnet_train(m.cost_regularization[0], torch.zeros(1, 8, 16, 16))
+    with pytest.raises(RuntimeError):
+        pathway_train(m, torch.zeros(3, 8, 10, 32), torch.zeros(3, 16, 16, 20), torch.zeros(3, 8, 32, 40))
