@@ -760,11 +760,22 @@ __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restr
           tp[t] = sv + ((size_t)(in[t] ? ty[t] : 0) * W + (in[t] ? tx[t] : 0)) * C;
         }
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-          const float a = in[0] ? tp[0][c] : 0.f, b = in[1] ? tp[1][c] : 0.f;
-          const float cc = in[2] ? tp[2][c] : 0.f, dd = in[3] ? tp[3][c] : 0.f;
-          const float val = fmaf(dd, wt[3], fmaf(cc, wt[2], fmaf(b, wt[1], a * wt[0])));
-          dr[c] = fmaf(g, val, dr[c]);
+        for (int c4 = 0; c4 < C / 4; ++c4) {  // rows are 16-B aligned (C % 4 == 0): one float4 per tap quad
+          // unconditional loads (an outside tap points at pixel 0, always valid), zeroed after: no
+          // per-element branches around the loads
+          const float4 a4 = *reinterpret_cast<const float4*>(tp[0] + 4 * c4);
+          const float4 b4 = *reinterpret_cast<const float4*>(tp[1] + 4 * c4);
+          const float4 c4v = *reinterpret_cast<const float4*>(tp[2] + 4 * c4);
+          const float4 d4 = *reinterpret_cast<const float4*>(tp[3] + 4 * c4);
+          const float av[4] = {in[0] ? a4.x : 0.f, in[0] ? a4.y : 0.f, in[0] ? a4.z : 0.f, in[0] ? a4.w : 0.f};
+          const float bv[4] = {in[1] ? b4.x : 0.f, in[1] ? b4.y : 0.f, in[1] ? b4.z : 0.f, in[1] ? b4.w : 0.f};
+          const float cv[4] = {in[2] ? c4v.x : 0.f, in[2] ? c4v.y : 0.f, in[2] ? c4v.z : 0.f, in[2] ? c4v.w : 0.f};
+          const float dv4[4] = {in[3] ? d4.x : 0.f, in[3] ? d4.y : 0.f, in[3] ? d4.z : 0.f, in[3] ? d4.w : 0.f};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float val = fmaf(dv4[e], wt[3], fmaf(cv[e], wt[2], fmaf(bv[e], wt[1], av[e] * wt[0])));
+            dr[4 * c4 + e] = fmaf(g, val, dr[4 * c4 + e]);
+          }
         }
       }
       // scatter coefficients w_tap * g, summed per source pixel across consecutive planes: the 4 taps
