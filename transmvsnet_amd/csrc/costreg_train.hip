@@ -38,10 +38,15 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_generic_kernel(
     int Wo, int stride, int transposed, int accumulate, float* __restrict__ y) {
   const int cob = blockIdx.y;
   const long nvox = (long)B * Do * Ho * Wo;
-  const long v = (long)blockIdx.x * kTrainBlock + threadIdx.x;
-  if (v >= nvox) return;
-  const int ow = (int)(v % Wo);
-  long t = v / Wo;
+  const long vl = (long)blockIdx.x * kTrainBlock + threadIdx.x;
+  if (vl >= nvox) return;
+  int ow = (int)(vl % Wo);
+  if (transposed && stride == 2) {  // even columns first, then odd: a wave's lanes share the kw tap set
+    const int ne = (Wo + 1) / 2;
+    ow = ow < ne ? 2 * ow : 2 * (ow - ne) + 1;
+  }
+  const long v = vl - (long)(vl % Wo) + ow;
+  long t = vl / Wo;
   const int oh = (int)(t % Ho);
   t /= Ho;
   const int od = (int)(t % Do);
