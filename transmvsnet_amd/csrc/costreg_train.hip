@@ -348,6 +348,103 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_small_kernel(
   if ((int)threadIdx.x < NPR) partial[((size_t)blockIdx.x * 27 + k) * NPR + threadIdx.x] = red[threadIdx.x][0];
 }
 
+// Few (a, b) pairs, one kd plane of taps per block row (grid.y = 3): a thread reads its voxel's
+// `direct` row once per kd and the 9 neighbours' `gathered` rows (L1/L2 hits), keeping 9 x A x BC fp32
+// sums over its voxels; then per value a fixed wave butterfly (fp64) and the 4 waves in order.
+// Replaces 27 passes over `direct` with 3.
+template <int A, int BC>
+__global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_taps_kernel(
+    const float* __restrict__ direct, const float* __restrict__ gath, int B, int Pd, int Ph, int Pw, int Gd, int Gh,
+    int Gw, int stride, long vpb, double* __restrict__ partial) {
+  constexpr int NPR = A * BC;
+  __shared__ double red[9 * NPR][kTrainBlock / 64];
+  const int kd = blockIdx.y;
+  const long nvox = (long)B * Pd * Ph * Pw;
+  const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
+  float acc[9][NPR];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) acc[k][q] = 0.f;
+  long v = v0 + threadIdx.x;
+  int pw = (int)(v % Pw), ph, pd, b;
+  {
+    const long t = v / Pw;
+    ph = (int)(t % Ph);
+    pd = (int)((t / Ph) % Pd);
+    b = (int)(t / ((long)Ph * Pd));
+  }
+  for (; v < v1; v += kTrainBlock) {
+    float dv[A];
+    if constexpr (A % 4 == 0) {
+#pragma unroll
+      for (int a = 0; a < A; a += 4) {
+        const float4 t4 = *reinterpret_cast<const float4*>(direct + v * A + a);
+        dv[a] = t4.x;
+        dv[a + 1] = t4.y;
+        dv[a + 2] = t4.z;
+        dv[a + 3] = t4.w;
+      }
+    } else {
+#pragma unroll
+      for (int a = 0; a < A; ++a) dv[a] = direct[v * A + a];
+    }
+    const float* gb = gath + (size_t)b * Gd * Gh * Gw * BC;
+    const int gd = pd * stride - 1 + kd;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int gh = ph * stride - 1 + k / 3, gw = pw * stride - 1 + k % 3;
+      const bool ok = gd >= 0 && gh >= 0 && gw >= 0 && gd < Gd && gh < Gh && gw < Gw;
+      const float* gp = gb + (ok ? (((size_t)gd * Gh + gh) * Gw + gw) * BC : 0);  // always a valid address
+      float gv[BC];  // unconditional loads, zeroed after: no branch per load
+      if constexpr (BC % 4 == 0) {
+#pragma unroll
+        for (int c = 0; c < BC; c += 4) {
+          const float4 t4 = *reinterpret_cast<const float4*>(gp + c);
+          gv[c] = ok ? t4.x : 0.f;
+          gv[c + 1] = ok ? t4.y : 0.f;
+          gv[c + 2] = ok ? t4.z : 0.f;
+          gv[c + 3] = ok ? t4.w : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < BC; ++c) {
+          const float t1 = gp[c];
+          gv[c] = ok ? t1 : 0.f;
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < A; ++a)
+#pragma unroll
+        for (int c = 0; c < BC; ++c) acc[k][a * BC + c] = fmaf(dv[a], gv[c], acc[k][a * BC + c]);
+    }
+    pw += kTrainBlock;
+    while (pw >= Pw) {
+      pw -= Pw;
+      if (++ph == Ph) {
+        ph = 0;
+        if (++pd == Pd) {
+          pd = 0;
+          ++b;
+        }
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      double x = (double)acc[k][q];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+      if (lane == 0) red[k * NPR + q][wv] = x;
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 9 * NPR; i += kTrainBlock)
+    partial[((size_t)blockIdx.x * 27 + kd * 9) * NPR + i] = (red[i][0] + red[i][1]) + (red[i][2] + red[i][3]);
+}
+
 // dw[i] = sum_j partial[j][i], j = 0..nblk-1 in order (fp64 accumulation)
 __global__ __launch_bounds__(kTrainBlock) void sum_partials_kernel(const double* __restrict__ partial, int nblk, long n,
                                                                    float* __restrict__ out) {
@@ -558,7 +655,10 @@ static int launch_wgrad(const float* direct, const float* gath, int B, int Pd, i
   const long nvox = (long)B * Pd * Ph * Pw;
   const long vpb = wgrad_vpb(nvox);
   const int nblk = (int)((nvox + vpb - 1) / vpb);
-  if constexpr (A * BC <= 16)
+  if constexpr (A * BC <= 8)
+    hipLaunchKernelGGL((conv3d_wgrad_taps_kernel<A, BC>), dim3(nblk, 3), dim3(kTrainBlock), 0, st, direct, gath, B,
+                       Pd, Ph, Pw, Gd, Gh, Gw, stride, vpb, ws);
+  else if constexpr (A * BC <= 16)
     hipLaunchKernelGGL((conv3d_wgrad_small_kernel<A, BC>), dim3(nblk, 27), dim3(kTrainBlock), 0, st, direct, gath, B,
                        Pd, Ph, Pw, Gd, Gh, Gw, stride, vpb, ws);
   else if constexpr (A >= 8 && BC >= 8)
