@@ -372,14 +372,20 @@ __global__ __launch_bounds__(kTB) void linattn_bwd_q_kernel(const float* __restr
   }
 }
 
-// dkv[g][i] = sum over the blocks of group g (in order) of partial[blk][i]
+// dkv[g][i] = sum over the blocks of group g of partial[blk][i]: 4 interleaved chains (block j in chain
+// j % 4) combined as (c0 + c1) + (c2 + c3) -- a fixed order
 __global__ void linattn_group_combine_kernel(const double* __restrict__ partial, int blocks_per_group,
                                              float* __restrict__ dkv) {
   const int g = blockIdx.x, i = threadIdx.x;
   if (i >= 160) return;
-  double s = 0.0;
-  for (int j = 0; j < blocks_per_group; ++j) s += partial[((size_t)g * blocks_per_group + j) * 160 + i];
-  dkv[(size_t)g * 160 + i] = (float)s;
+  const double* p = partial + (size_t)g * blocks_per_group * 160 + i;
+  double c[4] = {0.0, 0.0, 0.0, 0.0};
+  int j = 0;
+  for (; j + 4 <= blocks_per_group; j += 4)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) c[u] += p[(size_t)(j + u) * 160];
+  for (; j < blocks_per_group; ++j) c[j & 3] += p[(size_t)j * 160];
+  dkv[(size_t)g * 160 + i] = (float)((c[0] + c[1]) + (c[2] + c[3]));
 }
 
 // source side: dK[s,h,d] = sum_m dKV[h][m][d] V[s,h,m] + dKs[h][d]; dV[s,h,m] = sum_d dKV[h][m][d] K[s,h,d]
@@ -482,7 +488,7 @@ extern "C" int tmvs_layer_norm_fwd(const float* x, long tokens, const float* g, 
 }
 
 extern "C" size_t tmvs_layer_norm_bwd_workspace(long tokens) {
-  const long c = tok_chunk(tokens, 1024);
+  const long c = tok_chunk(tokens, 1024, 256);
   return (size_t)((tokens + c - 1) / c) * 64 * sizeof(double);
 }
 
@@ -490,7 +496,7 @@ extern "C" int tmvs_layer_norm_bwd(const float* dy, const float* x, long tokens,
                                    size_t workspace_bytes, float* dx, float* dgb, int accumulate, void* stream) {
   if (!dy || !x || !g || !workspace || !dx || !dgb || tokens <= 0) return TMVS_ERR_ARG;
   if (workspace_bytes < tmvs_layer_norm_bwd_workspace(tokens)) return TMVS_ERR_ARG;
-  const long c = tok_chunk(tokens, 1024);
+  const long c = tok_chunk(tokens, 1024, 256);
   const int nblk = (int)((tokens + c - 1) / c);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(layer_norm_bwd_kernel, dim3(nblk), dim3(kTB), 0, st, dy, x, tokens, g, c, dx, (double*)workspace);
@@ -512,7 +518,7 @@ extern "C" int tmvs_linattn_fwd(const float* q, long tokens, long tokens_per_gro
 
 // blocks of tpb tokens that never straddle a group: tpb divides tokens_per_group
 static long group_chunk(long tpg) {
-  long c = 1024;
+  long c = 256;  // one token per thread per head: ~4 blocks per CU at the C5 size
   while (c > 1 && tpg % c) c >>= 1;
   while (tpg / c > 512 && tpg % (2 * c) == 0) c *= 2;
   return c;
