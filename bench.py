@@ -370,6 +370,7 @@ def train_timing(steps, dev, world):
     gt = {f"stage{s + 1}": (425.0 + 500.0 * torch.rand(1, h5 >> (2 - s), w5 >> (2 - s), generator=g)).to(dev)
           for s in range(3)}
     mask = {k: torch.ones_like(v) for k, v in gt.items()}
+    dint = float(dv[0, 1] - dv[0, 0])  # the sample's depth_interval (finetune.py:159)
     params = [p for n, p in m.named_parameters()
               if n.startswith(("cost_regularization.", "DepthNet.", "FMT_with_pathway."))]
     ts = []
@@ -380,7 +381,8 @@ def train_timing(steps, dev, world):
         e0.record()
         st1 = fmt_train(m, leaves["stage1"])
         st2, st3 = pathway_train(m, st1, leaves["stage2"], leaves["stage3"])
-        depth_stages_train(m, {"stage1": st1, "stage2": st2, "stage3": st3}, proj, dv, gt, mask, (h5, w5))
+        depth_stages_train(m, {"stage1": st1, "stage2": st2, "stage3": st3}, proj, dv, gt, mask, (h5, w5),
+                           dlossw=(1.0, 1.0, 1.0), loss="focal_bld", depth_interval=dint)
         allreduce_gradients(params)
         e1.record()
         torch.cuda.synchronize()
@@ -398,7 +400,8 @@ def train_timing(steps, dev, world):
                         "features, forward + backward on HIP of the FMT (8 encoder layers), FMT_with_pathway's "
                         "lateral steps and the "
                         "DepthNet stages (hypotheses, per-view cost volumes + backward, view aggregation + train-mode "
-                        "PixelwiseNet + backward, CostRegNet train fwd/bwd, softmax/WTA, trans_mvsnet_loss + "
+                        "PixelwiseNet + backward, CostRegNet train fwd/bwd, softmax/WTA, focal_loss_bld with dlossw "
+                        "1,1,1 (finetune.py:42,159) + "
                         "d/dlogits) + DDP gradient all-reduce; FeatureNet's backward is not included (not native "
                         "yet)"}
 

@@ -302,13 +302,15 @@ def test_pathway_train_forward_backward():
     assert all(v < 1e-4 for v in rep.values()), rep
 
 
-@pytest.mark.parametrize("with_fmt", [False, True])
-def test_training_step_from_fmt_output(with_fmt):
+@pytest.mark.parametrize("with_fmt,loss", [(False, "trans_mvsnet"), (True, "trans_mvsnet"), (True, "focal_bld")])
+def test_training_step_from_fmt_output(with_fmt, loss):
     """The training step from the FMT output (with_fmt: from FeatureNet's stage-1 output, the FMT's 8
     encoder layers included) and FeatureNet's stage-2/3 features on: FMT_with_pathway's lateral steps,
     then the three DepthNet stages and trans_mvsnet_loss (all HIP), against torch autograd through the
     same chain on the CPU (128x160, N=3, 8/8/8): loss, d stage-1 input, d FeatureNet stage-2/3
-    features, the pathway (and FMT) weight gradients (1e-3 of max magnitude)."""
+    features, the pathway (and FMT) weight gradients (1e-3 of max magnitude). loss="focal_bld" is
+    config C5's loss (finetune.py:159, focal_loss_bld with dlossw 1,1,1) and also checks its EPE /
+    less1 / less3 against the reference's."""
     import torch.nn.functional as F
     from oracle import loss_ref
     from transmvsnet_amd import TransMVSNet, synthetic
@@ -330,11 +332,14 @@ def test_training_step_from_fmt_output(with_fmt):
     a2, a3 = s2.to(DEV).requires_grad_(), s3.to(DEV).requires_grad_()
     st1 = fmt_train(model, a1) if with_fmt else a1
     st2, st3 = pathway_train(model, st1, a2, a3)
-    total, _ = depth_stages_train(model, {"stage1": st1, "stage2": st2, "stage3": st3}, proj, dv.to(DEV),
-                                  {k: v.to(DEV) for k, v in gt.items()}, {k: v.to(DEV) for k, v in mask.items()},
-                                  (H, W))
+    dlossw = (1.0, 1.0, 1.0) if loss == "focal_bld" else (0.5, 1.0, 2.0)
+    dint = float(dv[0, 1] - dv[0, 0])
+    total, outs = depth_stages_train(model, {"stage1": st1, "stage2": st2, "stage3": st3}, proj, dv.to(DEV),
+                                     {k: v.to(DEV) for k, v in gt.items()}, {k: v.to(DEV) for k, v in mask.items()},
+                                     (H, W), dlossw=dlossw, loss=loss, depth_interval=dint)
     torch.cuda.synchronize()
     P = "FMT_with_pathway."
+    metrics = {}
 
     def reference(dt):
         rsd = {k: (v.to(dt).clone().requires_grad_() if v.is_floating_point() and "running" not in k
@@ -362,9 +367,14 @@ def test_training_step_from_fmt_output(with_fmt):
             logits = oracle.cost_reg_net(rsd, f"cost_regularization.{s}.", sim, training=True)[:, 0]
             prob = torch.exp(F.log_softmax(logits, dim=1))
             depth = torch.gather(hyp, 1, prob.argmax(1, keepdim=True)).squeeze(1)
-            outputs[name] = {"prob_volume": prob, "depth_values": hyp}
-        tot = loss_ref.trans_mvsnet_loss(outputs, {k: v.to(dt) for k, v in gt.items()},
-                                         {k: v.to(dt) for k, v in mask.items()}, dlossw=(0.5, 1.0, 2.0))[0]
+            outputs[name] = {"prob_volume": prob, "depth_values": hyp, "depth": depth.clamp(425.0, 935.0)}
+        gtd, mkd = {k: v.to(dt) for k, v in gt.items()}, {k: v.to(dt) for k, v in mask.items()}
+        if loss == "focal_bld":
+            res = loss_ref.focal_loss_bld(outputs, gtd, mkd, dint, dlossw=dlossw)
+            metrics[dt] = [float(x) for x in res[1:]]
+        else:
+            res = loss_ref.trans_mvsnet_loss(outputs, gtd, mkd, dlossw=dlossw)
+        tot = res[0]
         tot.backward()
         grads = {"d_stage1_input": c1.grad, "d_stage2": c2.grad, "d_stage3": c3.grad}
         grads.update({n: rsd[n].grad for n in sd if n.startswith(P) and rsd[n].grad is not None})
@@ -381,6 +391,10 @@ def test_training_step_from_fmt_output(with_fmt):
     got.update({n: params[n].grad for n in names if n.startswith(P)})
     rep = {"loss": abs(float(total) - ref_total) / abs(ref_total)}
     assert rep["loss"] < 1e-5, rep
+    if loss == "focal_bld":  # depth_loss, epe, less1, less3 of the stage-3 WTA depth
+        got_m = [float(outs["metrics"][k]) for k in ("depth_loss", "epe", "less1", "less3")]
+        # (a near-tie WTA flip moves one pixel of 20,480: rtol 1e-3)
+        assert np.allclose(got_m, metrics[torch.float32], rtol=1e-3, atol=1e-4), (got_m, metrics[torch.float32])
     if not with_fmt:
         rep.update({n: _rel(got[n], r32[n]) for n in names})
         print(rep)

@@ -464,16 +464,22 @@ def aggregate_train(sims, model, vw_given=None, vw_shift=0):
 
 
 def depth_stages_train(model, stage_features, proj_matrix, depth_values, depth_gt_ms, mask_ms, img_hw,
-                       dlossw=(0.5, 1.0, 2.0)):
+                       dlossw=(0.5, 1.0, 2.0), loss="trans_mvsnet", depth_interval=None):
     """One training step's DepthNet stages for ONE sample (B = 1), forward and backward.
 
     stage_features: {stage: [N, h, w, C]} NHWC FMT/pathway outputs, reference view first (leaf tensors
     that require grad collect d loss / d features); proj_matrix {stage: [1, N, 2, 4, 4]}; depth_values
     [1, 192]; depth_gt_ms / mask_ms {stage: [1, h, w]}. The CostRegNets and the PixelwiseNet run in train
-    mode (their BatchNorm running statistics are updated). Calls backward of trans_mvsnet_loss (dlossw:
-    train.py's default) and returns (total_loss, outputs) with outputs as TransMVSNet.forward's stage
-    dicts.
+    mode (their BatchNorm running statistics are updated). Calls backward of the loss and returns
+    (total_loss, outputs) with outputs as TransMVSNet.forward's stage dicts. loss="trans_mvsnet":
+    train.py:152's trans_mvsnet_loss (dlossw default 0.5,1,2); loss="focal_bld": finetune.py:159's
+    focal_loss_bld for BlendedMVS (config C5; pass dlossw=(1, 1, 1), finetune.py:42, and the sample's
+    depth_interval) -- outputs["metrics"] then holds its (depth_loss, epe, less1, less3).
     """
+    if loss not in ("trans_mvsnet", "focal_bld"):
+        raise ValueError(f"depth_stages_train: loss must be 'trans_mvsnet' or 'focal_bld', got {loss!r}")
+    if loss == "focal_bld" and depth_interval is None:
+        raise ValueError("depth_stages_train: focal_bld needs depth_interval")
     from . import loss as loss_mod
     from .model import DEPTH_CLAMP, STAGE_SCALES
     dev = stage_features["stage1"].device
@@ -496,8 +502,13 @@ def depth_stages_train(model, stage_features, proj_matrix, depth_values, depth_g
             outputs[name] = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}
             logits_all.append(logits)
             prev_raw = raw
-        total, depth_loss, _, _, grads = loss_mod.trans_mvsnet_loss(outputs, depth_gt_ms, mask_ms, dlossw=dlossw,
-                                                                    return_grad=True)
+        if loss == "focal_bld":
+            total, depth_loss, epe, less1, less3, grads = loss_mod.focal_loss_bld(
+                outputs, depth_gt_ms, mask_ms, depth_interval, dlossw=dlossw, return_grad=True)
+            outputs["metrics"] = {"depth_loss": depth_loss, "epe": epe, "less1": less1, "less3": less3}
+        else:
+            total, depth_loss, _, _, grads = loss_mod.trans_mvsnet_loss(outputs, depth_gt_ms, mask_ms, dlossw=dlossw,
+                                                                        return_grad=True)
         global _DEFERRED_FLAGS
         _DEFERRED_FLAGS = []
         try:
