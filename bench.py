@@ -355,7 +355,7 @@ def train_timing(steps, dev, world):
     (transmvsnet_amd.train.fmt_train + pathway_train + depth_stages_train), plus DDP's gradient
     all-reduce when world > 1. HIP events, median of `steps` after 1 warm-up; max over ranks."""
     from transmvsnet_amd import TransMVSNet, synthetic
-    from transmvsnet_amd.train import allreduce_gradients, depth_stages_train, fmt_train, pathway_train
+    from transmvsnet_amd.train import FlatAdam, depth_stages_train, fmt_train, pathway_train
     h5, w5, n5 = 576, 768, 4
     m = TransMVSNet()
     m.load_state_dict(synthetic.synthetic_state_dict(synthetic.state_dict_shapes(m), seed=0, sharpen=100.0))
@@ -373,17 +373,20 @@ def train_timing(steps, dev, world):
     dint = float(dv[0, 1] - dv[0, 0])  # the sample's depth_interval (finetune.py:159)
     params = [p for n, p in m.named_parameters()
               if n.startswith(("cost_regularization.", "DepthNet.", "FMT_with_pathway."))]
+    opt = FlatAdam(params, lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4)  # finetune.py:27,29,324
     ts = []
     for i in range(steps + 1):
-        for p in params + list(leaves.values()):
+        for p in leaves.values():
             p.grad = None
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
+        opt.zero_grad()  # train_sample's optimizer.zero_grad() (finetune.py:146)
         st1 = fmt_train(m, leaves["stage1"])
         st2, st3 = pathway_train(m, st1, leaves["stage2"], leaves["stage3"])
         depth_stages_train(m, {"stage1": st1, "stage2": st2, "stage3": st3}, proj, dv, gt, mask, (h5, w5),
                            dlossw=(1.0, 1.0, 1.0), loss="focal_bld", depth_interval=dint)
-        allreduce_gradients(params)
+        opt.allreduce()
+        opt.step()
         e1.record()
         torch.cuda.synchronize()
         if i > 0:
@@ -402,8 +405,8 @@ def train_timing(steps, dev, world):
                         "DepthNet stages (hypotheses, per-view cost volumes + backward, view aggregation + train-mode "
                         "PixelwiseNet + backward, CostRegNet train fwd/bwd, softmax/WTA, focal_loss_bld with dlossw "
                         "1,1,1 (finetune.py:42,159) + "
-                        "d/dlogits) + DDP gradient all-reduce; FeatureNet's backward is not included (not native "
-                        "yet)"}
+                        "d/dlogits) + DDP gradient all-reduce (one flat buffer) + Adam step (tmvs_adam_step, "
+                        "finetune.py:324); FeatureNet's backward is not included (not native yet)"}
 
 
 def host_cores():

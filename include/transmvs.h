@@ -325,6 +325,12 @@ int tmvs_linattn_bwd_q(const float* q, const float* dmsg, long tokens, long toke
 int tmvs_linattn_bwd_kv(const float* k, const float* v, long tokens, long tokens_per_group, const float* dkv,
                         float* dk, float* dv, void* stream);
 
+/* Adam over one flat fp32 buffer (finetune.py:324: torch.optim.Adam, L2 weight decay, no amsgrad),
+ * torch's single-tensor update order; step >= 1 is the 1-based step count (bias corrections).
+ * Scalars are doubles, as the Python floats torch receives (1 - beta is formed before rounding).  */
+int tmvs_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, double lr,
+                   double beta1, double beta2, double eps, double weight_decay, int step, void* stream);
+
 /* BatchNorm3d in train mode over z [nvox][C] (C divides 256): batch mean and biased variance
  * (fp64 partials, fixed-order combine); y = relu(fmaf(z, a, b)) [+ skip] with a = gamma /
  * sqrt(var + eps), b = beta - mean * a; the backward of that (incl. the ReLU mask) gives dz,

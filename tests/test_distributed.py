@@ -128,13 +128,23 @@ def _grad_worker(rank, world, port, q):
         for p in params:
             p.grad = torch.randn(p.shape, generator=g)
         allreduce_gradients(params, bucket_bytes=1024)  # forces several buckets
-        q.put((rank, [p.grad.clone() for p in params]))
+        got = [p.grad.clone() for p in params]
+        # the same sync on FlatAdam's single flat gradient buffer (its parameters are views of one buffer)
+        from transmvsnet_amd.train import FlatAdam
+        g = torch.Generator().manual_seed(100 + rank)
+        params2 = [torch.nn.Parameter(torch.zeros(n)) for n in (5, 300, 7)]
+        opt = FlatAdam(params2)
+        for p in params2:
+            p.grad = torch.randn(p.shape, generator=g)
+        opt.allreduce()
+        q.put((rank, got, [p.grad.clone() for p in params2]))
     finally:
         dist.destroy_process_group()
 
 
 def test_allreduce_gradients_is_the_rank_mean():
-    """train.allreduce_gradients (DDP's gradient sync) over gloo, world 2, multiple buckets."""
+    """train.allreduce_gradients (DDP's gradient sync) over gloo, world 2, multiple buckets; and
+    FlatAdam.allreduce (one all-reduce of the flat gradient buffer)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -142,7 +152,9 @@ def test_allreduce_gradients_is_the_rank_mean():
     procs = [ctx.Process(target=_grad_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(world))
+    out = [q.get(timeout=120) for _ in range(world)]
+    res = {r: g for r, g, _ in out}
+    res_flat = {r: g for r, _, g in out}
     for p in procs:
         p.join(timeout=60)
     expect = []
@@ -156,3 +168,25 @@ def test_allreduce_gradients_is_the_rank_mean():
     for r in range(world):
         for got, exp in zip(res[r], expect):
             torch.testing.assert_close(got, exp, rtol=1e-6, atol=1e-6)
+        for got, exp in zip(res_flat[r], expect):
+            torch.testing.assert_close(got, exp, rtol=1e-6, atol=1e-6)
+
+
+def test_flat_adam_views():
+    """FlatAdam (host side, no GPU): parameters keep their values and become views of one flat
+    buffer; the gradients autograd leaves are gathered into the flat gradient (a missing one as
+    zeros) and each .grad re-pointed at its slice; zero_grad drops them."""
+    from transmvsnet_amd.train import FlatAdam
+    ps = [torch.nn.Parameter(torch.randn(3, 4)), torch.nn.Parameter(torch.randn(7)), torch.nn.Parameter(torch.randn(2))]
+    vals = [p.detach().clone() for p in ps]
+    opt = FlatAdam(ps)
+    assert opt.flat.numel() == 21
+    for p, v in zip(ps, vals):
+        assert torch.equal(p.detach(), v)
+    assert ps[1].data_ptr() == opt.flat[12:].data_ptr()
+    (ps[0].sum() * 2 + ps[1].sum()).backward()
+    opt.allreduce()  # world 1: gathers only
+    assert torch.equal(opt.grad_flat, torch.cat([torch.full((12,), 2.0), torch.ones(7), torch.zeros(2)]))
+    assert ps[1].grad.data_ptr() == opt.grad_flat[12:].data_ptr()
+    opt.zero_grad()
+    assert all(p.grad is None for p in ps)

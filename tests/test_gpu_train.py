@@ -501,3 +501,43 @@ def test_fmt_train_forward_backward(nv, h, w):
                        "fp32 ref worst": ref_worst})
     for n, e_gpu, e_ref in errs:
         assert e_gpu <= max(1e-4, 2.0 * e_ref, ref_worst), (n, e_gpu, e_ref, ref_worst)
+
+
+def test_flat_adam_matches_torch_adam():
+    """FlatAdam / tmvs_adam_step (finetune.py:324's optimizer: Adam, betas 0.9/0.999, eps 1e-8,
+    weight_decay 1e-4, lr 1e-3) against torch.optim.Adam (single-tensor, CPU fp32) over 5 steps on
+    the CostRegNet parameters with random gradients: parameters and both moments within 2e-6 of
+    each quantity's max magnitude (fma contraction vs torch's separate ops: ulp-level)."""
+    from transmvsnet_amd.train import FlatAdam
+    sd = {k[len("cost_regularization.0."):]: v for k, v in golden_state_dict().items()
+          if k.startswith("cost_regularization.0.")}
+    cr_gpu, cr_cpu = CostRegNet(1, 8), CostRegNet(1, 8)
+    cr_gpu.load_state_dict(sd, strict=True)
+    cr_cpu.load_state_dict(sd, strict=True)
+    cr_gpu = cr_gpu.to(DEV)
+    pg = [p for p in cr_gpu.parameters()]
+    pc = [p for p in cr_cpu.parameters()]
+    opt = FlatAdam(pg, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4)
+    ref = torch.optim.Adam(pc, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4, foreach=False)
+    g = torch.Generator().manual_seed(3)
+    for _ in range(5):
+        grads = [torch.randn(p.shape, generator=g) * 0.1 for p in pc]
+        opt.zero_grad()
+        ref.zero_grad()
+        for p, q, gr in zip(pg, pc, grads):
+            p.grad = gr.to(DEV)
+            q.grad = gr.clone()
+        opt.step()
+        ref.step()
+    torch.cuda.synchronize()
+    worst = 0.0
+    off = 0
+    for p, q in zip(pg, pc):
+        st = ref.state[q]
+        n = q.numel()
+        for got, exp in ((p, q), (opt.exp_avg[off:off + n].view_as(q), st["exp_avg"]),
+                         (opt.exp_avg_sq[off:off + n].view_as(q), st["exp_avg_sq"])):
+            worst = max(worst, _rel(got, exp))
+        off += n
+    print("FlatAdam vs torch.optim.Adam, worst relative difference:", worst)
+    assert worst < 2e-6, worst

@@ -15,6 +15,7 @@ I = ctypes.c_int
 L = ctypes.c_long
 F = ctypes.c_float
 S = ctypes.c_size_t
+D = ctypes.c_double
 
 # name -> (restype, argtypes); every symbol include/transmvs.h declares
 SIGNATURES = {
@@ -72,6 +73,7 @@ SIGNATURES = {
     "tmvs_linattn_bwd_workspace": (S, [L, L]),
     "tmvs_linattn_bwd_q": (I, [P, P, L, L, P, L, P, S, P, P, P]),
     "tmvs_linattn_bwd_kv": (I, [P, P, L, L, P, P, P, P]),
+    "tmvs_adam_step": (I, [P, P, P, P, L, D, D, D, D, D, I, P]),
     "tmvs_conv3d_generic": (I, [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P]),
     "tmvs_conv3d_wgrad_workspace": (S, [I, I, I, I, I, I]),
     "tmvs_conv3d_wgrad": (I, [P, I, I, I, I, I, P, I, I, I, I, I, P, S, P, P]),

@@ -1,0 +1,44 @@
+// Adam for the training path (config C5: finetune.py:324, torch.optim.Adam(lr, betas=(0.9, 0.999),
+// weight_decay=wd), L2 weight decay, no amsgrad), over one flat fp32 parameter buffer: every
+// parameter of the model is a view of it (transmvsnet_amd.train.FlatAdam), so a step is one launch.
+// Per element, in torch's single-tensor order (torch/optim/adam.py _single_tensor_adam):
+//   g = grad + wd * p;  m = lerp(m, g, 1 - b1);  v = b2 * v + (1 - b2) * g * g
+//   p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+// HBM-bound: 4 streams read (p, g, m, v), 3 written (p, m, v): 28 B per parameter.
+#include "common.h"
+
+namespace tmvs {
+
+// The scalars arrive as the fp32 values torch's scalar arguments become: the complements 1 - beta are
+// formed in double from the double betas (as Python does) and only then rounded to fp32.
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long n, float omb1,
+                                                   float beta2, float omb2, float eps, float wd, float step_size,
+                                                   float bc2_sqrt) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float pv = p[i];
+  const float gr = wd != 0.f ? fmaf(wd, pv, g[i]) : g[i];
+  const float mv = m[i];
+  const float mn = fmaf(omb1, gr - mv, mv);  // torch.lerp (weight < 0.5): start + weight * (end - start)
+  const float vn = fmaf(omb2, gr * gr, beta2 * v[i]);
+  const float denom = sqrtf(vn) / bc2_sqrt + eps;
+  m[i] = mn;
+  v[i] = vn;
+  p[i] = fmaf(-step_size, mn / denom, pv);
+}
+
+}  // namespace tmvs
+
+using namespace tmvs;
+
+extern "C" int tmvs_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, double lr,
+                              double beta1, double beta2, double eps, double weight_decay, int step, void* stream) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq || n <= 0 || step <= 0) return TMVS_ERR_ARG;
+  const double bc1 = 1.0 - pow(beta1, (double)step), bc2 = 1.0 - pow(beta2, (double)step);
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, param, grad,
+                     exp_avg, exp_avg_sq, n, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
+                     (float)weight_decay, (float)(lr / bc1), (float)sqrt(bc2));
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}

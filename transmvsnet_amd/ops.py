@@ -852,9 +852,21 @@ def linattn_bwd_kv(k, v, dkv, tokens_per_group):
     return dk, dv
 
 
+def adam_step(param_flat, grad_flat, exp_avg, exp_avg_sq, lr, betas, eps, weight_decay, step):
+    """tmvs_adam_step: one Adam update (torch's order) of a flat fp32 parameter buffer, in place."""
+    for t, n in ((param_flat, "param"), (grad_flat, "grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+        _dev(t, n)
+        if t.numel() != param_flat.numel():
+            raise ValueError(f"adam_step: {n} must have {param_flat.numel()} elements")
+    with _Span("tmvs_adam_step"):
+        _lib.check(_lib_h().tmvs_adam_step(_ptr(param_flat), _ptr(grad_flat), _ptr(exp_avg), _ptr(exp_avg_sq),
+                                           param_flat.numel(), float(lr), float(betas[0]), float(betas[1]), float(eps),
+                                           float(weight_decay), int(step), _stream()), "tmvs_adam_step")
+
+
 for _name in ("conv3d_generic", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn_relu_backward", "warp_corr_backward",
               "upsample2_add_nhwc", "upsample2_backward_nhwc", "pixelwise_train_forward", "aggregate_train", "aggregate_train_backward", "pixelwise_train_backward",
               "token_linear", "token_wgrad", "layer_norm_fwd", "layer_norm_bwd", "linattn_fwd", "linattn_bwd_q",
-              "linattn_bwd_kv"):
+              "linattn_bwd_kv", "adam_step"):
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name

@@ -520,6 +520,66 @@ def depth_stages_train(model, stage_features, proj_matrix, depth_values, depth_g
     return total, outputs
 
 
+class FlatAdam:
+    """torch.optim.Adam as finetune.py:324 builds it (lr, betas=(0.9, 0.999), eps=1e-8, L2 weight_decay),
+    over ONE flat fp32 buffer: at construction every parameter's storage becomes a view of `flat`.
+    Gradients are left to autograd (no per-parameter accumulate kernels): `zero_grad` sets them to
+    None, and the first of `allreduce` / `step` gathers them into `grad_flat` with one concatenation,
+    re-pointing each .grad at its slice. The DDP sync is then one all-reduce of `grad_flat`, and a
+    step is one HIP launch (tmvs_adam_step)."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        self.params = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("FlatAdam: no parameters")
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.empty(n, device=dev)
+        self.grad_flat = torch.zeros(n, device=dev)
+        self._segs, off = [], 0
+        for p in self.params:
+            k = p.numel()
+            self.flat[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = self.flat[off:off + k].view_as(p)
+            self._segs.append((off, k))
+            off += k
+        self.exp_avg = torch.zeros(n, device=dev)
+        self.exp_avg_sq = torch.zeros(n, device=dev)
+        self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        self.step_count = 0
+        self._gathered = False
+
+    def zero_grad(self):
+        for p in self.params:
+            p.grad = None
+        self._gathered = False
+
+    def _gather(self):
+        if self._gathered:
+            return
+        parts = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=self.flat.device)
+                 for p in self.params]
+        torch.cat(parts, out=self.grad_flat)
+        for p, (off, k) in zip(self.params, self._segs):
+            p.grad = self.grad_flat[off:off + k].view_as(p)
+        self._gathered = True
+
+    def allreduce(self, group=None):
+        """DDP's gradient mean over ranks: one all_reduce(SUM) of the flat gradient, then 1/world."""
+        import torch.distributed as dist
+        self._gather()
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            dist.all_reduce(self.grad_flat, op=dist.ReduceOp.SUM, group=group)
+            self.grad_flat.div_(dist.get_world_size(group))
+
+    def step(self, lr=None):
+        self._gather()
+        self.step_count += 1
+        ops.adam_step(self.flat, self.grad_flat, self.exp_avg, self.exp_avg_sq, self.lr if lr is None else lr,
+                      self.betas, self.eps, self.weight_decay, self.step_count)
+        self._gathered = False  # the next backward adds into the current .grad views unless zero_grad runs
+
+
 def allreduce_gradients(params, group=None, bucket_bytes=64 << 20):
     """DDP's gradient synchronisation (train.py:363-366 wraps the model in DistributedDataParallel):
     the mean over ranks of every parameter gradient, as few flat buckets (one at this model's
