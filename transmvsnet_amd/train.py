@@ -353,8 +353,9 @@ class _CostRegNetTrain(torch.autograd.Function):
             wt, gm, bt = ws[3 * i], ws[3 * i + 1], ws[3 * i + 2]
             xin, idims, z, mean, var = ctx.layer_io[i]
             dy = dout.pop(name)
-            if skip is not None:  # y = skip + relu(bn(z)): the skip source receives dy as is
-                dout[skip] = dy.clone() if skip not in dout else dout[skip].add_(dy)
+            if skip is not None:  # y = skip + relu(bn(z)): the skip source receives dy as is (aliased: dy is
+                # only read again by bn_relu_backward below, stream-ordered before any in-place accumulation)
+                dout[skip] = dy if skip not in dout else dout[skip].add_(dy)
             dz, dgam, dbet = ops.bn_relu_backward(dy, z, mean, var, gm.detach(), bt.detach(), eps)
             if transposed:
                 dw = ops.conv3d_wgrad(xin, dz, 2)
