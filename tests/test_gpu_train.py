@@ -541,3 +541,42 @@ def test_flat_adam_matches_torch_adam():
         off += n
     print("FlatAdam vs torch.optim.Adam, worst relative difference:", worst)
     assert worst < 2e-6, worst
+
+
+def test_training_loop_reduces_loss():
+    """A C5-style loop on one fixed synthetic sample (128x160, N=3, 8/8/8): FMT -> pathway -> DepthNet
+    stages -> focal_loss_bld (dlossw 1,1,1) -> backward -> FlatAdam.step, 8 iterations, all HIP. The
+    loss must fall (the optimizer and every backward kernel point downhill together), stay finite,
+    and the BatchNorm running statistics must move."""
+    from transmvsnet_amd import TransMVSNet, synthetic
+    from transmvsnet_amd.train import FlatAdam, depth_stages_train, fmt_train, pathway_train
+    H, W, N, ND = 128, 160, 3, (8, 8, 8)
+    model = TransMVSNet(ndepths=list(ND))
+    model.load_state_dict(golden_state_dict(), strict=True)
+    model = model.to(DEV)
+    g = torch.Generator().manual_seed(23)
+    feats = [torch.randn(N, c, H // s, W // s, generator=g).to(DEV) for c, s in ((32, 4), (16, 2), (8, 1))]
+    proj = synthetic.synthetic_cameras(N, H, W, seed=1)
+    dv = synthetic.synthetic_depth_values(1).to(DEV)
+    gt = {f"stage{s + 1}": (425.0 + 500.0 * torch.rand(1, H >> (2 - s), W >> (2 - s), generator=g)).to(DEV)
+          for s in range(3)}
+    mask = {k: torch.ones_like(v) for k, v in gt.items()}
+    params = [p for n, p in model.named_parameters()
+              if n.startswith(("cost_regularization.", "DepthNet.", "FMT_with_pathway."))]
+    opt = FlatAdam(params, lr=1e-3, weight_decay=1e-4)
+    rm0 = model.cost_regularization[0].conv0.bn.running_mean.clone()
+    losses = []
+    for _ in range(8):
+        opt.zero_grad()
+        st1 = fmt_train(model, feats[0])
+        st2, st3 = pathway_train(model, st1, feats[1], feats[2])
+        total, _ = depth_stages_train(model, {"stage1": st1, "stage2": st2, "stage3": st3}, proj, dv, gt, mask,
+                                      (H, W), dlossw=(1.0, 1.0, 1.0), loss="focal_bld",
+                                      depth_interval=float(dv[0, 1] - dv[0, 0]))
+        opt.allreduce()
+        opt.step()
+        losses.append(float(total))
+    print("losses:", [f"{x:.4f}" for x in losses])
+    assert all(np.isfinite(losses)), losses
+    assert losses[-1] < 0.9 * losses[0], losses
+    assert not torch.equal(model.cost_regularization[0].conv0.bn.running_mean, rm0)
