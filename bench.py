@@ -34,6 +34,9 @@ C_STAGE = (32, 16, 8)
 SCALES = (4, 2, 1)
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 PEAK_F32_MFMA_TFS = 157.3  # MI355X_MICROARCH.md: fp32 MFMA dense peak
+# vector-memory address unit (TA) gather rate: 64 B/clk/CU (a 64-lane 16-B load costs >= 16 cycles,
+# measured by scripts/micro/ta_mask.hip) x 256 CUs x 2.4 GHz
+PEAK_TA_GBS = 64 * 256 * 2.4
 
 
 def _args():
@@ -91,6 +94,13 @@ def algorithmic():
         warp_bytes.append(4 * p * (C_STAGE[s] * (1 + v) + 2 * NDEPTHS[s] + v))
         cr_flop.append(6912 * NDEPTHS[s] * p)
     return warp_bytes, cr_flop
+
+
+def gather_bytes():
+    """Bilinear tap traffic of the warp per depth map through the vector L1 (SURVEY.md 8d companion
+    bound): 16 * C * D * P * V bytes per stage (4 taps x C fp32 per pixel, plane and source view)."""
+    v = NVIEWS - 1
+    return [16 * C_STAGE[s] * NDEPTHS[s] * (H // SCALES[s]) * (W // SCALES[s]) * v for s in range(3)]
 
 
 def make_inputs(device, seed_feat=2):
@@ -250,6 +260,17 @@ def run(args, world, rank, local):
                      "per": "depth map (3 launches: stages 1-3); achieved = algorithmic bytes / summed duration",
                      "algorithmic_bytes": int(sum(warp_bytes)),
                      "per_stage_ms": [round(float(x), 4) for x in per_launch]})
+    if warp_ms:  # the same launches against the address-unit bound that actually limits them
+        per_launch = np.array(warp_ms).reshape(steps_p, -1).mean(0)
+        gb = gather_bytes()
+        ach = sum(gb) / (per_launch.sum() * 1e-3) / 1e9
+        kern.append({"kernel": "tmvs_warp_corr (gather)", "bound": "ta", "achieved": round(ach, 1), "peak": PEAK_TA_GBS,
+                     "unit": "GB/s", "frac": round(ach / PEAK_TA_GBS, 4), "traffic": None,
+                     "ms_per_depth_map": round(float(per_launch.sum()), 4),
+                     "per": "depth map; achieved = bilinear tap bytes 16*C*D*P*V / summed duration; peak = the "
+                            "measured 64 B/clk/CU address-unit rate x 256 CUs x 2.4 GHz",
+                     "gather_bytes": int(sum(gb)),
+                     "per_stage_frac": [round(b / (t * 1e-3) / 1e9 / PEAK_TA_GBS, 3) for b, t in zip(gb, per_launch)]})
     if cr_ms:
         per_launch = np.array(cr_ms).reshape(steps_p, -1).mean(0)
         ach = sum(cr_flop) / (per_launch.sum() * 1e-3) / 1e12
