@@ -534,6 +534,10 @@ class FlatAdam:
         if not self.params:
             raise ValueError("FlatAdam: no parameters")
         dev = self.params[0].device
+        if any(p.device != dev or p.dtype != torch.float32 for p in self.params):
+            raise ValueError("FlatAdam: every parameter must be float32 on one device")
+        if len({id(p) for p in self.params}) != len(self.params):
+            raise ValueError("FlatAdam: a parameter is listed twice")
         n = sum(p.numel() for p in self.params)
         self.flat = torch.empty(n, device=dev)
         self.grad_flat = torch.zeros(n, device=dev)
