@@ -1,7 +1,7 @@
 // FMT backward for training: the pieces of EncoderLayer.forward
 // (models/FMT.py:96-111; AttentionLayer :56-75; LinearAttention :22-37) that autograd needs, as
 // token-wise kernels over [T][C] token matrices (C = 32, hidden 64, 8 heads x 4):
-//   tmvs_token_linear      y = x W^T (+ b) or y = x W (the data gradient), optionally accumulated
+//   tmvs_token_linear      y = x W^T (+ b) or y = x W (the data gradient), optionally accumulated (fp32 MFMA)
 //   tmvs_token_wgrad       dW = dy^T x and db = column sums of dy (fp64 block partials, fixed combine)
 //   tmvs_layer_norm_fwd    LayerNorm(32) forward (the backward recomputes its statistics)
 //   tmvs_layer_norm_bwd    dx, and dgamma / dbeta (deterministic reductions)
@@ -23,49 +23,79 @@ __device__ __forceinline__ float elu1f(float x) { return (x > 0.f ? x : expm1f(x
 __device__ __forceinline__ float elu1_grad(float x) { return x > 0.f ? 1.f : expf(x); }
 
 // y[t][o] = sum_i W[o][i] x[t][i] + b[o] for a torch Linear weight W [OUT][IN]; TRANS: y[t][o] = sum_i W[i][o] x[t][i]
-// for W [IN][OUT] (the data gradient dx = dy W of a Linear with weight W); relu_of masks y where relu_of <= 0.
-// One token per lane; the weights are wave-uniform (scalar loads, SGPR operands of v_fma_f32); rows move as float4.
+// for W [IN][OUT] (the data gradient dx = dy W of a Linear with weight W); relu_of masks y where relu_of <= 0;
+// accumulate adds into y. On fp32 MFMA (v_mfma_f32_16x16x4f32): a wave computes 16 tokens x 16 outputs
+// per block of OUT: A (16 x 4) = weights (lane l: output l & 15, k-group l >> 4), B (4 x 16) = tokens (lane l:
+// token l & 15, k-group l >> 4), D lane l = outputs 4 (l >> 4) .. +3 of token l & 15 (one float4 store).
+// The contraction runs over k = 16 i + 4 kg + e: a lane loads float4 chunk (i, kg) of its token's row, and
+// MFMA (i, e) takes element e of it in B and W[., 16 i + 4 kg + e] in A -- the same permutation of k in
+// both operands. A fragments stay in VGPRs for the wave's tiles; bias / ReLU mask / accumulate in the epilogue.
+constexpr int kLinTiles = 4;  // 16-token tiles per wave
 template <int IN, int OUT, bool TRANS>
-__global__ __launch_bounds__(kTB) void token_linear_kernel(const float* __restrict__ x, long T,
-                                                           const float* __restrict__ W, const float* __restrict__ b,
-                                                           const float* __restrict__ relu_of, int accumulate,
-                                                           float* __restrict__ y) {
-  const long t = (long)blockIdx.x * kTB + threadIdx.x;
-  if (t >= T) return;
-  float xv[IN], acc[OUT];
+__global__ __launch_bounds__(256) void token_linear_mfma_kernel(const float* __restrict__ x, long T,
+                                                                const float* __restrict__ W,
+                                                                const float* __restrict__ b,
+                                                                const float* __restrict__ relu_of, int accumulate,
+                                                                float* __restrict__ y) {
+  constexpr int NI = IN / 16, NB = OUT / 16;
+  const int lane = threadIdx.x & 63, kg = lane >> 4, col = lane & 15;
+  float afr[NB][NI][4];
 #pragma unroll
-  for (int i = 0; i < IN; i += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(x + t * IN + i);
-    xv[i] = v.x;
-    xv[i + 1] = v.y;
-    xv[i + 2] = v.z;
-    xv[i + 3] = v.w;
-  }
+  for (int ob = 0; ob < NB; ++ob)
 #pragma unroll
-  for (int o = 0; o < OUT; ++o) {
-    float a = 0.f;
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int i = 0; i < IN; ++i) a = fmaf(TRANS ? W[i * OUT + o] : W[o * IN + i], xv[i], a);
-    acc[o] = b ? a + b[o] : a;
-  }
+      for (int e = 0; e < 4; ++e) {
+        const int o = ob * 16 + col, k = 16 * i + 4 * kg + e;
+        afr[ob][i][e] = TRANS ? W[k * OUT + o] : W[o * IN + k];
+      }
+  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+#pragma unroll 1
+  for (int it = 0; it < kLinTiles; ++it) {
+    const long t0 = (wave * kLinTiles + it) * 16;
+    if (t0 >= T) break;  // wave-uniform
+    const long t = t0 + col;
+    const long tc = t < T ? t : T - 1;
+    float4 xb[NI];
 #pragma unroll
-  for (int o = 0; o < OUT; o += 4) {
-    float4 v = make_float4(acc[o], acc[o + 1], acc[o + 2], acc[o + 3]);
-    if (relu_of) {  // relu backward mask (the forward's pre-activation)
-      const float4 m = *reinterpret_cast<const float4*>(relu_of + t * OUT + o);
-      v.x = m.x > 0.f ? v.x : 0.f;
-      v.y = m.y > 0.f ? v.y : 0.f;
-      v.z = m.z > 0.f ? v.z : 0.f;
-      v.w = m.w > 0.f ? v.w : 0.f;
+    for (int i = 0; i < NI; ++i) xb[i] = *reinterpret_cast<const float4*>(x + tc * IN + 16 * i + 4 * kg);
+#pragma unroll
+    for (int ob = 0; ob < NB; ++ob) {
+      floatx4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(afr[ob][i][0], xb[i].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(afr[ob][i][1], xb[i].y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(afr[ob][i][2], xb[i].z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(afr[ob][i][3], xb[i].w, acc, 0, 0, 0);
+      }
+      // D: lane holds outputs ob*16 + 4 kg + r of token t0 + col
+      const int o0 = ob * 16 + 4 * kg;
+      float4 v = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      if (b) {
+        v.x += b[o0];
+        v.y += b[o0 + 1];
+        v.z += b[o0 + 2];
+        v.w += b[o0 + 3];
+      }
+      if (t < T) {
+        if (relu_of) {
+          const float4 m = *reinterpret_cast<const float4*>(relu_of + t * OUT + o0);
+          v.x = m.x > 0.f ? v.x : 0.f;
+          v.y = m.y > 0.f ? v.y : 0.f;
+          v.z = m.z > 0.f ? v.z : 0.f;
+          v.w = m.w > 0.f ? v.w : 0.f;
+        }
+        if (accumulate) {
+          const float4 pr = *reinterpret_cast<const float4*>(y + t * OUT + o0);
+          v.x = pr.x + v.x;
+          v.y = pr.y + v.y;
+          v.z = pr.z + v.z;
+          v.w = pr.w + v.w;
+        }
+        *reinterpret_cast<float4*>(y + t * OUT + o0) = v;
+      }
     }
-    if (accumulate) {
-      const float4 p = *reinterpret_cast<const float4*>(y + t * OUT + o);
-      v.x = p.x + v.x;
-      v.y = p.y + v.y;
-      v.z = p.z + v.z;
-      v.w = p.w + v.w;
-    }
-    *reinterpret_cast<float4*>(y + t * OUT + o) = v;
   }
 }
 
@@ -434,16 +464,16 @@ extern "C" int tmvs_token_linear(const float* x, long tokens, int in_features, i
                                  const float* b, int transpose_w, const float* relu_of, int accumulate, float* y,
                                  void* stream) {
   if (!x || !w || !y || tokens <= 0) return TMVS_ERR_ARG;
-  const dim3 grid((unsigned)((tokens + kTB - 1) / kTB));
+  const dim3 grid((unsigned)((tokens + 16L * 4 * kLinTiles - 1) / (16L * 4 * kLinTiles)));
   hipStream_t st = (hipStream_t)stream;
 #define TMVS_TL(I, O)                                                                                             \
   if (in_features == I && out_features == O) {                                                                    \
     if (transpose_w)                                                                                              \
-      hipLaunchKernelGGL((token_linear_kernel<I, O, true>), grid, dim3(kTB), 0, st, x, tokens, w, b, relu_of,     \
-                         accumulate, y);                                                                          \
+      hipLaunchKernelGGL((token_linear_mfma_kernel<I, O, true>), grid, dim3(256), 0, st, x, tokens, w, b,         \
+                         relu_of, accumulate, y);                                                                 \
     else                                                                                                          \
-      hipLaunchKernelGGL((token_linear_kernel<I, O, false>), grid, dim3(kTB), 0, st, x, tokens, w, b, relu_of,    \
-                         accumulate, y);                                                                          \
+      hipLaunchKernelGGL((token_linear_mfma_kernel<I, O, false>), grid, dim3(256), 0, st, x, tokens, w, b,        \
+                         relu_of, accumulate, y);                                                                 \
     TMVS_CHECK_LAUNCH();                                                                                          \
     return TMVS_OK;                                                                                               \
   }
