@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TMVS_ABI_VERSION 3
+#define TMVS_ABI_VERSION 4
 
 #define TMVS_OK 0
 #define TMVS_ERR_ARG (-1)    /* null pointer / non-positive size / bad enum        */
@@ -122,6 +122,13 @@ size_t tmvs_costregnet_workspace(int batch, int depth, int height, int width, in
 /* x: [B][D][H][W] (=NDHWC with C=1), logits: [B][D][H][W]. Needs D,H,W % 8 == 0. */
 int tmvs_costregnet(const float* x, int batch, int depth, int height, int width, const TmvsCostRegWeights* w,
                     void* workspace, size_t workspace_bytes, float* logits, void* stream);
+/* CostRegNet + softmax/WTA in one call (models/TransMVSNet.py:97-103,214-221): for ndepth 8 the
+ * prob conv, the softmax over D and the winner-take-all run as one kernel (the logits never reach
+ * HBM); for larger ndepth tmvs_costregnet's depth-chunked prob kernel + tmvs_softmax_wta. Outputs and their bits are those of tmvs_costregnet -> tmvs_softmax_wta.
+ * Same workspace as tmvs_costregnet; ndepth in {8, 16, 24, 32, 48, 64}.                        */
+int tmvs_costregnet_wta(const float* x, const float* hyp, int batch, int depth, int height, int width,
+                        const TmvsCostRegWeights* w, void* workspace, size_t workspace_bytes, float clamp_lo,
+                        float clamp_hi, float* prob, float* depth_out, float* depth_raw, float* conf, void* stream);
 
 /* Single layers (Conv3d / Deconv3d blocks, models/module.py:108-191), NDHWC in and out.
  * conv: stride 1 or 2, padding 1;  y = relu(fmaf(conv, alpha, shift)).

@@ -244,6 +244,20 @@ def test_deconv3d_layers(sd, model, layer, idx):
     np.testing.assert_allclose(to_np(y), y_ref.permute(0, 2, 3, 4, 1).numpy(), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("d,h,w,b", [(8, 232, 264, 2), (8, 16, 40, 1), (32, 232, 264, 2), (48, 24, 32, 2)])
+def test_costregnet_wta_equals_costregnet_then_softmax(model, d, h, w, b):
+    """tmvs_costregnet_wta (prob conv + softmax/WTA fused for D=8; the depth-chunked prob kernel +
+    softmax kernel otherwise) == tmvs_costregnet -> tmvs_softmax_wta, bit for bit."""
+    g = torch.Generator().manual_seed(d * 1000 + h)
+    x = torch.randn(b, d, h, w, generator=g).to(DEV)
+    hyp = (425.0 + torch.rand(b, d, h, w, generator=g).mul(510.0)).sort(dim=1).values.to(DEV)
+    st, _keep = model.cost_regularization[1].packed(DEV)
+    ref = ops.softmax_wta(ops.costregnet(x, st), hyp, (500.0, 900.0))
+    got = ops.costregnet_wta(x, st, hyp, (500.0, 900.0))
+    for name, a, r in zip(("prob", "depth", "depth_raw", "conf"), got, ref):
+        np.testing.assert_array_equal(to_np(a), to_np(r), err_msg=name)
+
+
 def test_softmax_wta_ties():
     g = golden("ops.npz")
     prob, depth, raw, conf = ops.softmax_wta(torch.from_numpy(g["wta_logits"]).to(DEV),

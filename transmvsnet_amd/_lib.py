@@ -28,6 +28,7 @@ SIGNATURES = {
     "tmvs_homo_warping": (I, [P, P, P, I, I, I, I, I, I, P, P]),
     "tmvs_costregnet_workspace": (S, [I, I, I, I, I]),
     "tmvs_costregnet": (I, [P, I, I, I, I, P, P, S, P, P]),
+    "tmvs_costregnet_wta": (I, [P, P, I, I, I, I, P, P, S, F, F, P, P, P, P, P]),
     "tmvs_conv3d_bn_relu": (I, [P, I, I, I, I, I, P, P, P, I, I, P, P]),
     "tmvs_deconv3d_bn_relu_add": (I, [P, I, I, I, I, I, P, P, P, I, P, P, P]),
     "tmvs_softmax_wta": (I, [P, P, I, I, I, I, F, F, P, P, P, P, P]),
@@ -83,7 +84,7 @@ SIGNATURES = {
     "tmvs_bn_relu_backward": (I, [P, P, L, I, P, P, P, P, F, P, S, P, P, P, P]),
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 PW_NPARAMS = 201
 ENC_NPARAMS = 8544
 KV_NFLOATS = 160

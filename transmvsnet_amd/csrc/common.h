@@ -49,4 +49,31 @@ __device__ __forceinline__ floatx4_t buf_load_f32x4(__amdgpu_buffer_rsrc_t r, un
   return __builtin_bit_cast(floatx4_t, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
 }
 
+// One pixel's softmax over D logits and winner-take-all (models/TransMVSNet.py:97-103,217-218):
+// prob = exp((x - max) - log(sum exp(x - max))) stored through put_prob(d, p); returns the first
+// maximum's index and its probability in best. Shared by softmax_wta_kernel (glue.hip) and the
+// fused prob_wta_kernel (costreg.hip) so both produce the same bits.
+template <int D, typename PutProb>
+__device__ __forceinline__ int softmax_first_max(const float (&x)[D], PutProb put_prob, float& best) {
+  float m = x[0];
+#pragma unroll
+  for (int d = 1; d < D; ++d) m = fmaxf(m, x[d]);
+  float s = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) s = s + expf(x[d] - m);
+  const float lse = logf(s);
+  best = -1.f;
+  int bi = 0;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const float pr = expf((x[d] - m) - lse);
+    put_prob(d, pr);
+    if (pr > best) {
+      best = pr;
+      bi = d;
+    }
+  }
+  return bi;
+}
+
 }  // namespace tmvs

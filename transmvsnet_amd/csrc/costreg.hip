@@ -668,6 +668,86 @@ __global__ __launch_bounds__(256) void prob_kernel(const float* __restrict__ x, 
   }
 }
 
+// ---------------------------------------------------------------- prob + softmax / WTA, fused
+// prob_kernel's row-segment D walk over all D planes of a column (no depth chunks), with the
+// column's logits parked in LDS ([D][256], thread-private slots, conflict-free) instead of HBM;
+// then softmax_first_max (common.h, the code softmax_wta_kernel runs) and the gather of the
+// winning hypothesis (models/TransMVSNet.py:97-103,217-221). Same FMA chains as prob_kernel, so
+// prob / depth / conf equal prob_kernel + softmax_wta_kernel bit for bit, without the logits'
+// 8·D bytes per pixel of HBM traffic and one launch.
+template <int D>
+__global__ __launch_bounds__(256) void prob_wta_kernel(const float* __restrict__ x, const float* __restrict__ wt,
+                                                       const float* __restrict__ hyp, int H, int W, float lo,
+                                                       float hi, float* __restrict__ prob, float* __restrict__ depth,
+                                                       float* __restrict__ depth_raw, float* __restrict__ conf) {
+  __shared__ float lg[D * 256];
+  const int HW = H * W;
+  const int nseg = (W + kProbCols - 1) / kProbCols, nrow = (H + 3) / 4;
+  int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int seg = lb % nseg;
+  lb /= nseg;
+  const int rowb = lb % nrow;
+  const int n = lb / nrow;
+  const int lane = threadIdx.x & 63;
+  const int h = rowb * 4 + (threadIdx.x >> 6);
+  if (h >= H) return;  // whole wave; no barriers below (LDS slots are thread-private)
+  const int w = seg * kProbCols + lane - 1;
+  const bool writes = lane >= 1 && lane <= kProbCols && w < W;
+  const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)n * D * HW * 8, (unsigned)(D * HW * 32));
+  const unsigned offw = (unsigned)w < (unsigned)W ? (unsigned)w * 32u : kOffOut;
+  auto load_row = [&](int i, int kh, float4 (&o)[2]) {
+    const int ih = h - 1 + kh;
+    const unsigned offr = ((unsigned)i < (unsigned)D && (unsigned)ih < (unsigned)H)
+                              ? ((unsigned)i * (unsigned)H + (unsigned)ih) * (unsigned)W * 32u
+                              : kOffOut;
+    const unsigned off = (offr + offw) | ((offr | offw) & kOffOut);
+    const floatx4 u = buf_load_f32x4(rx, off);
+    const floatx4 v = buf_load_f32x4(rx, off + 16u);
+    o[0] = make_float4(u[0], u[1], u[2], u[3]);
+    o[1] = make_float4(v[0], v[1], v[2], v[3]);
+  };
+  float* my = lg + threadIdx.x;
+  float2_v c12 = {0.f, 0.f};
+  float4 cur[2], nxt[2];
+  load_row(-1, 0, cur);
+  for (int i = -1; i <= D; ++i) {
+    float acc_next = 0.f;
+#pragma unroll 1
+    for (int kh = 0; kh < 3; ++kh) {
+      load_row(kh < 2 ? i : i + 1, kh < 2 ? kh + 1 : 0, nxt);
+      const float xc[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
+      const float* wk = wt + kh * 72;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const float xv = kw == 0 ? lane_from_left(xc[c]) : kw == 1 ? xc[c] : lane_from_right(xc[c]);
+          const float2_v wp = *reinterpret_cast<const float2_v*>(wk + 2 * (kw * 8 + c));
+          acc_next = fmaf(wk[48 + kw * 8 + c], xv, acc_next);
+          c12 = __builtin_elementwise_fma(wp, float2_v{xv, xv}, c12);
+        }
+      }
+      cur[0] = nxt[0];
+      cur[1] = nxt[1];
+    }
+    if (i >= 1) my[(i - 1) * 256] = c12.y;  // logit of plane i-1 complete
+    c12 = float2_v{acc_next, c12.x};
+  }
+  if (!writes) return;
+  float xl[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) xl[d] = my[d * 256];
+  const size_t base = (size_t)n * D * HW + (size_t)h * W + w;
+  float best;
+  const int bi = softmax_first_max<D>(xl, [&](int d, float pr) { prob[base + (size_t)d * HW] = pr; }, best);
+  const size_t o = (size_t)n * HW + (size_t)h * W + w;
+  const float dr = hyp[base + (size_t)bi * HW];
+  depth_raw[o] = dr;
+  depth[o] = fminf(fmaxf(dr, lo), hi);
+  conf[o] = best;
+}
+
+
 // ---------------------------------------------------------------- conv 16 -> 16, stride 1 (conv2)
 // Persistent form of conv3d_lds_kernel for the one stride-1 layer whose weights fit in LDS next
 // to a tile (27 x 16 x 16 fp32 = 27 KB): a workgroup stages them once, then walks its share of
@@ -1292,10 +1372,12 @@ extern "C" size_t tmvs_costregnet_workspace(int batch, int depth, int height, in
   return bytes;
 }
 
-extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height, int width,
-                               const TmvsCostRegWeights* w, void* workspace, size_t workspace_bytes, float* logits,
-                               void* stream) {
-  if (!x || !w || !workspace || !logits || batch <= 0) return TMVS_ERR_ARG;
+// CostRegNet up to conv11 + skip (models/module.py:447-455); *x11_out = the 8-channel
+// full-resolution NDHWC volume the prob conv reads, *c0_out = conv0's (dead once x11 exists).
+static int costregnet_trunk(const float* x, int batch, int depth, int height, int width, const TmvsCostRegWeights* w,
+                            void* workspace, size_t workspace_bytes, hipStream_t st, float** x11_out,
+                            float** c0_out) {
+  if (!x || !w || !workspace || batch <= 0) return TMVS_ERR_ARG;
   if (depth % 8 || height % 8 || width % 8) return TMVS_ERR_SHAPE;
   if (w->base_ch != 8) return TMVS_ERR_SHAPE;
   // conv0 / prob address one sample's 8-channel full-resolution volume with 32-bit offsets
@@ -1305,7 +1387,6 @@ extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height,
   for (int i = 0; i < 10; ++i)
     if (!w->alpha[i] || !w->shift[i]) return TMVS_ERR_ARG;
   if (workspace_bytes < tmvs_costregnet_workspace(batch, depth, height, width, w->base_ch)) return TMVS_ERR_ARG;
-  hipStream_t st = (hipStream_t)stream;
   const int c = w->base_ch;
   const size_t v0 = (size_t)batch * depth * height * width;
   const size_t v1 = v0 / 8, v2 = v0 / 64, v3 = v0 / 512;
@@ -1350,8 +1431,54 @@ extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height,
     return rc;
   if ((rc = deconv_dispatch(x9, batch, 2 * c, D1, H1, W1, w->w[9], w->alpha[9], w->shift[9], c, c0, x11, st)))
     return rc;
-  const dim3 g1((unsigned)(((W0 + kProbCols - 1) / kProbCols) * ((H0 + 3) / 4) * batch * ((D0 + kDChunk - 1) / kDChunk)));
-  hipLaunchKernelGGL(prob_kernel, g1, dim3(256), 0, st, x11, logits, D0, H0, W0, w->w[10]);
+  *x11_out = x11;
+  *c0_out = c0;
+  return TMVS_OK;
+}
+
+static dim3 prob_grid(int batch, int D, int H, int W, int dchunk) {
+  return dim3((unsigned)(((W + kProbCols - 1) / kProbCols) * ((H + 3) / 4) * batch * ((D + dchunk - 1) / dchunk)));
+}
+
+extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height, int width,
+                               const TmvsCostRegWeights* w, void* workspace, size_t workspace_bytes, float* logits,
+                               void* stream) {
+  if (!logits) return TMVS_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  float *x11, *c0;
+  int rc;
+  if ((rc = costregnet_trunk(x, batch, depth, height, width, w, workspace, workspace_bytes, st, &x11, &c0))) return rc;
+  hipLaunchKernelGGL(prob_kernel, prob_grid(batch, depth, height, width, kDChunk), dim3(256), 0, st, x11, logits, depth,
+                     height, width, w->w[10]);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+extern "C" int tmvs_costregnet_wta(const float* x, const float* hyp, int batch, int depth, int height, int width,
+                                   const TmvsCostRegWeights* w, void* workspace, size_t workspace_bytes,
+                                   float clamp_lo, float clamp_hi, float* prob, float* depth_out, float* depth_raw,
+                                   float* conf, void* stream) {
+  if (!hyp || !prob || !depth_out || !depth_raw || !conf) return TMVS_ERR_ARG;
+  switch (depth) {  // the D values tmvs_softmax_wta takes that CostRegNet's depth % 8 rule admits
+    case 8: case 16: case 24: case 32: case 48: case 64: break;
+    default: return TMVS_ERR_SHAPE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  float *x11, *c0;
+  int rc;
+  if ((rc = costregnet_trunk(x, batch, depth, height, width, w, workspace, workspace_bytes, st, &x11, &c0))) return rc;
+  if (depth > kDChunk) {
+    // the D walk needs depth chunks for enough parallelism (D=32 undivided measured 137 vs 93 + 16 us
+    // split, r07b): depth-chunked prob_kernel, logits in conv0's dead buffer, then the softmax kernel
+    hipLaunchKernelGGL(prob_kernel, prob_grid(batch, depth, height, width, kDChunk), dim3(256), 0, st, x11, c0, depth,
+                       height, width, w->w[10]);
+    TMVS_CHECK_LAUNCH();
+    return tmvs_softmax_wta(c0, hyp, batch, depth, height, width, clamp_lo, clamp_hi, prob, depth_out, depth_raw,
+                            conf, stream);
+  }
+  // D = 8 (stage 3): prob_kernel walks it undivided anyway; fused (104 vs 109 + 19 us, r07b)
+  hipLaunchKernelGGL(prob_wta_kernel<kDChunk>, prob_grid(batch, depth, height, width, kDChunk), dim3(256), 0, st, x11,
+                     w->w[10], hyp, height, width, clamp_lo, clamp_hi, prob, depth_out, depth_raw, conf);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }

@@ -102,24 +102,8 @@ __global__ __launch_bounds__(256) void softmax_wta_kernel(const float* __restric
   float x[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) x[d] = logits[base + (size_t)d * HW];
-  float m = x[0];
-#pragma unroll
-  for (int d = 1; d < D; ++d) m = fmaxf(m, x[d]);
-  float s = 0.f;
-#pragma unroll
-  for (int d = 0; d < D; ++d) s = s + expf(x[d] - m);
-  const float lse = logf(s);
-  float best = -1.f;
-  int bi = 0;
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    const float pr = expf((x[d] - m) - lse);
-    prob[base + (size_t)d * HW] = pr;
-    if (pr > best) {
-      best = pr;
-      bi = d;
-    }
-  }
+  float best;
+  const int bi = softmax_first_max<D>(x, [&](int d, float pr) { prob[base + (size_t)d * HW] = pr; }, best);
   const size_t o = (size_t)blockIdx.y * HW + p;
   const float dr = hyp[base + (size_t)bi * HW];
   depth_raw[o] = dr;

@@ -47,7 +47,7 @@ extern "C" int tmvs_fmt_forward(const float* stage1, long view_stride, const flo
 
 extern "C" size_t tmvs_depth_stage_workspace(int ndepth, int height, int width, int base_ch) {
   const size_t vol = (size_t)ndepth * height * width * 4;
-  return 2 * align_up256(vol) + align_up256(tmvs_costregnet_workspace(1, ndepth, height, width, base_ch));
+  return align_up256(vol) + align_up256(tmvs_costregnet_workspace(1, ndepth, height, width, base_ch));
 }
 
 // One cascade stage of TransMVSNet.forward for one sample (models/TransMVSNet.py:174-221):
@@ -65,9 +65,8 @@ extern "C" int tmvs_depth_stage(const float* depth_values, int n_values, const f
   const size_t vol = (size_t)ndepth * h * w;
   char* ws = (char*)workspace;
   float* sim = (float*)ws;
-  float* logits = (float*)(ws + align_up256(vol * 4));
-  char* crws = ws + 2 * align_up256(vol * 4);
-  const size_t crbytes = workspace_bytes - 2 * align_up256(vol * 4);
+  char* crws = ws + align_up256(vol * 4);
+  const size_t crbytes = workspace_bytes - align_up256(vol * 4);
   const int V = n_views - 1;
   int rc;
   if ((rc = tmvs_stage_hypotheses(depth_values, n_values, prev_depth, prev_h, prev_w, 1, ndepth, ratio, full_h, full_w,
@@ -83,7 +82,6 @@ extern "C" int tmvs_depth_stage(const float* depth_values, int n_values, const f
     rc = tmvs_warp_corr(ref, src, proj, hyp_out, view_w, vw_shift, 0, V, nullptr, 1, V, channels, ndepth, h, w,
                         warp_flags & TMVS_WARP_ROT_PLAIN, sim, nullptr, nullptr, stream);
   if (rc) return rc;
-  if ((rc = tmvs_costregnet(sim, 1, ndepth, h, w, cr, crws, crbytes, logits, stream))) return rc;
-  return tmvs_softmax_wta(logits, hyp_out, 1, ndepth, h, w, clamp_lo, clamp_hi, prob_out, depth_out, depth_raw_out,
-                          conf_out, stream);
+  return tmvs_costregnet_wta(sim, hyp_out, 1, ndepth, h, w, cr, crws, crbytes, clamp_lo, clamp_hi, prob_out, depth_out,
+                             depth_raw_out, conf_out, stream);
 }

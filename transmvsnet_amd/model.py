@@ -416,8 +416,7 @@ class TransMVSNet(nn.Module):
                     view_w = vw_new
                     if overlap:
                         pathway_side()
-                logits = ops.costregnet(sim, prep["cr"][s][0])
-                prob, depth, depth_raw, conf = ops.softmax_wta(logits, hyp, DEPTH_CLAMP)
+                prob, depth, depth_raw, conf = ops.costregnet_wta(sim, prep["cr"][s][0], hyp, DEPTH_CLAMP)
                 out = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}
             outputs[name] = out
         return outputs, view_w

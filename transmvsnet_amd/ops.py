@@ -258,6 +258,28 @@ def costregnet(x, weights: "_lib.CostRegWeights", keepalive=None):
     return out
 
 
+def costregnet_wta(x, weights: "_lib.CostRegWeights", hyp, clamp=(425.0, 935.0)):
+    """CostRegNet -> softmax/WTA (models/module.py:447-456, TransMVSNet.py:97-103,214-221) in one
+    call: prob, depth (clamped), depth_raw, conf, equal bit for bit to costregnet -> softmax_wta."""
+    _dev(x, "x")
+    _dev(hyp, "hyp")
+    b, d, h, w = x.shape
+    if tuple(hyp.shape) != (b, d, h, w):
+        raise ValueError(f"costregnet_wta: hyp shape {tuple(hyp.shape)} != volume shape {(b, d, h, w)}")
+    nbytes = _lib_h().tmvs_costregnet_workspace(b, d, h, w, weights.base_ch)
+    ws = torch.empty(nbytes // 4 + 64, device=x.device)
+    prob = torch.empty_like(x)
+    depth = torch.empty(b, h, w, device=x.device)
+    raw = torch.empty_like(depth)
+    conf = torch.empty_like(depth)
+    with _Span("tmvs_costregnet"):
+        _lib.check(_lib_h().tmvs_costregnet_wta(_ptr(x), _ptr(hyp), b, d, h, w, ctypes.byref(weights), _ptr(ws),
+                                                ws.numel() * 4, ctypes.c_float(clamp[0]), ctypes.c_float(clamp[1]),
+                                                _ptr(prob), _ptr(depth), _ptr(raw), _ptr(conf), _stream()),
+                   "tmvs_costregnet_wta")
+    return prob, depth, raw, conf
+
+
 def conv3d_bn_relu(x, wpk, alpha, shift, cout, stride):
     b, d, h, w, cin = x.shape
     do, ho, wo = ((d - 1) // 2 + 1, (h - 1) // 2 + 1, (w - 1) // 2 + 1) if stride == 2 else (d, h, w)
