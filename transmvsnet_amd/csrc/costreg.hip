@@ -669,28 +669,28 @@ __global__ __launch_bounds__(256) void prob_kernel(const float* __restrict__ x, 
 }
 
 // ---------------------------------------------------------------- prob + softmax / WTA, fused
-// prob_kernel's row-segment D walk over all D planes of a column (no depth chunks), with the
-// column's logits parked in LDS ([D][256], thread-private slots, conflict-free) instead of HBM;
-// then softmax_first_max (common.h, the code softmax_wta_kernel runs) and the gather of the
+// prob_kernel's row-segment D walk with the D / 8 depth chunks of one row segment as the waves of
+// one workgroup (wave k walks planes 8k-1 .. 8k+8, exactly prob_kernel's chunk k); each wave parks
+// its 8 logits per column in LDS ([D][64]) instead of HBM, and after one barrier wave 0 runs
+// softmax_first_max (common.h, the code softmax_wta_kernel runs) per column and gathers the
 // winning hypothesis (models/TransMVSNet.py:97-103,217-221). Same FMA chains as prob_kernel, so
 // prob / depth / conf equal prob_kernel + softmax_wta_kernel bit for bit, without the logits'
-// 8·D bytes per pixel of HBM traffic and one launch.
+// 8·D bytes per pixel of HBM traffic and one launch; same wave count as prob_kernel.
 template <int D>
-__global__ __launch_bounds__(256) void prob_wta_kernel(const float* __restrict__ x, const float* __restrict__ wt,
-                                                       const float* __restrict__ hyp, int H, int W, float lo,
-                                                       float hi, float* __restrict__ prob, float* __restrict__ depth,
-                                                       float* __restrict__ depth_raw, float* __restrict__ conf) {
-  __shared__ float lg[D * 256];
+__global__ __launch_bounds__(64 * (D / kDChunk)) void prob_wta_kernel(
+    const float* __restrict__ x, const float* __restrict__ wt, const float* __restrict__ hyp, int H, int W, float lo,
+    float hi, float* __restrict__ prob, float* __restrict__ depth, float* __restrict__ depth_raw,
+    float* __restrict__ conf) {
+  __shared__ float lg[D * 64];
   const int HW = H * W;
-  const int nseg = (W + kProbCols - 1) / kProbCols, nrow = (H + 3) / 4;
+  const int nseg = (W + kProbCols - 1) / kProbCols;
   int lb = xcd_remap(blockIdx.x, gridDim.x);
   const int seg = lb % nseg;
   lb /= nseg;
-  const int rowb = lb % nrow;
-  const int n = lb / nrow;
+  const int h = lb % H;
+  const int n = lb / H;
   const int lane = threadIdx.x & 63;
-  const int h = rowb * 4 + (threadIdx.x >> 6);
-  if (h >= H) return;  // whole wave; no barriers below (LDS slots are thread-private)
+  const int d0 = (threadIdx.x >> 6) * kDChunk, d1 = d0 + kDChunk;
   const int w = seg * kProbCols + lane - 1;
   const bool writes = lane >= 1 && lane <= kProbCols && w < W;
   const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)n * D * HW * 8, (unsigned)(D * HW * 32));
@@ -706,11 +706,10 @@ __global__ __launch_bounds__(256) void prob_wta_kernel(const float* __restrict__
     o[0] = make_float4(u[0], u[1], u[2], u[3]);
     o[1] = make_float4(v[0], v[1], v[2], v[3]);
   };
-  float* my = lg + threadIdx.x;
   float2_v c12 = {0.f, 0.f};
   float4 cur[2], nxt[2];
-  load_row(-1, 0, cur);
-  for (int i = -1; i <= D; ++i) {
+  load_row(d0 - 1, 0, cur);
+  for (int i = d0 - 1; i <= d1; ++i) {
     float acc_next = 0.f;
 #pragma unroll 1
     for (int kh = 0; kh < 3; ++kh) {
@@ -730,13 +729,14 @@ __global__ __launch_bounds__(256) void prob_wta_kernel(const float* __restrict__
       cur[0] = nxt[0];
       cur[1] = nxt[1];
     }
-    if (i >= 1) my[(i - 1) * 256] = c12.y;  // logit of plane i-1 complete
+    if (i - 1 >= d0) lg[(i - 1) * 64 + lane] = c12.y;  // logit of plane i-1 complete
     c12 = float2_v{acc_next, c12.x};
   }
-  if (!writes) return;
+  __syncthreads();
+  if (threadIdx.x >= 64 || !writes) return;
   float xl[D];
 #pragma unroll
-  for (int d = 0; d < D; ++d) xl[d] = my[d * 256];
+  for (int d = 0; d < D; ++d) xl[d] = lg[d * 64 + lane];
   const size_t base = (size_t)n * D * HW + (size_t)h * W + w;
   float best;
   const int bi = softmax_first_max<D>(xl, [&](int d, float pr) { prob[base + (size_t)d * HW] = pr; }, best);
@@ -1468,17 +1468,19 @@ extern "C" int tmvs_costregnet_wta(const float* x, const float* hyp, int batch, 
   int rc;
   if ((rc = costregnet_trunk(x, batch, depth, height, width, w, workspace, workspace_bytes, st, &x11, &c0))) return rc;
   if (depth > kDChunk) {
-    // the D walk needs depth chunks for enough parallelism (D=32 undivided measured 137 vs 93 + 16 us
-    // split, r07b): depth-chunked prob_kernel, logits in conv0's dead buffer, then the softmax kernel
+    // D > 8 fused (D/8 chunk waves per workgroup, wave 0 running the softmax after a barrier)
+    // measured 114 / 54 us vs 93 + 16 / 42 + 10 us split at D = 32 / 48 (r07d): split there, the
+    // logits in conv0's buffer (dead once conv11 has consumed it as its skip)
     hipLaunchKernelGGL(prob_kernel, prob_grid(batch, depth, height, width, kDChunk), dim3(256), 0, st, x11, c0, depth,
                        height, width, w->w[10]);
     TMVS_CHECK_LAUNCH();
     return tmvs_softmax_wta(c0, hyp, batch, depth, height, width, clamp_lo, clamp_hi, prob, depth_out, depth_raw,
                             conf, stream);
   }
-  // D = 8 (stage 3): prob_kernel walks it undivided anyway; fused (104 vs 109 + 19 us, r07b)
-  hipLaunchKernelGGL(prob_wta_kernel<kDChunk>, prob_grid(batch, depth, height, width, kDChunk), dim3(256), 0, st, x11,
-                     w->w[10], hyp, height, width, clamp_lo, clamp_hi, prob, depth_out, depth_raw, conf);
+  // D = 8 (stage 3): one wave per (sample, row, 62-column segment), 104 vs 109 + 19 us split (r07b/d)
+  hipLaunchKernelGGL(prob_wta_kernel<kDChunk>, dim3((unsigned)(((width + kProbCols - 1) / kProbCols) * height * batch)),
+                     dim3(64), 0, st, x11, w->w[10], hyp, height, width, clamp_lo, clamp_hi, prob, depth_out,
+                     depth_raw, conf);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
