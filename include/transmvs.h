@@ -122,9 +122,9 @@ size_t tmvs_costregnet_workspace(int batch, int depth, int height, int width, in
 /* x: [B][D][H][W] (=NDHWC with C=1), logits: [B][D][H][W]. Needs D,H,W % 8 == 0. */
 int tmvs_costregnet(const float* x, int batch, int depth, int height, int width, const TmvsCostRegWeights* w,
                     void* workspace, size_t workspace_bytes, float* logits, void* stream);
-/* CostRegNet + softmax/WTA in one call (models/TransMVSNet.py:97-103,214-221): for ndepth 8 the
- * prob conv, the softmax over D and the winner-take-all run as one kernel (the logits stay in LDS
- * and never reach HBM); for larger ndepth the depth-chunked prob kernel + tmvs_softmax_wta. Outputs and their bits are those of tmvs_costregnet -> tmvs_softmax_wta.
+/* CostRegNet + softmax/WTA in one call (models/TransMVSNet.py:97-103,214-221): for ndepth <= 32
+ * the prob conv, the softmax over D and the winner-take-all run as one kernel (the logits stay in
+ * LDS and never reach HBM); for 48 and 64 the depth-chunked prob kernel + tmvs_softmax_wta. Outputs and their bits are those of tmvs_costregnet -> tmvs_softmax_wta.
  * Same workspace as tmvs_costregnet; ndepth in {8, 16, 24, 32, 48, 64}.                        */
 int tmvs_costregnet_wta(const float* x, const float* hyp, int batch, int depth, int height, int width,
                         const TmvsCostRegWeights* w, void* workspace, size_t workspace_bytes, float clamp_lo,

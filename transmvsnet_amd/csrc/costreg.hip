@@ -1467,20 +1467,32 @@ extern "C" int tmvs_costregnet_wta(const float* x, const float* hyp, int batch, 
   float *x11, *c0;
   int rc;
   if ((rc = costregnet_trunk(x, batch, depth, height, width, w, workspace, workspace_bytes, st, &x11, &c0))) return rc;
-  if (depth > kDChunk) {
-    // D > 8 fused (D/8 chunk waves per workgroup, wave 0 running the softmax after a barrier)
-    // measured 114 / 54 us vs 93 + 16 / 42 + 10 us split at D = 32 / 48 (r07d): split there, the
-    // logits in conv0's buffer (dead once conv11 has consumed it as its skip)
+  if (depth > 32) {
+    // D = 48 (stage 1) fused measured 53.8 us vs 40.1 + 10.3 us split (r07d vs r07b): few columns
+    // and a 48-deep softmax tail behind the barrier. Split: the depth-chunked prob kernel, its
+    // logits in conv0's buffer (dead once conv11 has consumed it as its skip), then the softmax kernel
     hipLaunchKernelGGL(prob_kernel, prob_grid(batch, depth, height, width, kDChunk), dim3(256), 0, st, x11, c0, depth,
                        height, width, w->w[10]);
     TMVS_CHECK_LAUNCH();
     return tmvs_softmax_wta(c0, hyp, batch, depth, height, width, clamp_lo, clamp_hi, prob, depth_out, depth_raw,
                             conf, stream);
   }
-  // D = 8 (stage 3): one wave per (sample, row, 62-column segment), 104 vs 109 + 19 us split (r07b/d)
-  hipLaunchKernelGGL(prob_wta_kernel<kDChunk>, dim3((unsigned)(((width + kProbCols - 1) / kProbCols) * height * batch)),
-                     dim3(64), 0, st, x11, w->w[10], hyp, height, width, clamp_lo, clamp_hi, prob, depth_out,
-                     depth_raw, conf);
+  // D <= 32: one workgroup per (sample, row, 62-column segment), its D/8 waves prob_kernel's depth
+  // chunks. Measured (r07d vs r07b): D = 32 114.0 vs 108.4 + 15.7 us, D = 8 104.3 vs 90.9 + 18.6 us
+  const dim3 gf((unsigned)(((width + kProbCols - 1) / kProbCols) * height * batch));
+  const dim3 bf((unsigned)(64 * (depth / kDChunk)));
+#define TMVS_PW_CASE(DD)                                                                                      \
+  case DD:                                                                                                    \
+    hipLaunchKernelGGL(prob_wta_kernel<DD>, gf, bf, 0, st, x11, w->w[10], hyp, height, width, clamp_lo,       \
+                       clamp_hi, prob, depth_out, depth_raw, conf);                                           \
+    break;
+  switch (depth) {
+    TMVS_PW_CASE(8)
+    TMVS_PW_CASE(16)
+    TMVS_PW_CASE(24)
+    TMVS_PW_CASE(32)
+  }
+#undef TMVS_PW_CASE
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
