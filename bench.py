@@ -277,7 +277,7 @@ def run(args, world, rank, local):
         kern.append({"kernel": "tmvs_costregnet", "bound": "mfma", "achieved": round(ach, 2),
                      "peak": PEAK_F32_MFMA_TFS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_MFMA_TFS, 4),
                      "traffic": None, "ms_per_depth_map": round(float(per_launch.sum()), 4),
-                     "per": "depth map (3 tmvs_costregnet calls, 11 kernels each)",
+                     "per": "depth map (3 tmvs_costregnet_wta calls: 11 CostRegNet kernels each, the prob conv fused with softmax/WTA at stages 2/3, + the softmax kernel at stage 1)",
                      "algorithmic_flop": int(sum(cr_flop)),
                      "per_stage_ms": [round(float(x), 4) for x in per_launch]})
     # headline roofline: the north-star kernel (warp_corr_kernel, one launch per stage; its
