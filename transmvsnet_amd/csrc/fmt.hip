@@ -474,10 +474,13 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
 
 // Tiles per wave: as many as possible (small partial slabs, short combine) while the launch still
 // has >= 2048 waves (2 per SIMD); the one-view cross-attention K/V otherwise runs at 0.1 waves/SIMD.
+#ifndef TMVS_KV_MIN_WAVES
+#define TMVS_KV_MIN_WAVES 2048
+#endif
 static int kv_tiles_per_wave(int nv, int S) {
   const int tiles = (S + 15) / 16;
   int tpw = kKvTilesPerWave;
-  while (tpw > 2 && (long)nv * ((tiles + tpw - 1) / tpw) < 2048) tpw >>= 1;
+  while (tpw > 2 && (long)nv * ((tiles + tpw - 1) / tpw) < TMVS_KV_MIN_WAVES) tpw >>= 1;
   return tpw;
 }
 static int kv_nblk(int nv, int S) {
