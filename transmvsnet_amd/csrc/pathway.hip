@@ -19,6 +19,28 @@ struct Axis {
   float l0, l1;
 };
 
+// The lateral halo values (NCHW, the FeatureNet output) do not depend on the coarse reduction:
+// every thread requests its <= 2 halo pixels' CF channels before phase 1, so their HBM latency
+// overlaps the reduction instead of sitting after the first barrier. Out-of-image pixels read 0.
+#ifndef TMVS_PATHWAY_PREFETCH
+#define TMVS_PATHWAY_PREFETCH 1
+#endif
+constexpr int kHaloIters = (kHalo * kHalo + 255) / 256;
+
+template <int CF>
+__device__ __forceinline__ void load_lateral(const float* __restrict__ lv, int y0, int x0, int H, int W,
+                                             float (&lat)[kHaloIters][CF]) {
+#pragma unroll
+  for (int it = 0; it < kHaloIters; ++it) {
+    const int idx = threadIdx.x + 256 * it;
+    const int r = idx / kHalo, c = idx - r * kHalo;
+    const int y = y0 - 1 + r, x = x0 - 1 + c;
+    const bool ok = idx < kHalo * kHalo && y >= 0 && y < H && x >= 0 && x < W;
+#pragma unroll
+    for (int o = 0; o < CF; ++o) lat[it][o] = ok ? lv[((size_t)o * H + y) * W + x] : 0.f;
+  }
+}
+
 __device__ __forceinline__ Axis up_axis(int dst, int in_size, int out_size) {
   const float scale = (float)in_size / (float)out_size;
   float src = scale * ((float)dst + 0.5f) - 0.5f;
@@ -45,6 +67,11 @@ __global__ __launch_bounds__(256) void pathway_kernel(const float* __restrict__ 
   const int y0 = blockIdx.y * kTile, x0 = blockIdx.x * kTile;
   const int cy0 = y0 / 2 - 1, cx0 = x0 / 2 - 1;
   const float* cv = coarse + (size_t)v * h * w * CC;
+  const float* lv = lateral + (size_t)v * lat_stride;
+#if TMVS_PATHWAY_PREFETCH
+  float lat[kHaloIters][CF];
+  load_lateral<CF>(lv, y0, x0, H, W, lat);
+#endif
   // 1) 1x1 reduction of the coarse patch
   for (int idx = threadIdx.x; idx < kCoarse * kCoarse; idx += blockDim.x) {
     const int r = idx / kCoarse, c = idx - r * kCoarse;
@@ -72,8 +99,10 @@ __global__ __launch_bounds__(256) void pathway_kernel(const float* __restrict__ 
   }
   __syncthreads();
   // 2) bilinear x2 up-sampling + lateral over the 18x18 halo (zero outside the image)
-  const float* lv = lateral + (size_t)v * lat_stride;
-  for (int idx = threadIdx.x; idx < kHalo * kHalo; idx += blockDim.x) {
+#pragma unroll
+  for (int it = 0; it < kHaloIters; ++it) {
+    const int idx = threadIdx.x + 256 * it;
+    if (idx >= kHalo * kHalo) break;
     const int r = idx / kHalo, c = idx - r * kHalo;
     const int y = y0 - 1 + r, x = x0 - 1 + c;
     if (y < 0 || y >= H || x < 0 || x >= W) {
@@ -88,7 +117,11 @@ __global__ __launch_bounds__(256) void pathway_kernel(const float* __restrict__ 
       const float t0 = fmaf(red[o][r0][c0], ax.l0, red[o][r0][c1] * ax.l1);
       const float t1 = fmaf(red[o][r1][c0], ax.l0, red[o][r1][c1] * ax.l1);
       const float up = fmaf(t0, ay.l0, t1 * ay.l1);
+#if TMVS_PATHWAY_PREFETCH
+      inb[o][r][c] = up + lat[it][o];
+#else
       inb[o][r][c] = up + lv[((size_t)o * H + y) * W + x];
+#endif
     }
   }
   __syncthreads();
@@ -141,6 +174,11 @@ __global__ __launch_bounds__(256) void pathway16_mfma_kernel(const float* __rest
   const int y0 = blockIdx.y * kTile, x0 = blockIdx.x * kTile;
   const int cy0 = y0 / 2 - 1, cx0 = x0 / 2 - 1;
   const float* cv = coarse + (size_t)v * h * w * CC;
+  const float* lv = lateral + (size_t)v * lat_stride;
+#if TMVS_PATHWAY_PREFETCH
+  float lat[kHaloIters][CF];
+  load_lateral<CF>(lv, y0, x0, H, W, lat);
+#endif
   // 1) 1x1 reduction of the coarse patch (as pathway_kernel)
   for (int idx = threadIdx.x; idx < kCoarse * kCoarse; idx += blockDim.x) {
     const int r = idx / kCoarse, c = idx - r * kCoarse;
@@ -176,8 +214,10 @@ __global__ __launch_bounds__(256) void pathway16_mfma_kernel(const float* __rest
     for (int j = 0; j < 4; ++j) wa[t][j] = wsm[((4 * j + kgrp) * 9 + t) * CF + col];
   __syncthreads();
   // 2) bilinear x2 up-sampling + lateral over the 18x18 halo (zero outside the image)
-  const float* lv = lateral + (size_t)v * lat_stride;
-  for (int idx = threadIdx.x; idx < kHalo * kHalo; idx += blockDim.x) {
+#pragma unroll
+  for (int it = 0; it < kHaloIters; ++it) {
+    const int idx = threadIdx.x + 256 * it;
+    if (idx >= kHalo * kHalo) break;
     const int r = idx / kHalo, c = idx - r * kHalo;
     const int y = y0 - 1 + r, x = x0 - 1 + c;
     if (y < 0 || y >= H || x < 0 || x >= W) {
@@ -192,7 +232,11 @@ __global__ __launch_bounds__(256) void pathway16_mfma_kernel(const float* __rest
       const float t0 = fmaf(red[o][r0][c0], ax.l0, red[o][r0][c1] * ax.l1);
       const float t1 = fmaf(red[o][r1][c0], ax.l0, red[o][r1][c1] * ax.l1);
       const float up = fmaf(t0, ay.l0, t1 * ay.l1);
+#if TMVS_PATHWAY_PREFETCH
+      inb[halo16_index(idx, o)] = up + lat[it][o];
+#else
       inb[halo16_index(idx, o)] = up + lv[((size_t)o * H + y) * W + x];
+#endif
     }
   }
   __syncthreads();
