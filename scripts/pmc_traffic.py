@@ -18,7 +18,8 @@ from collections import defaultdict
 ENTRY_KERNELS = {
     "tmvs_warp_corr": ("warp_corr_kernel", "warp_pair_kernel"),
     "tmvs_costregnet": ("conv0_kernel", "conv3d_lds_kernel", "conv3d_direct_kernel", "conv3d_s2c8_tile_kernel",
-                        "conv3d_c16_kernel", "deconv3d_lds_kernel", "deconv3d_c8_kernel", "prob_kernel"),
+                        "conv3d_c16_kernel", "deconv3d_lds_kernel", "deconv3d_c8_kernel", "prob_kernel",
+                        "prob_wta_kernel", "softmax_wta_kernel"),
 }
 STEP_KERNEL = "fmt_embed_kernel"  # launched exactly once per forward step
 

@@ -18,9 +18,12 @@ for r in rows:
 tot = 0.0
 out = []
 for (name, grid), v in agg.items():
-    per_step = sum(v) / steps
+    # median per call x calls per step: one cold call (first touch of a fresh allocation in a
+    # warm-up step, e.g. 25 ms for a 255-MB conv0 output) must not stand in for the steady state
+    med = sorted(v)[len(v) // 2]
+    per_step = med * len(v) / steps
     tot += per_step
-    out.append((per_step, name, grid, len(v) / steps, sum(v) / len(v)))
+    out.append((per_step, name, grid, len(v) / steps, med))
 for per_step, name, grid, calls, mean in sorted(out, reverse=True):
     print(f"{per_step:9.1f} us/step  {calls:4.1f} calls x {mean:8.1f} us  grid={grid:>9}  {name}")
-print(f"{tot:9.1f} us/step total over {steps} steps")
+print(f"{tot:9.1f} us/step total over {steps} steps (median duration per call)")

@@ -27,6 +27,28 @@ struct Axis {
 #endif
 constexpr int kHaloIters = (kHalo * kHalo + 255) / 256;
 
+// Tiles are dealt out XCD-contiguously over a 1-D grid (x fastest, then y, then view): consecutive
+// block ids go to different XCDs, so with the plain 3-D grid a tile's x/y neighbours -- which read
+// the same 128-B lines of the halo rows (an 18-float NCHW row spans 2-3 lines) -- sat behind
+// different L2s and each re-fetched them.
+#ifndef TMVS_PATHWAY_XCD
+#define TMVS_PATHWAY_XCD 1
+#endif
+__device__ __forceinline__ void pathway_tile(int W, int H, int& v, int& y0, int& x0) {
+#if TMVS_PATHWAY_XCD
+  const int nbx = (W + kTile - 1) / kTile, nby = (H + kTile - 1) / kTile;
+  int lb = xcd_remap(blockIdx.x, gridDim.x);
+  x0 = (lb % nbx) * kTile;
+  lb /= nbx;
+  y0 = (lb % nby) * kTile;
+  v = lb / nby;
+#else
+  v = blockIdx.z;
+  y0 = blockIdx.y * kTile;
+  x0 = blockIdx.x * kTile;
+#endif
+}
+
 template <int CF>
 __device__ __forceinline__ void load_lateral(const float* __restrict__ lv, int y0, int x0, int H, int W,
                                              float (&lat)[kHaloIters][CF]) {
@@ -63,8 +85,8 @@ __global__ __launch_bounds__(256) void pathway_kernel(const float* __restrict__ 
   __shared__ float red[CF][kCoarse][kCoarse + 1];
   __shared__ float inb[CF][kHalo][kHalo + 1];
   const int H = 2 * h, W = 2 * w;
-  const int v = blockIdx.z;
-  const int y0 = blockIdx.y * kTile, x0 = blockIdx.x * kTile;
+  int v, y0, x0;
+  pathway_tile(W, H, v, y0, x0);
   const int cy0 = y0 / 2 - 1, cx0 = x0 / 2 - 1;
   const float* cv = coarse + (size_t)v * h * w * CC;
   const float* lv = lateral + (size_t)v * lat_stride;
@@ -170,8 +192,8 @@ __global__ __launch_bounds__(256) void pathway16_mfma_kernel(const float* __rest
   __shared__ float red[CF][kCoarse][kCoarse + 1];
   __shared__ __attribute__((aligned(16))) float inb[kHalo * kHalo * CF];
   const int H = 2 * h, W = 2 * w;
-  const int v = blockIdx.z;
-  const int y0 = blockIdx.y * kTile, x0 = blockIdx.x * kTile;
+  int v, y0, x0;
+  pathway_tile(W, H, v, y0, x0);
   const int cy0 = y0 / 2 - 1, cx0 = x0 / 2 - 1;
   const float* cv = coarse + (size_t)v * h * w * CC;
   const float* lv = lateral + (size_t)v * lat_stride;
@@ -277,7 +299,13 @@ extern "C" int tmvs_fmt_pathway(const float* coarse, const float* lateral, long 
                                 const float* w_reduce, const float* w_smooth, int nv, int cc, int cf, int h, int w,
                                 float* out, void* stream) {
   if (!coarse || !lateral || !w_reduce || !w_smooth || !out || nv <= 0 || h <= 0 || w <= 0) return TMVS_ERR_ARG;
+#if TMVS_PATHWAY_XCD
+  const long nblk = (long)((2 * w + kTile - 1) / kTile) * ((2 * h + kTile - 1) / kTile) * nv;
+  if (nblk > 0x7fffffffL) return TMVS_ERR_SHAPE;
+  const dim3 grid((unsigned)nblk);
+#else
   const dim3 grid((2 * w + kTile - 1) / kTile, (2 * h + kTile - 1) / kTile, nv);
+#endif
   hipStream_t st = (hipStream_t)stream;
   if (cc == 32 && cf == 16)
     hipLaunchKernelGGL((pathway16_mfma_kernel<32>), grid, dim3(256), 0, st, coarse, lateral, lat_view_stride,
