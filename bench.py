@@ -55,6 +55,8 @@ def _args():
     ap.add_argument("--no-overlap", action="store_true", help="run the FMT pathway on the main stream (A/B)")
     ap.add_argument("--e2e-steps", type=int, default=10,
                     help="timed full forward() passes (images -> depth, FeatureNet included); 0 = skip")
+    ap.add_argument("--side-priority", type=int, default=0,
+                    help="stream priority of the FMT-pathway side stream (lower = higher; A/B knob)")
     ap.add_argument("--train-steps", type=int, default=3,
                     help="timed C5 training steps of the DepthNet stages (transmvsnet_amd.train); 0 = skip")
     return ap.parse_args()
@@ -180,6 +182,7 @@ def run(args, world, rank, local):
     model.load_state_dict(synthetic.synthetic_state_dict(synthetic.state_dict_shapes(model), seed=0, sharpen=100.0))
     model = model.to(dev)
     model.overlap_pathway = not args.no_overlap
+    model.side_priority = args.side_priority
     feats_cpu, proj, dv = make_inputs(dev)
     feats = {k: v.to(dev) for k, v in feats_cpu.items()}
     dv_dev = dv.to(dev)

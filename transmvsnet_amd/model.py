@@ -227,6 +227,8 @@ class TransMVSNet(nn.Module):
         # the FMT pathway (stage-2/3 features) depends only on the FMT output: run it on a side
         # stream, concurrently with stage 1 (whose small CostRegNet grids leave the GPU idle)
         self.overlap_pathway = True
+        # priority of that side stream (torch.cuda.Stream: lower = higher priority; 0 = default)
+        self.side_priority = 0
         # rounding of homo_warping's rot·(x, y, 1) to reproduce: 'auto' = the host torch's
         # (ops.host_rot_order), or 'fma' / 'plain' to pin it (fixtures made on another machine)
         self.warp_rot_order = "auto"
@@ -370,7 +372,7 @@ class TransMVSNet(nn.Module):
             main = torch.cuda.current_stream(s1.device)
             side = self._side.get(s1.device)
             if side is None:
-                side = self._side[s1.device] = torch.cuda.Stream(s1.device)
+                side = self._side[s1.device] = torch.cuda.Stream(s1.device, priority=self.side_priority)
             ready = torch.cuda.Event()
             ready.record(main)
             side.wait_event(ready)
