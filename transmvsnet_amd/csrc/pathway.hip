@@ -169,6 +169,125 @@ __global__ __launch_bounds__(256) void pathway_kernel(const float* __restrict__ 
   for (int o4 = 0; o4 < CF / 4; ++o4) op[o4] = make_float4(acc[4 * o4], acc[4 * o4 + 1], acc[4 * o4 + 2], acc[4 * o4 + 3]);
 }
 
+// Stage-3 form with R output rows per thread: a workgroup owns a 16 x 16R tile, so the two
+// barriers, the coarse/halo staging and every scalar weight load are shared by R pixels. Tap
+// (i, k) feeds the R accumulator sets back to back; each output's chain keeps pathway_kernel's
+// (i, k, o) order, so the results are bitwise those of pathway_kernel.
+#ifndef TMVS_PW_R
+#define TMVS_PW_R 2
+#endif
+template <int CC, int CF, int R>
+__global__ __launch_bounds__(256) void pathway_rows_kernel(const float* __restrict__ coarse,
+                                                           const float* __restrict__ lateral, long lat_stride,
+                                                           const float* __restrict__ wred,
+                                                           const float* __restrict__ wsm, int h, int w,
+                                                           float* __restrict__ out) {
+  constexpr int TH = kTile * R, HH = TH + 2, CH = TH / 2 + 2;
+  constexpr int NIT = (HH * kHalo + 255) / 256;
+  __shared__ float red[CF][CH][kCoarse + 1];
+  __shared__ float inb[CF][HH][kHalo + 1];
+  const int H = 2 * h, W = 2 * w;
+  const int nbx = (W + kTile - 1) / kTile, nby = (H + TH - 1) / TH;
+  int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int x0 = (lb % nbx) * kTile;
+  lb /= nbx;
+  const int y0 = (lb % nby) * TH;
+  const int v = lb / nby;
+  const int cy0 = y0 / 2 - 1, cx0 = x0 / 2 - 1;
+  const float* cv = coarse + (size_t)v * h * w * CC;
+  const float* lv = lateral + (size_t)v * lat_stride;
+  float lat[NIT][CF];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int idx = threadIdx.x + 256 * it;
+    const int r = idx / kHalo, c = idx - r * kHalo;
+    const int y = y0 - 1 + r, x = x0 - 1 + c;
+    const bool ok = idx < HH * kHalo && y >= 0 && y < H && x >= 0 && x < W;
+#pragma unroll
+    for (int o = 0; o < CF; ++o) lat[it][o] = ok ? lv[((size_t)o * H + y) * W + x] : 0.f;
+  }
+  // 1) 1x1 reduction of the coarse patch
+  for (int idx = threadIdx.x; idx < CH * kCoarse; idx += 256) {
+    const int r = idx / kCoarse, c = idx - r * kCoarse;
+    const int cy = cy0 + r, cx = cx0 + c;
+    if (cy < 0 || cy >= h || cx < 0 || cx >= w) continue;
+    float xin[CC];
+    const float* p = cv + ((size_t)cy * w + cx) * CC;
+#pragma unroll
+    for (int i4 = 0; i4 < CC / 4; ++i4) {
+      const float4 t = *reinterpret_cast<const float4*>(p + 4 * i4);
+      xin[4 * i4] = t.x;
+      xin[4 * i4 + 1] = t.y;
+      xin[4 * i4 + 2] = t.z;
+      xin[4 * i4 + 3] = t.w;
+    }
+    float acc[CF];
+#pragma unroll
+    for (int o = 0; o < CF; ++o) acc[o] = 0.f;
+#pragma unroll 2
+    for (int i = 0; i < CC; ++i)
+#pragma unroll
+      for (int o = 0; o < CF; ++o) acc[o] = fmaf(wred[i * CF + o], xin[i], acc[o]);
+#pragma unroll
+    for (int o = 0; o < CF; ++o) red[o][r][c] = acc[o];
+  }
+  __syncthreads();
+  // 2) bilinear x2 up-sampling + lateral over the (16R+2) x 18 halo (zero outside the image)
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int idx = threadIdx.x + 256 * it;
+    if (idx >= HH * kHalo) break;
+    const int r = idx / kHalo, c = idx - r * kHalo;
+    const int y = y0 - 1 + r, x = x0 - 1 + c;
+    if (y < 0 || y >= H || x < 0 || x >= W) {
+#pragma unroll
+      for (int o = 0; o < CF; ++o) inb[o][r][c] = 0.f;
+      continue;
+    }
+    const Axis ay = up_axis(y, h, H), ax = up_axis(x, w, W);
+    const int r0 = ay.i0 - cy0, r1 = ay.i1 - cy0, c0 = ax.i0 - cx0, c1 = ax.i1 - cx0;
+#pragma unroll
+    for (int o = 0; o < CF; ++o) {
+      const float t0 = fmaf(red[o][r0][c0], ax.l0, red[o][r0][c1] * ax.l1);
+      const float t1 = fmaf(red[o][r1][c0], ax.l0, red[o][r1][c1] * ax.l1);
+      const float up = fmaf(t0, ay.l0, t1 * ay.l1);
+      inb[o][r][c] = up + lat[it][o];
+    }
+  }
+  __syncthreads();
+  // 3) 3x3 smoothing conv, R vertically adjacent output pixels per thread (rows R*ty .. R*ty+R-1)
+  const int ty = threadIdx.x / kTile, tx = threadIdx.x - ty * kTile;
+  const int x = x0 + tx;
+  if (x >= W || y0 + R * ty >= H) return;
+  float acc[R][CF];
+#pragma unroll
+  for (int q = 0; q < R; ++q)
+#pragma unroll
+    for (int o = 0; o < CF; ++o) acc[q][o] = 0.f;
+#pragma unroll 1
+  for (int i = 0; i < CF; ++i) {
+#pragma unroll 3
+    for (int k = 0; k < 9; ++k) {
+      const float* __restrict__ wk = wsm + (i * 9 + k) * CF;
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const float xv = inb[i][R * ty + q + k / 3][tx + k % 3];
+#pragma unroll
+        for (int o = 0; o < CF; ++o) acc[q][o] = fmaf(wk[o], xv, acc[q][o]);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const int y = y0 + R * ty + q;
+    if (y >= H) break;
+    float4* op = reinterpret_cast<float4*>(out + (((size_t)v * H + y) * W + x) * CF);
+#pragma unroll
+    for (int o4 = 0; o4 < CF / 4; ++o4)
+      op[o4] = make_float4(acc[q][4 * o4], acc[q][4 * o4 + 1], acc[q][4 * o4 + 2], acc[q][4 * o4 + 3]);
+  }
+}
+
 // 16-channel variant (stage-2 pathway, the larger one): the 3x3 smoothing conv runs on fp32
 // MFMA as an implicit GEMM -- M = 16 output channels, N = 16 pixels of a tile row,
 // K = 16 channels x 9 taps -- with B fragments from the LDS halo and A fragments (weights) in
@@ -310,9 +429,16 @@ extern "C" int tmvs_fmt_pathway(const float* coarse, const float* lateral, long 
   if (cc == 32 && cf == 16)
     hipLaunchKernelGGL((pathway16_mfma_kernel<32>), grid, dim3(256), 0, st, coarse, lateral, lat_view_stride,
                        w_reduce, w_smooth, h, w, out);
-  else if (cc == 16 && cf == 8)
+  else if (cc == 16 && cf == 8) {
+#if TMVS_PW_R > 1
+    const long nrb = (long)((2 * w + kTile - 1) / kTile) * ((2 * h + kTile * TMVS_PW_R - 1) / (kTile * TMVS_PW_R)) * nv;
+    hipLaunchKernelGGL((pathway_rows_kernel<16, 8, TMVS_PW_R>), dim3((unsigned)nrb), dim3(256), 0, st, coarse, lateral,
+                       lat_view_stride, w_reduce, w_smooth, h, w, out);
+#else
     hipLaunchKernelGGL((pathway_kernel<16, 8>), grid, dim3(256), 0, st, coarse, lateral, lat_view_stride, w_reduce,
                        w_smooth, h, w, out);
+#endif
+  }
   else
     return TMVS_ERR_SHAPE;
   TMVS_CHECK_LAUNCH();
