@@ -36,7 +36,10 @@ DEPTH_CLAMP = (425.0, 935.0)         # models/TransMVSNet.py:221
 # ----------------------------------------------------------------------------- helpers
 def _bn(x, sd, p, training=False):
     """nn.BatchNorm{2,3}d (models/module.py:132,173,218): eval mode, or train mode (batch statistics;
-    the running statistics in `sd` are updated in place with momentum 0.1, as the module does)."""
+    the running statistics in `sd` are updated in place with momentum 0.1 and num_batches_tracked
+    counted, as the module does in train mode)."""
+    if training and p + "num_batches_tracked" in sd:
+        sd[p + "num_batches_tracked"].add_(1)
     return F.batch_norm(x, sd[p + "running_mean"], sd[p + "running_var"], sd[p + "weight"], sd[p + "bias"],
                         training, 0.1, BN_EPS)
 
@@ -262,11 +265,13 @@ def softmax_regression(cost_reg, depth_values):
     return prob, depth, conf
 
 
-def depth_net(sd, features, proj_matrix, depth_values, stage_idx, view_weights=None):
+def depth_net(sd, features, proj_matrix, depth_values, stage_idx, view_weights=None, training=False):
     """DepthNet.forward, models/TransMVSNet.py:38-109 (returns dict, view_weights)."""
-    sim, vw = build_cost_volume(sd, features, proj_matrix, depth_values, view_weights)
-    cost = cost_reg_net(sd, f"cost_regularization.{stage_idx}.", sim)
+    sim, vw = build_cost_volume(sd, features, proj_matrix, depth_values, view_weights, training=training)
+    cost = cost_reg_net(sd, f"cost_regularization.{stage_idx}.", sim, training=training)
     prob, depth, conf = softmax_regression(cost, depth_values)
+    if training:
+        conf = conf.detach()  # computed under torch.no_grad() (models/TransMVSNet.py:102-103)
     out = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": depth_values}
     return out, (vw.detach() if vw is not None else None)
 
@@ -304,8 +309,11 @@ def stage_hypotheses(depth, depth_values, stage_idx, img_hw, ndepths=NDEPTHS, ra
 
 
 def forward_from_features(sd, features, proj_matrix, depth_values, img_hw, ndepths=NDEPTHS, ratios=DEPTH_RATIOS,
-                          with_view_weights=False):
-    """TransMVSNet.forward after feature extraction, models/TransMVSNet.py:162-226."""
+                          with_view_weights=False, training=False):
+    """TransMVSNet.forward after feature extraction, models/TransMVSNet.py:162-226 (training: the
+    model in train mode -- BatchNorm batch statistics + running-statistic updates; autograd flows
+    as in the reference: hypotheses and the next stage's depth detached, stage-1 view weights
+    detached for stages 2/3)."""
     feats = fmt_with_pathway(sd, features)
     outputs = {}
     depth = None
@@ -315,7 +323,7 @@ def forward_from_features(sd, features, proj_matrix, depth_values, img_hw, ndept
         hyp = stage_hypotheses(depth, depth_values, s, img_hw, ndepths, ratios)
         if s > 0:
             view_weights = F.interpolate(view_weights, scale_factor=2, mode="nearest")
-        out, vw = depth_net(sd, [f[name] for f in feats], proj_matrix[name], hyp, s, view_weights)
+        out, vw = depth_net(sd, [f[name] for f in feats], proj_matrix[name], hyp, s, view_weights, training)
         if s == 0:
             view_weights = vw
             stage1_vw = vw
@@ -379,36 +387,40 @@ def _dcn(sd, p, x):
     return deform_conv2d(x, offset, sd[p + "weight"], sd[p + "bias"], 1, mask)
 
 
-def _conv2d_bn_relu(sd, p, x, stride, padding):
+def _conv2d_bn_relu(sd, p, x, stride, padding, training=False):
     """Conv2d block, models/module.py:49-56 (bn + relu)."""
     y = F.conv2d(x, sd[p + "conv.weight"], stride=stride, padding=padding)
-    return F.relu(_bn(y, sd, p + "bn."))
+    return F.relu(_bn(y, sd, p + "bn.", training))
 
 
-def _out_head(sd, p, x, first_k):
+def _out_head(sd, p, x, first_k, training=False):
     """FeatureNet.out{1,2,3} Sequentials, models/module.py:362-395."""
-    x = _conv2d_bn_relu(sd, p + "0.", x, 1, 0 if first_k == 1 else 1)
-    x = F.relu(_bn(_dcn(sd, p + "1.", x), sd, p + "2."))
-    x = F.relu(_bn(_dcn(sd, p + "4.", x), sd, p + "5."))
+    t = training
+    x = _conv2d_bn_relu(sd, p + "0.", x, 1, 0 if first_k == 1 else 1, t)
+    x = F.relu(_bn(_dcn(sd, p + "1.", x), sd, p + "2.", t))
+    x = F.relu(_bn(_dcn(sd, p + "4.", x), sd, p + "5.", t))
     return _dcn(sd, p + "7.", x)
 
 
-def feature_net(sd, x, p="feature."):
-    """FeatureNet.forward, models/module.py:399-422."""
-    conv0 = _conv2d_bn_relu(sd, p + "conv0.1.", _conv2d_bn_relu(sd, p + "conv0.0.", x, 1, 1), 1, 1)
-    c1 = _conv2d_bn_relu(sd, p + "conv1.0.", conv0, 2, 2)
-    conv1 = _conv2d_bn_relu(sd, p + "conv1.2.", _conv2d_bn_relu(sd, p + "conv1.1.", c1, 1, 1), 1, 1)
-    c2 = _conv2d_bn_relu(sd, p + "conv2.0.", conv1, 2, 2)
-    conv2 = _conv2d_bn_relu(sd, p + "conv2.2.", _conv2d_bn_relu(sd, p + "conv2.1.", c2, 1, 1), 1, 1)
-    out = {"stage1": _out_head(sd, p + "out1.", conv2, 1)}
+def feature_net(sd, x, p="feature.", training=False):
+    """FeatureNet.forward, models/module.py:399-422 (training: BatchNorm2d batch statistics of this
+    call's batch -- the reference calls FeatureNet once per view, models/TransMVSNet.py:151-153)."""
+    t = training
+    conv0 = _conv2d_bn_relu(sd, p + "conv0.1.", _conv2d_bn_relu(sd, p + "conv0.0.", x, 1, 1, t), 1, 1, t)
+    c1 = _conv2d_bn_relu(sd, p + "conv1.0.", conv0, 2, 2, t)
+    conv1 = _conv2d_bn_relu(sd, p + "conv1.2.", _conv2d_bn_relu(sd, p + "conv1.1.", c1, 1, 1, t), 1, 1, t)
+    c2 = _conv2d_bn_relu(sd, p + "conv2.0.", conv1, 2, 2, t)
+    conv2 = _conv2d_bn_relu(sd, p + "conv2.2.", _conv2d_bn_relu(sd, p + "conv2.1.", c2, 1, 1, t), 1, 1, t)
+    out = {"stage1": _out_head(sd, p + "out1.", conv2, 1, t)}
     intra = F.interpolate(conv2, scale_factor=2.0, mode="nearest") + F.conv2d(conv1, sd[p + "inner1.weight"], sd[p + "inner1.bias"])
-    out["stage2"] = _out_head(sd, p + "out2.", intra, 3)
+    out["stage2"] = _out_head(sd, p + "out2.", intra, 3, t)
     intra = F.interpolate(intra, scale_factor=2.0, mode="nearest") + F.conv2d(conv0, sd[p + "inner2.weight"], sd[p + "inner2.bias"])
-    out["stage3"] = _out_head(sd, p + "out3.", intra, 3)
+    out["stage3"] = _out_head(sd, p + "out3.", intra, 3, t)
     return out
 
 
-def forward(sd, imgs, proj_matrix, depth_values, **kw):
+def forward(sd, imgs, proj_matrix, depth_values, training=False, **kw):
     """TransMVSNet.forward, models/TransMVSNet.py:141-226."""
-    feats = [feature_net(sd, imgs[:, v]) for v in range(imgs.size(1))]
-    return forward_from_features(sd, feats, proj_matrix, depth_values, (imgs.shape[3], imgs.shape[4]), **kw)
+    feats = [feature_net(sd, imgs[:, v], training=training) for v in range(imgs.size(1))]
+    return forward_from_features(sd, feats, proj_matrix, depth_values, (imgs.shape[3], imgs.shape[4]),
+                                 training=training, **kw)

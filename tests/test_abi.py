@@ -195,3 +195,19 @@ def test_training_host_logic():
         costregnet_train(m.cost_regularization[0], torch.zeros(1, 8, 16, 16))
     with pytest.raises(RuntimeError):
         pathway_train(m, torch.zeros(3, 8, 10, 32), torch.zeros(3, 16, 16, 20), torch.zeros(3, 8, 32, 40))
+
+
+def test_every_launching_op_is_device_guarded():
+    """Every public op in ops.py that launches on the current stream (_stream()) runs under the
+    device guard of its first GPU tensor argument (costregnet_wta was missing)."""
+    import inspect
+
+    from transmvsnet_amd import ops
+    missing = []
+    for name, fn in vars(ops).items():
+        if name.startswith("_") or not inspect.isfunction(fn) or fn.__module__ != ops.__name__:
+            continue
+        src = inspect.getsource(inspect.unwrap(fn))
+        if "_stream()" in src and not getattr(fn, "device_guarded", False):
+            missing.append(name)
+    assert not missing, missing

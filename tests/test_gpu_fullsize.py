@@ -1,27 +1,26 @@
 """Full-size forwards on one GPU: the C2 / C3 / C4 shapes of SURVEY.md 8 (needs an MI355X; -m gpu).
 
-C2 (DTU 864x1152, N=5, 48/32/8) and C3's shape (DTU, N=11) run TransMVSNet.forward_features against
-the oracle's forward_from_features (models/TransMVSNet.py:162-226) on the bench's inputs
-(synthetic.stacked_features seed 2, synthetic_cameras seed 1, key-seeded weights with logit
-sharpening). Depth parity is judged per stage with the near-tie rule of SURVEY.md 8c:
+C2 (DTU 864x1152, N=5, 48/32/8), C3's shape (DTU, N=11) and C4's shape (TnT 1056x1920, N=11) run
+TransMVSNet.forward_features against the oracle's forward_from_features (models/TransMVSNet.py:162-226)
+on the bench's inputs (synthetic.stacked_features seed 2, synthetic_cameras seed 1, key-seeded
+weights with logit sharpening). Depth parity is judged per stage with the near-tie
+rule of SURVEY.md 8c:
 
   * a pixel whose reference top-2 log-prob margin is < 1e-4 may legitimately flip its argmax
-    (the reference's own fp32 result moves such pixels with the thread count); flips outside it
-    are reported per stage;
-  * the assertion allows a flip where the margin is below twice the GPU CostRegNet's measured
-    deviation from the reference's logits on identical input (2.75e-4 at DTU stage 3, max|logit|
-    687: MFMA vs mkldnn k-order, profiles/r05c/flip_origin.txt), i.e. < 5.5e-4; any other differing
-    pixel (|d_gpu - d_ref| > 1e-3 mm) is a failure;
-  * the cascaded stage-3 mean |Δdepth| must be <= 1e-4 mm (the north-star bar).
+    (the reference's own fp32 result moves such pixels with the thread count);
+  * any other differing pixel (|d_gpu - d_ref| > 1e-3 mm) is a failure, unless it is listed in
+    EXACT_ARITHMETIC_PICKS: pixels where the fp32 reference's argmax is itself wrong -- float64
+    evaluation of the whole stage from the same inputs and weights picks the GPU's index with a
+    margin larger than the reference's (scripts/diag/c3_flip.py; evidence in DESIGN.md 5 and
+    profiles/r09a/c3_flip.txt);
+  * the cascaded stage-3 mean |Δdepth| must be <= 1e-4 mm (the north-star bar) when stages 1-2
+    agree on every pixel; a legitimate near-tie flip upstream moves the next stage's hypotheses
+    around that pixel, so the downstream stages are then judged by the fed runs below.
 
 Stages 2 and 3 are checked twice: in the cascaded forward, and re-run on the GPU from the
-ORACLE's previous-stage depth, so a near-tie flip upstream (which moves the next stage's
-hypotheses) is separated from the stage's own arithmetic. The cascaded stage-3 mean |Δdepth| is
-printed (the north-star 'Abs depth L1 vs ref'; bench.py reports it per run).
-
-C4's shape (TnT 1056x1920, N=11) is checked by properties only (the oracle would take minutes):
-finite outputs, probabilities summing to 1, depth inside the clamp range and equal to the
-hypothesis at the argmax, and the view-sharded path on one rank equal to the fused path.
+ORACLE's previous-stage depth ("fed"), so a near-tie flip upstream (which moves the next stage's
+hypotheses) is separated from the stage's own arithmetic. The C4 shape is additionally checked by
+properties (probabilities, clamp, WTA consistency, the view-sharded path).
 """
 import numpy as np
 import pytest
@@ -33,8 +32,12 @@ from transmvsnet_amd.model import DEPTH_CLAMP, STAGE_SCALES
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-MARGIN = 1e-4          # reported near-tie margin
-MARGIN_ASSERT = 5.5e-4  # 2 x the measured logit deviation (module docstring)
+MARGIN = 1e-4          # near-tie margin, reported and asserted
+# (n_views, H, W, stage) -> {(y, x)}: the fp32 reference's argmax is not the exact one (module docstring).
+# C3 stage 3, pixel (431, 451): reference logits d4 208.8793 vs d6 208.8791 (margin 1.98e-4, picks 4);
+# float64 through FMT, pathway, cost volume and CostRegNet: d6 208.8781 vs d4 208.8774 (margin 7.4e-4,
+# picks 6 = the GPU's pick); the reference's 1 / 4 / 16 torch threads all give 4 (profiles/r09a/c3_flip.txt).
+EXACT_ARITHMETIC_PICKS = {(11, 864, 1152, "stage3"): {(431, 451)}}
 
 
 @pytest.fixture(scope="module")
@@ -55,16 +58,18 @@ def _raw_depth(stage_out):
     return torch.gather(stage_out["depth_values"], 1, idx).squeeze(1)
 
 
-def _classify(depth_gpu, ref_stage):
+def _classify(depth_gpu, ref_stage, allowed=frozenset()):
     g = depth_gpu.detach().float().cpu().numpy().astype(np.float64)
     r = ref_stage["depth"].numpy().astype(np.float64)
     srt = np.sort(ref_stage["prob_volume"].numpy().astype(np.float64), axis=1)
-    near = (np.log(np.maximum(srt[:, -1], 1e-30)) - np.log(np.maximum(srt[:, -2], 1e-30))) < MARGIN
-    diff = np.abs(g - r) > 1e-3
     marg = (np.log(np.maximum(srt[:, -1], 1e-30)) - np.log(np.maximum(srt[:, -2], 1e-30)))
+    near = marg < MARGIN
+    diff = np.abs(g - r) > 1e-3
+    other = [(int(y), int(x)) for _, y, x in np.argwhere(diff & ~near)]
     return {"mean_abs_mm": float(np.abs(g - r).mean()), "differing": int(diff.sum()),
-            "near_tie_flips": int((diff & near).sum()), "other_flips": int((diff & ~near).sum()),
-            "max_flip_margin": float(marg[diff].max()) if diff.any() else 0.0}
+            "near_tie_flips": int((diff & near).sum()), "other_flips": len(other),
+            "max_flip_margin": float(marg[diff].max()) if diff.any() else 0.0,
+            "unexplained": [p for p in other if p not in allowed], "exact_arithmetic_picks": [p for p in other if p in allowed]}
 
 
 def _pyramid(model, feats_dev):
@@ -87,7 +92,9 @@ def _full_size_parity(model, sd, n_views, H, W):
         out, vw = model.forward_features(feats_dev, proj, dv.to(DEV), (H, W), return_view_weights=True)
         ref = oracle.forward_from_features(sd, [{k: v[:, i] for k, v in feats.items()} for i in range(n_views)],
                                            proj, dv, (H, W))
-        report = {f"cascade_stage{s}": _classify(out[f"stage{s}"]["depth"], ref[f"stage{s}"]) for s in (1, 2, 3)}
+        allowed = {s: EXACT_ARITHMETIC_PICKS.get((n_views, H, W, f"stage{s}"), frozenset()) for s in (1, 2, 3)}
+        report = {f"cascade_stage{s}": _classify(out[f"stage{s}"]["depth"], ref[f"stage{s}"], allowed[s])
+                  for s in (1, 2, 3)}
         # stages 2/3 again, each from the oracle's previous-stage depth (cascade flips removed)
         prep, st = _pyramid(model, feats_dev)
         dv0 = dv.to(DEV)
@@ -97,25 +104,38 @@ def _full_size_parity(model, sd, n_views, H, W):
                                    model.depth_interals_ratio[s], (H, W), STAGE_SCALES[s], rows[0], None, vw, s,
                                    prep["cr"][s][0], DEPTH_CLAMP)
             np.testing.assert_array_equal(o["depth_values"].cpu().numpy(), ref[f"stage{s + 1}"]["depth_values"].numpy())
-            report[f"fed_stage{s + 1}"] = _classify(o["depth"], ref[f"stage{s + 1}"])
+            report[f"fed_stage{s + 1}"] = _classify(o["depth"], ref[f"stage{s + 1}"], allowed[s + 1])
     torch.cuda.synchronize()
     print(f"\nN={n_views} {H}x{W}:", report)
     for k in ("cascade_stage1", "fed_stage2", "fed_stage3"):
-        assert report[k]["max_flip_margin"] < MARGIN_ASSERT, (k, report)
-    assert report["cascade_stage3"]["mean_abs_mm"] <= 1e-4, report
+        assert not report[k]["unexplained"], (k, report)
+    if report["cascade_stage1"]["differing"] == 0 and report["cascade_stage2"]["differing"] == 0:
+        for k in ("cascade_stage2", "cascade_stage3"):
+            assert not report[k]["unexplained"], (k, report)
+        assert report["cascade_stage3"]["mean_abs_mm"] <= 1e-4, report
     return report
 
 
 def test_c2_dtu_full_forward_parity(model, sd):
     """C2: DTU 864x1152, N=5, 48/32/8 -- the bench workload."""
     rep = _full_size_parity(model, sd, 5, 864, 1152)
-    # stage 3 from the oracle's stage-2 depth: its own arithmetic is within the north-star bar
+    # the bench workload: the cascade itself (not only the fed stages) meets the bar, with no flip
+    # outside the 1e-4 near-tie margin anywhere
+    assert rep["cascade_stage1"]["differing"] == 0 and rep["cascade_stage2"]["differing"] == 0, rep
+    assert rep["cascade_stage3"]["mean_abs_mm"] <= 1e-4 and rep["cascade_stage3"]["other_flips"] == 0, rep
     assert rep["fed_stage3"]["mean_abs_mm"] <= 1e-4, rep
 
 
 def test_c3_dtu_11_views_full_forward_parity(model, sd):
     """C3's shape on one GPU: DTU 864x1152, N=11 (10 source views)."""
     rep = _full_size_parity(model, sd, 11, 864, 1152)
+    assert rep["fed_stage3"]["mean_abs_mm"] <= 1e-4, rep
+
+
+def test_c4_tnt_full_forward_parity(model, sd):
+    """C4's shape on one GPU: Tanks&Temples 1056x1920, N=11, 48/32/8 against the oracle
+    (models/TransMVSNet.py:141-226 at datasets/tnt_eval.py:24-40 sizes)."""
+    rep = _full_size_parity(model, sd, 11, 1056, 1920)
     assert rep["fed_stage3"]["mean_abs_mm"] <= 1e-4, rep
 
 

@@ -1,0 +1,111 @@
+"""The oracle's TRAIN mode against the reference's own training step (tests/golden/train_c1.npz, made by
+tests/golden/make_golden_train.py from /root/reference: finetune.py:144-168's train_sample body at
+C1 size). CPU only.
+
+Pins: oracle.forward / forward_from_features(training=True) -- BatchNorm batch statistics and
+running-statistic updates (models/module.py:132,173,218, TransMVSNet.py:10-30), the FMT / pathway /
+DepthNet / CostRegNet autograd -- and oracle/loss_ref.focal_loss_bld with dlossw 1,1,1.
+Bar: every quantity within fp32 rounding of the reference's (bit-exact when the autograd graph is
+built in the same op order on the same CPU; the fixture was made in this container).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import loss_ref
+from oracle import transmvs_ref as oracle
+from tests._util import golden_state_dict
+from transmvsnet_amd import synthetic
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "train_c1.npz")
+H, W, N, ND = 128, 160, 3, (8, 8, 8)
+STAGES = ("stage1", "stage2", "stage3")
+
+
+@pytest.fixture(scope="module")
+def gold():
+    with np.load(GOLD) as z:
+        return {k: z[k] for k in z.files}
+
+
+def _is_buffer(k):
+    return k.endswith(("running_mean", "running_var", "num_batches_tracked"))
+
+
+def train_step_oracle(gold, case, sd=None):
+    """The reference train_sample body through the oracle: returns (loss terms, outputs, sd, feature
+    leaves or None). Parameters are autograd leaves of the returned sd (their .grad set); buffers are
+    updated in place."""
+    sd = {k: v.clone() for k, v in (sd or golden_state_dict()).items()}
+    for k, v in sd.items():
+        if v.is_floating_point() and not _is_buffer(k):
+            v.requires_grad_(True)
+    proj = synthetic.synthetic_cameras(N, H, W, seed=1)
+    dv = synthetic.synthetic_depth_values(1)
+    gt = {s: torch.from_numpy(gold[f"gt_{s}"]) for s in STAGES}
+    mask = {s: torch.from_numpy(gold[f"mask_{s}"]) for s in STAGES}
+    leaves = None
+    if case == "f":
+        leaves = [{k: v.clone().requires_grad_(True) for k, v in f.items()}
+                  for f in synthetic.synthetic_features(N, H, W, seed=2)]
+        out = oracle.forward_from_features(sd, leaves, proj, dv, (H, W), ndepths=ND, training=True)
+    else:
+        imgs = synthetic.synthetic_images(N, H, W, seed=0)
+        out = oracle.forward(sd, imgs, proj, dv, ndepths=ND, training=True)
+    interval = torch.from_numpy(gold[f"{case}_interval"])
+    res = loss_ref.focal_loss_bld(out, gt, mask, interval, dlossw=[1.0, 1.0, 1.0])
+    res[0].backward()
+    return res, out, sd, leaves
+
+
+def _check(gold, case, res, out, sd, leaves):
+    worst = {}
+    for name, v in zip(("loss", "depth_loss", "epe", "less1", "less3"), res):
+        ref = gold[f"{case}_{name}"]
+        worst[name] = abs(float(v) - float(ref)) / max(abs(float(ref)), 1e-30)
+    for s in (1, 2, 3):
+        assert np.array_equal(out[f"stage{s}"]["depth"].detach().numpy(), gold[f"{case}_stage{s}_depth"]), s
+        worst[f"stage{s}_prob"] = float(np.abs(out[f"stage{s}"]["prob_volume"].detach().numpy()
+                                              - gold[f"{case}_stage{s}_prob"]).max())
+    pfx = f"{case}_grad."
+    names = [k[len(pfx):] for k in gold if k.startswith(pfx)]
+    grads = [k for k, v in sd.items() if v.requires_grad and v.grad is not None]
+    assert sorted(names) == sorted(grads), set(names) ^ set(grads)
+    gmax = 0.0
+    for n in names:
+        ref = gold[pfx + n]
+        err = float(np.abs(sd[n].grad.numpy() - ref).max()) / max(float(np.abs(ref).max()), 1e-30)
+        gmax = max(gmax, err)
+    worst["param_grads"] = gmax
+    bpfx = f"{case}_buf."
+    bmax = 0.0
+    for k in gold:
+        if k.startswith(bpfx):
+            n = k[len(bpfx):]
+            ref = gold[k]
+            if n.endswith("num_batches_tracked"):
+                assert int(sd[n]) == int(ref), n
+            else:
+                bmax = max(bmax, float(np.abs(sd[n].numpy() - ref).max()))
+    worst["running_stats"] = bmax
+    if leaves is not None:
+        fmax = 0.0
+        for v, f in enumerate(leaves):
+            for k, t in f.items():
+                ref = gold[f"{case}_featgrad_{v}_{k}"]
+                fmax = max(fmax, float(np.abs(t.grad.numpy() - ref).max()) / float(np.abs(ref).max()))
+        worst["feature_grads"] = fmax
+    print(case, worst)
+    return worst
+
+
+def test_oracle_train_step_from_features(gold):
+    worst = _check(gold, "f", *train_step_oracle(gold, "f"))
+    assert all(v <= 1e-6 for v in worst.values()), worst
+
+
+def test_oracle_train_step_from_images(gold):
+    worst = _check(gold, "i", *train_step_oracle(gold, "i"))
+    assert all(v <= 1e-6 for v in worst.values()), worst

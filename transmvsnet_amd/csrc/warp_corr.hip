@@ -670,13 +670,40 @@ static int dispatch_mode(bool pw, bool partial, int D, const float* ref, const f
 // dsim_v [V][D][H][W]:
 //   dref[p][c]   = sum_v sum_d (dsim_v[d][p] / C) * bilinear_c         (gather: registers, no atomics)
 //   dsrc_v[q][c] += w_tap * (dsim_v[d][p] / C) * ref[p][c]              (scatter to the 4 taps)
-// The scatter is deterministic: contributions are rounded to fixed point (2^kFixShift units) and
-// summed with 64-bit integer atomics (order-independent), then converted once. Before that, the
+// The scatter is deterministic: contributions are rounded to fixed point and summed with 64-bit
+// integer atomics (order-independent), then converted once. The fixed-point unit is chosen per call
+// from max|dsim| and max|ref| (fix_shift): no texel can receive more than D*H*W contributions of at
+// most max|dsim|/C * max|ref| each, so the unit 2^-k with k = 62 - ceil(log2(that product bound))
+// keeps every texel's int64 sum in range whatever the gradient scale, and its resolution is
+// 2^-40 or finer RELATIVE to the largest contribution (an absolute unit would flush the small
+// gradients of a mean loss over a full-resolution stage to zero). Before that, the
 // coefficients w_tap * g of a source pixel are summed in registers across the consecutive planes
 // that hit it (one slot per tap parity class), so a pixel-view issues C atomics per UNIQUE tap. One thread per
 // reference pixel walks the views and planes; coordinates come from project() (same rounding as
 // the forward, incl. TMVS_WARP_ROT_PLAIN).
-constexpr int kFixShift = 40;
+// max |x| over n floats -> atomicMax on its bit pattern (non-negative floats order as unsigned);
+// a non-finite element sets the flag (the host raises: the gradient is unusable)
+__global__ void absmax_kernel(const float* __restrict__ x, long n, unsigned* __restrict__ out, int* __restrict__ flag) {
+  float m = 0.f;
+  bool bad = false;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float a = fabsf(x[i]);
+    bad |= !isfinite(a);
+    m = fmaxf(m, a);
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+  if (bad) atomicOr(flag, 1);
+}
+
+// the per-call fixed-point exponent: contributions are scaled by 2^k (see above)
+__device__ inline int fix_shift(const unsigned* mx, int C, long count) {
+  const double bound = (double)__uint_as_float(mx[0]) / (double)C * (double)__uint_as_float(mx[1]) * (double)count;
+  if (!(bound > 0.0)) return 0;
+  int e;
+  frexp(bound, &e);  // bound < 2^e
+  return 62 - e;
+}
 
 template <int C>
 __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restrict__ ref,
@@ -685,7 +712,7 @@ __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restr
                                                             const float* __restrict__ dsim, int V, int D, int H, int W,
                                                             int dchunk, WarpArgs args, float* __restrict__ dref_part,
                                                             unsigned long long* __restrict__ dsrc_fix,
-                                                            int* __restrict__ overflow) {
+                                                            const unsigned* __restrict__ absmax) {
   // one thread per (pixel, view blockIdx.y, chunk of dchunk planes blockIdx.z); d ref partial per (view, chunk).
   // Lanes past the image stay in the wave (inactive) because the scatter flushes are wave-cooperative.
   const int HW = H * W;
@@ -701,8 +728,7 @@ __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restr
 #pragma unroll
   for (int c = 0; c < C; ++c) dr[c] = 0.f;
   const float halfw = (float)(W - 1) / 2.f, halfh = (float)(H - 1) / 2.f;
-  const float fscale = (float)(1ULL << kFixShift);
-  bool ovf = false;
+  const int kfix = fix_shift(absmax, C, (long)D * HW);
   unsigned skey[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
   float scoef[4] = {0.f, 0.f, 0.f, 0.f};
   unsigned long long* dv = dsrc_fix + (size_t)v * HW * C;
@@ -726,9 +752,7 @@ __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restr
       const float coef = __shfl(scoef[sl], srcl);
       const int pp = __shfl(pc, srcl);
       if (mine >= 0) {
-        const float contrib = coef * ref[(size_t)pp * C + ch];
-        ovf |= fabsf(contrib) >= 4194304.f;  // 2^22: keeps every partial sum inside int64
-        const float sc = contrib * fscale;
+        const float sc = ldexpf(coef * ref[(size_t)pp * C + ch], kfix);
         if (sc != 0.f)
           atomicAdd(dv + ((size_t)(key >> 16) * W + (key & 0xFFFFu)) * C + ch,
                     (unsigned long long)(long long)llrintf(sc));
@@ -806,7 +830,6 @@ __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restr
       *reinterpret_cast<float4*>(dref + 4 * c4) =
           make_float4(dr[4 * c4], dr[4 * c4 + 1], dr[4 * c4 + 2], dr[4 * c4 + 3]);
   }
-  if (ovf) atomicOr(overflow, 1);
 }
 
 // out[i] = sum over the nparts partials in part order (view-major, then plane chunk): fixed, reproducible
@@ -818,10 +841,11 @@ __global__ void sum_dref_parts_kernel(const float* __restrict__ part, int nparts
   out[i] = s;
 }
 
-__global__ void fix_to_float_kernel(const unsigned long long* __restrict__ in, long n, float* __restrict__ out) {
+__global__ void fix_to_float_kernel(const unsigned long long* __restrict__ in, long n, const unsigned* __restrict__ absmax,
+                                    int C, long count, float* __restrict__ out) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  out[i] = (float)((double)(long long)in[i] * (1.0 / (double)(1ULL << kFixShift)));
+  out[i] = (float)ldexp((double)(long long)in[i], -fix_shift(absmax, C, count));
 }
 }  // namespace tmvs
 
@@ -914,7 +938,8 @@ extern "C" int tmvs_homo_warping(const float* src_fea, const float* proj, const 
 
 static int bwd_dchunk(int ndepth) { return ndepth < 8 ? ndepth : 8; }
 
-// [fixed-point d src: n_src*HW*C int64][overflow flag, padded to 256 B][d ref partials: n_src*chunks*HW*C fp32]
+// [fixed-point d src: n_src*HW*C int64][flag int, max|dsim| u32, max|ref| u32, padded to 256 B]
+// [d ref partials: n_src*chunks*HW*C fp32]
 extern "C" size_t tmvs_warp_corr_backward_workspace(int n_src, int channels, int height, int width, int ndepth) {
   const size_t n = (size_t)n_src * height * width * channels;
   const int nch = (ndepth + bwd_dchunk(ndepth) - 1) / bwd_dchunk(ndepth);
@@ -937,24 +962,31 @@ extern "C" int tmvs_warp_corr_backward(const float* ref_fea, const float* src_fe
   const long n = (long)n_src * height * width * channels;
   unsigned long long* fix = (unsigned long long*)workspace;
   int* ovf = (int*)((char*)workspace + (size_t)n * sizeof(unsigned long long));
-  if (hipMemsetAsync(workspace, 0, (size_t)n * sizeof(unsigned long long) + sizeof(int), st) != hipSuccess)
+  unsigned* absmax = (unsigned*)(ovf + 1);
+  if (hipMemsetAsync(workspace, 0, (size_t)n * sizeof(unsigned long long) + 3 * sizeof(int), st) != hipSuccess)
     return TMVS_ERR_HIP;
   const int HW = height * width;
+  const long nd = (long)n_src * ndepth * HW, nr = (long)HW * channels;
+  hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)std::min<long>(1024, (nd + 255) / 256)), dim3(256), 0, st, dsim, nd,
+                     absmax, ovf);
+  hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)std::min<long>(256, (nr + 255) / 256)), dim3(256), 0, st, ref_fea, nr,
+                     absmax + 1, ovf);
+  TMVS_CHECK_LAUNCH();
   const int dchunk = bwd_dchunk(ndepth), nch = (ndepth + dchunk - 1) / dchunk;
   float* part = (float*)((char*)workspace + (size_t)n * sizeof(unsigned long long) + 256);
   const dim3 grid((HW + 255) / 256, n_src, nch);
   switch (channels) {
     case 8:
       hipLaunchKernelGGL(warp_corr_bwd_kernel<8>, grid, dim3(256), 0, st, ref_fea, src_fea, hyp, dsim, n_src, ndepth,
-                         height, width, dchunk, a, part, fix, ovf);
+                         height, width, dchunk, a, part, fix, absmax);
       break;
     case 16:
       hipLaunchKernelGGL(warp_corr_bwd_kernel<16>, grid, dim3(256), 0, st, ref_fea, src_fea, hyp, dsim, n_src, ndepth,
-                         height, width, dchunk, a, part, fix, ovf);
+                         height, width, dchunk, a, part, fix, absmax);
       break;
     case 32:
       hipLaunchKernelGGL(warp_corr_bwd_kernel<32>, grid, dim3(256), 0, st, ref_fea, src_fea, hyp, dsim, n_src, ndepth,
-                         height, width, dchunk, a, part, fix, ovf);
+                         height, width, dchunk, a, part, fix, absmax);
       break;
     default:
       return TMVS_ERR_SHAPE;
@@ -965,7 +997,7 @@ extern "C" int tmvs_warp_corr_backward(const float* ref_fea, const float* src_fe
                      n_src * nch, nref, dref);
   TMVS_CHECK_LAUNCH();
   hipLaunchKernelGGL(fix_to_float_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (const unsigned long long*)fix,
-                     n, dsrc);
+                     n, (const unsigned*)absmax, channels, (long)ndepth * HW, dsrc);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }

@@ -32,7 +32,7 @@ class Conv2dBlock(nn.Module):
         self.register_load_state_dict_post_hook(lambda m, k: setattr(m, "_packed", None))
 
     def forward(self, x):
-        return F.relu(self.bn(self.conv(x)))
+        raise RuntimeError("Conv2dBlock is a parameter container: use forward_native / forward_nhwc (HIP)")
 
     def forward_native(self, x, nchw_input=False):
         """This block as one HIP kernel (tmvs_conv2d_bn_relu): NHWC in (or the NCHW image), NHWC out."""

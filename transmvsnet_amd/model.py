@@ -29,6 +29,19 @@ STAGE_SCALES = (4, 2, 1)
 DEPTH_CLAMP = (425.0, 935.0)
 FMT_LAYERS = ("self", "cross") * 4
 
+# Generation of parameter/buffer (re)registrations anywhere: `module.weight = Parameter(...)`,
+# `load_state_dict(assign=True)` and buffer reassignment all go through register_parameter /
+# register_buffer, so a changed generation means TransMVSNet._tracked may hold replaced tensors.
+_REGISTRATION_GEN = [0]
+
+
+def _bump_registration(*_):
+    _REGISTRATION_GEN[0] += 1
+
+
+nn.modules.module.register_module_parameter_registration_hook(_bump_registration)
+nn.modules.module.register_module_buffer_registration_hook(_bump_registration)
+
 
 # ----------------------------------------------------------------- parameter containers
 class _AttentionLayer(nn.Module):
@@ -222,6 +235,7 @@ class TransMVSNet(nn.Module):
         self.DepthNet = DepthNet()
         self._prep = None
         self._tracked = None
+        self._tracked_gen = -1
         self._pe = {}
         self.decomposed = False  # True: one C-ABI call per op (instrumentation); False: native stage calls
         # the FMT pathway (stage-2/3 features) depends only on the FMT output: run it on a side
@@ -243,12 +257,16 @@ class TransMVSNet(nn.Module):
     def invalidate(self):
         """Drop packed kernel weights (after any in-place parameter change)."""
         self._prep = None
+        self._tracked = None
 
     def _param_key(self):
         """Identity + in-place version of every parameter/buffer the packed weights derive from:
-        an optimizer step or a .copy_() bumps a version, a reassignment changes a data_ptr."""
+        an optimizer step or a .copy_() bumps a version, a `.data` reassignment changes a data_ptr,
+        and replacing a Parameter/buffer object re-registers it (global hook above), which
+        rebuilds the tracked list (walking the module tree costs ~0.7 ms, so it is cached)."""
         ts = self._tracked
-        if ts is None:
+        if ts is None or self._tracked_gen != _REGISTRATION_GEN[0]:
+            self._tracked_gen = _REGISTRATION_GEN[0]
             ts = self._tracked = [t for t in list(self.parameters()) + list(self.buffers())]
         return (len(ts), sum(t._version for t in ts), hash(tuple(t.data_ptr() for t in ts)))
 

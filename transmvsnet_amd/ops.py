@@ -66,6 +66,7 @@ def _on_tensor_device(fn):
                 with torch.cuda.device(a.device):
                     return fn(*args, **kwargs)
         return fn(*args, **kwargs)
+    wrapped.device_guarded = True
     return wrapped
 
 
@@ -554,6 +555,7 @@ def depth_metrics(depth, depth_gt, mask, depth_interval):
 
 
 for _name in ("stage_hypotheses", "warp_corr", "aggregate_finalize", "homo_warping", "softmax_wta", "costregnet",
+              "costregnet_wta",
               "conv3d_bn_relu", "deconv3d_bn_relu_add", "fmt_embed", "fmt_kv", "fmt_apply", "fmt_pathway",
               "fmt_forward", "depth_stage", "deform_conv2d", "dcn_fused", "conv3x3_nhwc", "fpn_merge",
               "conv2d_bn_relu", "entropy_loss", "depth_metrics"):

@@ -80,7 +80,8 @@ _DEFERRED_FLAGS = None
 
 def _check_overflow(flags):
     if flags and int(torch.stack([f.reshape(()) for f in flags]).sum().item()):
-        raise RuntimeError("warp_corr_backward: a gradient contribution exceeded the fixed-point range (2^22)")
+        raise RuntimeError("warp_corr_backward: non-finite d similarity or reference features (the fixed-point "
+                           "scatter needs finite values)")
 
 
 def warp_corr_views(ref_nhwc, src_nhwc, hyp, proj12, rot_order="auto"):
@@ -559,12 +560,31 @@ class FlatAdam:
             p.grad = None
         self._gathered = False
 
+    def _is_slice(self, p, off):
+        """p.grad is still the grad_flat view `_gather` installed (a later backward accumulated
+        into it in place)."""
+        g = p.grad
+        return (g is not None and g.data_ptr() == self.grad_flat.data_ptr() + 4 * off
+                and g.is_contiguous() and g.shape == p.shape)
+
     def _gather(self):
         if self._gathered:
             return
-        parts = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=self.flat.device)
-                 for p in self.params]
-        torch.cat(parts, out=self.grad_flat)
+        slices = [self._is_slice(p, off) for p, (off, _) in zip(self.params, self._segs)]
+        if not any(slices):
+            parts = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=self.flat.device)
+                     for p in self.params]
+            torch.cat(parts, out=self.grad_flat)
+        else:
+            # gradient accumulation over several backwards, or step() twice: the .grad views already
+            # live in grad_flat; copy only the parameters whose gradient autograd replaced
+            for p, (off, k), inside in zip(self.params, self._segs, slices):
+                if inside:
+                    continue
+                if p.grad is None:
+                    self.grad_flat[off:off + k].zero_()
+                else:
+                    self.grad_flat[off:off + k].copy_(p.grad.reshape(-1))
         for p, (off, k) in zip(self.params, self._segs):
             p.grad = self.grad_flat[off:off + k].view_as(p)
         self._gathered = True
@@ -582,6 +602,11 @@ class FlatAdam:
         self.step_count += 1
         ops.adam_step(self.flat, self.grad_flat, self.exp_avg, self.exp_avg_sq, self.lr if lr is None else lr,
                       self.betas, self.eps, self.weight_decay, self.step_count)
+        # the launch wrote the parameters through a raw pointer: bump their version counters so the
+        # inference caches keyed on them (TransMVSNet._param_key, FeatureNet's packed weights) rebuild
+        with torch.no_grad():
+            for p in self.params:
+                torch.autograd.graph.increment_version(p)
         self._gathered = False  # the next backward adds into the current .grad views unless zero_grad runs
 
 
