@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TMVS_ABI_VERSION 4
+#define TMVS_ABI_VERSION 5
 
 #define TMVS_OK 0
 #define TMVS_ERR_ARG (-1)    /* null pointer / non-positive size / bad enum        */
@@ -255,8 +255,9 @@ int tmvs_conv3d_wgrad(const float* direct, int a_ch, int batch, int pd, int ph, 
  *   dref [H][W][C] = sum_v sum_d dsim/C * bilinear(src_v)          (NHWC, overwritten)
  *   dsrc [V][H][W][C] = the bilinear scatter of dsim/C * ref          (NHWC, overwritten)
  * ref/src/hyp/proj/flags as tmvs_warp_corr (one sample, C in {8,16,32}). The scatter is summed
- * in 2^-40 fixed point with 64-bit integer atomics: deterministic; |a single contribution| must
- * stay below 2^22 (checked: the workspace's int after the buffer is set to 1 otherwise). One
+ * in fixed point with 64-bit integer atomics (deterministic); the unit is chosen per call from
+ * max|dsim| and max|ref| so that no texel's sum can overflow (ABI 5; it was a fixed 2^-40). The
+ * workspace's int after the buffer is set to 1 when dsim or ref holds a non-finite value. One
  * thread per (pixel, view, chunk of 8 planes); dref is the fixed-order sum of those partials.
  * ABI 3: the workspace size takes ndepth (the d ref partials live in it).                      */
 size_t tmvs_warp_corr_backward_workspace(int n_src, int channels, int height, int width, int ndepth);
@@ -438,6 +439,53 @@ int tmvs_entropy_loss(const float* prob, const float* depth_values, int dv_per_p
 size_t tmvs_depth_metrics_workspace(int n);
 int tmvs_depth_metrics(const float* depth, const float* depth_gt, const float* mask, int n, float depth_interval,
                        void* workspace, size_t workspace_bytes, float* out, void* stream);
+
+/* ------------------------------------------------------------------ FeatureNet training
+ * The backward of FeatureNet (models/module.py:343-422) and of its DCNs (models/dcn.py:66-80 ->
+ * torchvision.ops.deform_conv2d), and of the softmax of prob_volume (models/TransMVSNet.py:99).
+ * NHWC fp32 activations; every pixel reduction is block partials + a fixed-order fp64 combine.
+ *
+ * tmvs_conv2d_generic: y [B][h_out][w_out][cout] = bias + conv (k x k taps, weights w [k*k][cout][cin]):
+ *   strided (flags 0): y[o] = sum_k W[k] x[o*stride - pad + k]       (Conv2d; replaces cuDNN's forward)
+ *   TMVS_CONV_TRANSPOSED: y[i] = sum_k W[k] x[(i + pad - k)/stride] where stride divides (the data
+ *   gradient of a Conv2d with W[k][ci][co] = its weight transposed); TMVS_CONV_ACCUMULATE: y +=.
+ *   bias nullable. cin in {3, 8, 16, 27, 32}; cout a multiple of 8, or 27 (cin 8/16/32).
+ * tmvs_conv2d_wgrad: dw [k*k][a_ch][b_ch] = sum_p direct[p][a] gathered[p*stride - pad + k][b] (a Conv2d's
+ *   weight gradient: direct = dz [B][ph][pw][a], gathered = x [B][gh][gw][b]). (a, b) in {8,16,27,32} x
+ *   {8,16,32} with a <= 32, or (8, 3).
+ * tmvs_colsum: out[c] = sum_p x[p][c] over x [n][channels] (a bias gradient), channels <= 32.
+ * tmvs_dcn_forward_train: tmvs_dcn_fused without BatchNorm / ReLU that also writes the offset/mask
+ *   tensor the backward needs: offset_mask_out [B][27][H][W] (= conv_offset_mask(x) + bias).
+ * tmvs_dcn_backward: given dy_nhwc [B][H][W][cout] (d loss / d DCN output) and the forward's
+ *   x_nhwc [B][H][W][32], offset_mask [B][27][H][W], w_taps [9][cout][32] (the weight [cout][32][3][3]
+ *   as [tap][co][ci]):
+ *     dx_nhwc  [B][H][W][32]  += the bilinear scatter of mask * dcol (fp32 atomics, as torchvision)
+ *     dom_nhwc [B][H][W][27]   = d offsets (channels 2k, 2k+1) and d mask logits (18 + k)
+ *     dw_taps  [9][cout][32]   = the weight gradient (the bias gradient is tmvs_colsum of dy).
+ *   cout in {8, 16, 32}. The offset/mask conv's gradients are tmvs_conv2d_wgrad / _generic of dom.
+ * tmvs_nearest_up2_backward_nhwc: dprev [n][h][w][C] (+)= the 2x2 sums of d [n][2h][2w][C] (the
+ *   adjoint of interpolate(scale 2, nearest), models/module.py:413,417).
+ * tmvs_softmax_backward: dlogits = prob * (dprob - sum_d prob * dprob), [B][D][H][W].            */
+int tmvs_conv2d_generic(const float* x, int batch, int cin, int h_in, int w_in, const float* w, const float* bias,
+                        int cout, int h_out, int w_out, int k, int stride, int pad, int flags, float* y, void* stream);
+size_t tmvs_conv2d_wgrad_workspace(int batch, int h, int w, int a_ch, int b_ch, int k);
+int tmvs_conv2d_wgrad(const float* direct, int a_ch, int batch, int ph, int pw, const float* gathered, int b_ch,
+                      int gh, int gw, int k, int stride, int pad, void* workspace, size_t workspace_bytes, float* dw,
+                      void* stream);
+size_t tmvs_colsum_workspace(long n, int channels);
+int tmvs_colsum(const float* x, long n, int channels, void* workspace, size_t workspace_bytes, float* out,
+                void* stream);
+int tmvs_dcn_forward_train(const float* x_nhwc, const float* wom_packed, const float* bom, const float* w_packed,
+                           const float* bias, int batch, int cin, int cout, int height, int width, float* out,
+                           float* out_nhwc, float* offset_mask_out, void* stream);
+size_t tmvs_dcn_backward_workspace(int batch, int cout, int height, int width);
+int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, const float* w_taps, const float* dy_nhwc,
+                      int batch, int cin, int cout, int height, int width, void* workspace, size_t workspace_bytes,
+                      float* dx_nhwc, float* dom_nhwc, float* dw_taps, void* stream);
+int tmvs_nearest_up2_backward_nhwc(const float* d, int n, int h, int w, int channels, int accumulate, float* dprev,
+                                   void* stream);
+int tmvs_softmax_backward(const float* prob, const float* dprob, int batch, int ndepth, int height, int width,
+                          float* dlogits, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,242 @@
+"""The HIP training path against the REFERENCE's own training step (tests/golden/train_c1.npz, made by
+tests/golden/make_golden_train.py from /root/reference: finetune.py:144-168's train_sample body at C1
+size, 128x160, N=3, 8/8/8, key-seeded weights). Needs an MI355X (-m gpu).
+
+  * from features (case "f"): fmt_train -> pathway_train -> depth_stages_forward_train ->
+    transmvsnet_amd.loss.focal_loss_bld(...)[0].backward(): the loss terms, WTA depths, prob volumes,
+    the gradient of every FMT / pathway / PixelwiseNet / CostRegNet parameter and of the stage
+    features, the BatchNorm running statistics;
+  * from images (case "i"), the reference's train_sample body unchanged on the drop-in model:
+        model.train(); optimizer.zero_grad(); outputs = model(imgs, proj_matrix, depth_values)
+        loss, depth_loss, epe, less1, less3 = focal_loss_bld(outputs, depth_gt_ms, mask_ms, interval,
+                                                             dlossw=[1.0, 1.0, 1.0])
+        loss.backward(); optimizer.step()
+    with focal_loss_bld both the HIP loss (transmvsnet_amd.loss) and the reference's torch-op loss
+    (restated in oracle/loss_ref.py, the code a reference user already calls), which backpropagates
+    through prob_volume (the HIP softmax backward). All 318 parameter gradients incl. FeatureNet +
+    DCN (models/module.py:343-422, models/dcn.py:66-80), and the running statistics.
+
+Bar: the reference's fp32 numbers are themselves rounded; every gradient is compared with a float64
+evaluation of the same step (the oracle, pinned bit-exact to these fixtures by
+tests/test_train_oracle.py) and must be within max(1e-4, 3x the fp32 reference's own distance from
+it, 2e-3 x the worst such distance over all gradients) of its max magnitude; loss terms within 1e-5
+relative, prob volumes within 1e-4, WTA depths identical, running statistics within 1e-5.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests._util import golden_rot, golden_state_dict
+from tests.test_train_oracle import GOLD, H, ND, N, STAGES, train_step_oracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def gold():
+    with np.load(GOLD) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="module")
+def exact():
+    """float64 evaluations of both cases (the CPU oracle)."""
+    with np.load(GOLD) as z:
+        g = {k: z[k] for k in z.files}
+    out = {}
+    for case in ("f", "i"):
+        res, o, sd, leaves = train_step_oracle(g, case, dtype=torch.float64)
+        grads = {k: v.grad.detach().numpy() for k, v in sd.items() if v.requires_grad and v.grad is not None}
+        fg = {} if leaves is None else {f"{v}_{k}": t.grad.numpy() for v, f in enumerate(leaves) for k, t in f.items()}
+        out[case] = (grads, fg)
+    return out
+
+
+def _model():
+    from transmvsnet_amd import TransMVSNet
+    m = TransMVSNet(ndepths=list(ND))
+    m.load_state_dict(golden_state_dict(), strict=True)
+    return m.to(DEV)
+
+
+def _targets(gold):
+    gt = {s: torch.from_numpy(gold[f"gt_{s}"]).to(DEV) for s in STAGES}
+    mask = {s: torch.from_numpy(gold[f"mask_{s}"]).to(DEV) for s in STAGES}
+    return gt, mask
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max()) / max(float(np.abs(b).max()), 1e-30)
+
+
+def _judge(gold, exact_grads, case, got):
+    """got: {name: gradient (numpy)} -> report; asserts the module docstring's bar."""
+    pfx = f"{case}_grad."
+    names = sorted(k[len(pfx):] for k in gold if k.startswith(pfx))
+    missing = [n for n in names if n not in got]
+    assert not missing, f"no gradient for {missing[:8]} ({len(missing)} of {len(names)})"
+    ref_err = {n: _rel(gold[pfx + n], exact_grads[n]) for n in names}
+    worst_ref = max(ref_err.values())
+    rows = []
+    for n in names:
+        e = _rel(got[n], exact_grads[n])
+        bar = max(1e-4, 3.0 * ref_err[n], 2e-3 * worst_ref)
+        rows.append((e / bar, n, e, ref_err[n]))
+    rows.sort(reverse=True)
+    print(f"{case}: worst gradient errors vs fp64 (ratio to bar, name, gpu, fp32 reference):",
+          [(f"{r:.2f}", n, f"{e:.1e}", f"{f:.1e}") for r, n, e, f in rows[:6]])
+    bad = [(n, e, f) for r, n, e, f in rows if r > 1.0]
+    assert not bad, bad[:10]
+
+
+def _check_outputs(gold, case, outputs, loss_terms):
+    for name, v in zip(("loss", "depth_loss", "epe", "less1", "less3"), loss_terms):
+        ref = float(gold[f"{case}_{name}"])
+        assert abs(float(v) - ref) <= 1e-5 * max(abs(ref), 1.0), (name, float(v), ref)
+    for s in (1, 2, 3):
+        o = outputs[f"stage{s}"]
+        np.testing.assert_array_equal(o["depth_values"].detach().cpu().numpy(), gold[f"{case}_stage{s}_hyp"])
+        dp = float(np.abs(o["prob_volume"].detach().cpu().numpy() - gold[f"{case}_stage{s}_prob"]).max())
+        assert dp < 1e-4, (s, dp)
+        np.testing.assert_array_equal(o["depth"].detach().cpu().numpy(), gold[f"{case}_stage{s}_depth"])
+
+
+def _check_buffers(gold, case, model):
+    bufs = dict(model.named_buffers())
+    worst = 0.0
+    for k in gold:
+        if k.startswith(f"{case}_buf."):
+            n = k[len(case) + 5:]
+            if n.endswith("num_batches_tracked"):
+                assert int(bufs[n]) == int(gold[k]), n
+            else:
+                worst = max(worst, float(np.abs(bufs[n].cpu().numpy() - gold[k]).max()))
+    assert worst < 1e-5, worst
+
+
+def test_train_step_from_features_vs_reference(gold, exact):
+    from transmvsnet_amd import loss as hip_loss
+    from transmvsnet_amd import synthetic
+    from transmvsnet_amd.train import depth_stages_forward_train, fmt_train, pathway_train
+    model = _model()
+    model.train()
+    feats = synthetic.synthetic_features(N, H, H * 5 // 4, seed=2)
+    leaves = {k: torch.cat([f[k] for f in feats], 0).to(DEV).requires_grad_() for k in STAGES}
+    proj = synthetic.synthetic_cameras(N, H, H * 5 // 4, seed=1)
+    dv = synthetic.synthetic_depth_values(1).to(DEV)
+    gt, mask = _targets(gold)
+    with golden_rot(model):
+        st1 = fmt_train(model, leaves["stage1"])
+        st2, st3 = pathway_train(model, st1, leaves["stage2"], leaves["stage3"])
+        outputs = depth_stages_forward_train(model, {"stage1": st1, "stage2": st2, "stage3": st3}, proj, dv,
+                                             (H, H * 5 // 4))
+        terms = hip_loss.focal_loss_bld(outputs, gt, mask, torch.tensor([float(gold["f_interval"])]),
+                                        dlossw=[1.0, 1.0, 1.0])
+        terms[0].backward()
+    torch.cuda.synchronize()
+    _check_outputs(gold, "f", outputs, terms)
+    got = {n: p.grad.detach().cpu().numpy() for n, p in model.named_parameters() if p.grad is not None}
+    _judge(gold, exact["f"][0], "f", got)
+    ref_fg = exact["f"][1]
+    for k in STAGES:
+        g = leaves[k].grad.detach().cpu().numpy()
+        for v in range(N):
+            e = _rel(g[v], ref_fg[f"{v}_{k}"])
+            f32 = _rel(gold[f"f_featgrad_{v}_{k}"], ref_fg[f"{v}_{k}"])
+            assert e <= max(1e-4, 3.0 * f32), (k, v, e, f32)
+    _check_buffers(gold, "f", model)
+
+
+@pytest.mark.parametrize("loss_impl", ["hip", "reference_torch_ops"])
+def test_train_sample_unchanged_body_vs_reference(gold, exact, loss_impl):
+    """finetune.py:144-168 on the drop-in model (FeatureNet + DCN backward included)."""
+    from oracle import loss_ref
+    from transmvsnet_amd import loss as hip_loss
+    from transmvsnet_amd import synthetic
+    from transmvsnet_amd.train import FlatAdam
+    focal_loss_bld = hip_loss.focal_loss_bld if loss_impl == "hip" else loss_ref.focal_loss_bld
+    model = _model()
+    optimizer = FlatAdam([p for p in model.parameters()], lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4)
+    imgs = synthetic.synthetic_images(N, H, H * 5 // 4, seed=0).to(DEV)
+    proj = synthetic.synthetic_cameras(N, H, H * 5 // 4, seed=1)
+    dv = synthetic.synthetic_depth_values(1).to(DEV)
+    depth_gt_ms, mask_ms = _targets(gold)
+    interval = torch.tensor([float(gold["i_interval"])], device=DEV)
+    with golden_rot(model):
+        # ---- the reference's train_sample body (finetune.py:145-168)
+        model.train()
+        optimizer.zero_grad()
+        outputs = model(imgs, proj, dv)
+        loss, depth_loss, epe, less1, less3 = focal_loss_bld(outputs, depth_gt_ms, mask_ms, interval,
+                                                             dlossw=[1.0, 1.0, 1.0])
+        loss.backward()
+        grads = {n: p.grad.detach().cpu().numpy().copy() for n, p in model.named_parameters() if p.grad is not None}
+        optimizer.step()
+    torch.cuda.synchronize()
+    _check_outputs(gold, "i", outputs, (loss, depth_loss, epe, less1, less3))
+    _judge(gold, exact["i"][0], "i", grads)
+    _check_buffers(gold, "i", model)
+    # the step moved every parameter that has a gradient, and eval mode sees the new weights
+    model.eval()
+    with torch.no_grad():
+        out = model(imgs, proj, dv)
+    assert torch.isfinite(out["depth"]).all()
+
+
+def test_flat_adam_accumulates_two_backwards_and_invalidates_inference_cache():
+    """gradients accumulated over two backward passes before step() (no zero_grad between),
+    step() twice, and an eval forward after the step sees the stepped weights (packed-weight caches
+    keyed on parameter versions)."""
+    from transmvsnet_amd import TransMVSNet, synthetic
+    from transmvsnet_amd.train import FlatAdam
+    torch.manual_seed(0)
+    m = _model()
+    params = [p for n, p in m.named_parameters() if n.startswith("cost_regularization.0.")]
+    ref_params = [p.detach().clone().requires_grad_() for p in params]
+    opt = FlatAdam(params, lr=1e-2, betas=(0.9, 0.999), weight_decay=1e-4)
+    ref_opt = torch.optim.Adam(ref_params, lr=1e-2, betas=(0.9, 0.999), weight_decay=1e-4)
+    # no zero_grad anywhere: after the first step the .grad tensors are views into FlatAdam's flat
+    # buffer, and the next "backwards" accumulate into them in place (two per step here)
+    for step in range(3):
+        for rep in range(2):
+            g = [torch.randn_like(p) for p in params]
+            for p, gg in zip(params, g):
+                if p.grad is None:
+                    p.grad = gg.clone()
+                else:
+                    p.grad.add_(gg)
+            for p, gg in zip(ref_params, g):
+                p.grad = gg.clone() if p.grad is None else p.grad + gg
+        opt.step()
+        ref_opt.step()
+    opt.zero_grad()
+    for p, r in zip(params, ref_params):
+        assert float((p.detach() - r.detach()).abs().max()) < 1e-6
+    # eval forward after the step == a model freshly loaded with the stepped weights
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    fresh = TransMVSNet(ndepths=list(ND))
+    fresh.load_state_dict(sd, strict=True)
+    fresh = fresh.to(DEV).eval()
+    m.eval()
+    feats = synthetic.synthetic_features(N, H, H * 5 // 4, seed=2)
+    proj = synthetic.synthetic_cameras(N, H, H * 5 // 4, seed=1)
+    dv = synthetic.synthetic_depth_values(1).to(DEV)
+    fd = [{k: v.to(DEV) for k, v in f.items()} for f in feats]
+    with torch.no_grad():
+        a = fresh.forward_features(fd, proj, dv, (H, H * 5 // 4))
+        b = m.forward_features(fd, proj, dv, (H, H * 5 // 4))
+        # a second step with no forward in between, then eval again: still the current weights
+        for p in params:
+            p.grad = torch.randn_like(p)
+        opt.step()
+        sd2 = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+        fresh.load_state_dict(sd2, strict=True)
+        c = fresh.forward_features(fd, proj, dv, (H, H * 5 // 4))
+        d = m.forward_features(fd, proj, dv, (H, H * 5 // 4))
+    torch.cuda.synchronize()
+    assert torch.equal(a["prob_volume"], b["prob_volume"])
+    assert torch.equal(c["prob_volume"], d["prob_volume"])
+    assert not torch.equal(a["prob_volume"], c["prob_volume"])

@@ -34,27 +34,29 @@ def _is_buffer(k):
     return k.endswith(("running_mean", "running_var", "num_batches_tracked"))
 
 
-def train_step_oracle(gold, case, sd=None):
+def train_step_oracle(gold, case, sd=None, dtype=torch.float32):
     """The reference train_sample body through the oracle: returns (loss terms, outputs, sd, feature
     leaves or None). Parameters are autograd leaves of the returned sd (their .grad set); buffers are
-    updated in place."""
-    sd = {k: v.clone() for k, v in (sd or golden_state_dict()).items()}
+    updated in place. dtype=torch.float64 evaluates the same step in double precision (the exact
+    value the fp32 reference and the GPU are both judged against)."""
+    cast = (lambda t: t.to(dtype) if t.is_floating_point() else t)  # noqa: E731
+    sd = {k: cast(v.clone()) for k, v in (sd or golden_state_dict()).items()}
     for k, v in sd.items():
         if v.is_floating_point() and not _is_buffer(k):
             v.requires_grad_(True)
-    proj = synthetic.synthetic_cameras(N, H, W, seed=1)
-    dv = synthetic.synthetic_depth_values(1)
-    gt = {s: torch.from_numpy(gold[f"gt_{s}"]) for s in STAGES}
-    mask = {s: torch.from_numpy(gold[f"mask_{s}"]) for s in STAGES}
+    proj = {k: cast(v) for k, v in synthetic.synthetic_cameras(N, H, W, seed=1).items()}
+    dv = cast(synthetic.synthetic_depth_values(1))
+    gt = {s: cast(torch.from_numpy(gold[f"gt_{s}"])) for s in STAGES}
+    mask = {s: cast(torch.from_numpy(gold[f"mask_{s}"])) for s in STAGES}
     leaves = None
     if case == "f":
-        leaves = [{k: v.clone().requires_grad_(True) for k, v in f.items()}
+        leaves = [{k: cast(v).clone().requires_grad_(True) for k, v in f.items()}
                   for f in synthetic.synthetic_features(N, H, W, seed=2)]
         out = oracle.forward_from_features(sd, leaves, proj, dv, (H, W), ndepths=ND, training=True)
     else:
-        imgs = synthetic.synthetic_images(N, H, W, seed=0)
+        imgs = cast(synthetic.synthetic_images(N, H, W, seed=0))
         out = oracle.forward(sd, imgs, proj, dv, ndepths=ND, training=True)
-    interval = torch.from_numpy(gold[f"{case}_interval"])
+    interval = cast(torch.from_numpy(gold[f"{case}_interval"]))
     res = loss_ref.focal_loss_bld(out, gt, mask, interval, dlossw=[1.0, 1.0, 1.0])
     res[0].backward()
     return res, out, sd, leaves
@@ -64,7 +66,7 @@ def _check(gold, case, res, out, sd, leaves):
     worst = {}
     for name, v in zip(("loss", "depth_loss", "epe", "less1", "less3"), res):
         ref = gold[f"{case}_{name}"]
-        worst[name] = abs(float(v) - float(ref)) / max(abs(float(ref)), 1e-30)
+        worst[name] = abs(float(v.detach()) - float(ref)) / max(abs(float(ref)), 1e-30)
     for s in (1, 2, 3):
         assert np.array_equal(out[f"stage{s}"]["depth"].detach().numpy(), gold[f"{case}_stage{s}_depth"]), s
         worst[f"stage{s}_prob"] = float(np.abs(out[f"stage{s}"]["prob_volume"].detach().numpy()

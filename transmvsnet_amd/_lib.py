@@ -82,9 +82,19 @@ SIGNATURES = {
     "tmvs_bn_stats": (I, [P, L, I, P, S, P, P, P]),
     "tmvs_bn_relu_train": (I, [P, L, I, P, P, P, P, F, P, P, P]),
     "tmvs_bn_relu_backward": (I, [P, P, L, I, P, P, P, P, F, P, S, P, P, P, P]),
+    "tmvs_conv2d_generic": (I, [P, I, I, I, I, P, P, I, I, I, I, I, I, I, P, P]),
+    "tmvs_conv2d_wgrad_workspace": (S, [I, I, I, I, I, I]),
+    "tmvs_conv2d_wgrad": (I, [P, I, I, I, I, P, I, I, I, I, I, I, P, S, P, P]),
+    "tmvs_colsum_workspace": (S, [L, I]),
+    "tmvs_colsum": (I, [P, L, I, P, S, P, P]),
+    "tmvs_dcn_forward_train": (I, [P, P, P, P, P, I, I, I, I, I, P, P, P, P]),
+    "tmvs_dcn_backward_workspace": (S, [I, I, I, I]),
+    "tmvs_dcn_backward": (I, [P, P, P, P, I, I, I, I, I, P, S, P, P, P, P]),
+    "tmvs_nearest_up2_backward_nhwc": (I, [P, I, I, I, I, I, P, P]),
+    "tmvs_softmax_backward": (I, [P, P, I, I, I, I, P, P]),
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 PW_NPARAMS = 201
 ENC_NPARAMS = 8544
 KV_NFLOATS = 160

@@ -21,7 +21,7 @@ ARCH = os.environ.get("TMVS_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["host.hip", "glue.hip", "warp_corr.hip", "costreg.hip", "fmt.hip", "pathway.hip", "pipeline.hip", "featurenet.hip",
            "conv2d.hip", "fusion.hip", "loss.hip", "costreg_train.hip", "pw_train.hip", "pathway_train.hip",
-           "fmt_train.hip", "optim.hip"]
+           "fmt_train.hip", "optim.hip", "featurenet_train.hip"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fno-gpu-rdc",
           "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include")]
 

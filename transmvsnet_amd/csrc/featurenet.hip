@@ -129,7 +129,8 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
                                                          const float* __restrict__ alpha,
                                                          const float* __restrict__ shift, int relu, int B, int H,
                                                          int W, float* __restrict__ out,
-                                                         float* __restrict__ out_nhwc) {
+                                                         float* __restrict__ out_nhwc,
+                                                         float* __restrict__ om_out) {
   constexpr int MT = (CO + 15) / 16;
   constexpr int NA4 = 9 * MT * 2 * 64;  // A fragments [tap][mt][half][lane] float4
   constexpr int NO4 = FUSED ? 9 * 2 * 2 * 64 : 1;  // offset-conv A fragments (27 rows padded to 32)
@@ -227,7 +228,12 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int c = 16 * m + 4 * j + i;
-          if (c < 27) omt[n * 33 + c] = ao[m][i] + bom[c];
+          if (c < 27) {
+            const float o = ao[m][i] + bom[c];
+            omt[n * 33 + c] = o;
+            // training: the offset/mask tensor the backward needs ([B][27][H][W])
+            if (om_out && n < nvalid) om_out[((size_t)b * 27 + c) * HW + (size_t)row * W + x0t + n] = o;
+          }
         }
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
@@ -472,7 +478,7 @@ namespace {
 template <int CO, bool FUSED>
 int dcn_launch(const float* x, const float* om, const float* wom, const float* bom, const float* w,
                const float* bias, const float* alpha, const float* shift, int relu, int batch, int height, int width,
-               float* out, float* out_nhwc, hipStream_t st) {
+               float* out, float* out_nhwc, hipStream_t st, float* om_out = nullptr) {
   // persistent grid: one block per CU slot the kernel's LDS/VGPR footprint allows
   static int grid = 0;
   if (!grid) {
@@ -486,7 +492,7 @@ int dcn_launch(const float* x, const float* om, const float* wom, const float* b
       (long long)batch * ((height + dcn::WAVES - 1) / dcn::WAVES) * ((width + dcn::TW - 1) / dcn::TW);
   const int nblk = (int)std::min<long long>(grid, nunits);
   hipLaunchKernelGGL((dcn_window_kernel<CO, FUSED>), dim3(nblk), dim3(512), 0, st, x, om, wom, bom, w, bias, alpha,
-                     shift, relu, batch, height, width, out, out_nhwc);
+                     shift, relu, batch, height, width, out, out_nhwc, om_out);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -518,6 +524,23 @@ extern "C" int tmvs_deform_conv2d(const float* x_nhwc, const float* offset_mask,
                                  batch, height, width, out, out_nhwc, st);
   return dcn_launch<8, false>(x_nhwc, offset_mask, nullptr, nullptr, w_packed, bias, bn_alpha, bn_shift, relu, batch,
                               height, width, out, out_nhwc, st);
+}
+
+extern "C" int tmvs_dcn_forward_train(const float* x_nhwc, const float* wom_packed, const float* bom,
+                                      const float* w_packed, const float* bias, int batch, int cin, int cout, int height,
+                                      int width, float* out, float* out_nhwc, float* offset_mask_out, void* stream) {
+  if (!wom_packed || !bom || !offset_mask_out || (!out && !out_nhwc)) return TMVS_ERR_ARG;
+  const int rc = dcn_check(x_nhwc, w_packed, bias, nullptr, nullptr, batch, cin, cout, height, width);
+  if (rc != TMVS_OK) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (cout == 32)
+    return dcn_launch<32, true>(x_nhwc, nullptr, wom_packed, bom, w_packed, bias, nullptr, nullptr, 0, batch, height,
+                                width, out, out_nhwc, st, offset_mask_out);
+  if (cout == 16)
+    return dcn_launch<16, true>(x_nhwc, nullptr, wom_packed, bom, w_packed, bias, nullptr, nullptr, 0, batch, height,
+                                width, out, out_nhwc, st, offset_mask_out);
+  return dcn_launch<8, true>(x_nhwc, nullptr, wom_packed, bom, w_packed, bias, nullptr, nullptr, 0, batch, height,
+                             width, out, out_nhwc, st, offset_mask_out);
 }
 
 extern "C" int tmvs_dcn_fused(const float* x_nhwc, const float* wom_packed, const float* bom, const float* w_packed,

@@ -1,0 +1,712 @@
+// FeatureNet training: the pieces of the backward of
+// models/module.py:343-422 (Conv2d blocks, FPN merges) and models/dcn.py:66-80 (DCNv2 ->
+// torchvision.ops.deform_conv2d) that the inference kernels do not already cover, plus the softmax
+// backward of prob_volume = exp(log_softmax(logits)) (models/TransMVSNet.py:99).
+//
+// Layout: NHWC fp32 activations (as featurenet.hip), the offset/mask tensor om [B][27][H][W] as
+// the DCN kernels read it (channel 2k / 2k+1 = dy / dx of tap k = 3i + j, 18 + k = mask logit).
+//
+//   conv2d_generic   strided:    y[o][co] = b[co] + sum_{k,ci} W[k][co][ci] x[o*s - pad + k][ci]
+//                    transposed: y[i][co] = b[co] + sum_{k,ci} W[k][co][ci] x[(i + pad - k)/s][ci]
+//                    (the data gradient of a strided conv; taps with s not dividing are skipped)
+//   conv2d_wgrad     dW[k][a][b] = sum_p direct[p][a] * gathered[p*s - pad + k][b]
+//   dcn backward     with col_k[p][c] = m_k(p) * bilinear_c(x, pos_k(p)) the forward's column and
+//                    dcol_k[p][c] = sum_o dy[p][o] W[o][c][k]:
+//                      dW[k][o][c]  = sum_p dy[p][o] col_k[p][c]
+//                      d mask logit = m (1 - m) sum_c dcol * bilinear_c
+//                      d pos_y      = m sum_c dcol * (hx (v10 - v00) + lx (v11 - v01))   (x alike)
+//                      dx           = the bilinear scatter of m * dcol (torchvision's col2im)
+//                    with torchvision's conventions (a sample outside (-1, H) x (-1, W) is zero and
+//                    carries no gradient; corners outside the image read 0 and receive nothing).
+//
+// Determinism: every reduction over pixels (weight / bias gradients) is block partials in fp64 plus
+// a fixed-order combine. The DCN input gradient is a scatter with data-dependent targets; it is
+// accumulated in fp32 LDS windows (per block tile + a halo of kR px) flushed with global fp32
+// atomics, as torchvision's deformable_col2im adds with atomicAdd: the sum is exact up to fp32
+// rounding order (bitwise run-to-run stability is not promised for dx, as in the reference).
+#include "common.h"
+
+namespace tmvs {
+namespace {
+
+constexpr int kBlk = 256;
+
+// ---------------------------------------------------------------- generic 2-D conv (VALU)
+template <int CIN, int COB>
+__global__ __launch_bounds__(kBlk) void conv2d_generic_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                             const float* __restrict__ bias, int cout, int B, int Hi,
+                                                             int Wi, int Ho, int Wo, int K, int stride, int pad,
+                                                             int transposed, int accumulate, float* __restrict__ y) {
+  const int cob = blockIdx.y;
+  const long np = (long)B * Ho * Wo;
+  const long p = (long)blockIdx.x * kBlk + threadIdx.x;
+  if (p >= np) return;
+  const int ow = (int)(p % Wo);
+  const long t = p / Wo;
+  const int oh = (int)(t % Ho), b = (int)(t / Ho);
+  float acc[COB];
+#pragma unroll
+  for (int c = 0; c < COB; ++c) acc[c] = 0.f;
+  const float* xb = x + (size_t)b * Hi * Wi * CIN;
+#pragma unroll 1
+  for (int kh = 0; kh < K; ++kh) {
+    int ih;
+    if (transposed) {
+      const int th = oh + pad - kh;
+      if (th < 0 || th % stride) continue;
+      ih = th / stride;
+    } else {
+      ih = oh * stride - pad + kh;
+    }
+    if (ih < 0 || ih >= Hi) continue;
+#pragma unroll 1
+    for (int kw = 0; kw < K; ++kw) {
+      int iw;
+      if (transposed) {
+        const int tw = ow + pad - kw;
+        if (tw < 0 || tw % stride) continue;
+        iw = tw / stride;
+      } else {
+        iw = ow * stride - pad + kw;
+      }
+      if (iw < 0 || iw >= Wi) continue;
+      const float* xp = xb + ((size_t)ih * Wi + iw) * CIN;
+      const float* wk = w + ((size_t)(kh * K + kw) * cout + cob * COB) * CIN;  // wave-uniform
+      if constexpr (CIN % 4 == 0) {
+#pragma unroll 4
+        for (int c4 = 0; c4 < CIN / 4; ++c4) {
+          const float4 xv = *reinterpret_cast<const float4*>(xp + 4 * c4);
+#pragma unroll
+          for (int co = 0; co < COB; ++co) {
+            const float* wc = wk + co * CIN + 4 * c4;
+            acc[co] = fmaf(wc[0], xv.x, acc[co]);
+            acc[co] = fmaf(wc[1], xv.y, acc[co]);
+            acc[co] = fmaf(wc[2], xv.z, acc[co]);
+            acc[co] = fmaf(wc[3], xv.w, acc[co]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int ci = 0; ci < CIN; ++ci) {
+          const float xv = xp[ci];
+#pragma unroll
+          for (int co = 0; co < COB; ++co) acc[co] = fmaf(wk[co * CIN + ci], xv, acc[co]);
+        }
+      }
+    }
+  }
+  float* yp = y + (size_t)p * cout + cob * COB;
+#pragma unroll
+  for (int c = 0; c < COB; ++c) {
+    float v = acc[c];
+    if (bias) v = v + bias[cob * COB + c];
+    if (accumulate) v = yp[c] + v;
+    yp[c] = v;
+  }
+}
+
+// ---------------------------------------------------------------- pixel-reduction helpers
+// A register-tiled reduction sum_p a[p][i] * b[p][j] over a block's pixel range [v0, v1): chunks of
+// 64 rows are staged in LDS by the callers' row loaders (float4 quads, zero rows where the gathered
+// tap is outside); lane (ai, ci) of each wave owns a TA x TB block, fp32 per chunk, fp64 across
+// chunks; the 4 waves combine in the fixed order ((w0 + w1) + w2) + w3. A = rows of `a` (padded to
+// a multiple of 8 by the loader), BC = columns of `b` (multiple of 8).
+template <int A, int BC, typename LoadA, typename LoadB>
+__device__ __forceinline__ void tile_reduce(long v0, long v1, LoadA load_a, LoadB load_b, double* __restrict__ out) {
+  constexpr int CH = 64, TA = A / 8, TB = BC / 8, SA = A + 4, SB = BC + 4;
+  static_assert(A % 8 == 0 && BC % 8 == 0, "tile");
+  static_assert(CH * (SA + SB) * 4 >= A * BC * 8, "combine buffer fits the staging LDS");
+  __shared__ __attribute__((aligned(16))) float lds[CH * (SA + SB)];
+  float* sa = lds;
+  float* sb = lds + CH * SA;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ci = lane & 7, ai = lane >> 3;
+  double acc[TA][TB];
+#pragma unroll
+  for (int i = 0; i < TA; ++i)
+#pragma unroll
+    for (int j = 0; j < TB; ++j) acc[i][j] = 0.0;
+#pragma unroll 1
+  for (long vb = v0; vb < v1; vb += CH) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < CH * A / 4; i += kBlk) {
+      const int r = i / (A / 4), q = i % (A / 4);
+      const long v = vb + r;
+      *reinterpret_cast<float4*>(sa + r * SA + 4 * q) = v < v1 ? load_a(v, q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    for (int i = threadIdx.x; i < CH * BC / 4; i += kBlk) {
+      const int r = i / (BC / 4), q = i % (BC / 4);
+      const long v = vb + r;
+      *reinterpret_cast<float4*>(sb + r * SB + 4 * q) = v < v1 ? load_b(v, q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    float s[TA][TB];
+#pragma unroll
+    for (int i = 0; i < TA; ++i)
+#pragma unroll
+      for (int j = 0; j < TB; ++j) s[i][j] = 0.f;
+#pragma unroll 4
+    for (int r = wv; r < CH; r += 4) {
+      float av[TA], bv[TB];
+#pragma unroll
+      for (int i = 0; i < TA; ++i) av[i] = sa[r * SA + ai * TA + i];
+#pragma unroll
+      for (int j = 0; j < TB; ++j) bv[j] = sb[r * SB + ci * TB + j];
+#pragma unroll
+      for (int i = 0; i < TA; ++i)
+#pragma unroll
+        for (int j = 0; j < TB; ++j) s[i][j] = fmaf(av[i], bv[j], s[i][j]);
+    }
+#pragma unroll
+    for (int i = 0; i < TA; ++i)
+#pragma unroll
+      for (int j = 0; j < TB; ++j) acc[i][j] += (double)s[i][j];
+  }
+  double* cmb = reinterpret_cast<double*>(lds);
+#pragma unroll 1
+  for (int w = 1; w < 4; ++w) {
+    __syncthreads();
+    if (wv == w)
+#pragma unroll
+      for (int i = 0; i < TA; ++i)
+#pragma unroll
+        for (int j = 0; j < TB; ++j) cmb[(ai * TA + i) * BC + ci * TB + j] = acc[i][j];
+    __syncthreads();
+    if (wv == 0)
+#pragma unroll
+      for (int i = 0; i < TA; ++i)
+#pragma unroll
+        for (int j = 0; j < TB; ++j) acc[i][j] += cmb[(ai * TA + i) * BC + ci * TB + j];
+  }
+  if (wv == 0)
+#pragma unroll
+    for (int i = 0; i < TA; ++i)
+#pragma unroll
+      for (int j = 0; j < TB; ++j) out[(ai * TA + i) * BC + ci * TB + j] = acc[i][j];
+}
+
+__device__ __forceinline__ float4 load_row4(const float* __restrict__ base, long v, int ch, int q) {
+  // 4 channels 4q..4q+3 of row v of a [.][ch] tensor, zero past ch (ch = 27 rows are not 16-B aligned)
+  const float* r = base + (size_t)v * ch;
+  const int c = 4 * q;
+  if (ch % 4 == 0) return *reinterpret_cast<const float4*>(r + c);
+  return make_float4(c < ch ? r[c] : 0.f, c + 1 < ch ? r[c + 1] : 0.f, c + 2 < ch ? r[c + 2] : 0.f,
+                     c + 3 < ch ? r[c + 3] : 0.f);
+}
+
+// dW[k][a][b] (a padded to AP rows, b = BC): grid (nblk, K*K)
+template <int AP, int BC>
+__global__ __launch_bounds__(kBlk) void conv2d_wgrad_kernel(const float* __restrict__ direct, int a_ch,
+                                                           const float* __restrict__ gath, int B, int Ph, int Pw,
+                                                           int Gh, int Gw, int K, int stride, int pad, long ppb,
+                                                           double* __restrict__ partial) {
+  const int k = blockIdx.y, kh = k / K, kw = k % K;
+  const long np = (long)B * Ph * Pw;
+  const long v0 = (long)blockIdx.x * ppb, v1 = v0 + ppb < np ? v0 + ppb : np;
+  auto la = [&](long v, int q) { return load_row4(direct, v, a_ch, q); };
+  auto lb = [&](long v, int q) {
+    const int pw = (int)(v % Pw);
+    const long t = v / Pw;
+    const int ph = (int)(t % Ph), b = (int)(t / Ph);
+    const int gh = ph * stride - pad + kh, gw = pw * stride - pad + kw;
+    if (gh < 0 || gw < 0 || gh >= Gh || gw >= Gw) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return *reinterpret_cast<const float4*>(gath + (((size_t)b * Gh + gh) * Gw + gw) * BC + 4 * q);
+  };
+  tile_reduce<AP, BC>(v0, v1, la, lb, partial + ((size_t)blockIdx.x * K * K + k) * AP * BC);
+}
+
+// few channels on the gathered side (the image: 3): thread t owns pairs t, t+256, .. of a x b,
+// straight from global memory (L1 hits), fp32 over a block's pixels in 8 interleaved chains, fp64 after
+template <int A, int BC>
+__global__ __launch_bounds__(kBlk) void conv2d_wgrad_small_kernel(const float* __restrict__ direct,
+                                                                 const float* __restrict__ gath, int B, int Ph, int Pw,
+                                                                 int Gh, int Gw, int K, int stride, int pad, long ppb,
+                                                                 double* __restrict__ partial) {
+  constexpr int NPR = A * BC;
+  __shared__ double red[NPR][kBlk / 64];
+  const int k = blockIdx.y, kh = k / K, kw = k % K;
+  const long np = (long)B * Ph * Pw;
+  const long v0 = (long)blockIdx.x * ppb, v1 = v0 + ppb < np ? v0 + ppb : np;
+  float acc[NPR];
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) acc[q] = 0.f;
+  for (long v = v0 + threadIdx.x; v < v1; v += kBlk) {
+    const int pw = (int)(v % Pw);
+    const long t = v / Pw;
+    const int ph = (int)(t % Ph), b = (int)(t / Ph);
+    const int gh = ph * stride - pad + kh, gw = pw * stride - pad + kw;
+    if (gh < 0 || gw < 0 || gh >= Gh || gw >= Gw) continue;
+    const float* gp = gath + (((size_t)b * Gh + gh) * Gw + gw) * BC;
+    float gv[BC];
+#pragma unroll
+    for (int c = 0; c < BC; ++c) gv[c] = gp[c];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const float d = direct[v * A + a];
+#pragma unroll
+      for (int c = 0; c < BC; ++c) acc[a * BC + c] = fmaf(d, gv[c], acc[a * BC + c]);
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    double x = (double)acc[q];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    if (lane == 0) red[q][wv] = x;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NPR; i += kBlk)
+    partial[((size_t)blockIdx.x * K * K + k) * NPR + i] = (red[i][0] + red[i][1]) + (red[i][2] + red[i][3]);
+}
+
+// out[i] = sum_j partial[j][i] in a fixed order (8 interleaved chains, then the chains in order)
+__global__ __launch_bounds__(kBlk) void sum_partials_f32_kernel(const double* __restrict__ partial, int nblk, long n,
+                                                                float* __restrict__ out) {
+  __shared__ double red[8][32];
+  const int g = threadIdx.x >> 5, q = threadIdx.x & 31;
+  const long i = (long)blockIdx.x * 32 + q;
+  double s = 0.0;
+  if (i < n)
+    for (int j = g; j < nblk; j += 8) s += partial[(size_t)j * n + i];
+  red[g][q] = s;
+  __syncthreads();
+  if (g == 0 && i < n) {
+    double t = red[0][q];
+#pragma unroll
+    for (int c = 1; c < 8; ++c) t += red[c][q];
+    out[i] = (float)t;
+  }
+}
+
+// the same with [nblk][taps][ap][b] partials (rows padded to ap) -> dw [taps][a][b]
+__global__ __launch_bounds__(kBlk) void sum_partials_rows_kernel(const double* __restrict__ partial, int nblk, int ap,
+                                                                 int a, int bc, long n, float* __restrict__ out) {
+  __shared__ double red[8][32];
+  const int g = threadIdx.x >> 5, q = threadIdx.x & 31;
+  const long i = (long)blockIdx.x * 32 + q;
+  const long per = (long)a * bc;
+  const long src = i < n ? ((i / per) * ap + (i % per) / bc) * bc + i % bc : 0;
+  const long np = n / per * ap * bc;
+  double s = 0.0;
+  if (i < n)
+    for (int j = g; j < nblk; j += 8) s += partial[(size_t)j * np + src];
+  red[g][q] = s;
+  __syncthreads();
+  if (g == 0 && i < n) {
+    double t = red[0][q];
+#pragma unroll
+    for (int c = 1; c < 8; ++c) t += red[c][q];
+    out[i] = (float)t;
+  }
+}
+
+// per-block fp64 partial column sums of x [n][C] (C <= 32): thread (r, c) = (t / 32, t % 32)
+__global__ __launch_bounds__(kBlk) void colsum_partial_kernel(const float* __restrict__ x, long n, int C, long ppb,
+                                                              double* __restrict__ partial) {
+  __shared__ double red[8][32];
+  const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;
+  const long v0 = (long)blockIdx.x * ppb, v1 = v0 + ppb < n ? v0 + ppb : n;
+  double s = 0.0;
+  if (c < C)
+    for (long v = v0 + r0; v < v1; v += 8) s += (double)x[v * C + c];
+  red[r0][c] = s;
+  __syncthreads();
+  if (r0 == 0 && c < C) {
+    double t = red[0][c];
+#pragma unroll
+    for (int r = 1; r < 8; ++r) t += red[r][c];
+    partial[(size_t)blockIdx.x * C + c] = t;
+  }
+}
+
+// ---------------------------------------------------------------- DCN backward
+// torchvision's sample geometry (models/dcn.py:71-80 -> deform_conv2d, stride 1, pad 1, dil 1) and
+// the forward kernel's exact mask (featurenet.hip: fast sigmoid) and bilinear weights
+struct DcnSample {
+  bool inside;
+  int y0, x0;
+  float ly, lx, hy, hx, m;
+};
+__device__ __forceinline__ DcnSample dcn_sample(const float* __restrict__ omp, size_t HW, int y, int x, int k, int H,
+                                                int W) {
+  DcnSample s;
+  const int ki = k / 3, kj = k - 3 * ki;
+  const float py = (float)(y + ki - 1) + omp[(size_t)(2 * k) * HW];
+  const float px = (float)(x + kj - 1) + omp[(size_t)(2 * k + 1) * HW];
+  s.m = __frcp_rn(1.f + __expf(-omp[(size_t)(18 + k) * HW]));
+  s.inside = py > -1.f && py < (float)H && px > -1.f && px < (float)W;
+  const float y0 = floorf(py), x0 = floorf(px);
+  s.ly = py - y0;
+  s.lx = px - x0;
+  s.hy = 1.f - s.ly;
+  s.hx = 1.f - s.lx;
+  s.y0 = s.inside ? (int)y0 : 0;
+  s.x0 = s.inside ? (int)x0 : 0;
+  return s;
+}
+
+namespace dbw {
+constexpr int TY = 8, TX = 32;          // block tile of reference pixels (one thread each)
+constexpr int R = 2;                    // offsets up to R px keep every corner in the LDS window
+constexpr int CC = 8;                   // channels per pass
+constexpr int WR = TY + 2 * R + 3, WC = TX + 2 * R + 3;
+}  // namespace dbw
+
+// dcol, d om (NHWC [B][H][W][27]) and the scatter of m * dcol into dx (accumulated)
+template <int CO>
+__global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ om,
+                                                           const float* __restrict__ wt, const float* __restrict__ dy,
+                                                           int B, int H, int W, float* __restrict__ dx,
+                                                           float* __restrict__ dom) {
+  using namespace dbw;
+  __shared__ float wl[9 * CO * 32];
+  __shared__ float win[WR * WC * CC];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 9 * CO * 32; i += kBlk) wl[i] = wt[i];
+  const int ntx = (W + TX - 1) / TX, nty = (H + TY - 1) / TY;
+  int blk = blockIdx.x;
+  const int bx = blk % ntx;
+  blk /= ntx;
+  const int by = blk % nty, b = blk / nty;
+  const int y = by * TY + tid / TX, xq = bx * TX + tid % TX;
+  const bool live = y < H && xq < W;
+  const size_t HW = (size_t)H * W;
+  const int wy0 = by * TY - R - 1, wx0 = bx * TX - R - 1;
+  const size_t pix = (size_t)b * HW + (size_t)(live ? y : 0) * W + (live ? xq : 0);
+  float g[CO];
+#pragma unroll
+  for (int o4 = 0; o4 < CO / 4; ++o4) {
+    const float4 t = live ? *reinterpret_cast<const float4*>(dy + pix * CO + 4 * o4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    g[4 * o4] = t.x;
+    g[4 * o4 + 1] = t.y;
+    g[4 * o4 + 2] = t.z;
+    g[4 * o4 + 3] = t.w;
+  }
+  const float* xb = x + (size_t)b * HW * 32;
+  float* dxb = dx + (size_t)b * HW * 32;
+  const float* omp = om + (size_t)b * 27 * HW + (size_t)(live ? y : 0) * W + (live ? xq : 0);
+  float aY[9], aX[9], aM[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) aY[k] = aX[k] = aM[k] = 0.f;
+#pragma unroll 1
+  for (int cc = 0; cc < 32 / CC; ++cc) {
+    for (int i = tid; i < WR * WC * CC; i += kBlk) win[i] = 0.f;
+    __syncthreads();
+    if (live) {
+#pragma unroll 1
+      for (int k = 0; k < 9; ++k) {
+        const DcnSample s = dcn_sample(omp, HW, y, xq, k, H, W);
+        if (!s.inside) continue;  // the column is 0 and carries no gradient (torchvision)
+        float dc[CC];
+#pragma unroll
+        for (int c = 0; c < CC; ++c) {
+          float a = 0.f;
+#pragma unroll
+          for (int o = 0; o < CO; ++o) a = fmaf(g[o], wl[(k * CO + o) * 32 + cc * CC + c], a);
+          dc[c] = a;
+        }
+        const float wq[4] = {s.hy * s.hx, s.hy * s.lx, s.ly * s.hx, s.ly * s.lx};
+        float v[4][CC];
+        bool ok[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int cy = s.y0 + (q >> 1), cx = s.x0 + (q & 1);
+          ok[q] = (unsigned)cy < (unsigned)H && (unsigned)cx < (unsigned)W;
+          const float* p = xb + ((size_t)(ok[q] ? cy : 0) * W + (ok[q] ? cx : 0)) * 32 + cc * CC;
+          const float4 u0 = *reinterpret_cast<const float4*>(p), u1 = *reinterpret_cast<const float4*>(p + 4);
+          const float t[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+          for (int c = 0; c < CC; ++c) v[q][c] = ok[q] ? t[c] : 0.f;
+        }
+        float sm = 0.f, sy = 0.f, sx = 0.f;
+#pragma unroll
+        for (int c = 0; c < CC; ++c) {
+          float val = wq[0] * v[0][c];
+          val = val + wq[1] * v[1][c];
+          val = val + wq[2] * v[2][c];
+          val = val + wq[3] * v[3][c];
+          sm = fmaf(dc[c], val, sm);
+          sy = fmaf(dc[c], s.hx * (v[2][c] - v[0][c]) + s.lx * (v[3][c] - v[1][c]), sy);
+          sx = fmaf(dc[c], s.hy * (v[1][c] - v[0][c]) + s.ly * (v[3][c] - v[2][c]), sx);
+        }
+        aM[k] += sm;
+        aY[k] += sy;
+        aX[k] += sx;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (!ok[q]) continue;
+          const int cy = s.y0 + (q >> 1), cx = s.x0 + (q & 1);
+          const int ry = cy - wy0, rx = cx - wx0;
+          const float f = s.m * wq[q];
+          if ((unsigned)ry < (unsigned)WR && (unsigned)rx < (unsigned)WC) {
+            float* wp = win + (ry * WC + rx) * CC;
+#pragma unroll
+            for (int c = 0; c < CC; ++c) atomicAdd(wp + c, f * dc[c]);
+          } else {  // an offset beyond the window: straight to global memory
+            float* gp = dxb + ((size_t)cy * W + cx) * 32 + cc * CC;
+#pragma unroll
+            for (int c = 0; c < CC; ++c) unsafeAtomicAdd(gp + c, f * dc[c]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < WR * WC * CC; i += kBlk) {
+      const float v = win[i];
+      if (v != 0.f) {  // only in-image corners were added
+        const int cell = i / CC, c = i - cell * CC;
+        const int gy = wy0 + cell / WC, gx = wx0 + cell % WC;
+        unsafeAtomicAdd(dxb + ((size_t)gy * W + gx) * 32 + cc * CC + c, v);
+      }
+    }
+    __syncthreads();
+  }
+  if (live) {
+    float* dp = dom + pix * 27;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const float m = __frcp_rn(1.f + __expf(-omp[(size_t)(18 + k) * HW]));
+      dp[2 * k] = m * aY[k];
+      dp[2 * k + 1] = m * aX[k];
+      dp[18 + k] = aM[k] * (m * (1.f - m));
+    }
+  }
+}
+
+// dW[k][o][c] = sum_p dy[p][o] col_k[p][c]: grid (nblk, 9), block partials [nblk][9][CO][32]
+template <int CO>
+__global__ __launch_bounds__(kBlk) void dcn_bwd_weight_kernel(const float* __restrict__ x, const float* __restrict__ om,
+                                                             const float* __restrict__ dy, int B, int H, int W, long ppb,
+                                                             double* __restrict__ partial) {
+  const int k = blockIdx.y;
+  const long HW = (long)H * W, np = (long)B * HW;
+  const long v0 = (long)blockIdx.x * ppb, v1 = v0 + ppb < np ? v0 + ppb : np;
+  auto la = [&](long v, int q) { return *reinterpret_cast<const float4*>(dy + (size_t)v * CO + 4 * q); };
+  auto lb = [&](long v, int q) {
+    const int b = (int)(v / HW);
+    const long p = v - (long)b * HW;
+    const int yy = (int)(p / W), xx = (int)(p % W);
+    const DcnSample s = dcn_sample(om + (size_t)b * 27 * HW + p, (size_t)HW, yy, xx, k, H, W);
+    if (!s.inside) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float wq[4] = {s.hy * s.hx, s.hy * s.lx, s.ly * s.hx, s.ly * s.lx};
+    const float* xb = x + (size_t)b * HW * 32 + 4 * q;
+    float4 v4[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int cy = s.y0 + (c >> 1), cx = s.x0 + (c & 1);
+      const bool ok = (unsigned)cy < (unsigned)H && (unsigned)cx < (unsigned)W;
+      v4[c] = ok ? *reinterpret_cast<const float4*>(xb + ((size_t)cy * W + cx) * 32) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    auto blend = [&](float a0, float a1, float a2, float a3) {
+      float val = wq[0] * a0;
+      val = val + wq[1] * a1;
+      val = val + wq[2] * a2;
+      val = val + wq[3] * a3;
+      return s.m * val;  // the forward's column value (featurenet.hip: mk * val)
+    };
+    return make_float4(blend(v4[0].x, v4[1].x, v4[2].x, v4[3].x), blend(v4[0].y, v4[1].y, v4[2].y, v4[3].y),
+                       blend(v4[0].z, v4[1].z, v4[2].z, v4[3].z), blend(v4[0].w, v4[1].w, v4[2].w, v4[3].w));
+  };
+  tile_reduce<CO, 32>(v0, v1, la, lb, partial + ((size_t)blockIdx.x * 9 + k) * CO * 32);
+}
+
+// ---------------------------------------------------------------- small backward pieces
+// d prev [n][h][w][C] (+)= sum of the 2x2 block of d [n][2h][2w][C] (nearest x2 up-sampling's adjoint,
+// models/module.py:413,417)
+__global__ __launch_bounds__(kBlk) void nearest_up2_bwd_kernel(const float* __restrict__ d, int n, int h, int w, int C,
+                                                              int accumulate, float* __restrict__ dprev) {
+  const long i = (long)blockIdx.x * kBlk + threadIdx.x;
+  const long tot = (long)n * h * w * C;
+  if (i >= tot) return;
+  const int c = (int)(i % C);
+  long t = i / C;
+  const int xx = (int)(t % w);
+  t /= w;
+  const int yy = (int)(t % h), b = (int)(t / h);
+  const size_t row = (size_t)2 * w * C;
+  const float* p = d + (((size_t)b * 2 * h + 2 * yy) * 2 * w + 2 * xx) * C + c;
+  float s = (p[0] + p[C]) + (p[row] + p[row + C]);
+  if (accumulate) s = dprev[i] + s;
+  dprev[i] = s;
+}
+
+// d logits = p * (dp - sum_d p dp) per pixel (prob = exp(log_softmax(x)), models/TransMVSNet.py:99)
+__global__ __launch_bounds__(kBlk) void softmax_bwd_kernel(const float* __restrict__ prob, const float* __restrict__ dprob,
+                                                          int B, int D, long HW, float* __restrict__ dx) {
+  const long i = (long)blockIdx.x * kBlk + threadIdx.x;
+  if (i >= (long)B * HW) return;
+  const long b = i / HW, p = i - b * HW;
+  const float* pp = prob + (size_t)b * D * HW + p;
+  const float* gp = dprob + (size_t)b * D * HW + p;
+  float s = 0.f;
+  for (int d = 0; d < D; ++d) s = fmaf(pp[(size_t)d * HW], gp[(size_t)d * HW], s);
+  float* op = dx + (size_t)b * D * HW + p;
+  for (int d = 0; d < D; ++d) op[(size_t)d * HW] = pp[(size_t)d * HW] * (gp[(size_t)d * HW] - s);
+}
+
+long ppb_for(long n, int max_blocks) {
+  long ppb = 1024;
+  while ((n + ppb - 1) / ppb > max_blocks) ppb *= 2;
+  return ppb;
+}
+
+}  // namespace
+}  // namespace tmvs
+
+using namespace tmvs;
+
+extern "C" int tmvs_conv2d_generic(const float* x, int batch, int cin, int h_in, int w_in, const float* w,
+                                   const float* bias, int cout, int h_out, int w_out, int k, int stride, int pad,
+                                   int flags, float* y, void* stream) {
+  if (!x || !w || !y || batch <= 0 || h_in <= 0 || w_in <= 0 || h_out <= 0 || w_out <= 0) return TMVS_ERR_ARG;
+  if (k < 1 || k > 7 || (stride != 1 && stride != 2) || pad < 0) return TMVS_ERR_SHAPE;
+  const int tr = (flags & TMVS_CONV_TRANSPOSED) ? 1 : 0, acc = (flags & TMVS_CONV_ACCUMULATE) ? 1 : 0;
+  hipStream_t st = (hipStream_t)stream;
+  const long np = (long)batch * h_out * w_out;
+  const unsigned gx = (unsigned)((np + kBlk - 1) / kBlk);
+#define TMVS_C2G(CI, CB)                                                                                       \
+  if (cin == CI && cout % CB == 0) {                                                                           \
+    hipLaunchKernelGGL((conv2d_generic_kernel<CI, CB>), dim3(gx, cout / CB), dim3(kBlk), 0, st, x, w, bias,   \
+                       cout, batch, h_in, w_in, h_out, w_out, k, stride, pad, tr, acc, y);                      \
+    TMVS_CHECK_LAUNCH();                                                                                       \
+    return TMVS_OK;                                                                                            \
+  }
+  if (cout % 8 == 0) {
+    TMVS_C2G(3, 8) TMVS_C2G(8, 8) TMVS_C2G(16, 8) TMVS_C2G(27, 8) TMVS_C2G(32, 8)
+  } else {
+    TMVS_C2G(32, 9) TMVS_C2G(16, 9) TMVS_C2G(8, 9)
+  }
+#undef TMVS_C2G
+  return TMVS_ERR_SHAPE;
+}
+
+static int wgrad_ap(int a) { return (a + 7) / 8 * 8; }
+
+extern "C" size_t tmvs_conv2d_wgrad_workspace(int batch, int h, int w, int a_ch, int b_ch, int k) {
+  const long np = (long)batch * h * w;
+  const long ppb = ppb_for(np, 512);
+  return (size_t)((np + ppb - 1) / ppb) * k * k * wgrad_ap(a_ch) * b_ch * sizeof(double);
+}
+
+// dw [k*k][a_ch][b_ch]
+extern "C" int tmvs_conv2d_wgrad(const float* direct, int a_ch, int batch, int ph, int pw, const float* gathered,
+                                 int b_ch, int gh, int gw, int k, int stride, int pad, void* workspace,
+                                 size_t workspace_bytes, float* dw, void* stream) {
+  if (!direct || !gathered || !workspace || !dw || batch <= 0 || ph <= 0 || pw <= 0 || gh <= 0 || gw <= 0)
+    return TMVS_ERR_ARG;
+  if (k < 1 || k > 7 || (stride != 1 && stride != 2)) return TMVS_ERR_SHAPE;
+  if (workspace_bytes < tmvs_conv2d_wgrad_workspace(batch, ph, pw, a_ch, b_ch, k)) return TMVS_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const long np = (long)batch * ph * pw;
+  const long ppb = ppb_for(np, 512);
+  const int nblk = (int)((np + ppb - 1) / ppb);
+  double* part = (double*)workspace;
+  int ap = wgrad_ap(a_ch);
+  bool done = false;
+#define TMVS_WG2(AP, BC)                                                                                         \
+  if (!done && ap == AP && b_ch == BC) {                                                                         \
+    hipLaunchKernelGGL((conv2d_wgrad_kernel<AP, BC>), dim3(nblk, k * k), dim3(kBlk), 0, st, direct, a_ch, gathered, \
+                       batch, ph, pw, gh, gw, k, stride, pad, ppb, part);                                        \
+    done = true;                                                                                                 \
+  }
+  TMVS_WG2(8, 8) TMVS_WG2(16, 8) TMVS_WG2(16, 16) TMVS_WG2(32, 8) TMVS_WG2(32, 16) TMVS_WG2(32, 32)
+#undef TMVS_WG2
+  if (!done && a_ch == 8 && b_ch == 3) {
+    hipLaunchKernelGGL((conv2d_wgrad_small_kernel<8, 3>), dim3(nblk, k * k), dim3(kBlk), 0, st, direct, gathered,
+                       batch, ph, pw, gh, gw, k, stride, pad, ppb, part);
+    ap = 8;
+    done = true;
+  }
+  if (!done) return TMVS_ERR_SHAPE;
+  TMVS_CHECK_LAUNCH();
+  // combine [nblk][k*k][ap][b] -> [k*k][a][b] (rows >= a_ch are padding)
+  const long n = (long)k * k * a_ch * b_ch;
+  hipLaunchKernelGGL(sum_partials_rows_kernel, dim3((unsigned)((n + 31) / 32)), dim3(kBlk), 0, st, (const double*)part,
+                     nblk, ap, a_ch, b_ch, n, dw);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+extern "C" size_t tmvs_colsum_workspace(long n, int channels) {
+  const long ppb = ppb_for(n, 1024);
+  return (size_t)((n + ppb - 1) / ppb) * channels * sizeof(double);
+}
+
+extern "C" int tmvs_colsum(const float* x, long n, int channels, void* workspace, size_t workspace_bytes, float* out,
+                           void* stream) {
+  if (!x || !workspace || !out || n <= 0 || channels <= 0 || channels > 32) return TMVS_ERR_ARG;
+  if (workspace_bytes < tmvs_colsum_workspace(n, channels)) return TMVS_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const long ppb = ppb_for(n, 1024);
+  const int nblk = (int)((n + ppb - 1) / ppb);
+  double* part = (double*)workspace;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(nblk), dim3(kBlk), 0, st, x, n, channels, ppb, part);
+  TMVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sum_partials_f32_kernel, dim3((unsigned)((channels + 31) / 32)), dim3(kBlk), 0, st,
+                     (const double*)part, nblk, (long)channels, out);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+extern "C" size_t tmvs_dcn_backward_workspace(int batch, int cout, int height, int width) {
+  const long np = (long)batch * height * width;
+  const long ppb = ppb_for(np, 512);
+  return (size_t)((np + ppb - 1) / ppb) * 9 * cout * 32 * sizeof(double);
+}
+
+extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, const float* w_taps, const float* dy_nhwc,
+                                 int batch, int cin, int cout, int height, int width, void* workspace,
+                                 size_t workspace_bytes, float* dx_nhwc, float* dom_nhwc, float* dw_taps, void* stream) {
+  if (!x_nhwc || !offset_mask || !w_taps || !dy_nhwc || !workspace || !dx_nhwc || !dom_nhwc || !dw_taps)
+    return TMVS_ERR_ARG;
+  if (batch <= 0 || height <= 0 || width <= 0) return TMVS_ERR_ARG;
+  if (cin != 32 || (cout != 8 && cout != 16 && cout != 32)) return TMVS_ERR_SHAPE;
+  if (workspace_bytes < tmvs_dcn_backward_workspace(batch, cout, height, width)) return TMVS_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned nbd = (unsigned)(batch * ((height + dbw::TY - 1) / dbw::TY) * ((width + dbw::TX - 1) / dbw::TX));
+  const long np = (long)batch * height * width;
+  const long ppb = ppb_for(np, 512);
+  const int nblk = (int)((np + ppb - 1) / ppb);
+  double* part = (double*)workspace;
+#define TMVS_DCNB(CO)                                                                                             \
+  case CO:                                                                                                        \
+    hipLaunchKernelGGL(dcn_bwd_data_kernel<CO>, dim3(nbd), dim3(kBlk), 0, st, x_nhwc, offset_mask, w_taps, dy_nhwc, \
+                       batch, height, width, dx_nhwc, dom_nhwc);                                                  \
+    TMVS_CHECK_LAUNCH();                                                                                          \
+    hipLaunchKernelGGL(dcn_bwd_weight_kernel<CO>, dim3(nblk, 9), dim3(kBlk), 0, st, x_nhwc, offset_mask, dy_nhwc,   \
+                       batch, height, width, ppb, part);                                                          \
+    break;
+  switch (cout) {
+    TMVS_DCNB(8)
+    TMVS_DCNB(16)
+    TMVS_DCNB(32)
+  }
+#undef TMVS_DCNB
+  TMVS_CHECK_LAUNCH();
+  const long n = 9L * cout * 32;
+  hipLaunchKernelGGL(sum_partials_f32_kernel, dim3((unsigned)((n + 31) / 32)), dim3(kBlk), 0, st, (const double*)part,
+                     nblk, n, dw_taps);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+extern "C" int tmvs_nearest_up2_backward_nhwc(const float* d, int n, int h, int w, int channels, int accumulate,
+                                              float* dprev, void* stream) {
+  if (!d || !dprev || n <= 0 || h <= 0 || w <= 0 || channels <= 0) return TMVS_ERR_ARG;
+  const long tot = (long)n * h * w * channels;
+  hipLaunchKernelGGL(nearest_up2_bwd_kernel, dim3((unsigned)((tot + kBlk - 1) / kBlk)), dim3(kBlk), 0,
+                     (hipStream_t)stream, d, n, h, w, channels, accumulate, dprev);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+extern "C" int tmvs_softmax_backward(const float* prob, const float* dprob, int batch, int ndepth, int height, int width,
+                                     float* dlogits, void* stream) {
+  if (!prob || !dprob || !dlogits || batch <= 0 || ndepth <= 0 || height <= 0 || width <= 0) return TMVS_ERR_ARG;
+  const long HW = (long)height * width;
+  hipLaunchKernelGGL(softmax_bwd_kernel, dim3((unsigned)((batch * HW + kBlk - 1) / kBlk)), dim3(kBlk), 0,
+                     (hipStream_t)stream, prob, dprob, batch, ndepth, HW, dlogits);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}

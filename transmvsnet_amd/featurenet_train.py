@@ -1,0 +1,253 @@
+"""FeatureNet in train mode with its backward on HIP.
+
+``featurenet_train(fnet, imgs)`` is FeatureNet.forward (models/module.py:399-422) of one sample's N
+views [N,3,H,W] with every BatchNorm in train mode, as the reference runs it inside train_sample
+(finetune.py:144-168: ``model.train()``; the reference calls FeatureNet once per view,
+models/TransMVSNet.py:151-153, so batch statistics are per view and each BatchNorm's running
+statistics are updated once per view, in view order, momentum 0.1, unbiased variance). Returns the
+stage features NCHW (stage1 [N,32,H/4,W/4], stage2 [N,16,H/2,W/2], stage3 [N,8,H,W]),
+differentiable w.r.t. every FeatureNet parameter (the image needs no gradient).
+
+Forward: the inference kernels without their folded BatchNorm -- tmvs_conv2d_bn_relu (trunk and the
+stage-1 head's 1x1), tmvs_conv3x3_nhwc (stage-2/3 heads' 3x3), tmvs_fpn_merge, and each DCN as ONE
+tmvs_dcn_forward_train launch (offset/mask conv + deformable conv, also writing the offset/mask
+tensor for the backward) -- then tmvs_bn_stats / tmvs_bn_relu_train per view.
+Backward (csrc/featurenet_train.hip + the BatchNorm kernels of costreg_train.hip): per layer in
+reverse, tmvs_bn_relu_backward per view, weight gradients tmvs_conv2d_wgrad, data gradients
+tmvs_conv2d_generic (transposed gathers), the DCN by tmvs_dcn_backward (dcol, d offsets / d mask
+logits, dW, the bilinear scatter into dx) followed by its offset/mask conv's gradients, bias
+gradients tmvs_colsum, the FPN merges' nearest x2 adjoint tmvs_nearest_up2_backward_nhwc.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+BN_MOMENTUM = 0.1
+
+
+def _taps(w):
+    """Conv2d weight [Co][Ci][k][k] -> [k*k][Co][Ci] (the forward gather)."""
+    co, ci, k, _ = w.shape
+    return w.detach().float().permute(2, 3, 0, 1).reshape(k * k, co, ci).contiguous()
+
+
+def _taps_t(w):
+    """[Co][Ci][k][k] -> [k*k][Ci][Co] (the data gradient's transposed gather)."""
+    co, ci, k, _ = w.shape
+    return w.detach().float().permute(2, 3, 1, 0).reshape(k * k, ci, co).contiguous()
+
+
+def _untaps(dw, shape):
+    """[k*k][Co][Ci] -> [Co][Ci][k][k]."""
+    co, ci, k, _ = shape
+    return dw.reshape(k, k, co, ci).permute(2, 3, 0, 1).contiguous()
+
+
+class _Tape:
+    """What the forward keeps for the backward, and the BatchNorm statistics per view."""
+
+    def __init__(self, n_views):
+        self.n = n_views
+        self.stats = []  # (bn module, [(mean, var)] per view, pixels per view)
+
+
+def _bn_relu_views(tape, z, bn):
+    """relu(BatchNorm_train(z)) with statistics per view (z [N,h,w,C] NHWC)."""
+    y = torch.empty_like(z)
+    per = []
+    for v in range(tape.n):
+        mean, var = ops.bn_stats(z[v])
+        y[v] = ops.bn_relu_train(z[v], mean, var, bn.weight.detach(), bn.bias.detach(), bn.eps)
+        per.append((mean, var))
+    tape.stats.append((bn, per, z.shape[1] * z.shape[2]))
+    return y, per
+
+
+def _bn_relu_views_backward(dy, z, per, bn):
+    dz = torch.empty_like(z)
+    dg = db = None
+    for v, (mean, var) in enumerate(per):
+        dzv, dgv, dbv = ops.bn_relu_backward(dy[v].contiguous(), z[v], mean, var, bn.weight.detach(), bn.bias.detach(),
+                                             bn.eps)
+        dz[v] = dzv
+        dg = dgv if dg is None else dg + dgv
+        db = dbv if db is None else db + dbv
+    return dz, dg, db
+
+
+# ------------------------------------------------------------------------- layers: forward records
+def _block_fwd(tape, blk, x, k, stride, nchw_input=False, head3x3=False):
+    """Conv2d (no bias) + BatchNorm (train) + ReLU (models/module.py:24-61) -> (y NHWC, record)."""
+    w = blk.conv.weight
+    cout = w.shape[0]
+    if head3x3:
+        _, z = ops.conv3x3_nhwc(x, ops.deform_conv2d_pack(w).to(x.device), bn=None, relu=False)
+    else:
+        z = ops.conv2d_bn_relu(x, ops.conv2d_pack(w).to(x.device), cout, k, stride, bn=None, relu=False,
+                               nchw_input=nchw_input)
+    y, per = _bn_relu_views(tape, z, blk.bn)
+    return y, ("block", blk, x, z, per, k, stride, nchw_input)
+
+
+def _dcn_fwd(dcn, x, want_nchw=False):
+    com = dcn.conv_offset_mask
+    u, om, out = ops.dcn_forward_train(x, ops.deform_conv2d_pack(com.weight).to(x.device),
+                                       com.bias.detach().float().contiguous(),
+                                       ops.deform_conv2d_pack(dcn.weight).to(x.device),
+                                       dcn.bias.detach().float().contiguous(), dcn.cout, want_nchw=want_nchw)
+    return u, om, out
+
+
+def _head_fwd(tape, seq, x, first_k):
+    """out{1,2,3} (models/module.py:362-395): block, DCN-BN-ReLU, DCN-BN-ReLU, DCN -> NCHW output."""
+    h0, r0 = _block_fwd(tape, seq[0], x, first_k, 1, head3x3=first_k == 3)
+    u1, om1, _ = _dcn_fwd(seq[1], h0)
+    h1, p1 = _bn_relu_views(tape, u1, seq[2])
+    u2, om2, _ = _dcn_fwd(seq[4], h1)
+    h2, p2 = _bn_relu_views(tape, u2, seq[5])
+    _, om3, out = _dcn_fwd(seq[7], h2, want_nchw=True)
+    return out, ("head", seq, r0, (h0, om1, u1, p1), (h1, om2, u2, p2), (h2, om3))
+
+
+# ------------------------------------------------------------------------- layers: backward
+def _acc(grads, p, g):
+    grads[id(p)] = g if id(p) not in grads else grads[id(p)] + g
+
+
+def _block_bwd(rec, dy, grads, need_dx=True):
+    _, blk, x, z, per, k, stride, nchw_input = rec
+    dz, dg, db = _bn_relu_views_backward(dy, z, per, blk.bn)
+    _acc(grads, blk.bn.weight, dg)
+    _acc(grads, blk.bn.bias, db)
+    w = blk.conv.weight
+    pad = k // 2
+    xg = x.permute(0, 2, 3, 1).contiguous() if nchw_input else x
+    _acc(grads, w, _untaps(ops.conv2d_wgrad(dz, xg, k, stride, pad), w.shape))
+    if not need_dx:
+        return None
+    return ops.conv2d_generic(dz, _taps_t(w), w.shape[1], (xg.shape[1], xg.shape[2]), k, stride, pad, transposed=True)
+
+
+def _dcn_bwd(dcn, x, om, dy, grads):
+    """DCN.forward's backward: (dcol, d offsets / mask logits, dW, dx scatter) then the offset/mask
+    conv (3x3, 32 -> 27, bias). Returns dx [N,h,w,32]."""
+    w = dcn.weight
+    cout = w.shape[0]
+    dx = torch.zeros_like(x)
+    w_taps = w.detach().float().reshape(cout, 32, 9).permute(2, 0, 1).contiguous()
+    dom, dw = ops.dcn_backward(x, om, w_taps, dy, dx)
+    _acc(grads, w, dw.permute(1, 2, 0).reshape(cout, 32, 3, 3).contiguous())
+    _acc(grads, dcn.bias, ops.colsum(dy))
+    com = dcn.conv_offset_mask
+    _acc(grads, com.weight, _untaps(ops.conv2d_wgrad(dom, x, 3, 1, 1), com.weight.shape))
+    _acc(grads, com.bias, ops.colsum(dom))
+    ops.conv2d_generic(dom, _taps_t(com.weight), 32, (x.shape[1], x.shape[2]), 3, 1, 1, transposed=True, out=dx)
+    return dx
+
+
+def _head_bwd(rec, dout_nchw, grads):
+    _, seq, r0, (h0, om1, u1, p1), (h1, om2, u2, p2), (h2, om3) = rec
+    dy3 = dout_nchw.permute(0, 2, 3, 1).contiguous()
+    dh2 = _dcn_bwd(seq[7], h2, om3, dy3, grads)
+    du2, dg, db = _bn_relu_views_backward(dh2, u2, p2, seq[5])
+    _acc(grads, seq[5].weight, dg)
+    _acc(grads, seq[5].bias, db)
+    dh1 = _dcn_bwd(seq[4], h1, om2, du2, grads)
+    du1, dg, db = _bn_relu_views_backward(dh1, u1, p1, seq[2])
+    _acc(grads, seq[2].weight, dg)
+    _acc(grads, seq[2].bias, db)
+    dh0 = _dcn_bwd(seq[1], h0, om1, du1, grads)
+    return _block_bwd(r0, dh0, grads)
+
+
+def _inner_bwd(conv, d, lat, grads):
+    """inner{1,2} = Conv2d(cl, 32, 1, bias) of the FPN merge: grads, and d lat [N,h,w,cl]."""
+    w = conv.weight
+    _acc(grads, w, _untaps(ops.conv2d_wgrad(d, lat, 1, 1, 0), w.shape))
+    _acc(grads, conv.bias, ops.colsum(d))
+    return ops.conv2d_generic(d, _taps_t(w), w.shape[1], (lat.shape[1], lat.shape[2]), 1, 1, 0)
+
+
+class _FeatureNetTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, imgs, fnet, tape, *params):
+        x = imgs.float().contiguous()
+        c00, r00 = _block_fwd(tape, fnet.conv0[0], x, 3, 1, nchw_input=True)
+        conv0, r01 = _block_fwd(tape, fnet.conv0[1], c00, 3, 1)
+        c10, r10 = _block_fwd(tape, fnet.conv1[0], conv0, 5, 2)
+        c11, r11 = _block_fwd(tape, fnet.conv1[1], c10, 3, 1)
+        conv1, r12 = _block_fwd(tape, fnet.conv1[2], c11, 3, 1)
+        c20, r20 = _block_fwd(tape, fnet.conv2[0], conv1, 5, 2)
+        c21, r21 = _block_fwd(tape, fnet.conv2[1], c20, 3, 1)
+        conv2, r22 = _block_fwd(tape, fnet.conv2[2], c21, 3, 1)
+        s1, h1 = _head_fwd(tape, fnet.out1, conv2, 1)
+        intra1 = ops.fpn_merge(conv2, conv1, *fnet._inner(fnet.inner1, conv2.device))
+        s2, h2 = _head_fwd(tape, fnet.out2, intra1, 3)
+        intra2 = ops.fpn_merge(intra1, conv0, *fnet._inner(fnet.inner2, conv2.device))
+        s3, h3 = _head_fwd(tape, fnet.out3, intra2, 3)
+        ctx.recs = (r00, r01, r10, r11, r12, r20, r21, r22, h1, h2, h3)
+        ctx.lat = (conv0, conv1)
+        ctx.fnet = fnet
+        ctx.param_ids = [id(p) for p in params]
+        return s1, s2, s3
+
+    @staticmethod
+    def backward(ctx, d1, d2, d3):
+        r00, r01, r10, r11, r12, r20, r21, r22, h1, h2, h3 = ctx.recs
+        conv0, conv1 = ctx.lat
+        fnet = ctx.fnet
+        grads = {}
+        # out3 head on intra2 = up2(intra1) + inner2(conv0)
+        dconv0 = dintra1 = None
+        if d3 is not None:
+            dintra2 = _head_bwd(h3, d3, grads)
+            dintra1 = ops.nearest_up2_backward_nhwc(dintra2)
+            dconv0 = _inner_bwd(fnet.inner2, dintra2, conv0, grads)
+        # out2 head on intra1 = up2(conv2) + inner1(conv1)
+        if d2 is not None:
+            dh = _head_bwd(h2, d2, grads)
+            dintra1 = dh if dintra1 is None else dintra1.add_(dh)
+        dconv2 = dconv1 = None
+        if dintra1 is not None:
+            dconv2 = ops.nearest_up2_backward_nhwc(dintra1)
+            dconv1 = _inner_bwd(fnet.inner1, dintra1, conv1, grads)
+        if d1 is not None:
+            dh = _head_bwd(h1, d1, grads)
+            dconv2 = dh if dconv2 is None else dconv2.add_(dh)
+        # trunk, in reverse; gradients meeting at conv1 / conv0 are summed
+        if dconv2 is None:
+            dconv2 = torch.zeros_like(r22[3])
+        d = _block_bwd(r22, dconv2, grads)
+        d = _block_bwd(r21, d, grads)
+        d = _block_bwd(r20, d, grads)
+        d = d if dconv1 is None else d.add_(dconv1)
+        d = _block_bwd(r12, d, grads)
+        d = _block_bwd(r11, d, grads)
+        d = _block_bwd(r10, d, grads)
+        d = d if dconv0 is None else d.add_(dconv0)
+        d = _block_bwd(r01, d, grads)
+        _block_bwd(r00, d, grads, need_dx=False)
+        return (None, None, None, *[grads.get(i) for i in ctx.param_ids])
+
+
+def featurenet_train(fnet, imgs):
+    """FeatureNet.forward in train mode for one sample's views imgs [N,3,H,W] -> (stage1, stage2, stage3)
+    NCHW, differentiable w.r.t. fnet's parameters; updates the BatchNorm running statistics per view
+    as the reference's per-view calls do."""
+    if not imgs.is_cuda:
+        raise RuntimeError("featurenet_train runs on the GPU only (no CPU fallback)")
+    if imgs.dim() != 4 or imgs.shape[1] != 3:
+        raise ValueError("featurenet_train: imgs must be [N, 3, H, W] (one sample's views)")
+    tape = _Tape(imgs.shape[0])
+    params = list(fnet.parameters())
+    with torch.cuda.device(imgs.device):
+        s1, s2, s3 = _FeatureNetTrain.apply(imgs, fnet, tape, *params)
+        with torch.no_grad():
+            for bn, per, n in tape.stats:
+                for mean, var in per:  # views in order, as the reference's per-view calls
+                    bn.running_mean.mul_(1.0 - BN_MOMENTUM).add_(mean, alpha=BN_MOMENTUM)
+                    bn.running_var.mul_(1.0 - BN_MOMENTUM).add_(var * (n / max(n - 1, 1)), alpha=BN_MOMENTUM)
+                    bn.num_batches_tracked.add_(1)
+    return s1, s2, s3

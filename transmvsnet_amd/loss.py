@@ -1,7 +1,9 @@
 """Training losses, reference names and return values, on the HIP kernels
-of csrc/loss.hip. The HIP path has no autograd: instead of a graph, each stage's gradient of the
-total loss w.r.t. its CostRegNet logits (prob_volume = softmax(logits), models/TransMVSNet.py) is
-returned by the same pass -- the seed of the backward chain.
+of csrc/loss.hip. Each stage's gradient of the total loss w.r.t. its CostRegNet logits
+(prob_volume = softmax(logits), models/TransMVSNet.py) comes from the same pass as the loss: with
+return_grad=True it is returned (the seed of a backward chain), and when the outputs come from a
+train-mode TransMVSNet.forward (their prob_volume carries its logits) the returned total loss is
+connected to those logits, so ``loss.backward()`` works as in the reference's train_sample.
 
   entropy_loss      models/module.py:495-529
   trans_mvsnet_loss models/module.py:532-556 (train.py: dlossw default 0.5,1.0,2.0)
@@ -33,7 +35,46 @@ def _stage_keys(inputs):
     return [k for k in inputs.keys() if "stage" in k]
 
 
+class _AttachLogitGrads(torch.autograd.Function):
+    """total (no graph) -> the same value whose backward hands each stage's logits its precomputed
+    d total / d logits (scaled by the incoming gradient)."""
+
+    @staticmethod
+    def forward(ctx, total, *logits_and_grads):
+        n = len(logits_and_grads) // 2
+        ctx.n = n
+        ctx.save_for_backward(*logits_and_grads[n:])
+        return total.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return (None, *[gr * g for gr in ctx.saved_tensors], *([None] * ctx.n))
+
+
+def _graph_logits(inputs):
+    """{stage: logits} when every stage's prob_volume comes from a train-mode forward, else None."""
+    if not torch.is_grad_enabled():
+        return None
+    out = {}
+    for key in _stage_keys(inputs):
+        lg = getattr(inputs[key]["prob_volume"], "_tmvs_logits", None)
+        if lg is None or not lg.requires_grad:
+            return None
+        out[key] = lg
+    return out
+
+
 def _stage_losses(inputs, depth_gt_ms, mask_ms, dlossw, want_grad):
+    logits = _graph_logits(inputs)
+    total, depth_loss, total_entropy, depth_entropy, grads = _stage_values(inputs, depth_gt_ms, mask_ms, dlossw,
+                                                                           want_grad or logits is not None)
+    if logits is not None:
+        keys = list(logits)
+        total = _AttachLogitGrads.apply(total, *[logits[k] for k in keys], *[grads[k] for k in keys])
+    return total, depth_loss, total_entropy, depth_entropy, grads
+
+
+def _stage_values(inputs, depth_gt_ms, mask_ms, dlossw, want_grad):
     total = torch.zeros((), device=mask_ms["stage1"].device)
     total_entropy = torch.zeros((), device=mask_ms["stage1"].device)
     grads, depth_loss, depth_entropy = {}, None, None

@@ -301,7 +301,14 @@ class TransMVSNet(nn.Module):
     # --------------------------------------------------------- forward
     def forward(self, imgs, proj_matrix, depth_values):
         """models/TransMVSNet.py:141-226. FeatureNet runs once over all B*N views (the reference
-        loops over views, :151-153; eval BatchNorm is per sample, so batching is exact)."""
+        loops over views, :151-153; eval BatchNorm is per sample, so batching is exact). In train
+        mode (model.train()) the whole forward runs on the HIP training kernels with autograd
+        (transmvsnet_amd.train.forward_train): BatchNorm batch statistics, running statistics
+        updated, gradients to every parameter through loss.backward()."""
+        if self.training:
+            from .train import forward_train
+            self._prep = None  # parameters are about to change: drop the packed inference weights
+            return forward_train(self, imgs, proj_matrix, depth_values)
         self._check_eval()
         b, n = imgs.shape[:2]
         with torch.cuda.device(imgs.device):
@@ -311,8 +318,8 @@ class TransMVSNet(nn.Module):
 
     def _check_eval(self):
         if self.training:
-            raise RuntimeError("transmvsnet_amd.TransMVSNet runs inference only (BatchNorm folded with running "
-                               "statistics); call .eval() first")
+            raise RuntimeError("transmvsnet_amd.TransMVSNet.forward_features runs inference only (BatchNorm folded "
+                               "with running statistics); call .eval() first, or forward() for training")
 
     @staticmethod
     def stack_features(features):

@@ -894,3 +894,114 @@ for _name in ("conv3d_generic", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn
               "linattn_bwd_kv", "adam_step"):
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name
+
+
+# ----------------------------------------------------------------- FeatureNet training (featurenet_train.py)
+def conv2d_generic(x, w_taps, cout, out_hw, k, stride, pad, bias=None, transposed=False, out=None):
+    """tmvs_conv2d_generic: x NHWC [B,H,W,Cin], w_taps [k*k][cout][Cin] -> y [B,*out_hw,cout] (+ bias);
+    accumulated into `out` when given."""
+    _dev(x, "x")
+    _dev(w_taps, "w_taps")
+    _dev(bias, "bias")
+    b, h, w, cin = x.shape
+    flags = (_lib.CONV_TRANSPOSED if transposed else 0) | (_lib.CONV_ACCUMULATE if out is not None else 0)
+    y = torch.empty(b, *out_hw, cout, device=x.device) if out is None else out
+    if tuple(y.shape) != (b, *out_hw, cout) or not y.is_contiguous():
+        raise ValueError("conv2d_generic: out must be a contiguous [B, H, W, cout] tensor")
+    with _Span("tmvs_conv2d_generic"):
+        _lib.check(_lib_h().tmvs_conv2d_generic(_ptr(x), b, cin, h, w, _ptr(w_taps), _ptr(bias), cout, out_hw[0],
+                                                out_hw[1], k, stride, pad, flags, _ptr(y), _stream()),
+                   "tmvs_conv2d_generic")
+    return y
+
+
+def conv2d_wgrad(direct, gathered, k, stride, pad):
+    """tmvs_conv2d_wgrad: direct [B,ph,pw,A] (dz), gathered [B,gh,gw,BC] (x) -> dw [k*k][A][BC]."""
+    _dev(direct, "direct")
+    _dev(gathered, "gathered")
+    b, ph, pw, a = direct.shape
+    _, gh, gw, bc = gathered.shape
+    nbytes = _lib_h().tmvs_conv2d_wgrad_workspace(b, ph, pw, a, bc, k)
+    ws = torch.empty(nbytes // 4 + 64, device=direct.device)
+    dw = torch.empty(k * k, a, bc, device=direct.device)
+    with _Span("tmvs_conv2d_wgrad"):
+        _lib.check(_lib_h().tmvs_conv2d_wgrad(_ptr(direct), a, b, ph, pw, _ptr(gathered), bc, gh, gw, k, stride, pad,
+                                              _ptr(ws), ws.numel() * 4, _ptr(dw), _stream()), "tmvs_conv2d_wgrad")
+    return dw
+
+
+def colsum(x):
+    """tmvs_colsum: x [..., C] -> [C] (sum over every other axis; C <= 32)."""
+    _dev(x, "x")
+    c = x.shape[-1]
+    n = x.numel() // c
+    ws = torch.empty(_lib_h().tmvs_colsum_workspace(n, c) // 4 + 64, device=x.device)
+    out = torch.empty(c, device=x.device)
+    with _Span("tmvs_colsum"):
+        _lib.check(_lib_h().tmvs_colsum(_ptr(x), n, c, _ptr(ws), ws.numel() * 4, _ptr(out), _stream()), "tmvs_colsum")
+    return out
+
+
+def dcn_forward_train(x_nhwc, wom_packed, bom, w_packed, bias, cout, want_nchw=False):
+    """tmvs_dcn_forward_train: DCN.forward without BN/ReLU -> (out_nhwc [B,H,W,cout], offset_mask
+    [B,27,H,W], out_nchw or None)."""
+    for t, n in ((x_nhwc, "x_nhwc"), (wom_packed, "wom_packed"), (bom, "bom"), (w_packed, "w_packed"), (bias, "bias")):
+        _dev(t, n)
+    b, h, w, cin = x_nhwc.shape
+    out_nhwc = torch.empty(b, h, w, cout, device=x_nhwc.device)
+    out = torch.empty(b, cout, h, w, device=x_nhwc.device) if want_nchw else None
+    om = torch.empty(b, 27, h, w, device=x_nhwc.device)
+    with _Span("tmvs_dcn_forward_train"):
+        _lib.check(_lib_h().tmvs_dcn_forward_train(_ptr(x_nhwc), _ptr(wom_packed), _ptr(bom), _ptr(w_packed), _ptr(bias),
+                                                   b, cin, cout, h, w, _ptr(out), _ptr(out_nhwc), _ptr(om), _stream()),
+                   "tmvs_dcn_forward_train")
+    return out_nhwc, om, out
+
+
+def dcn_backward(x_nhwc, offset_mask, w_taps, dy_nhwc, dx_nhwc):
+    """tmvs_dcn_backward: -> (dom [B,H,W,27], dw_taps [9][cout][32]); dx_nhwc is accumulated into."""
+    for t, n in ((x_nhwc, "x_nhwc"), (offset_mask, "offset_mask"), (w_taps, "w_taps"), (dy_nhwc, "dy_nhwc"),
+                 (dx_nhwc, "dx_nhwc")):
+        _dev(t, n)
+    b, h, w, cin = x_nhwc.shape
+    cout = dy_nhwc.shape[-1]
+    if tuple(offset_mask.shape) != (b, 27, h, w) or tuple(dy_nhwc.shape) != (b, h, w, cout) or \
+            tuple(w_taps.shape) != (9, cout, cin) or tuple(dx_nhwc.shape) != tuple(x_nhwc.shape):
+        raise ValueError("dcn_backward: shape mismatch")
+    ws = torch.empty(_lib_h().tmvs_dcn_backward_workspace(b, cout, h, w) // 4 + 64, device=x_nhwc.device)
+    dom = torch.empty(b, h, w, 27, device=x_nhwc.device)
+    dw = torch.empty(9, cout, cin, device=x_nhwc.device)
+    with _Span("tmvs_dcn_backward"):
+        _lib.check(_lib_h().tmvs_dcn_backward(_ptr(x_nhwc), _ptr(offset_mask), _ptr(w_taps), _ptr(dy_nhwc), b, cin, cout,
+                                              h, w, _ptr(ws), ws.numel() * 4, _ptr(dx_nhwc), _ptr(dom), _ptr(dw),
+                                              _stream()), "tmvs_dcn_backward")
+    return dom, dw
+
+
+def nearest_up2_backward_nhwc(d, out=None):
+    """tmvs_nearest_up2_backward_nhwc: d [n,2h,2w,C] -> [n,h,w,C] (accumulated into `out` when given)."""
+    _dev(d, "d")
+    n, h2, w2, c = d.shape
+    y = torch.empty(n, h2 // 2, w2 // 2, c, device=d.device) if out is None else out
+    with _Span("tmvs_nearest_up2_backward_nhwc"):
+        _lib.check(_lib_h().tmvs_nearest_up2_backward_nhwc(_ptr(d), n, h2 // 2, w2 // 2, c, int(out is not None), _ptr(y),
+                                                           _stream()), "tmvs_nearest_up2_backward_nhwc")
+    return y
+
+
+def softmax_backward(prob, dprob):
+    """tmvs_softmax_backward: prob, dprob [B,D,H,W] -> d logits."""
+    _dev(prob, "prob")
+    _dev(dprob, "dprob")
+    b, d, h, w = prob.shape
+    out = torch.empty_like(prob)
+    with _Span("tmvs_softmax_backward"):
+        _lib.check(_lib_h().tmvs_softmax_backward(_ptr(prob), _ptr(dprob), b, d, h, w, _ptr(out), _stream()),
+                   "tmvs_softmax_backward")
+    return out
+
+
+for _name in ("conv2d_generic", "conv2d_wgrad", "colsum", "dcn_forward_train", "dcn_backward",
+              "nearest_up2_backward_nhwc", "softmax_backward"):
+    globals()[_name] = _on_tensor_device(globals()[_name])
+del _name

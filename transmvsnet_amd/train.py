@@ -465,6 +465,63 @@ def aggregate_train(sims, model, vw_given=None, vw_shift=0):
     return sim, vw
 
 
+class _SoftmaxWTA(torch.autograd.Function):
+    """prob = exp(log_softmax(logits)), depth / confidence by WTA (models/TransMVSNet.py:97-103,
+    217-221) on tmvs_softmax_wta; the backward of prob is tmvs_softmax_backward (depth, the raw
+    depth and the confidence carry no gradient, as in the reference)."""
+
+    @staticmethod
+    def forward(ctx, logits, hyp):
+        from .model import DEPTH_CLAMP
+        prob, depth, raw, conf = ops.softmax_wta(logits.detach().contiguous(), hyp, DEPTH_CLAMP)
+        ctx.save_for_backward(prob)
+        ctx.mark_non_differentiable(depth, raw, conf)
+        return prob, depth, raw, conf
+
+    @staticmethod
+    def backward(ctx, dprob, _d, _r, _c):
+        if dprob is None:
+            return None, None
+        (prob,) = ctx.saved_tensors
+        return ops.softmax_backward(prob, dprob.contiguous()), None
+
+
+def depth_stages_forward_train(model, stage_features, proj_matrix, depth_values, img_hw):
+    """The three DepthNet stages of a training forward for ONE sample (B = 1): TransMVSNet.forward's
+    stage loop (models/TransMVSNet.py:168-221) in train mode, returning its output dict (per stage
+    depth / photo_confidence / prob_volume / depth_values, plus the stage-3 keys at the top level).
+    prob_volume is differentiable (through the HIP softmax, CostRegNet, aggregation / PixelwiseNet
+    and cost-volume backward into the stage features); each prob_volume also carries its logits as
+    `_tmvs_logits`, so transmvsnet_amd.loss can seed the backward with d loss / d logits directly.
+
+    stage_features: {stage: [N, h, w, C]} NHWC FMT/pathway outputs, reference view first; proj_matrix
+    {stage: [1, N, 2, 4, 4]}; depth_values [1, 192]. The CostRegNets and the PixelwiseNet run in
+    train mode (their BatchNorm running statistics are updated)."""
+    from .model import STAGE_SCALES
+    dev = stage_features["stage1"].device
+    with torch.cuda.device(dev):
+        dv = depth_values.to(dev, torch.float32).contiguous()
+        outputs, prev_raw, vw_det = {}, None, None
+        for s in range(3):
+            name = f"stage{s + 1}"
+            f = stage_features[name]
+            hyp = ops.stage_hypotheses(dv, prev_raw, model.ndepths[s], model.depth_interals_ratio[s], img_hw,
+                                       STAGE_SCALES[s])
+            rows = ops.proj_rows(proj_matrix[name])[0]
+            sims = warp_corr_views(f[0], f[1:], hyp[0], rows, rot_order=model.warp_rot_order)  # [V,D,h,w]
+            if s == 0:  # TransMVSNet.py:107 returns the stage-1 view weights detached
+                sim, vw_det = aggregate_train(sims, model)
+            else:       # nearest x2 per stage (:194) = reading the stage-1 map at (y >> s, x >> s)
+                sim, _ = aggregate_train(sims, model, vw_det, s)
+            logits = costregnet_train(model.cost_regularization[s].train(), sim.unsqueeze(0))
+            prob, depth, raw, conf = _SoftmaxWTA.apply(logits, hyp)
+            prob._tmvs_logits = logits
+            outputs[name] = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}
+            outputs.update(outputs[name])
+            prev_raw = raw
+    return outputs
+
+
 def depth_stages_train(model, stage_features, proj_matrix, depth_values, depth_gt_ms, mask_ms, img_hw,
                        dlossw=(0.5, 1.0, 2.0), loss="trans_mvsnet", depth_interval=None):
     """One training step's DepthNet stages for ONE sample (B = 1), forward and backward.
@@ -483,34 +540,18 @@ def depth_stages_train(model, stage_features, proj_matrix, depth_values, depth_g
     if loss == "focal_bld" and depth_interval is None:
         raise ValueError("depth_stages_train: focal_bld needs depth_interval")
     from . import loss as loss_mod
-    from .model import DEPTH_CLAMP, STAGE_SCALES
     dev = stage_features["stage1"].device
     with torch.cuda.device(dev):
-        dv = depth_values.to(dev, torch.float32).contiguous()
-        outputs, logits_all, prev_raw, vw_det = {}, [], None, None
-        for s in range(3):
-            name = f"stage{s + 1}"
-            f = stage_features[name]
-            hyp = ops.stage_hypotheses(dv, prev_raw, model.ndepths[s], model.depth_interals_ratio[s], img_hw,
-                                       STAGE_SCALES[s])
-            rows = ops.proj_rows(proj_matrix[name])[0]
-            sims = warp_corr_views(f[0], f[1:], hyp[0], rows, rot_order=model.warp_rot_order)  # [V,D,h,w]
-            if s == 0:  # TransMVSNet.py:107 returns the stage-1 view weights detached
-                sim, vw_det = aggregate_train(sims, model)
-            else:       # nearest x2 per stage (:194) = reading the stage-1 map at (y >> s, x >> s)
-                sim, _ = aggregate_train(sims, model, vw_det, s)
-            logits = costregnet_train(model.cost_regularization[s].train(), sim.unsqueeze(0))
-            prob, depth, raw, conf = ops.softmax_wta(logits.detach(), hyp, DEPTH_CLAMP)
-            outputs[name] = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}
-            logits_all.append(logits)
-            prev_raw = raw
-        if loss == "focal_bld":
-            total, depth_loss, epe, less1, less3, grads = loss_mod.focal_loss_bld(
-                outputs, depth_gt_ms, mask_ms, depth_interval, dlossw=dlossw, return_grad=True)
-            outputs["metrics"] = {"depth_loss": depth_loss, "epe": epe, "less1": less1, "less3": less3}
-        else:
-            total, depth_loss, _, _, grads = loss_mod.trans_mvsnet_loss(outputs, depth_gt_ms, mask_ms, dlossw=dlossw,
-                                                                        return_grad=True)
+        outputs = depth_stages_forward_train(model, stage_features, proj_matrix, depth_values, img_hw)
+        logits_all = [outputs[f"stage{s + 1}"]["prob_volume"]._tmvs_logits for s in range(3)]
+        with torch.no_grad():
+            if loss == "focal_bld":
+                total, depth_loss, epe, less1, less3, grads = loss_mod.focal_loss_bld(
+                    outputs, depth_gt_ms, mask_ms, depth_interval, dlossw=dlossw, return_grad=True)
+                outputs["metrics"] = {"depth_loss": depth_loss, "epe": epe, "less1": less1, "less3": less3}
+            else:
+                total, depth_loss, _, _, grads = loss_mod.trans_mvsnet_loss(outputs, depth_gt_ms, mask_ms,
+                                                                            dlossw=dlossw, return_grad=True)
         global _DEFERRED_FLAGS
         _DEFERRED_FLAGS = []
         try:
@@ -520,6 +561,28 @@ def depth_stages_train(model, stage_features, proj_matrix, depth_values, depth_g
             _DEFERRED_FLAGS = None
         _check_overflow(flags)
     return total, outputs
+
+
+def forward_train(model, imgs, proj_matrix, depth_values):
+    """TransMVSNet.forward (models/TransMVSNet.py:141-226) in train mode, on HIP: FeatureNet
+    (featurenet_train), the FMT (fmt_train), FMT_with_pathway's lateral steps (pathway_train) and the
+    three DepthNet stages (depth_stages_forward_train), every block differentiable through its HIP
+    backward, so the reference's train_sample body (finetune.py:144-168) runs unchanged:
+    ``model.train(); outputs = model(imgs, proj, dv); loss = focal_loss_bld(outputs, ...)[0];
+    loss.backward(); optimizer.step()``. One sample per call (B = 1: C5's DDP runs one sample per
+    rank, finetune.py batch_size 1 per process)."""
+    from .featurenet_train import featurenet_train
+    if imgs.dim() != 5 or imgs.shape[0] != 1:
+        raise ValueError("TransMVSNet train-mode forward takes one sample per call: imgs [1, N, 3, H, W]")
+    if not imgs.is_cuda:
+        raise RuntimeError("TransMVSNet (HIP) needs GPU inputs; the HIP path has no CPU fallback")
+    h, w = imgs.shape[3], imgs.shape[4]
+    with torch.cuda.device(imgs.device):
+        s1, s2, s3 = featurenet_train(model.feature, imgs[0])
+        st1 = fmt_train(model, s1)
+        st2, st3 = pathway_train(model, st1, s2, s3)
+        return depth_stages_forward_train(model, {"stage1": st1, "stage2": st2, "stage3": st3}, proj_matrix,
+                                          depth_values, (h, w))
 
 
 class FlatAdam:
