@@ -1,6 +1,6 @@
 """The HIP training path against the REFERENCE's own training step (tests/golden/train_c1.npz, made by
 tests/golden/make_golden_train.py from /root/reference: finetune.py:144-168's train_sample body at C1
-size, 128x160, N=3, 8/8/8, key-seeded weights). Needs an MI355X (-m gpu).
+size, 128x160, N=3, 8/8/8, key-seeded weights, prob.weight x10). Needs an MI355X (-m gpu).
 
   * from features (case "f"): fmt_train -> pathway_train -> depth_stages_forward_train ->
     transmvsnet_amd.loss.focal_loss_bld(...)[0].backward(): the loss terms, WTA depths, prob volumes,
@@ -18,16 +18,20 @@ size, 128x160, N=3, 8/8/8, key-seeded weights). Needs an MI355X (-m gpu).
 
 Bar: the reference's fp32 numbers are themselves rounded; every gradient is compared with a float64
 evaluation of the same step (the oracle, pinned bit-exact to these fixtures by
-tests/test_train_oracle.py) and must be within max(1e-4, 3x the fp32 reference's own distance from
-it, 2e-3 x the worst such distance over all gradients) of its max magnitude; loss terms within 1e-5
-relative, prob volumes within 1e-4, WTA depths identical, running statistics within 1e-5.
+tests/test_train_oracle.py) and must be within max(1e-4, 2x the fp32 spread) of its max magnitude,
+the fp32 spread being the worst distance from fp64 over the fixture's own fp32 run and 4 fp32 oracle
+runs whose inputs are jittered by ~1 ulp (some gradients are ill-conditioned: at C1 a 2e-7 input
+jitter moves the reference's stage-3 conv5 gradient between 1e-3 and 4e-2 of its magnitude, a ReLU /
+argmax flip away; scripts/diag/train_cond.py, profiles/r09c/); loss terms within 1e-5
+relative, prob volumes within max(1e-4, 3x the fp32 reference's distance from fp64), WTA depths
+identical outside the 1e-4 near-tie margin, running statistics within 1e-5.
 """
 import numpy as np
 import pytest
 import torch
 
 from tests._util import golden_rot, golden_state_dict
-from tests.test_train_oracle import GOLD, H, ND, N, STAGES, train_step_oracle
+from tests.test_train_oracle import GOLD, H, ND, N, STAGES, TRAIN_SHARPEN, train_step_oracle
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -39,24 +43,35 @@ def gold():
         return {k: z[k] for k in z.files}
 
 
+ENSEMBLE = 4  # perturbed fp32 oracle runs per case
+
+
 @pytest.fixture(scope="module")
 def exact():
-    """float64 evaluations of both cases (the CPU oracle)."""
+    """Per case: float64 evaluations (the CPU oracle) and, per gradient, the worst relative distance
+    from them over the fixture's fp32 run and ENSEMBLE fp32 oracle runs with ~1-ulp input jitter."""
     with np.load(GOLD) as z:
         g = {k: z[k] for k in z.files}
+    torch.set_num_threads(min(16, torch.get_num_threads()))
     out = {}
     for case in ("f", "i"):
         res, o, sd, leaves = train_step_oracle(g, case, dtype=torch.float64)
         grads = {k: v.grad.detach().numpy() for k, v in sd.items() if v.requires_grad and v.grad is not None}
         fg = {} if leaves is None else {f"{v}_{k}": t.grad.numpy() for v, f in enumerate(leaves) for k, t in f.items()}
-        out[case] = (grads, fg)
+        prob = {s: o[f"stage{s}"]["prob_volume"].detach().numpy() for s in (1, 2, 3)}
+        spread = {n: _rel(g[f"{case}_grad.{n}"], grads[n]) for n in grads}
+        for e in range(ENSEMBLE):
+            sd_e = train_step_oracle(g, case, perturb_seed=1000 + e)[2]
+            for n in grads:
+                spread[n] = max(spread[n], _rel(sd_e[n].grad.detach().numpy(), grads[n]))
+        out[case] = (grads, fg, prob, spread)
     return out
 
 
 def _model():
     from transmvsnet_amd import TransMVSNet
     m = TransMVSNet(ndepths=list(ND))
-    m.load_state_dict(golden_state_dict(), strict=True)
+    m.load_state_dict(golden_state_dict(sharpen=TRAIN_SHARPEN), strict=True)
     return m.to(DEV)
 
 
@@ -72,36 +87,58 @@ def _rel(a, b):
     return float(np.abs(a - b).max()) / max(float(np.abs(b).max()), 1e-30)
 
 
-def _judge(gold, exact_grads, case, got):
-    """got: {name: gradient (numpy)} -> report; asserts the module docstring's bar."""
+def _judge(gold, ex, case, got):
+    """got: {name: gradient (numpy)} -> report; asserts the module docstring's bar.
+
+    A gradient that is zero in exact arithmetic (a bias feeding a train-mode BatchNorm: the batch
+    mean removes it, e.g. feature.out*.{1,4}.bias) has no relative scale: it is judged in absolute
+    terms, within 3x the fp32 reference's own absolute noise, and kept out of the shared bar."""
+    exact_grads, spread = ex[0], ex[3]
     pfx = f"{case}_grad."
     names = sorted(k[len(pfx):] for k in gold if k.startswith(pfx))
     missing = [n for n in names if n not in got]
     assert not missing, f"no gradient for {missing[:8]} ({len(missing)} of {len(names)})"
-    ref_err = {n: _rel(gold[pfx + n], exact_grads[n]) for n in names}
-    worst_ref = max(ref_err.values())
+    scale = float(np.median([np.abs(exact_grads[n]).max() for n in names]))
+    degenerate = {n for n in names if float(np.abs(exact_grads[n]).max()) < 1e-7 * scale}
     rows = []
     for n in names:
+        if n in degenerate:
+            e = float(np.abs(np.asarray(got[n], np.float64) - exact_grads[n]).max())
+            f = float(np.abs(gold[pfx + n].astype(np.float64) - exact_grads[n]).max())
+            assert e <= max(3.0 * f, 1e-7 * scale), (n, "exactly-zero gradient", e, f)
+            continue
         e = _rel(got[n], exact_grads[n])
-        bar = max(1e-4, 3.0 * ref_err[n], 2e-3 * worst_ref)
-        rows.append((e / bar, n, e, ref_err[n]))
+        bar = max(1e-4, 2.0 * spread[n])
+        rows.append((e / bar, n, e, spread[n]))
     rows.sort(reverse=True)
-    print(f"{case}: worst gradient errors vs fp64 (ratio to bar, name, gpu, fp32 reference):",
-          [(f"{r:.2f}", n, f"{e:.1e}", f"{f:.1e}") for r, n, e, f in rows[:6]])
+    print(f"{case}: {len(rows)} gradients (+{len(degenerate)} exactly zero in fp64); worst errors vs fp64 "
+          f"(ratio to bar, name, gpu, fp32 spread):", [(f"{r:.2f}", n, f"{e:.1e}", f"{f:.1e}") for r, n, e, f in
+                                                     rows[:8]])
     bad = [(n, e, f) for r, n, e, f in rows if r > 1.0]
     assert not bad, bad[:10]
 
 
-def _check_outputs(gold, case, outputs, loss_terms):
+def _check_outputs(gold, case, outputs, loss_terms, exact_prob):
     for name, v in zip(("loss", "depth_loss", "epe", "less1", "less3"), loss_terms):
         ref = float(gold[f"{case}_{name}"])
         assert abs(float(v) - ref) <= 1e-5 * max(abs(ref), 1.0), (name, float(v), ref)
+    rep = {}
     for s in (1, 2, 3):
         o = outputs[f"stage{s}"]
         np.testing.assert_array_equal(o["depth_values"].detach().cpu().numpy(), gold[f"{case}_stage{s}_hyp"])
-        dp = float(np.abs(o["prob_volume"].detach().cpu().numpy() - gold[f"{case}_stage{s}_prob"]).max())
-        assert dp < 1e-4, (s, dp)
-        np.testing.assert_array_equal(o["depth"].detach().cpu().numpy(), gold[f"{case}_stage{s}_depth"])
+        ref = gold[f"{case}_stage{s}_prob"].astype(np.float64)
+        # WTA depth identical except where the reference's top-2 log-prob margin is a near tie (SURVEY 8c)
+        srt = np.sort(ref, axis=1)
+        near = (np.log(np.maximum(srt[:, -1], 1e-30)) - np.log(np.maximum(srt[:, -2], 1e-30))) < 1e-4
+        diff = o["depth"].detach().cpu().numpy() != gold[f"{case}_stage{s}_depth"]
+        assert not (diff & ~near).any(), (s, int(diff.sum()), int((diff & ~near).sum()))
+        # prob volumes: against float64, within 3x the fp32 reference's own distance (or 1e-4)
+        ex = exact_prob[s]
+        e_gpu = float(np.abs(o["prob_volume"].detach().cpu().numpy() - ex).max())
+        e_ref = float(np.abs(ref - ex).max())
+        rep[s] = (e_gpu, e_ref)
+        assert e_gpu <= max(1e-4, 3.0 * e_ref), (s, e_gpu, e_ref)
+    print(case, "prob vs fp64 per stage (gpu, fp32 reference):", rep)
 
 
 def _check_buffers(gold, case, model):
@@ -137,9 +174,9 @@ def test_train_step_from_features_vs_reference(gold, exact):
                                         dlossw=[1.0, 1.0, 1.0])
         terms[0].backward()
     torch.cuda.synchronize()
-    _check_outputs(gold, "f", outputs, terms)
+    _check_outputs(gold, "f", outputs, terms, exact["f"][2])
     got = {n: p.grad.detach().cpu().numpy() for n, p in model.named_parameters() if p.grad is not None}
-    _judge(gold, exact["f"][0], "f", got)
+    _judge(gold, exact["f"], "f", got)
     ref_fg = exact["f"][1]
     for k in STAGES:
         g = leaves[k].grad.detach().cpu().numpy()
@@ -176,8 +213,8 @@ def test_train_sample_unchanged_body_vs_reference(gold, exact, loss_impl):
         grads = {n: p.grad.detach().cpu().numpy().copy() for n, p in model.named_parameters() if p.grad is not None}
         optimizer.step()
     torch.cuda.synchronize()
-    _check_outputs(gold, "i", outputs, (loss, depth_loss, epe, less1, less3))
-    _judge(gold, exact["i"][0], "i", grads)
+    _check_outputs(gold, "i", outputs, (loss, depth_loss, epe, less1, less3), exact["i"][2])
+    _judge(gold, exact["i"], "i", grads)
     _check_buffers(gold, "i", model)
     # the step moved every parameter that has a gradient, and eval mode sees the new weights
     model.eval()

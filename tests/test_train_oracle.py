@@ -21,6 +21,7 @@ from transmvsnet_amd import synthetic
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden", "train_c1.npz")
 H, W, N, ND = 128, 160, 3, (8, 8, 8)
+TRAIN_SHARPEN = 10.0  # tests/golden/make_golden_train.py
 STAGES = ("stage1", "stage2", "stage3")
 
 
@@ -34,13 +35,24 @@ def _is_buffer(k):
     return k.endswith(("running_mean", "running_var", "num_batches_tracked"))
 
 
-def train_step_oracle(gold, case, sd=None, dtype=torch.float32):
+def train_step_oracle(gold, case, sd=None, dtype=torch.float32, perturb_seed=None):
     """The reference train_sample body through the oracle: returns (loss terms, outputs, sd, feature
     leaves or None). Parameters are autograd leaves of the returned sd (their .grad set); buffers are
     updated in place. dtype=torch.float64 evaluates the same step in double precision (the exact
-    value the fp32 reference and the GPU are both judged against)."""
+    value the fp32 reference and the GPU are both judged against). perturb_seed: the inputs (images
+    or features) multiplied by 1 + 2e-7 * N(0, 1) (about one fp32 ulp) -- an ensemble of such runs
+    measures how far fp32 rounding alone moves each gradient (ReLU / argmax flips make some of them
+    ill-conditioned: the spread is much wider than one run's error suggests)."""
     cast = (lambda t: t.to(dtype) if t.is_floating_point() else t)  # noqa: E731
-    sd = {k: cast(v.clone()) for k, v in (sd or golden_state_dict()).items()}
+    if perturb_seed is not None:
+        gen = torch.Generator().manual_seed(int(perturb_seed))
+
+        def jitter(t):
+            return (t * (1 + 2e-7 * torch.randn(t.shape, generator=gen, dtype=torch.float64))).to(t.dtype)
+    else:
+        def jitter(t):
+            return t
+    sd = {k: cast(v.clone()) for k, v in (sd or golden_state_dict(sharpen=TRAIN_SHARPEN)).items()}
     for k, v in sd.items():
         if v.is_floating_point() and not _is_buffer(k):
             v.requires_grad_(True)
@@ -50,11 +62,11 @@ def train_step_oracle(gold, case, sd=None, dtype=torch.float32):
     mask = {s: cast(torch.from_numpy(gold[f"mask_{s}"])) for s in STAGES}
     leaves = None
     if case == "f":
-        leaves = [{k: cast(v).clone().requires_grad_(True) for k, v in f.items()}
+        leaves = [{k: cast(jitter(v)).clone().requires_grad_(True) for k, v in f.items()}
                   for f in synthetic.synthetic_features(N, H, W, seed=2)]
         out = oracle.forward_from_features(sd, leaves, proj, dv, (H, W), ndepths=ND, training=True)
     else:
-        imgs = cast(synthetic.synthetic_images(N, H, W, seed=0))
+        imgs = cast(jitter(synthetic.synthetic_images(N, H, W, seed=0)))
         out = oracle.forward(sd, imgs, proj, dv, ndepths=ND, training=True)
     interval = cast(torch.from_numpy(gold[f"{case}_interval"]))
     res = loss_ref.focal_loss_bld(out, gt, mask, interval, dlossw=[1.0, 1.0, 1.0])
