@@ -460,7 +460,8 @@ int tmvs_depth_metrics(const float* depth, const float* depth_gt, const float* m
  *   x_nhwc [B][H][W][32], offset_mask [B][27][H][W], w_taps [9][cout][32] (the weight [cout][32][3][3]
  *   as [tap][co][ci]):
  *     dx_nhwc  [B][H][W][32]  += the bilinear scatter of mask * dcol (fp32 atomics, as torchvision)
- *     dom_nhwc [B][H][W][27]   = d offsets (channels 2k, 2k+1) and d mask logits (18 + k)
+ *     dom_nhwc [B][H][W][32]   = d offsets (channels 2k, 2k+1) and d mask logits (18 + k); channels
+ *                                27..31 are written 0 (aligned rows for the offset/mask conv's gradients)
  *     dw_taps  [9][cout][32]   = the weight gradient (the bias gradient is tmvs_colsum of dy).
  *   cout in {8, 16, 32}. The offset/mask conv's gradients are tmvs_conv2d_wgrad / _generic of dom.
  * tmvs_nearest_up2_backward_nhwc: dprev [n][h][w][C] (+)= the 2x2 sums of d [n][2h][2w][C] (the

@@ -211,3 +211,19 @@ def test_every_launching_op_is_device_guarded():
         if "_stream()" in src and not getattr(fn, "device_guarded", False):
             missing.append(name)
     assert not missing, missing
+
+
+def test_training_device_packs_equal_host_packs():
+    """featurenet_train packs weights on the device (no host sync per step) with index gathers that
+    must reproduce the host packers tmvs_conv2d_pack / tmvs_deform_conv2d_pack bit for bit."""
+    import torch
+
+    from transmvsnet_amd import ops
+    from transmvsnet_amd.featurenet_train import device_pack
+    g = torch.Generator().manual_seed(0)
+    for co, ci, k in ((8, 3, 3), (8, 8, 3), (16, 8, 5), (16, 16, 3), (32, 16, 5), (32, 32, 3), (32, 32, 1)):
+        w = torch.randn(co, ci, k, k, generator=g)
+        assert torch.equal(ops.conv2d_pack(w), device_pack("conv2d", w)), (co, ci, k)
+    for co in (8, 16, 27, 32):
+        w = torch.randn(co, 32, 3, 3, generator=g)
+        assert torch.equal(ops.deform_conv2d_pack(w), device_pack("dcn", w)), co

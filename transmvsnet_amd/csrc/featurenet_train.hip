@@ -353,17 +353,15 @@ constexpr int CC = 8;                   // channels per pass
 constexpr int WR = TY + 2 * R + 3, WC = TX + 2 * R + 3;
 }  // namespace dbw
 
-// dcol, d om (NHWC [B][H][W][27]) and the scatter of m * dcol into dx (accumulated)
+// dcol, d om (NHWC [B][H][W][32], channels 27..31 zero) and the scatter of m * dcol into dx (accumulated)
 template <int CO>
 __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ om,
                                                            const float* __restrict__ wt, const float* __restrict__ dy,
                                                            int B, int H, int W, float* __restrict__ dx,
                                                            float* __restrict__ dom) {
   using namespace dbw;
-  __shared__ float wl[9 * CO * 32];
   __shared__ float win[WR * WC * CC];
   const int tid = threadIdx.x;
-  for (int i = tid; i < 9 * CO * 32; i += kBlk) wl[i] = wt[i];
   const int ntx = (W + TX - 1) / TX, nty = (H + TY - 1) / TY;
   int blk = blockIdx.x;
   const int bx = blk % ntx;
@@ -398,14 +396,15 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
       for (int k = 0; k < 9; ++k) {
         const DcnSample s = dcn_sample(omp, HW, y, xq, k, H, W);
         if (!s.inside) continue;  // the column is 0 and carries no gradient (torchvision)
+        // dcol: the tap's weights are block-uniform -- scalar loads, SGPR operands of the FMAs
+        const float* wk = wt + (size_t)k * CO * 32 + cc * CC;
         float dc[CC];
 #pragma unroll
-        for (int c = 0; c < CC; ++c) {
-          float a = 0.f;
+        for (int c = 0; c < CC; ++c) dc[c] = 0.f;
 #pragma unroll
-          for (int o = 0; o < CO; ++o) a = fmaf(g[o], wl[(k * CO + o) * 32 + cc * CC + c], a);
-          dc[c] = a;
-        }
+        for (int o = 0; o < CO; ++o)
+#pragma unroll
+          for (int c = 0; c < CC; ++c) dc[c] = fmaf(g[o], wk[o * 32 + c], dc[c]);
         const float wq[4] = {s.hy * s.hx, s.hy * s.lx, s.ly * s.hx, s.ly * s.lx};
         float v[4][CC];
         bool ok[4];
@@ -462,15 +461,20 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
     }
     __syncthreads();
   }
-  if (live) {
-    float* dp = dom + pix * 27;
+  if (live) {  // one 128-byte row per pixel: 27 gradients + 5 zeros (16-byte aligned for the consumers)
+    float r[32];
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
       const float m = __frcp_rn(1.f + __expf(-omp[(size_t)(18 + k) * HW]));
-      dp[2 * k] = m * aY[k];
-      dp[2 * k + 1] = m * aX[k];
-      dp[18 + k] = aM[k] * (m * (1.f - m));
+      r[2 * k] = m * aY[k];
+      r[2 * k + 1] = m * aX[k];
+      r[18 + k] = aM[k] * (m * (1.f - m));
     }
+#pragma unroll
+    for (int c = 27; c < 32; ++c) r[c] = 0.f;
+    float4* dp = reinterpret_cast<float4*>(dom + pix * 32);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dp[q] = make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
   }
 }
 

@@ -20,11 +20,47 @@ gradients tmvs_colsum, the FPN merges' nearest x2 adjoint tmvs_nearest_up2_backw
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import ops
 
 BN_MOMENTUM = 0.1
+_PACK_INDEX = {}
+
+
+def _pack_index(kind, cout, cin, k, device):
+    """Flat gather indices reproducing the host packers tmvs_deform_conv2d_pack / tmvs_conv2d_pack
+    (csrc/featurenet.hip, csrc/conv2d.hip) into a weight flattened [cout][cin][k*k] plus one trailing
+    zero (index cout*cin*k*k = a padding slot), so training packs on the device with no host sync."""
+    key = (kind, cout, cin, k, str(device))
+    if key not in _PACK_INDEX:
+        zero = cout * cin * k * k
+        if kind == "dcn":  # [tap][m-tile][half][lane][e] <- W[16m + (l & 15)][16h + 4 (l >> 4) + e][tap]
+            mt = (cout + 15) // 16
+            t, m, h, lane, e = np.meshgrid(np.arange(9), np.arange(mt), np.arange(2), np.arange(64), np.arange(4),
+                                           indexing="ij")
+            co, ci = 16 * m + (lane & 15), 16 * h + 4 * (lane >> 4) + e
+            idx = np.where(co < cout, (co * cin + ci) * 9 + t, zero)
+        else:  # conv2d: [k-block b][m-tile][lane][e], pair idx = 4b + (l >> 4) -> (tap, channel chunk)
+            cip = max(cin, 4)
+            g = cip // 4
+            nidx = k * k * g
+            nb, mt = (nidx + 3) // 4, (cout + 15) // 16
+            b, m, lane, e = np.meshgrid(np.arange(nb), np.arange(mt), np.arange(64), np.arange(4), indexing="ij")
+            pair, co = 4 * b + (lane >> 4), 16 * m + (lane & 15)
+            tap, c = pair // g, 4 * (pair % g) + e
+            ok = (pair < nidx) & (co < cout) & (c < cin)
+            idx = np.where(ok, (co * cin + np.minimum(c, cin - 1)) * k * k + np.minimum(tap, k * k - 1), zero)
+        _PACK_INDEX[key] = torch.from_numpy(idx.reshape(-1).astype(np.int64)).to(device)
+    return _PACK_INDEX[key]
+
+
+def device_pack(kind, w):
+    """The kernels' packed weight layout, gathered on the weight's device ('dcn' or 'conv2d')."""
+    co, ci, k, _ = w.shape
+    flat = torch.cat([w.detach().float().reshape(-1), w.new_zeros(1, dtype=torch.float32)])
+    return flat[_pack_index(kind, co, ci, k, w.device)].contiguous()
 
 
 def _taps(w):
@@ -59,7 +95,7 @@ def _bn_relu_views(tape, z, bn):
     per = []
     for v in range(tape.n):
         mean, var = ops.bn_stats(z[v])
-        y[v] = ops.bn_relu_train(z[v], mean, var, bn.weight.detach(), bn.bias.detach(), bn.eps)
+        ops.bn_relu_train(z[v], mean, var, bn.weight.detach(), bn.bias.detach(), bn.eps, out=y[v])
         per.append((mean, var))
     tape.stats.append((bn, per, z.shape[1] * z.shape[2]))
     return y, per
@@ -67,11 +103,11 @@ def _bn_relu_views(tape, z, bn):
 
 def _bn_relu_views_backward(dy, z, per, bn):
     dz = torch.empty_like(z)
+    dy = dy.contiguous()
     dg = db = None
     for v, (mean, var) in enumerate(per):
-        dzv, dgv, dbv = ops.bn_relu_backward(dy[v].contiguous(), z[v], mean, var, bn.weight.detach(), bn.bias.detach(),
-                                             bn.eps)
-        dz[v] = dzv
+        _, dgv, dbv = ops.bn_relu_backward(dy[v], z[v], mean, var, bn.weight.detach(), bn.bias.detach(), bn.eps,
+                                           dz=dz[v])
         dg = dgv if dg is None else dg + dgv
         db = dbv if db is None else db + dbv
     return dz, dg, db
@@ -83,9 +119,9 @@ def _block_fwd(tape, blk, x, k, stride, nchw_input=False, head3x3=False):
     w = blk.conv.weight
     cout = w.shape[0]
     if head3x3:
-        _, z = ops.conv3x3_nhwc(x, ops.deform_conv2d_pack(w).to(x.device), bn=None, relu=False)
+        _, z = ops.conv3x3_nhwc(x, device_pack("dcn", w), bn=None, relu=False)
     else:
-        z = ops.conv2d_bn_relu(x, ops.conv2d_pack(w).to(x.device), cout, k, stride, bn=None, relu=False,
+        z = ops.conv2d_bn_relu(x, device_pack("conv2d", w), cout, k, stride, bn=None, relu=False,
                                nchw_input=nchw_input)
     y, per = _bn_relu_views(tape, z, blk.bn)
     return y, ("block", blk, x, z, per, k, stride, nchw_input)
@@ -93,10 +129,9 @@ def _block_fwd(tape, blk, x, k, stride, nchw_input=False, head3x3=False):
 
 def _dcn_fwd(dcn, x, want_nchw=False):
     com = dcn.conv_offset_mask
-    u, om, out = ops.dcn_forward_train(x, ops.deform_conv2d_pack(com.weight).to(x.device),
-                                       com.bias.detach().float().contiguous(),
-                                       ops.deform_conv2d_pack(dcn.weight).to(x.device),
-                                       dcn.bias.detach().float().contiguous(), dcn.cout, want_nchw=want_nchw)
+    u, om, out = ops.dcn_forward_train(x, device_pack("dcn", com.weight), com.bias.detach().float().contiguous(),
+                                       device_pack("dcn", dcn.weight), dcn.bias.detach().float().contiguous(),
+                                       dcn.cout, want_nchw=want_nchw)
     return u, om, out
 
 
@@ -140,10 +175,15 @@ def _dcn_bwd(dcn, x, om, dy, grads):
     dom, dw = ops.dcn_backward(x, om, w_taps, dy, dx)
     _acc(grads, w, dw.permute(1, 2, 0).reshape(cout, 32, 3, 3).contiguous())
     _acc(grads, dcn.bias, ops.colsum(dy))
+    # the offset/mask conv (3x3, 32 -> 27, bias) on dom padded to 32 channels (27..31 zero): its
+    # weight gradient rows 27..31 are dropped, its data gradient reads them against zero weights
     com = dcn.conv_offset_mask
-    _acc(grads, com.weight, _untaps(ops.conv2d_wgrad(dom, x, 3, 1, 1), com.weight.shape))
-    _acc(grads, com.bias, ops.colsum(dom))
-    ops.conv2d_generic(dom, _taps_t(com.weight), 32, (x.shape[1], x.shape[2]), 3, 1, 1, transposed=True, out=dx)
+    dwo = ops.conv2d_wgrad(dom, x, 3, 1, 1)[:, :27].contiguous()
+    _acc(grads, com.weight, _untaps(dwo, com.weight.shape))
+    _acc(grads, com.bias, ops.colsum(dom)[:27].contiguous())
+    wt = torch.zeros(9, 32, 32, device=x.device)
+    wt[:, :, :27] = _taps_t(com.weight)
+    ops.conv2d_generic(dom, wt, 32, (x.shape[1], x.shape[2]), 3, 1, 1, transposed=True, out=dx)
     return dx
 
 

@@ -613,12 +613,12 @@ def bn_stats(z):
     return mean, var
 
 
-def bn_relu_train(z, mean, var, gamma, beta, eps, skip=None):
-    """tmvs_bn_relu_train: relu(BN_batch(z)) [+ skip], z [..., C]."""
-    for t, n in ((z, "z"), (mean, "mean"), (var, "var"), (gamma, "gamma"), (beta, "beta"), (skip, "skip")):
+def bn_relu_train(z, mean, var, gamma, beta, eps, skip=None, out=None):
+    """tmvs_bn_relu_train: relu(BN_batch(z)) [+ skip], z [..., C] (written into `out` when given)."""
+    for t, n in ((z, "z"), (mean, "mean"), (var, "var"), (gamma, "gamma"), (beta, "beta"), (skip, "skip"), (out, "out")):
         _dev(t, n)
     c = z.shape[-1]
-    out = torch.empty_like(z)
+    out = torch.empty_like(z) if out is None else out
     with _Span("tmvs_bn_relu_train"):
         _lib.check(_lib_h().tmvs_bn_relu_train(_ptr(z), z.numel() // c, c, _ptr(mean), _ptr(var), _ptr(gamma),
                                                _ptr(beta), ctypes.c_float(eps), _ptr(skip), _ptr(out), _stream()),
@@ -626,14 +626,14 @@ def bn_relu_train(z, mean, var, gamma, beta, eps, skip=None):
     return out
 
 
-def bn_relu_backward(dy, z, mean, var, gamma, beta, eps):
-    """tmvs_bn_relu_backward -> (dz, dgamma, dbeta)."""
-    for t, n in ((dy, "dy"), (z, "z"), (mean, "mean"), (var, "var"), (gamma, "gamma"), (beta, "beta")):
+def bn_relu_backward(dy, z, mean, var, gamma, beta, eps, dz=None):
+    """tmvs_bn_relu_backward -> (dz, dgamma, dbeta) (dz written into `dz` when given)."""
+    for t, n in ((dy, "dy"), (z, "z"), (mean, "mean"), (var, "var"), (gamma, "gamma"), (beta, "beta"), (dz, "dz")):
         _dev(t, n)
     c = z.shape[-1]
     nvox = z.numel() // c
     ws = _bn_ws(nvox, c, z.device)
-    dz = torch.empty_like(z)
+    dz = torch.empty_like(z) if dz is None else dz
     dg = torch.empty(c, device=z.device)
     db = torch.empty(c, device=z.device)
     with _Span("tmvs_bn_relu_backward"):
@@ -959,7 +959,8 @@ def dcn_forward_train(x_nhwc, wom_packed, bom, w_packed, bias, cout, want_nchw=F
 
 
 def dcn_backward(x_nhwc, offset_mask, w_taps, dy_nhwc, dx_nhwc):
-    """tmvs_dcn_backward: -> (dom [B,H,W,27], dw_taps [9][cout][32]); dx_nhwc is accumulated into."""
+    """tmvs_dcn_backward: -> (dom [B,H,W,32] (channels 27..31 zero), dw_taps [9][cout][32]); dx_nhwc is
+    accumulated into."""
     for t, n in ((x_nhwc, "x_nhwc"), (offset_mask, "offset_mask"), (w_taps, "w_taps"), (dy_nhwc, "dy_nhwc"),
                  (dx_nhwc, "dx_nhwc")):
         _dev(t, n)
@@ -969,7 +970,7 @@ def dcn_backward(x_nhwc, offset_mask, w_taps, dy_nhwc, dx_nhwc):
             tuple(w_taps.shape) != (9, cout, cin) or tuple(dx_nhwc.shape) != tuple(x_nhwc.shape):
         raise ValueError("dcn_backward: shape mismatch")
     ws = torch.empty(_lib_h().tmvs_dcn_backward_workspace(b, cout, h, w) // 4 + 64, device=x_nhwc.device)
-    dom = torch.empty(b, h, w, 27, device=x_nhwc.device)
+    dom = torch.empty(b, h, w, 32, device=x_nhwc.device)
     dw = torch.empty(9, cout, cin, device=x_nhwc.device)
     with _Span("tmvs_dcn_backward"):
         _lib.check(_lib_h().tmvs_dcn_backward(_ptr(x_nhwc), _ptr(offset_mask), _ptr(w_taps), _ptr(dy_nhwc), b, cin, cout,
