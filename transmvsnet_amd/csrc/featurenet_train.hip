@@ -438,10 +438,12 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
           const int cy = s.y0 + (q >> 1), cx = s.x0 + (q & 1);
           const int ry = cy - wy0, rx = cx - wx0;
           const float f = s.m * wq[q];
+          if (f == 0.f) continue;  // a zero bilinear weight (integer sample positions: 3 of 4 corners)
           if ((unsigned)ry < (unsigned)WR && (unsigned)rx < (unsigned)WC) {
-            float* wp = win + (ry * WC + rx) * CC;
+            // channel-major window: neighbouring pixels' corners are neighbouring words (no bank conflicts)
+            float* wp = win + ry * WC + rx;
 #pragma unroll
-            for (int c = 0; c < CC; ++c) atomicAdd(wp + c, f * dc[c]);
+            for (int c = 0; c < CC; ++c) atomicAdd(wp + c * (WR * WC), f * dc[c]);
           } else {  // an offset beyond the window: straight to global memory
             float* gp = dxb + ((size_t)cy * W + cx) * 32 + cc * CC;
 #pragma unroll
@@ -452,9 +454,9 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
     }
     __syncthreads();
     for (int i = tid; i < WR * WC * CC; i += kBlk) {
-      const float v = win[i];
+      const int cell = i / CC, c = i - cell * CC;  // thread i reads channel c of cell: one 32-byte row per 8 lanes
+      const float v = win[c * (WR * WC) + cell];
       if (v != 0.f) {  // only in-image corners were added
-        const int cell = i / CC, c = i - cell * CC;
         const int gy = wy0 + cell / WC, gx = wx0 + cell % WC;
         unsafeAtomicAdd(dxb + ((size_t)gy * W + gx) * 32 + cc * CC + c, v);
       }

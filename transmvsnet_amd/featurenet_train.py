@@ -151,6 +151,29 @@ def _acc(grads, p, g):
     grads[id(p)] = g if id(p) not in grads else grads[id(p)] + g
 
 
+def _flip_t(w):
+    """The data gradient of a stride-1 'same' conv is a forward conv of dz with the weight transposed
+    (in <-> out) and flipped in both spatial axes: W'[ci][co][kh][kw] = W[co][ci][k-1-kh][k-1-kw]."""
+    return w.detach().float().flip(2, 3).transpose(0, 1).contiguous()
+
+
+# (dz channels, dx channels, k) that tmvs_conv2d_bn_relu takes as a forward conv (stride 1)
+_MFMA_DGRAD = {(8, 8, 3), (16, 16, 3), (32, 32, 1)}
+
+
+def dgrad_same(dz, w, out_hw):
+    """Data gradient of Conv2d(k, stride 1, padding k//2) (models/module.py:24-61) as a forward conv on
+    the MFMA inference kernels (tmvs_conv3x3_nhwc for 32 -> 32 3x3, tmvs_conv2d_bn_relu otherwise),
+    falling back to the VALU transposed gather for shapes those kernels do not take."""
+    co, ci, k, _ = w.shape
+    wf = _flip_t(w)
+    if ci == 32 and co == 32 and k == 3:
+        return ops.conv3x3_nhwc(dz, device_pack("dcn", wf), bn=None, relu=False)[1]
+    if (co, ci, k) in _MFMA_DGRAD:
+        return ops.conv2d_bn_relu(dz, device_pack("conv2d", wf), ci, k, 1, bn=None, relu=False)
+    return ops.conv2d_generic(dz, _taps_t(w), ci, out_hw, k, 1, k // 2, transposed=True)
+
+
 def _block_bwd(rec, dy, grads, need_dx=True):
     _, blk, x, z, per, k, stride, nchw_input = rec
     dz, dg, db = _bn_relu_views_backward(dy, z, per, blk.bn)
@@ -162,6 +185,8 @@ def _block_bwd(rec, dy, grads, need_dx=True):
     _acc(grads, w, _untaps(ops.conv2d_wgrad(dz, xg, k, stride, pad), w.shape))
     if not need_dx:
         return None
+    if stride == 1:
+        return dgrad_same(dz, w, (xg.shape[1], xg.shape[2]))
     return ops.conv2d_generic(dz, _taps_t(w), w.shape[1], (xg.shape[1], xg.shape[2]), k, stride, pad, transposed=True)
 
 
@@ -181,9 +206,9 @@ def _dcn_bwd(dcn, x, om, dy, grads):
     dwo = ops.conv2d_wgrad(dom, x, 3, 1, 1)[:, :27].contiguous()
     _acc(grads, com.weight, _untaps(dwo, com.weight.shape))
     _acc(grads, com.bias, ops.colsum(dom)[:27].contiguous())
-    wt = torch.zeros(9, 32, 32, device=x.device)
-    wt[:, :, :27] = _taps_t(com.weight)
-    ops.conv2d_generic(dom, wt, 32, (x.shape[1], x.shape[2]), 3, 1, 1, transposed=True, out=dx)
+    wp = torch.zeros(32, 32, 3, 3, device=x.device)  # [co 27 + 5 zero rows][ci][3][3]
+    wp[:27] = com.weight.detach().float()
+    dx.add_(dgrad_same(dom, wp, (x.shape[1], x.shape[2])))
     return dx
 
 
