@@ -21,9 +21,10 @@
 //
 // Determinism: every reduction over pixels (weight / bias gradients) is block partials in fp64 plus
 // a fixed-order combine. The DCN input gradient is a scatter with data-dependent targets; it is
-// accumulated in fp32 LDS windows (per block tile + a halo of kR px) flushed with global fp32
-// atomics, as torchvision's deformable_col2im adds with atomicAdd: the sum is exact up to fp32
-// rounding order (bitwise run-to-run stability is not promised for dx, as in the reference).
+// accumulated in fp32 LDS windows (per block tile + a halo of R px; LDS atomics, so the rounding
+// order inside a window varies run to run) that are summed per texel in a fixed block order; only
+// corners beyond the window (offsets over R px) go to global memory with fp32 atomics, as
+// torchvision's deformable_col2im adds every contribution with atomicAdd.
 #include "common.h"
 
 namespace tmvs {
@@ -354,11 +355,15 @@ constexpr int WR = TY + 2 * R + 3, WC = TX + 2 * R + 3;
 }  // namespace dbw
 
 // dcol, d om (NHWC [B][H][W][32], channels 27..31 zero) and the scatter of m * dcol into dx (accumulated)
+// The block's LDS window of each 8-channel pass is written whole to scratch [block][cell][32] (plain,
+// coalesced stores); dcn_gather_windows_kernel then sums, for every texel, the <= 4 windows covering
+// it in a fixed block order (deterministic, no global atomics). Corners beyond the window (offsets
+// over kR px) are added to dx with fp32 atomics before that pass.
 template <int CO>
 __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ om,
                                                            const float* __restrict__ wt, const float* __restrict__ dy,
                                                            int B, int H, int W, float* __restrict__ dx,
-                                                           float* __restrict__ dom) {
+                                                           float* __restrict__ dom, float* __restrict__ scratch) {
   using namespace dbw;
   __shared__ float win[WR * WC * CC];
   const int tid = threadIdx.x;
@@ -453,13 +458,10 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
       }
     }
     __syncthreads();
+    float* sb = scratch + (size_t)blockIdx.x * (WR * WC) * 32 + cc * CC;
     for (int i = tid; i < WR * WC * CC; i += kBlk) {
-      const int cell = i / CC, c = i - cell * CC;  // thread i reads channel c of cell: one 32-byte row per 8 lanes
-      const float v = win[c * (WR * WC) + cell];
-      if (v != 0.f) {  // only in-image corners were added
-        const int gy = wy0 + cell / WC, gx = wx0 + cell % WC;
-        unsafeAtomicAdd(dxb + ((size_t)gy * W + gx) * 32 + cc * CC + c, v);
-      }
+      const int cell = i / CC, c = i - cell * CC;  // 8 lanes = one cell's 32-byte channel chunk
+      sb[(size_t)cell * 32 + c] = win[c * (WR * WC) + cell];
     }
     __syncthreads();
   }
@@ -478,6 +480,32 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
 #pragma unroll
     for (int q = 0; q < 8; ++q) dp[q] = make_float4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
   }
+}
+
+// dx[q][c] += sum over the blocks whose windows cover texel q (block rows / columns ascending) of their
+// window value: one thread per (texel, channel)
+__global__ __launch_bounds__(kBlk) void dcn_gather_windows_kernel(const float* __restrict__ scratch, int B, int H,
+                                                                 int W, float* __restrict__ dx) {
+  using namespace dbw;
+  const long i = (long)blockIdx.x * kBlk + threadIdx.x;
+  if (i >= (long)B * H * W * 32) return;
+  const int c = (int)(i & 31);
+  long t = i >> 5;
+  const int xq = (int)(t % W);
+  t /= W;
+  const int y = (int)(t % H), b = (int)(t / H);
+  const int ntx = (W + TX - 1) / TX, nty = (H + TY - 1) / TY;
+  // block row by covers window rows [by*TY - R - 1, by*TY - R - 1 + WR)
+  const int by0 = max(0, (y + R + 1 - WR + 1 + TY - 1) / TY), by1 = min(nty - 1, (y + R + 1) / TY);
+  const int bx0 = max(0, (xq + R + 1 - WC + 1 + TX - 1) / TX), bx1 = min(ntx - 1, (xq + R + 1) / TX);
+  float s = 0.f;
+  for (int by = by0; by <= by1; ++by)
+    for (int bx = bx0; bx <= bx1; ++bx) {
+      const int cell = (y - (by * TY - R - 1)) * WC + (xq - (bx * TX - R - 1));
+      const size_t blk = ((size_t)b * nty + by) * ntx + bx;
+      s += scratch[(blk * (WR * WC) + cell) * 32 + c];
+    }
+  dx[i] = dx[i] + s;
 }
 
 // dW[k][o][c] = sum_p dy[p][o] col_k[p][c]: grid (nblk, 9), block partials [nblk][9][CO][32]
@@ -655,10 +683,20 @@ extern "C" int tmvs_colsum(const float* x, long n, int channels, void* workspace
   return TMVS_OK;
 }
 
-extern "C" size_t tmvs_dcn_backward_workspace(int batch, int cout, int height, int width) {
+static size_t dcn_partials_bytes(int batch, int cout, int height, int width) {
   const long np = (long)batch * height * width;
   const long ppb = ppb_for(np, 512);
-  return (size_t)((np + ppb - 1) / ppb) * 9 * cout * 32 * sizeof(double);
+  return ((size_t)((np + ppb - 1) / ppb) * 9 * cout * 32 * sizeof(double) + 255) & ~(size_t)255;
+}
+
+static long dcn_data_blocks(int batch, int height, int width) {
+  return (long)batch * ((height + dbw::TY - 1) / dbw::TY) * ((width + dbw::TX - 1) / dbw::TX);
+}
+
+// [weight-gradient partials (fp64)][per-block scatter windows: blocks x WR*WC x 32 fp32]
+extern "C" size_t tmvs_dcn_backward_workspace(int batch, int cout, int height, int width) {
+  return dcn_partials_bytes(batch, cout, height, width) +
+         (size_t)dcn_data_blocks(batch, height, width) * dbw::WR * dbw::WC * 32 * sizeof(float);
 }
 
 extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, const float* w_taps, const float* dy_nhwc,
@@ -670,15 +708,19 @@ extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, 
   if (cin != 32 || (cout != 8 && cout != 16 && cout != 32)) return TMVS_ERR_SHAPE;
   if (workspace_bytes < tmvs_dcn_backward_workspace(batch, cout, height, width)) return TMVS_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  const unsigned nbd = (unsigned)(batch * ((height + dbw::TY - 1) / dbw::TY) * ((width + dbw::TX - 1) / dbw::TX));
+  const unsigned nbd = (unsigned)dcn_data_blocks(batch, height, width);
   const long np = (long)batch * height * width;
   const long ppb = ppb_for(np, 512);
   const int nblk = (int)((np + ppb - 1) / ppb);
   double* part = (double*)workspace;
+  float* scratch = (float*)((char*)workspace + dcn_partials_bytes(batch, cout, height, width));
 #define TMVS_DCNB(CO)                                                                                             \
   case CO:                                                                                                        \
     hipLaunchKernelGGL(dcn_bwd_data_kernel<CO>, dim3(nbd), dim3(kBlk), 0, st, x_nhwc, offset_mask, w_taps, dy_nhwc, \
-                       batch, height, width, dx_nhwc, dom_nhwc);                                                  \
+                       batch, height, width, dx_nhwc, dom_nhwc, scratch);                                         \
+    TMVS_CHECK_LAUNCH();                                                                                          \
+    hipLaunchKernelGGL(dcn_gather_windows_kernel, dim3((unsigned)((np * 32 + kBlk - 1) / kBlk)), dim3(kBlk), 0, st,  \
+                       (const float*)scratch, batch, height, width, dx_nhwc);                                     \
     TMVS_CHECK_LAUNCH();                                                                                          \
     hipLaunchKernelGGL(dcn_bwd_weight_kernel<CO>, dim3(nblk, 9), dim3(kBlk), 0, st, x_nhwc, offset_mask, dy_nhwc,   \
                        batch, height, width, ppb, part);                                                          \
