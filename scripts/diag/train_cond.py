@@ -31,3 +31,10 @@ for n in NAMES:
     b = ex[n].grad.double().numpy()
     print(f"{n:62s} fixture {float(np.abs(f - b).max() / np.abs(b).max()):.1e}  "
           + "  ".join(f"{nt}thr {e:.1e}" for nt, e in rows[n]), flush=True)
+# ~1-ulp input jitter (train_step_oracle's perturb_seed): the fp32 spread the GPU test's bar uses
+torch.set_num_threads(16)
+for seed in range(6):
+    sd = train_step_oracle(g, case, perturb_seed=1000 + seed)[2]
+    print(f"jitter seed {seed}: " + "  ".join(
+        f"{n.split('.', 1)[-1][-28:]} {float(np.abs(sd[n].grad.double().numpy() - ex[n].grad.double().numpy()).max() / np.abs(ex[n].grad.double().numpy()).max()):.1e}"
+        for n in NAMES), flush=True)
