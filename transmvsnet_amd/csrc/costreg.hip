@@ -1033,175 +1033,6 @@ __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __re
   }
 }
 
-// ---------------------------------------------------------------- conv1 with conv0 recomputed in its staging
-// conv3d_s2c8_tile_kernel's tiles and MFMA loop, but the 8-channel full-resolution conv0 output is
-// never read from (or written to) HBM: per tile the 1-channel cost volume footprint (+1 voxel halo,
-// (2TD+3) x (2TH+3) x 35 floats) is staged in LDS, and conv0 + BN + ReLU (models/module.py:447,
-// conv0 = Conv3d(1, 8) k3 p1) is evaluated there for the tile's 5 x 9 x 33 input voxels with exactly
-// conv0_kernel's FMA chain (taps in (kd, kh, kw) order, zero padding, relu(fmaf(acc, alpha, shift)))
-// -- bit-identical to the materialised conv0 -- and written into the same parity-split tile layout.
-// Input voxels outside the volume stay 0 (conv1's own zero padding). The next tile's footprint is
-// fetched into registers during the current tile's MFMAs.
-template <int TD, int TH>
-__global__ __launch_bounds__(256) void conv1_c0_tile_kernel(const float* __restrict__ sim, const float* __restrict__ w0,
-                                                            const float* __restrict__ al0,
-                                                            const float* __restrict__ sh0,
-                                                            const float* __restrict__ wpk,
-                                                            const float* __restrict__ alpha,
-                                                            const float* __restrict__ shift, float* __restrict__ y,
-                                                            Geo g, int ntiles) {
-  constexpr int COUT = 16, NBW = TD * TH / 4;
-  constexpr int LW = 33, LH = 2 * TH + 1, LD = 2 * TD + 1, SW = 17;
-  constexpr int NROW = LD * LH, NVOX = NROW * LW;
-  constexpr int XW = LW + 2, XH = LH + 2, XD = LD + 2, NX = XD * XH * XW;  // cost-volume footprint
-  constexpr int NLD = (NX + 255) / 256;
-  __shared__ __attribute__((aligned(16))) float tile[NROW * 2 * SW * 8];
-  __shared__ __attribute__((aligned(16))) float wts[28 * 16 * 8];
-  __shared__ float simt[NX];
-  const int nws = (g.Wo + 15) / 16, nhs = (g.Ho + TH - 1) / TH, nds = (g.Do + TD - 1) / TD;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int col = lane & 15, kgrp = lane >> 4;
-  const int half = kgrp & 1, side = kgrp >> 1;
-  const int nxcd = gridDim.x >= 8 ? 8 : 1, per_xcd = gridDim.x / nxcd;
-  const int xcd = blockIdx.x % nxcd, kx = blockIdx.x / nxcd;
-  const int t_lo = (int)((long)ntiles * xcd / nxcd), t_hi = (int)((long)ntiles * (xcd + 1) / nxcd);
-  if (kx >= per_xcd) return;
-  struct TileCoord {
-    int n, od0, oh0, ow0;
-  };
-  auto coord = [&](int t) {
-    TileCoord c;
-    c.ow0 = (t % nws) * 16;
-    t /= nws;
-    c.oh0 = (t % nhs) * TH;
-    t /= nhs;
-    c.od0 = (t % nds) * TD;
-    c.n = t / nds;
-    return c;
-  };
-  float pf[NLD];
-  auto fetch = [&](int t) {  // the tile's cost-volume footprint (origin: conv0 footprint - 1), zeros outside
-    const TileCoord c = coord(t);
-    const float* sb = sim + (size_t)c.n * g.Di * g.Hi * g.Wi;
-#pragma unroll
-    for (int k = 0; k < NLD; ++k) {
-      const int idx = threadIdx.x + 256 * k;
-      const int xw = idx % XW, rr = idx / XW, xh = rr % XH, xd = rr / XH;
-      const int iw = 2 * c.ow0 - 2 + xw, ih = 2 * c.oh0 - 2 + xh, id = 2 * c.od0 - 2 + xd;
-      pf[k] = 0.f;
-      if (idx < NX && (unsigned)iw < (unsigned)g.Wi && (unsigned)ih < (unsigned)g.Hi && (unsigned)id < (unsigned)g.Di)
-        pf[k] = sb[((size_t)id * g.Hi + ih) * g.Wi + iw];
-    }
-  };
-  auto commit = [&](int t) {  // footprint -> LDS, then conv0 of the tile's input voxels -> tile
-    const TileCoord c = coord(t);
-#pragma unroll
-    for (int k = 0; k < NLD; ++k) {
-      const int idx = threadIdx.x + 256 * k;
-      if (idx < NX) simt[idx] = pf[k];
-    }
-    __syncthreads();
-    for (int v = threadIdx.x; v < NVOX; v += 256) {
-      const int lw = v % LW, row = v / LW, lh = row % LH, ld = row / LH;
-      const int iw = 2 * c.ow0 - 1 + lw, ih = 2 * c.oh0 - 1 + lh, id = 2 * c.od0 - 1 + ld;
-      float o[8];
-      if ((unsigned)iw < (unsigned)g.Wi && (unsigned)ih < (unsigned)g.Hi && (unsigned)id < (unsigned)g.Di) {
-        float a[8];
-#pragma unroll
-        for (int ch = 0; ch < 8; ++ch) a[ch] = 0.f;
-#pragma unroll
-        for (int tp = 0; tp < 27; ++tp) {
-          const float xv = simt[((ld + tp / 9) * XH + lh + (tp / 3) % 3) * XW + lw + tp % 3];
-#pragma unroll
-          for (int ch = 0; ch < 8; ++ch) a[ch] = fmaf(w0[tp * 8 + ch], xv, a[ch]);
-        }
-#pragma unroll
-        for (int ch = 0; ch < 8; ++ch) o[ch] = relu(fmaf(a[ch], al0[ch], sh0[ch]));
-      } else {
-#pragma unroll
-        for (int ch = 0; ch < 8; ++ch) o[ch] = 0.f;
-      }
-      float* tp4 = tile + ((row * 2 + (lw & 1)) * SW + (lw >> 1)) * 8;
-      *reinterpret_cast<float4*>(tp4) = make_float4(o[0], o[1], o[2], o[3]);
-      *reinterpret_cast<float4*>(tp4 + 4) = make_float4(o[4], o[5], o[6], o[7]);
-    }
-  };
-  for (int idx = threadIdx.x; idx < 28 * 16 * 2; idx += 256) {  // tap 27: zero (the empty half of pair 13)
-    const int q = idx & 1, row = (idx >> 1) & 15, tap = idx >> 5;
-    const float4 v = tap < 27 ? *reinterpret_cast<const float4*>(wpk + ((size_t)tap * COUT + row) * 8 + 4 * q)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
-    *reinterpret_cast<float4*>(wts + (tap * 16 + row) * 8 + 4 * q) = v;
-  }
-  const int co = kgrp * 4;
-  const float4 al = *reinterpret_cast<const float4*>(alpha + co);
-  const float4 sh = *reinterpret_cast<const float4*>(shift + co);
-  int t = t_lo + kx;
-  if (t < t_hi) {
-    fetch(t);
-    commit(t);
-  }
-  __syncthreads();
-  for (; t < t_hi; t += per_xcd) {
-    const TileCoord c = coord(t);
-    const int tn = t + per_xcd;
-    if (tn < t_hi) fetch(tn);
-    floatx4 acc[NBW];
-#pragma unroll
-    for (int r = 0; r < NBW; ++r) acc[r] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int pr = 0; pr < 14; ++pr) {
-      const int tap = 2 * pr + side;
-      const int tp = tap < 27 ? tap : 26;
-      const int kd = tp / 9, kh = (tp / 3) % 3, kw = tp % 3;
-      const float4 a = *reinterpret_cast<const float4*>(wts + (tap * 16 + col) * 8 + 4 * half);
-      float4 b[NBW];
-#pragma unroll
-      for (int r = 0; r < NBW; ++r) {
-        const int rr = wv * NBW + r;
-        const int odl = rr / TH, ohl = rr - odl * TH;
-        const int row = (2 * odl + kd) * LH + 2 * ohl + kh;
-        b[r] = *reinterpret_cast<const float4*>(tile + ((row * 2 + (kw & 1)) * SW + col + (kw >> 1)) * 8 + 4 * half);
-      }
-#pragma unroll
-      for (int r = 0; r < NBW; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[r].x, acc[r], 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < NBW; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[r].y, acc[r], 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < NBW; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[r].z, acc[r], 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < NBW; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[r].w, acc[r], 0, 0, 0);
-    }
-    const int ow = c.ow0 + col;
-    const size_t out_n = (size_t)c.n * g.Do * g.Ho * g.Wo;
-#pragma unroll
-    for (int r = 0; r < NBW; ++r) {
-      const int rr = wv * NBW + r;
-      const int od = c.od0 + rr / TH, oh = c.oh0 + rr % TH;
-      if (ow >= g.Wo || od >= g.Do || oh >= g.Ho) continue;
-      float4 o;
-      o.x = relu(fmaf(acc[r][0], al.x, sh.x));
-      o.y = relu(fmaf(acc[r][1], al.y, sh.y));
-      o.z = relu(fmaf(acc[r][2], al.z, sh.z));
-      o.w = relu(fmaf(acc[r][3], al.w, sh.w));
-      *reinterpret_cast<float4*>(y + (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co) = o;
-    }
-    __syncthreads();
-    if (tn < t_hi) commit(tn);
-    __syncthreads();
-  }
-}
-
-template <int TD, int TH>
-static int launch_conv1_c0(const float* sim, const float* w0, const float* al0, const float* sh0, const float* w,
-                           const float* al, const float* sh, float* y, int B, const Geo& g, hipStream_t st) {
-  const long ntiles = (long)B * ((g.Do + TD - 1) / TD) * ((g.Ho + TH - 1) / TH) * ((g.Wo + 15) / 16);
-  const int grid = persistent_grid(conv1_c0_tile_kernel<TD, TH>, ntiles);
-  hipLaunchKernelGGL((conv1_c0_tile_kernel<TD, TH>), dim3(grid), dim3(256), 0, st, sim, w0, al0, sh0, w, al, sh, y, g,
-                     (int)ntiles);
-  TMVS_CHECK_LAUNCH();
-  return TMVS_OK;
-}
-
 template <int TD, int TH>
 static int launch_conv_s2c8_tile(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
                                  const Geo& g, hipStream_t st) {
@@ -1250,17 +1081,12 @@ static int launch_conv_direct(const float* x, const float* w, const float* al, c
 // are requested before the MFMAs too, so neither latency sits between MFMA phases.
 // Tiles are dealt out XCD-contiguously (an XCD's workgroups share one L2: neighbouring tiles
 // share their halo voxels).
-// C0SKIP: the skip tensor is conv0's output, recomputed here from the 1-channel cost volume `skip`
-// (conv0 weights w0 [27][8], BN al0/sh0) with conv0_kernel's exact FMA chain instead of being read:
-// the 8-channel full-resolution conv0 volume never exists (conv1_c0_tile_kernel recomputes it too).
-template <int TDI, int THI, bool C0SKIP = false>
+template <int TDI, int THI>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void deconv3d_c8_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                           const float* __restrict__ alpha,
                                                           const float* __restrict__ shift,
                                                           const float* __restrict__ skip, float* __restrict__ y,
-                                                          Geo g, int ntiles, const float* __restrict__ w0 = nullptr,
-                                                          const float* __restrict__ al0 = nullptr,
-                                                          const float* __restrict__ sh0 = nullptr) {
+                                                          Geo g, int ntiles) {
   constexpr int CIN = 16, COUT = 8, PL = 4;
   constexpr int NBW = TDI * THI / 4;
   constexpr int LW = 17, LH = THI + 1, LD = TDI + 1, VST = 16;
@@ -1354,34 +1180,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const int md = c.md0 + rr / THI, mh = c.mh0 + rr % THI;
       ok[r] = md < g.Di && mh < g.Hi && ow < 2 * g.Wi;
       oo[r] = (out_n + ((size_t)(2 * md) * g.Ho + 2 * mh) * g.Wo + ow) * 8 + (lane & 1) * 4;
-      if constexpr (!C0SKIP) {
 #pragma unroll
-        for (int pdh = 0; pdh < 4; ++pdh)
-          sk[r][pdh] = ok[r] ? *reinterpret_cast<const float4*>(skip + oo[r] + (pdh >> 1) * plane + (pdh & 1) * row)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        // conv0 (Cin 1 -> 8, k3 p1) + BN + ReLU of this lane's 4 channels at its 4 output voxels
-        const int c0 = (lane & 1) * 4;
-        const int Dd = g.Do, Hh = g.Ho, Ww = g.Wo;
-        const __amdgpu_buffer_rsrc_t rs = raw_rsrc(skip + (size_t)c.n * Dd * Hh * Ww, (unsigned)(Dd * Hh * Ww * 4));
-#pragma unroll
-        for (int pdh = 0; pdh < 4; ++pdh) {
-          const int od = 2 * md + (pdh >> 1), oh = 2 * mh + (pdh & 1);
-          float a[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int tp = 0; tp < 27; ++tp) {
-            const int dd = od + tp / 9 - 1, hh = oh + (tp / 3) % 3 - 1, ww = ow + tp % 3 - 1;
-            const bool in = (unsigned)dd < (unsigned)Dd && (unsigned)hh < (unsigned)Hh && (unsigned)ww < (unsigned)Ww;
-            const float xv = buf_load_f32(rs, in ? (unsigned)(((dd * Hh + hh) * Ww + ww) * 4) : kOffOut);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) a[q] = fmaf(w0[tp * 8 + c0 + q], xv, a[q]);
-          }
-          sk[r][pdh] = ok[r] ? make_float4(relu(fmaf(a[0], al0[c0], sh0[c0])), relu(fmaf(a[1], al0[c0 + 1], sh0[c0 + 1])),
-                                           relu(fmaf(a[2], al0[c0 + 2], sh0[c0 + 2])),
-                                           relu(fmaf(a[3], al0[c0 + 3], sh0[c0 + 3])))
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-      }
+      for (int pdh = 0; pdh < 4; ++pdh)
+        sk[r][pdh] = ok[r] ? *reinterpret_cast<const float4*>(skip + oo[r] + (pdh >> 1) * plane + (pdh & 1) * row)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     floatx4 acc[NBW][4];
 #pragma unroll
@@ -1451,20 +1253,7 @@ static int launch_deconv_c8(const float* x, const float* w, const float* al, con
   const long ntiles = (long)B * ((g.Di + TDI - 1) / TDI) * ((g.Hi + THI - 1) / THI) * ((g.Wi + 15) / 16);
   const long grid = persistent_grid(deconv3d_c8_kernel<TDI, THI>, ntiles);
   hipLaunchKernelGGL((deconv3d_c8_kernel<TDI, THI>), dim3((unsigned)grid), dim3(256), 0, st, x, w, al, sh, skip, y, g,
-                     (int)ntiles, nullptr, nullptr, nullptr);
-  TMVS_CHECK_LAUNCH();
-  return TMVS_OK;
-}
-
-// conv11 with its skip (conv0's output) recomputed from the cost volume `sim` (see deconv3d_c8_kernel)
-template <int TDI, int THI>
-static int launch_deconv_c8_c0(const float* x, const float* w, const float* al, const float* sh, const float* sim,
-                               const float* w0, const float* al0, const float* sh0, float* y, int B, const Geo& g,
-                               hipStream_t st) {
-  const long ntiles = (long)B * ((g.Di + TDI - 1) / TDI) * ((g.Hi + THI - 1) / THI) * ((g.Wi + 15) / 16);
-  const long grid = persistent_grid(deconv3d_c8_kernel<TDI, THI, true>, ntiles);
-  hipLaunchKernelGGL((deconv3d_c8_kernel<TDI, THI, true>), dim3((unsigned)grid), dim3(256), 0, st, x, w, al, sh, sim, y,
-                     g, (int)ntiles, w0, al0, sh0);
+                     (int)ntiles);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -1622,19 +1411,10 @@ static int costregnet_trunk(const float* x, int batch, int depth, int height, in
   const int D2 = D1 / 2, H2 = H1 / 2, W2 = W1 / 2;
   const int D3 = D2 / 2, H3 = H2 / 2, W3 = W2 / 2;
   int rc;
-  // conv0 is never materialised: conv1 and conv11 recompute it from the cost volume x
-  {
-    Geo g1;
-    g1.Di = D0;
-    g1.Hi = H0;
-    g1.Wi = W0;
-    g1.Do = D1;
-    g1.Ho = H1;
-    g1.Wo = W1;
-    if ((rc = launch_conv1_c0<2, 4>(x, w->w[0], w->alpha[0], w->shift[0], w->w[1], w->alpha[1], w->shift[1], c1, batch,
-                                    g1, st)))
-      return rc;
-  }
+  const dim3 g0x((unsigned)(((W0 + kProbCols - 1) / kProbCols) * ((H0 + 3) / 4) * batch * ((D0 + kDChunk - 1) / kDChunk)));
+  hipLaunchKernelGGL(conv0_kernel, g0x, dim3(256), 0, st, x, c0, D0, H0, W0, w->w[0], w->alpha[0], w->shift[0]);
+  TMVS_CHECK_LAUNCH();
+  if ((rc = conv_dispatch(c0, batch, c, D0, H0, W0, w->w[1], w->alpha[1], w->shift[1], 2 * c, 2, c1, st))) return rc;
   if ((rc = conv_dispatch(c1, batch, 2 * c, D1, H1, W1, w->w[2], w->alpha[2], w->shift[2], 2 * c, 1, c2, st)))
     return rc;
   if ((rc = conv_dispatch(c2, batch, 2 * c, D1, H1, W1, w->w[3], w->alpha[3], w->shift[3], 4 * c, 2, c3, st)))
@@ -1649,20 +1429,8 @@ static int costregnet_trunk(const float* x, int batch, int depth, int height, in
     return rc;
   if ((rc = deconv_dispatch(x7, batch, 4 * c, D2, H2, W2, w->w[8], w->alpha[8], w->shift[8], 2 * c, c2, x9, st)))
     return rc;
-  {
-    Geo g11;
-    g11.Di = D1;
-    g11.Hi = H1;
-    g11.Wi = W1;
-    g11.Do = D0;
-    g11.Ho = H0;
-    g11.Wo = W0;
-    rc = (D1 % 2 == 0) ? launch_deconv_c8_c0<2, 2>(x9, w->w[9], w->alpha[9], w->shift[9], x, w->w[0], w->alpha[0],
-                                                    w->shift[0], x11, batch, g11, st)
-                       : launch_deconv_c8_c0<1, 4>(x9, w->w[9], w->alpha[9], w->shift[9], x, w->w[0], w->alpha[0],
-                                                    w->shift[0], x11, batch, g11, st);
-    if (rc) return rc;
-  }
+  if ((rc = deconv_dispatch(x9, batch, 2 * c, D1, H1, W1, w->w[9], w->alpha[9], w->shift[9], c, c0, x11, st)))
+    return rc;
   *x11_out = x11;
   *c0_out = c0;
   return TMVS_OK;
