@@ -237,6 +237,14 @@ def run(args, world, rank, local):
             shard.timer = None
         model.decomposed = False
         spans = timer.durations()
+        # the same instrumentation on the timed step's own form (fused stage calls, pathway on its side
+        # stream concurrently with stage 1): per-call durations as they overlap in the timed region
+        otimer = EventTimer()
+        ops.set_timer(otimer)
+        for _ in range(args.profile_steps):
+            step()
+        ops.set_timer(None)
+        ospans = otimer.durations()
 
         e2e = end_to_end(model, args.e2e_steps, proj, dv_dev, dev) if args.e2e_steps > 0 and shard is None else None
     train = train_timing(args.train_steps, dev, world) if args.train_steps > 0 and shard is None else None
@@ -248,6 +256,10 @@ def run(args, world, rank, local):
         per_kernel.setdefault(n, []).append(ms)
     steps_p = max(1, args.profile_steps)
     breakdown = {n: round(sum(v) / steps_p, 4) for n, v in per_kernel.items()}
+    overlapped = {}
+    for n, ms in ospans:
+        overlapped[n] = overlapped.get(n, 0.0) + ms / steps_p
+    overlapped = {n: round(v, 4) for n, v in overlapped.items()}
 
     warp_bytes, cr_flop = algorithmic()
     warp_ms = per_kernel.get("tmvs_warp_corr", [])
@@ -291,8 +303,12 @@ def run(args, world, rank, local):
     if os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc))
+            src = traffic.get("_meta", {}).get("source", "profiles/pmc_traffic.json")
             for k in kern:
-                k["traffic"] = traffic.get(k["kernel"])
+                if k["kernel"] in traffic:
+                    # NOT measured in this run: rocprofv3 PMC passes of an earlier round (provenance below)
+                    k["traffic"] = traffic[k["kernel"]]
+                    k["traffic_source"] = f"profiles/pmc_traffic.json: {src}"
         except Exception:
             pass
 
@@ -330,6 +346,10 @@ def run(args, world, rank, local):
             "roofline": dominant,
             "roofline_kernels": kern,
             "kernel_ms_per_depth_map": breakdown,
+            "kernel_ms_source": "HIP events per C-ABI call in a DECOMPOSED pass (one call per op, pathway overlap "
+                                "off; roofline_kernels use it); call_ms_overlapped = the timed step's own calls "
+                                "(fused tmvs_depth_stage at stages 2/3, pathway on its side stream)",
+            "call_ms_overlapped": overlapped,
             "cpu_baseline": cpu,
             "abs_depth_l1_vs_ref": l1,
             "end_to_end": e2e,

@@ -57,6 +57,8 @@ def _oracle_partial(sd, feats, proj):
     def partial(fs, rows, hyp, stage, view_w, pw, sim_out, wsum_out, views=None):
         ref = feats[0]
         vws = []
+        sim_out.zero_()   # the HIP partial overwrites its outputs (ViewShard hands it uninitialised memory)
+        wsum_out.zero_()
         for v in views:
             warped = oracle.homo_warping(feats[1 + v], oracle.compose_proj(projs[1 + v]),
                                          oracle.compose_proj(projs[0]), hyp)

@@ -75,11 +75,14 @@ class ViewShard:
         fs: [1+n_local, h, w, C] NHWC (reference first); rows: [1, n_local, 12] host array.
         """
         d, h, w = hyp.shape[1], hyp.shape[2], hyp.shape[3]
-        buf = torch.zeros(1, d + 1, h, w, device=hyp.device, dtype=torch.float32)
+        # the partial kernels overwrite sim_sum / w_sum; only a rank without source views contributes zeros
+        buf = torch.empty(1, d + 1, h, w, device=hyp.device, dtype=torch.float32)
         sim_sum, w_sum = buf[:, :d], buf[:, d]
         new_vw = view_w
         if self.src_views:
             new_vw = self._partial(fs, rows, hyp, stage, view_w, pw, sim_sum, w_sum, rot_order=rot_order)
+        else:
+            buf.zero_()
         self.allreduce(buf)
         sim = buf[:, :d]
         self._finalize(sim, buf[:, d])
