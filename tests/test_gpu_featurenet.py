@@ -165,3 +165,51 @@ def test_conv2d_bn_relu_shapes(cin, cout, k, stride, h, w):
     out = ops.conv2d_bn_relu(xin.to(DEV), ops.conv2d_pack(weight).to(DEV), cout, k, stride, bn=fold, relu=True,
                              nchw_input=(cin == 3))
     np.testing.assert_allclose(to_np(out), to_np(ref.permute(0, 2, 3, 1)), rtol=1e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("cout,h,w,scale", [(32, 20, 28, 2.5), (16, 37, 45, 1.0), (8, 9, 70, 4.0), (32, 33, 40, 0.3)])
+def test_dcn_backward_vs_autograd(cout, h, w, scale):
+    """tmvs_dcn_backward (dx scatter, d offsets / mask logits, dW) against fp64 autograd through the
+    oracle's deform_conv2d. Offsets of `scale` std: at 2.5 / 4.0 many corners fall beyond the LDS
+    window's R = 2 px halo (the global-atomic path) and outside the image; one corner region sits at
+    exact integer positions (right-sided bilinear derivative, as torchvision's backward).
+    Bar: 2e-5 of each gradient's max |value| (fp32 dot products of <= 288 terms vs exact)."""
+    from transmvsnet_amd.featurenet_train import _taps, _untaps
+    torch.manual_seed(cout + h)
+    b = 2
+    x = torch.randn(b, 32, h, w, dtype=torch.float64)
+    om = torch.randn(b, 27, h, w, dtype=torch.float64)
+    om[:, :18] *= scale
+    om[0, :18, :3, :3] = 0.0
+    weight = torch.randn(cout, 32, 3, 3, dtype=torch.float64) * 0.06
+    dy = torch.randn(b, cout, h, w, dtype=torch.float64)
+    x32, om32, w32 = x.float(), om.float(), weight.float()
+    # the exact reference: fp64 autograd at the fp32-rounded inputs
+    xr = x32.double().requires_grad_(True)
+    offr = om32[:, :18].double().requires_grad_(True)
+    mlr = om32[:, 18:].double().requires_grad_(True)
+    wr = w32.double().requires_grad_(True)
+    out = oracle.deform_conv2d(xr, offr, wr, None, 1, torch.sigmoid(mlr))
+    (out * dy.float().double()).sum().backward()
+    dx = torch.zeros(b, h, w, 32, device=DEV)
+    dom, dw = ops.dcn_backward(x32.permute(0, 2, 3, 1).contiguous().to(DEV), om32.contiguous().to(DEV),
+                               _taps(w32).to(DEV), dy.float().permute(0, 2, 3, 1).contiguous().to(DEV), dx)
+    torch.cuda.synchronize()
+
+    def close(got, ref, tag):
+        ref = ref.detach()
+        err = float((got.double().cpu() - ref).abs().max()) / max(float(ref.abs().max()), 1e-30)
+        assert err <= 2e-5, (tag, err)
+
+    close(dx.permute(0, 3, 1, 2), xr.grad, "dx")
+    close(dom[..., :18].permute(0, 3, 1, 2), offr.grad, "d offset")
+    close(dom[..., 18:27].permute(0, 3, 1, 2), mlr.grad, "d mask logit")
+    assert float(dom[..., 27:].abs().max()) == 0.0
+    close(_untaps(dw, tuple(weight.shape)), wr.grad, "dW")
+    # determinism: the in-window scatter is integer (order-free); a second call gives the same bits
+    # when no corner leaves the window
+    if scale <= 0.3:
+        dx2 = torch.zeros_like(dx)
+        ops.dcn_backward(x32.permute(0, 2, 3, 1).contiguous().to(DEV), om32.contiguous().to(DEV),
+                         _taps(w32).to(DEV), dy.float().permute(0, 2, 3, 1).contiguous().to(DEV), dx2)
+        assert torch.equal(dx, dx2)

@@ -21,10 +21,11 @@
 //
 // Determinism: every reduction over pixels (weight / bias gradients) is block partials in fp64 plus
 // a fixed-order combine. The DCN input gradient is a scatter with data-dependent targets; it is
-// accumulated in fp32 LDS windows (per block tile + a halo of R px; LDS atomics, so the rounding
-// order inside a window varies run to run) that are summed per texel in a fixed block order; only
-// corners beyond the window (offsets over R px) go to global memory with fp32 atomics, as
-// torchvision's deformable_col2im adds every contribution with atomicAdd.
+// accumulated in LDS windows (per block tile + a halo of R px) of 64-bit fixed point -- integer LDS
+// atomics are order-independent, and on gfx950 ds_add_u64 is ~20x the rate of ds_add_f32 (193
+// cycles per wave-instruction per CU, scripts/micro/lds_atomic.hip) -- converted once and summed per
+// texel in a fixed block order; only corners beyond the window (offsets over R px) go to global
+// memory with fp32 atomics, as torchvision's deformable_col2im adds every contribution with atomicAdd.
 #include "common.h"
 
 namespace tmvs {
@@ -352,20 +353,49 @@ constexpr int TY = 8, TX = 32;          // block tile of reference pixels (one t
 constexpr int R = 2;                    // offsets up to R px keep every corner in the LDS window
 constexpr int CC = 8;                   // channels per pass
 constexpr int WR = TY + 2 * R + 3, WC = TX + 2 * R + 3;
+// one cell of one pass receives at most TY*TX pixels x 9 taps contributions
+constexpr long kMaxAdds = (long)TY * TX * 9;
 }  // namespace dbw
 
+// max |x| over n floats of two tensors -> atomicMax on the bit patterns (non-negative floats order as
+// unsigned): mx[0] over a (n_a), mx[1] over b (n_b)
+__global__ __launch_bounds__(kBlk) void absmax2_kernel(const float* __restrict__ a, long n_a,
+                                                       const float* __restrict__ b, long n_b,
+                                                       unsigned* __restrict__ mx) {
+  const float* x = blockIdx.y ? b : a;
+  const long n = blockIdx.y ? n_b : n_a;
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * kBlk + threadIdx.x; i < n; i += (long)gridDim.x * kBlk) m = fmaxf(m, fabsf(x[i]));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(mx + blockIdx.y, __float_as_uint(m));
+}
+
+// the window's fixed-point exponent: a contribution m * w_bilinear * dcol_c has magnitude at most
+// CO max|dy| max|W| (m, w_bilinear <= 1), a cell at most kMaxAdds of them: with 2^e above that
+// bound, units of 2^-(62 - e) keep every cell's int64 sum in range, at a resolution 2^-40 or finer
+// relative to the largest possible contribution
+__device__ __forceinline__ int dcn_fix_shift(const unsigned* __restrict__ mx, int CO) {
+  const double bound = (double)__uint_as_float(mx[0]) * (double)__uint_as_float(mx[1]) * CO * (double)dbw::kMaxAdds;
+  if (!(bound > 0.0) || !(bound < 1e300)) return 0;
+  int e;
+  frexp(bound, &e);
+  return 62 - e;
+}
+
 // dcol, d om (NHWC [B][H][W][32], channels 27..31 zero) and the scatter of m * dcol into dx (accumulated)
-// The block's LDS window of each 8-channel pass is written whole to scratch [block][cell][32] (plain,
-// coalesced stores); dcn_gather_windows_kernel then sums, for every texel, the <= 4 windows covering
-// it in a fixed block order (deterministic, no global atomics). Corners beyond the window (offsets
-// over kR px) are added to dx with fp32 atomics before that pass.
+// The block's LDS window of each 8-channel pass (int64 fixed point, see the header) is converted and
+// written whole to scratch [block][cell][32] (plain, coalesced stores); dcn_gather_windows_kernel then
+// sums, for every texel, the <= 4 windows covering it in a fixed block order (no global atomics).
+// Corners beyond the window (offsets over R px) are added to dx with fp32 atomics before that pass.
 template <int CO>
 __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ om,
                                                            const float* __restrict__ wt, const float* __restrict__ dy,
-                                                           int B, int H, int W, float* __restrict__ dx,
-                                                           float* __restrict__ dom, float* __restrict__ scratch) {
+                                                           int B, int H, int W, const unsigned* __restrict__ absmax,
+                                                           float* __restrict__ dx, float* __restrict__ dom,
+                                                           float* __restrict__ scratch) {
   using namespace dbw;
-  __shared__ float win[WR * WC * CC];
+  __shared__ unsigned long long win[WR * WC * CC];
+  const int kfix = dcn_fix_shift(absmax, CO);
   const int tid = threadIdx.x;
   const int ntx = (W + TX - 1) / TX, nty = (H + TY - 1) / TY;
   int blk = blockIdx.x;
@@ -394,7 +424,7 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
   for (int k = 0; k < 9; ++k) aY[k] = aX[k] = aM[k] = 0.f;
 #pragma unroll 1
   for (int cc = 0; cc < 32 / CC; ++cc) {
-    for (int i = tid; i < WR * WC * CC; i += kBlk) win[i] = 0.f;
+    for (int i = tid; i < WR * WC * CC; i += kBlk) win[i] = 0ull;
     __syncthreads();
     if (live) {
 #pragma unroll 1
@@ -445,10 +475,12 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
           const float f = s.m * wq[q];
           if (f == 0.f) continue;  // a zero bilinear weight (integer sample positions: 3 of 4 corners)
           if ((unsigned)ry < (unsigned)WR && (unsigned)rx < (unsigned)WC) {
-            // channel-major window: neighbouring pixels' corners are neighbouring words (no bank conflicts)
-            float* wp = win + ry * WC + rx;
+            // channel-major window: neighbouring pixels' corners are neighbouring words
+            unsigned long long* wp = win + ry * WC + rx;
 #pragma unroll
-            for (int c = 0; c < CC; ++c) atomicAdd(wp + c * (WR * WC), f * dc[c]);
+            for (int c = 0; c < CC; ++c)
+              atomicAdd(wp + c * (WR * WC),
+                        (unsigned long long)__double2ll_rn(ldexp((double)(f * dc[c]), kfix)));
           } else {  // an offset beyond the window: straight to global memory
             float* gp = dxb + ((size_t)cy * W + cx) * 32 + cc * CC;
 #pragma unroll
@@ -461,7 +493,7 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
     float* sb = scratch + (size_t)blockIdx.x * (WR * WC) * 32 + cc * CC;
     for (int i = tid; i < WR * WC * CC; i += kBlk) {
       const int cell = i / CC, c = i - cell * CC;  // 8 lanes = one cell's 32-byte channel chunk
-      sb[(size_t)cell * 32 + c] = win[c * (WR * WC) + cell];
+      sb[(size_t)cell * 32 + c] = (float)ldexp((double)(long long)win[c * (WR * WC) + cell], -kfix);
     }
     __syncthreads();
   }
@@ -693,10 +725,13 @@ static long dcn_data_blocks(int batch, int height, int width) {
   return (long)batch * ((height + dbw::TY - 1) / dbw::TY) * ((width + dbw::TX - 1) / dbw::TX);
 }
 
-// [weight-gradient partials (fp64)][per-block scatter windows: blocks x WR*WC x 32 fp32]
+static size_t dcn_scratch_bytes(int batch, int height, int width) {
+  return (size_t)dcn_data_blocks(batch, height, width) * dbw::WR * dbw::WC * 32 * sizeof(float);
+}
+
+// [weight-gradient partials (fp64)][per-block scatter windows: blocks x WR*WC x 32 fp32][absmax: 2 u32]
 extern "C" size_t tmvs_dcn_backward_workspace(int batch, int cout, int height, int width) {
-  return dcn_partials_bytes(batch, cout, height, width) +
-         (size_t)dcn_data_blocks(batch, height, width) * dbw::WR * dbw::WC * 32 * sizeof(float);
+  return dcn_partials_bytes(batch, cout, height, width) + dcn_scratch_bytes(batch, height, width) + 256;
 }
 
 extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, const float* w_taps, const float* dy_nhwc,
@@ -714,10 +749,15 @@ extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, 
   const int nblk = (int)((np + ppb - 1) / ppb);
   double* part = (double*)workspace;
   float* scratch = (float*)((char*)workspace + dcn_partials_bytes(batch, cout, height, width));
+  unsigned* absmax = (unsigned*)((char*)scratch + dcn_scratch_bytes(batch, height, width));
+  if (hipMemsetAsync(absmax, 0, 2 * sizeof(unsigned), st) != hipSuccess) return TMVS_ERR_HIP;
+  hipLaunchKernelGGL(absmax2_kernel, dim3((unsigned)std::min<long>(1024, (np * cout + kBlk - 1) / kBlk), 2),
+                     dim3(kBlk), 0, st, dy_nhwc, np * cout, w_taps, 9L * cout * 32, absmax);
+  TMVS_CHECK_LAUNCH();
 #define TMVS_DCNB(CO)                                                                                             \
   case CO:                                                                                                        \
     hipLaunchKernelGGL(dcn_bwd_data_kernel<CO>, dim3(nbd), dim3(kBlk), 0, st, x_nhwc, offset_mask, w_taps, dy_nhwc, \
-                       batch, height, width, dx_nhwc, dom_nhwc, scratch);                                         \
+                       batch, height, width, (const unsigned*)absmax, dx_nhwc, dom_nhwc, scratch);                \
     TMVS_CHECK_LAUNCH();                                                                                          \
     hipLaunchKernelGGL(dcn_gather_windows_kernel, dim3((unsigned)((np * 32 + kBlk - 1) / kBlk)), dim3(kBlk), 0, st,  \
                        (const float*)scratch, batch, height, width, dx_nhwc);                                     \
