@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TMVS_ABI_VERSION 5
+#define TMVS_ABI_VERSION 6
 
 #define TMVS_OK 0
 #define TMVS_ERR_ARG (-1)    /* null pointer / non-positive size / bad enum        */
@@ -240,6 +240,18 @@ int tmvs_depth_stage(const float* depth_values, int n_values, const float* prev_
 #define TMVS_CONV_ACCUMULATE 2
 int tmvs_conv3d_generic(const float* x, int batch, int cin, int d_in, int h_in, int w_in, const float* w, int cout,
                         int d_out, int h_out, int w_out, int stride, int flags, float* y, void* stream);
+
+/* The same convolutions on the inference layers' MFMA kernels (tmvs_conv3d_bn_relu /
+ * tmvs_deconv3d_bn_relu_add) with the raw epilogue (no BN, no ReLU): y = conv(x) (+ skip).
+ * transposed = 0: Conv3d k3 p1, stride 1 or 2 (the train forward of conv1..conv6; the dgrad of
+ * conv7/9/11 with their ConvTranspose weight tensor read as a Conv3d [Ci_t][Co_t] weight);
+ * transposed = 1: ConvTranspose3d k3 s2 p1 op1, output 2x input (the train forward of conv7/9/11;
+ * the dgrad of the stride-2 Conv3d layers, whose weight read as ConvTranspose [Co][Ci] is the
+ * adjoint), skip (nullable, transposed only, must not alias y) added. wpk [27][cout][cin].
+ * Shapes: the inference layers' (cin, cout) pairs -- stride 1: 16->16, 32->32, 64->64; stride 2:
+ * 8->16, 16->32, 32->64; transposed: 64->32, 32->16, 16->8 -- else TMVS_ERR_SHAPE.            */
+int tmvs_conv3d_mfma(const float* x, int batch, int cin, int d, int h, int w, const float* wpk, int cout, int stride,
+                     int transposed, const float* skip, float* y, void* stream);
 
 /* dw[k][a][b] = sum_p direct[p][a] * gathered[p*stride - 1 + k][b] over every voxel p of direct
  * [B][pd][ph][pw][a_ch] (taps outside gathered [B][gd][gh][gw][b_ch] are zero): the weight

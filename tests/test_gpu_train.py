@@ -84,6 +84,37 @@ def test_costregnet_train_forward_backward(shape):
     print(shape, rep)
 
 
+@pytest.mark.parametrize("cin,cout,stride,transposed", [(16, 16, 1, False), (32, 32, 1, False), (64, 64, 1, False),
+                                                         (8, 16, 2, False), (16, 32, 2, False), (32, 64, 2, False),
+                                                         (64, 32, 2, True), (32, 16, 2, True), (16, 8, 2, True)])
+@pytest.mark.parametrize("dims", [(4, 10, 20), (1, 6, 37)])
+def test_conv3d_mfma_raw_vs_torch(cin, cout, stride, transposed, dims):
+    """tmvs_conv3d_mfma (the inference layers' MFMA kernels with the raw epilogue) against torch's
+    fp32 conv3d / conv_transpose3d (k3 p1, op1), incl. ragged H/W and depth 1, negative outputs kept
+    (no ReLU) and the transposed form's skip add. Bar: 2e-6 of max|y| (K = 27 cin fp32 terms)."""
+    import torch.nn.functional as F
+    from transmvsnet_amd import ops
+    from transmvsnet_amd.train import _pack_fwd
+    torch.manual_seed(cin + cout + dims[2])
+    x = torch.randn(1, cin, *dims)
+    w = torch.randn(*((cin, cout) if transposed else (cout, cin)), 3, 3, 3) * 0.1
+    if transposed:
+        ref = F.conv_transpose3d(x, w, stride=2, padding=1, output_padding=1)
+        skip = torch.randn(ref.shape)
+        ref = ref + skip
+    else:
+        ref = F.conv3d(x, w, stride=stride, padding=1)
+        skip = None
+    got = ops.conv3d_mfma(x.permute(0, 2, 3, 4, 1).contiguous().to(DEV), _pack_fwd(w, transposed).to(DEV), cout,
+                          stride, transposed,
+                          skip=None if skip is None else skip.permute(0, 2, 3, 4, 1).contiguous().to(DEV))
+    got = got.permute(0, 4, 1, 2, 3).cpu()
+    assert got.shape == ref.shape
+    assert float(got.min()) < 0.0
+    err = float((got - ref).abs().max()) / float(ref.abs().max())
+    assert err < 2e-6, err
+
+
 @pytest.mark.parametrize("c,d,h,w,nv,scale", [(8, 8, 24, 32, 3, 1.0), (32, 48, 144, 192, 3, 1.0),
                                               (16, 32, 288, 384, 3, 1.0), (8, 8, 576, 768, 3, 1.0),
                                               (8, 8, 576, 768, 3, 1e-9), (32, 48, 144, 192, 3, 1e-7)])

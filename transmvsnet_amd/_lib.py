@@ -76,6 +76,7 @@ SIGNATURES = {
     "tmvs_linattn_bwd_kv": (I, [P, P, L, L, P, P, P, P]),
     "tmvs_adam_step": (I, [P, P, P, P, L, D, D, D, D, D, I, P]),
     "tmvs_conv3d_generic": (I, [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P]),
+    "tmvs_conv3d_mfma": (I, [P, I, I, I, I, I, P, I, I, I, P, P, P]),
     "tmvs_conv3d_wgrad_workspace": (S, [I, I, I, I, I, I]),
     "tmvs_conv3d_wgrad": (I, [P, I, I, I, I, I, P, I, I, I, I, I, P, S, P, P]),
     "tmvs_bn_train_workspace": (S, [L, I]),
@@ -94,7 +95,7 @@ SIGNATURES = {
     "tmvs_softmax_backward": (I, [P, P, I, I, I, I, P, P]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 PW_NPARAMS = 201
 ENC_NPARAMS = 8544
 KV_NFLOATS = 160

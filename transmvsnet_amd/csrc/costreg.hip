@@ -1,7 +1,10 @@
 // CostRegNet (models/module.py:425-456) on MI355X.
 //
 // Layout: NDHWC fp32 activations. Eval-mode BN is an (alpha, shift) epilogue,
-// y = relu(fmaf(acc, alpha, shift)) (tmvs_bn_fold; the reference CPU kernel's exact form).
+// y = relu(fmaf(acc, alpha, shift)) (tmvs_bn_fold; the reference CPU kernel's exact form). The MFMA
+// layers' epilogue is act(v, lo) = v > lo ? v : lo: lo = 0 is that ReLU; lo = -inf with alpha = 1,
+// shift = 0 and no skip gives the raw convolution the training path runs them for
+// (tmvs_conv3d_mfma: train-mode forward before BatchNorm, and the data gradients).
 //
 // Mid layers (conv1..conv6, deconv conv7/9/11) are LDS-staged implicit GEMMs on the exact-fp32 matrix
 // cores, v_mfma_f32_16x16x4_f32 (64 FLOP/clk/SIMD, the fp32 peak; no xf32 on gfx950):
@@ -51,7 +54,10 @@ struct VecN<2> {
 struct Geo {
   int Di, Hi, Wi;  // input dims
   int Do, Ho, Wo;  // output dims
+  float lo;        // epilogue floor: 0 = ReLU, -inf = none
 };
+
+__device__ __forceinline__ float act(float v, float lo) { return v > lo ? v : lo; }
 
 // ---------------------------------------------------------------- conv3d k3 p1, stride S
 // Workgroup tile: 16 output voxels along w x TH rows x TD depth slices, MBB blocks of 16
@@ -192,10 +198,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
       const int od = od0 + rr / TH, oh = oh0 + rr % TH;
       if (od >= g.Do || oh >= g.Ho) continue;
       float4 o;
-      o.x = relu(fmaf(acc[r][m][0], al.x, sh.x));
-      o.y = relu(fmaf(acc[r][m][1], al.y, sh.y));
-      o.z = relu(fmaf(acc[r][m][2], al.z, sh.z));
-      o.w = relu(fmaf(acc[r][m][3], al.w, sh.w));
+      o.x = act(fmaf(acc[r][m][0], al.x, sh.x), g.lo);
+      o.y = act(fmaf(acc[r][m][1], al.y, sh.y), g.lo);
+      o.z = act(fmaf(acc[r][m][2], al.z, sh.z), g.lo);
+      o.w = act(fmaf(acc[r][m][3], al.w, sh.w), g.lo);
       *reinterpret_cast<float4*>(y + (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co) = o;
     }
   }
@@ -295,10 +301,10 @@ __global__ __launch_bounds__(256) void conv3d_direct_kernel(const float* __restr
       const int oh = hg * NBW + r;
       if (oh >= g.Ho) continue;
       float4 o;
-      o.x = relu(fmaf(acc[r][m][0], al.x, sh.x));
-      o.y = relu(fmaf(acc[r][m][1], al.y, sh.y));
-      o.z = relu(fmaf(acc[r][m][2], al.z, sh.z));
-      o.w = relu(fmaf(acc[r][m][3], al.w, sh.w));
+      o.x = act(fmaf(acc[r][m][0], al.x, sh.x), g.lo);
+      o.y = act(fmaf(acc[r][m][1], al.y, sh.y), g.lo);
+      o.z = act(fmaf(acc[r][m][2], al.z, sh.z), g.lo);
+      o.w = act(fmaf(acc[r][m][3], al.w, sh.w), g.lo);
       *reinterpret_cast<float4*>(y + (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co) = o;
     }
   }
@@ -438,8 +444,8 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
           for (int pw = 0; pw < 2; ++pw) {
             const floatx4 a = acc[r][pdh * 2 + pw][0];
             *reinterpret_cast<float4*>(eb + (2 * col + pw) * 8 + co) =
-                make_float4(relu(fmaf(a[0], al.x, sh.x)), relu(fmaf(a[1], al.y, sh.y)),
-                            relu(fmaf(a[2], al.z, sh.z)), relu(fmaf(a[3], al.w, sh.w)));
+                make_float4(act(fmaf(a[0], al.x, sh.x), g.lo), act(fmaf(a[1], al.y, sh.y), g.lo),
+                            act(fmaf(a[2], al.z, sh.z), g.lo), act(fmaf(a[3], al.w, sh.w), g.lo));
           }
         }
         __builtin_amdgcn_wave_barrier();
@@ -448,7 +454,7 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
         const int od = 2 * md + (pdh >> 1), oh = 2 * mh + (pdh & 1);
         if (md < g.Di && mh < g.Hi && ow < 2 * g.Wi) {
           const size_t o = (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * 8 + (lane & 1) * 4;
-          const float4 s = *reinterpret_cast<const float4*>(skip + o);
+          const float4 s = skip ? *reinterpret_cast<const float4*>(skip + o) : make_float4(0.f, 0.f, 0.f, 0.f);
           *reinterpret_cast<float4*>(y + o) = make_float4(s.x + v.x, s.y + v.y, s.z + v.z, s.w + v.w);
         }
       }
@@ -472,12 +478,12 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
       for (int cls = 0; cls < 8; ++cls) {
         const int od = 2 * md + (cls >> 2), oh = 2 * mh + ((cls >> 1) & 1), ow = 2 * mw + (cls & 1);
         const size_t o = (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co;
-        const float4 s = *reinterpret_cast<const float4*>(skip + o);
+        const float4 s = skip ? *reinterpret_cast<const float4*>(skip + o) : make_float4(0.f, 0.f, 0.f, 0.f);
         float4 v;
-        v.x = s.x + relu(fmaf(acc[r][cls][m][0], al.x, sh.x));
-        v.y = s.y + relu(fmaf(acc[r][cls][m][1], al.y, sh.y));
-        v.z = s.z + relu(fmaf(acc[r][cls][m][2], al.z, sh.z));
-        v.w = s.w + relu(fmaf(acc[r][cls][m][3], al.w, sh.w));
+        v.x = s.x + act(fmaf(acc[r][cls][m][0], al.x, sh.x), g.lo);
+        v.y = s.y + act(fmaf(acc[r][cls][m][1], al.y, sh.y), g.lo);
+        v.z = s.z + act(fmaf(acc[r][cls][m][2], al.z, sh.z), g.lo);
+        v.w = s.w + act(fmaf(acc[r][cls][m][3], al.w, sh.w), g.lo);
         *reinterpret_cast<float4*>(y + o) = v;
       }
     }
@@ -856,10 +862,10 @@ __global__ __launch_bounds__(256) void conv3d_c16_kernel(const float* __restrict
       const int od = c.od0 + rr / TH, oh = c.oh0 + rr % TH;
       if (ow >= g.Wo || od >= g.Do || oh >= g.Ho) continue;
       float4 o;
-      o.x = relu(fmaf(acc[r][0], al.x, sh.x));
-      o.y = relu(fmaf(acc[r][1], al.y, sh.y));
-      o.z = relu(fmaf(acc[r][2], al.z, sh.z));
-      o.w = relu(fmaf(acc[r][3], al.w, sh.w));
+      o.x = act(fmaf(acc[r][0], al.x, sh.x), g.lo);
+      o.y = act(fmaf(acc[r][1], al.y, sh.y), g.lo);
+      o.z = act(fmaf(acc[r][2], al.z, sh.z), g.lo);
+      o.w = act(fmaf(acc[r][3], al.w, sh.w), g.lo);
       *reinterpret_cast<float4*>(y + (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * C + kgrp * 4) = o;
     }
     __syncthreads();  // every wave is done with the tile
@@ -1021,10 +1027,10 @@ __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __re
       const int od = c.od0 + rr / TH, oh = c.oh0 + rr % TH;
       if (ow >= g.Wo || od >= g.Do || oh >= g.Ho) continue;
       float4 o;
-      o.x = relu(fmaf(acc[r][0], al.x, sh.x));
-      o.y = relu(fmaf(acc[r][1], al.y, sh.y));
-      o.z = relu(fmaf(acc[r][2], al.z, sh.z));
-      o.w = relu(fmaf(acc[r][3], al.w, sh.w));
+      o.x = act(fmaf(acc[r][0], al.x, sh.x), g.lo);
+      o.y = act(fmaf(acc[r][1], al.y, sh.y), g.lo);
+      o.z = act(fmaf(acc[r][2], al.z, sh.z), g.lo);
+      o.w = act(fmaf(acc[r][3], al.w, sh.w), g.lo);
       *reinterpret_cast<float4*>(y + (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co) = o;
     }
     __syncthreads();
@@ -1182,7 +1188,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       oo[r] = (out_n + ((size_t)(2 * md) * g.Ho + 2 * mh) * g.Wo + ow) * 8 + (lane & 1) * 4;
 #pragma unroll
       for (int pdh = 0; pdh < 4; ++pdh)
-        sk[r][pdh] = ok[r] ? *reinterpret_cast<const float4*>(skip + oo[r] + (pdh >> 1) * plane + (pdh & 1) * row)
+        sk[r][pdh] = (ok[r] && skip) ? *reinterpret_cast<const float4*>(skip + oo[r] + (pdh >> 1) * plane + (pdh & 1) * row)
                            : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     floatx4 acc[NBW][4];
@@ -1232,8 +1238,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       for (int pdh = 0; pdh < 4; ++pdh) {
         const floatx4 a = acc[r][pdh];
         *reinterpret_cast<float4*>(eb + (2 * col + (kgrp >> 1)) * 8 + cq) =
-            make_float4(relu(fmaf(a[0], al.x, sh.x)), relu(fmaf(a[1], al.y, sh.y)), relu(fmaf(a[2], al.z, sh.z)),
-                        relu(fmaf(a[3], al.w, sh.w)));
+            make_float4(act(fmaf(a[0], al.x, sh.x), g.lo), act(fmaf(a[1], al.y, sh.y), g.lo), act(fmaf(a[2], al.z, sh.z), g.lo),
+                        act(fmaf(a[3], al.w, sh.w), g.lo));
         __builtin_amdgcn_wave_barrier();
         const float4 v = *reinterpret_cast<const float4*>(eb + lane * 4);
         __builtin_amdgcn_wave_barrier();
@@ -1270,8 +1276,9 @@ static int launch_deconv(const float* x, const float* w, const float* al, const 
 }
 
 static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, const float* wpk, const float* al,
-                         const float* sh, int cout, int stride, float* y, hipStream_t st) {
+                         const float* sh, int cout, int stride, float* y, hipStream_t st, float lo = 0.f) {
   Geo g;
+  g.lo = lo;
   g.Di = d;
   g.Hi = h;
   g.Wi = w;
@@ -1311,8 +1318,9 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
 }
 
 static int deconv_dispatch(const float* x, int B, int cin, int d, int h, int w, const float* wpk, const float* al,
-                           const float* sh, int cout, const float* skip, float* y, hipStream_t st) {
+                           const float* sh, int cout, const float* skip, float* y, hipStream_t st, float lo = 0.f) {
   Geo g;
+  g.lo = lo;
   g.Di = d;
   g.Hi = h;
   g.Wi = w;
@@ -1352,6 +1360,36 @@ extern "C" int tmvs_deconv3d_bn_relu_add(const float* x, int batch, int cin, int
   if (!x || !wpk || !alpha || !shift || !skip || !y || batch <= 0 || d <= 0 || h <= 0 || w <= 0)
     return TMVS_ERR_ARG;
   return deconv_dispatch(x, batch, cin, d, h, w, wpk, alpha, shift, cout, skip, y, (hipStream_t)stream);
+}
+
+// alpha = 1, shift = 0 for the raw (training) form of the MFMA layers (64 = the widest layer)
+__device__ float kUnitAlpha[64] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f,
+                                   1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f,
+                                   1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f,
+                                   1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+__device__ float kZeroShift[64];
+
+extern "C" int tmvs_conv3d_mfma(const float* x, int batch, int cin, int d, int h, int w, const float* wpk, int cout,
+                                int stride, int transposed, const float* skip, float* y, void* stream) {
+  if (!x || !wpk || !y || batch <= 0 || d <= 0 || h <= 0 || w <= 0) return TMVS_ERR_ARG;
+  if (transposed ? stride != 2 : (stride != 1 && stride != 2)) return TMVS_ERR_ARG;
+  if (skip && !transposed) return TMVS_ERR_ARG;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return TMVS_ERR_HIP;
+  static const float* unit[64][2];  // per device: the symbols' addresses
+  if (!unit[dev][0]) {
+    void *a, *b;
+    if (hipGetSymbolAddress(&a, HIP_SYMBOL(kUnitAlpha)) != hipSuccess ||
+        hipGetSymbolAddress(&b, HIP_SYMBOL(kZeroShift)) != hipSuccess)
+      return TMVS_ERR_HIP;
+    unit[dev][1] = (const float*)b;
+    unit[dev][0] = (const float*)a;
+  }
+  const float *al = unit[dev][0], *sh = unit[dev][1];
+  const float lo = -__builtin_huge_valf();
+  hipStream_t st = (hipStream_t)stream;
+  if (transposed) return deconv_dispatch(x, batch, cin, d, h, w, wpk, al, sh, cout, skip, y, st, lo);
+  return conv_dispatch(x, batch, cin, d, h, w, wpk, al, sh, cout, stride, y, st, lo);
 }
 
 static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }

@@ -580,6 +580,34 @@ def conv3d_generic(x, w_packed, cout, out_dhw, stride, transposed=False, out=Non
     return y
 
 
+# (cin, cout, stride) of the inference layers' MFMA kernels (tmvs_conv3d_mfma); transposed: (cin, cout)
+MFMA_CONV = {(16, 16, 1), (32, 32, 1), (64, 64, 1), (8, 16, 2), (16, 32, 2), (32, 64, 2)}
+MFMA_DECONV = {(64, 32), (32, 16), (16, 8)}
+
+
+def conv3d_mfma(x, w_packed, cout, stride, transposed=False, skip=None):
+    """tmvs_conv3d_mfma: x NDHWC [B,D,H,W,Cin], w_packed [27][cout][Cin] -> y [B,D',H',W',cout], the raw
+    convolution (no BN / ReLU) on the inference MFMA kernels; transposed = ConvTranspose3d k3 s2 p1 op1
+    (+ skip, a separate [B,2D,2H,2W,cout] tensor)."""
+    _dev(x, "x")
+    _dev(w_packed, "w_packed")
+    _dev(skip, "skip")
+    b, d, h, w, cin = x.shape
+    if transposed:
+        dims = (2 * d, 2 * h, 2 * w)
+    else:
+        dims = (d, h, w) if stride == 1 else ((d - 1) // 2 + 1, (h - 1) // 2 + 1, (w - 1) // 2 + 1)
+    y = torch.empty(b, *dims, cout, device=x.device)
+    if skip is not None and (tuple(skip.shape) != tuple(y.shape) or not skip.is_contiguous()):
+        raise ValueError("conv3d_mfma: skip must be a contiguous tensor of the output's shape")
+    if tuple(w_packed.shape) != (27, cout, cin):
+        raise ValueError("conv3d_mfma: w_packed must be [27, cout, cin]")
+    with _Span("tmvs_conv3d_mfma"):
+        _lib.check(_lib_h().tmvs_conv3d_mfma(_ptr(x.contiguous()), b, cin, d, h, w, _ptr(w_packed), cout, stride,
+                                             int(transposed), _ptr(skip), _ptr(y), _stream()), "tmvs_conv3d_mfma")
+    return y
+
+
 def conv3d_wgrad(direct, gathered, stride):
     """tmvs_conv3d_wgrad: direct [B,pd,ph,pw,A], gathered [B,gd,gh,gw,BC] -> dw [27][A][BC]."""
     _dev(direct, "direct")
@@ -888,7 +916,7 @@ def adam_step(param_flat, grad_flat, exp_avg, exp_avg_sq, lr, betas, eps, weight
                                            float(weight_decay), int(step), _stream()), "tmvs_adam_step")
 
 
-for _name in ("conv3d_generic", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn_relu_backward", "warp_corr_backward",
+for _name in ("conv3d_generic", "conv3d_mfma", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn_relu_backward", "warp_corr_backward",
               "upsample2_add_nhwc", "upsample2_backward_nhwc", "pixelwise_train_forward", "aggregate_train", "aggregate_train_backward", "pixelwise_train_backward",
               "token_linear", "token_wgrad", "layer_norm_fwd", "layer_norm_bwd", "linattn_fwd", "linattn_bwd_q",
               "linattn_bwd_kv", "adam_step"):

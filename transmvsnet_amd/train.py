@@ -298,6 +298,39 @@ def _pack_dgrad(w, transposed):
     return w.reshape(co, ci, 27).permute(2, 1, 0).contiguous()
 
 
+def _conv_fwd(x, w, cout, odims, stride, transposed):
+    """A CostRegNet layer's raw convolution (before train-mode BN): the inference layers' MFMA kernels
+    (tmvs_conv3d_mfma) where they cover the (cin, cout, stride), else tmvs_conv3d_generic (conv0's
+    Cin = 1)."""
+    cin = x.shape[-1]
+    if (cin, cout) in ops.MFMA_DECONV if transposed else (cin, cout, stride) in ops.MFMA_CONV:
+        return ops.conv3d_mfma(x, _pack_fwd(w, transposed), cout, stride, transposed)
+    return ops.conv3d_generic(x, _pack_fwd(w, transposed), cout, odims, stride, transposed)
+
+
+def _conv_dgrad(dz, w, cin, idims, stride, transposed, acc):
+    """d input of a layer (+ acc, the gradient already gathered for that tensor through a skip):
+      ConvTranspose3d -> Conv3d stride 2 of dz with the same weight tensor read as [Ci_t][Co_t];
+      Conv3d stride 2 -> ConvTranspose3d of dz with the weight read as ConvTranspose [Co][Ci];
+      Conv3d stride 1 -> Conv3d of dz with the taps reversed and [Co][Ci] transposed.
+    On the MFMA kernels where they cover the shape, else the generic gathers."""
+    cout = dz.shape[-1]
+    pk = _pack_dgrad(w, transposed)  # [27][Ci][Co]
+    if transposed and (cout, cin, 2) in ops.MFMA_CONV:
+        dx = ops.conv3d_mfma(dz, pk, cin, 2)
+    elif not transposed and stride == 2 and (cout, cin) in ops.MFMA_DECONV:
+        return ops.conv3d_mfma(dz, pk, cin, 2, transposed=True, skip=acc)
+    elif not transposed and stride == 1 and (cout, cin, 1) in ops.MFMA_CONV:
+        dx = ops.conv3d_mfma(dz, pk.flip(0).contiguous(), cin, 1)
+    elif transposed:  # strided gather of dz
+        return ops.conv3d_generic(dz, pk, cin, idims, 2, False, out=acc)
+    else:  # transposed gather of dz
+        return ops.conv3d_generic(dz, pk, cin, idims, stride, True, out=acc)
+    if acc is None:
+        return dx
+    return acc.add_(dx)
+
+
 def _unpack_wgrad(dw27, shape):
     """[27][A][B] -> the torch weight layout [A][B][3][3][3] (A, B = Co, Ci or Ci, Co)."""
     return dw27.permute(1, 2, 0).reshape(shape).contiguous()
@@ -321,7 +354,7 @@ class _CostRegNetTrain(torch.autograd.Function):
             wt, g, bt = ws[3 * i], ws[3 * i + 1], ws[3 * i + 2]
             cout = wt.shape[1] if transposed else wt.shape[0]
             odims = tuple(2 * n for n in dims) if transposed else (dims if stride == 1 else _down(dims))
-            z = ops.conv3d_generic(cur, _pack_fwd(wt.detach(), transposed), cout, odims, stride, transposed)
+            z = _conv_fwd(cur, wt.detach(), cout, odims, stride, transposed)
             mean, var = ops.bn_stats(z)
             y = ops.bn_relu_train(z, mean, var, g.detach(), bt.detach(), eps,
                                   skip=acts[skip][0] if skip is not None else None)
@@ -367,11 +400,7 @@ class _CostRegNetTrain(torch.autograd.Function):
             prev = _LAYERS[i - 1][0] if i > 0 else "input"
             cin = xin.shape[-1]
             acc = dout.get(prev)
-            if transposed:   # dgrad of ConvTranspose3d: strided gather of dz
-                dx = ops.conv3d_generic(dz, _pack_dgrad(wt.detach(), True), cin, idims, 2, False, out=acc)
-            else:            # dgrad of Conv3d: transposed gather of dz
-                dx = ops.conv3d_generic(dz, _pack_dgrad(wt.detach(), False), cin, idims, stride, True, out=acc)
-            dout[prev] = dx
+            dout[prev] = _conv_dgrad(dz, wt.detach(), cin, idims, stride, transposed, acc)
         dx = dout["input"].view(b, d, h, w)
         return (dx, None, None, *grads)
 
