@@ -392,14 +392,7 @@ def end_to_end(model, steps, proj, dv_dev, dev):
                         "path above"}
 
 
-def train_timing(steps, dev, world):
-    """C5 training step (BlendedMVS 768x576, N=4, 48/32/8, one sample per rank): the reference's
-    train_sample body (finetune.py:144-168) on the drop-in model -- model.train(); zero_grad;
-    outputs = model(imgs, proj, depth_values) (FeatureNet + DCN, FMT, pathway, 3 DepthNet stages, all
-    HIP with autograd); focal_loss_bld (dlossw 1,1,1) -> loss.backward() (HIP backward of every block,
-    FeatureNet/DCN included); DDP's gradient all-reduce when world > 1; Adam step (FlatAdam). HIP
-    events, median of `steps` after 1 warm-up; max over ranks. Also times the same step from
-    FeatureNet's outputs (the round-2 measurement, for continuity)."""
+def _train_setup(dev):
     from transmvsnet_amd import TransMVSNet, loss as hip_loss, synthetic
     from transmvsnet_amd.train import FlatAdam, depth_stages_train, fmt_train, pathway_train
     h5, w5, n5 = 576, 768, 4
@@ -440,6 +433,25 @@ def train_timing(steps, dev, world):
                            dlossw=(1.0, 1.0, 1.0), loss="focal_bld", depth_interval=dint)
         opt.allreduce()
         opt.step()
+
+    return full_step, features_step, m
+
+
+def train_steps(dev):
+    """The C5 training closures (full_step, features_step, model) train_timing times (also run alone
+    by scripts/diag/train_prof.py under rocprofv3)."""
+    return _train_setup(dev)
+
+
+def train_timing(steps, dev, world):
+    """C5 training step (BlendedMVS 768x576, N=4, 48/32/8, one sample per rank): the reference's
+    train_sample body (finetune.py:144-168) on the drop-in model -- model.train(); zero_grad;
+    outputs = model(imgs, proj, depth_values) (FeatureNet + DCN, FMT, pathway, 3 DepthNet stages, all
+    HIP with autograd); focal_loss_bld (dlossw 1,1,1) -> loss.backward() (HIP backward of every block,
+    FeatureNet/DCN included); DDP's gradient all-reduce when world > 1; Adam step (FlatAdam). HIP
+    events, median of `steps` after 1 warm-up; max over ranks. Also times the same step from
+    FeatureNet's outputs (the round-2 measurement, for continuity)."""
+    full_step, features_step, m = _train_setup(dev)
 
     def timed(fn):
         ts = []

@@ -1,33 +1,22 @@
-"""Build an experimental copy of the library with extra compile flags (A/B kernel experiments).
+"""A/B variant of the library: recompile ONE translation unit with extra -D flags, link it with the
+product objects into variants/NAME/libtransmvs_hip.so (load with TMVS_LIB_PATH=...).
 
-    python scripts/build_variant.py NAME -DFLAG=1 ...   ->  variants/NAME/libtransmvs_hip.so
-
-Load it with TMVS_LIB_PATH=variants/NAME/libtransmvs_hip.so (transmvsnet_amd/_lib.py).
+    python scripts/build_variant.py NAME SOURCE.hip -DFLAG=VALUE [...]
 """
-import concurrent.futures as cf
 import os
 import subprocess
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from transmvsnet_amd import build as B  # noqa: E402
+from transmvsnet_amd import build as b  # noqa: E402
 
-name, extra = sys.argv[1], sys.argv[2:]
-out = os.path.join(B.ROOT, "variants", name)
+name, src, flags = sys.argv[1], sys.argv[2], sys.argv[3:]
+b.build()
+out = os.path.join(b.ROOT, "variants", name)
 os.makedirs(out, exist_ok=True)
-
-
-def comp(src):
-    o = os.path.join(out, src.replace(".hip", ".o"))
-    r = subprocess.run([B.HIPCC, *B.CFLAGS, *extra, "-c", os.path.join(B.CSRC, src), "-o", o], capture_output=True,
-                       text=True)
-    if r.returncode:
-        raise SystemExit(r.stderr)
-    return o
-
-
-with cf.ThreadPoolExecutor(8) as ex:
-    objs = list(ex.map(comp, B.SOURCES))
+obj = os.path.join(out, src.replace(".hip", ".o"))
+subprocess.run([b.HIPCC, *b.CFLAGS, *flags, "-c", os.path.join(b.CSRC, src), "-o", obj], check=True)
+objs = [obj if s == src else os.path.join(b.OBJ, s.replace(".hip", ".o")) for s in b.SOURCES]
 lib = os.path.join(out, "libtransmvs_hip.so")
-subprocess.run([B.HIPCC, "-shared", f"--offload-arch={B.ARCH}", "-fno-gpu-rdc", "-o", lib, *objs], check=True)
+subprocess.run([b.HIPCC, "-shared", f"--offload-arch={b.ARCH}", "-fno-gpu-rdc", "-o", lib, *objs], check=True)
 print(lib)

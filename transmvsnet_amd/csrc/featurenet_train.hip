@@ -363,9 +363,12 @@ __global__ __launch_bounds__(kBlk) void absmax2_kernel(const float* __restrict__
                                                        const float* __restrict__ b, long n_b,
                                                        unsigned* __restrict__ mx) {
   const float* x = blockIdx.y ? b : a;
-  const long n = blockIdx.y ? n_b : n_a;
+  const long n = blockIdx.y ? n_b : n_a;  // a multiple of 4 (16-byte aligned tensors)
   float m = 0.f;
-  for (long i = (long)blockIdx.x * kBlk + threadIdx.x; i < n; i += (long)gridDim.x * kBlk) m = fmaxf(m, fabsf(x[i]));
+  for (long i = (long)blockIdx.x * kBlk + threadIdx.x; 4 * i < n; i += (long)gridDim.x * kBlk) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0) atomicMax(mx + blockIdx.y, __float_as_uint(m));
 }
@@ -751,7 +754,7 @@ extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, 
   float* scratch = (float*)((char*)workspace + dcn_partials_bytes(batch, cout, height, width));
   unsigned* absmax = (unsigned*)((char*)scratch + dcn_scratch_bytes(batch, height, width));
   if (hipMemsetAsync(absmax, 0, 2 * sizeof(unsigned), st) != hipSuccess) return TMVS_ERR_HIP;
-  hipLaunchKernelGGL(absmax2_kernel, dim3((unsigned)std::min<long>(1024, (np * cout + kBlk - 1) / kBlk), 2),
+  hipLaunchKernelGGL(absmax2_kernel, dim3((unsigned)std::min<long>(8192, (np * cout / 4 + kBlk - 1) / kBlk), 2),
                      dim3(kBlk), 0, st, dy_nhwc, np * cout, w_taps, 9L * cout * 32, absmax);
   TMVS_CHECK_LAUNCH();
 #define TMVS_DCNB(CO)                                                                                             \

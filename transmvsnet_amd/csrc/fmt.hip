@@ -229,11 +229,6 @@ __device__ __forceinline__ void load_token_frag(const float* __restrict__ row, f
   }
 }
 
-constexpr int kTilesPerWave = 8;  // 16-token tiles per wave (kv): amortises the weight-fragment loads
-#ifndef TMVS_APPLY_TPW
-#define TMVS_APPLY_TPW 4
-#endif
-constexpr int kApplyTilesPerWave = TMVS_APPLY_TPW;  // apply: weights come from LDS; more, shorter waves
 constexpr int kKvTilesPerWave = 8;     // kv: at most this many tiles per wave (see kv_tiles_per_wave)
 
 // (KV, Ksum) partial sums: per wave, tiles of 16 source tokens; K, V by MFMA; per lane the
@@ -369,16 +364,25 @@ __global__ __launch_bounds__(1024) void fmt_kv_combine_kernel(const float* __res
 
 // The rest of EncoderLayer.forward for tiles of 16 query tokens, entirely in registers;
 // kApplyNT tiles are processed together so their MFMA chains interleave.
-constexpr int kApplyNT = 1;
+#ifndef TMVS_APPLY_NT
+#define TMVS_APPLY_NT 1
+#endif
+constexpr int kApplyNT = TMVS_APPLY_NT;
 __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, int L, const float* __restrict__ kvg,
-                                                        long kv_stride, const float* __restrict__ w) {
+                                                        long kv_stride, const float* __restrict__ w, int tpw) {
   __shared__ float kvs[kKV];
-  __shared__ float vec[TMVS_ENC_NPARAMS - TMVS_ENC_LN1G];  // LN params
+  // the per-feature vectors, read from LDS in the tile loop: a global load there is a full memory
+  // latency, and its vmcnt(0) wait also drains the next tile's token prefetch
+  // [0, 32) BQ  [32, 64) BO  [64, 128) B1  [128, 160) B2  [160, 288) LN1G LN1B LN2G LN2B
+  constexpr int kVB2 = 128, kVLN = 160;
+  __shared__ float vec[288];
   const int v = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4;
   if (threadIdx.x < kKV) kvs[threadIdx.x] = kvg[(size_t)v * kv_stride + threadIdx.x];
-  if (threadIdx.x < 128) vec[threadIdx.x] = w[TMVS_ENC_LN1G + threadIdx.x];
+  for (int i = threadIdx.x; i < 288; i += blockDim.x)
+    vec[i] = i < 32 ? w[TMVS_ENC_BQ + i] : i < 64 ? w[TMVS_ENC_BO + i - 32] : i < 128 ? w[TMVS_ENC_B1 + i - 64]
+                                                                                      : w[TMVS_ENC_B2 + i - kVB2];
   __shared__ __attribute__((aligned(16))) float frag[32 * 32 * 2 + 64 * 32 * 2];  // Wq, Wo, W1, W2 fragments
   stage_afrag<32, 32, false>(w + TMVS_ENC_WQ, frag);
   stage_afrag<32, 32, false>(w + TMVS_ENC_WO, frag + 1024);
@@ -386,33 +390,33 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
   stage_afrag<32, 64, true>(w + TMVS_ENC_W2T, frag + 4096);
   __syncthreads();
   float* xv = x + (size_t)v * L * kD;
-  const int tile0 = (blockIdx.x * 4 + wv) * kApplyTilesPerWave;
-  static_assert(kApplyNT == 1, "the token prefetch below assumes one tile per iteration");
-  floatx4 xnext[2];  // the next tile's tokens, loaded while this tile computes
-  if (tile0 * 16 < L) {
-    const int t = tile0 * 16 + (lane & 15);
-    load_token_frag(xv + (size_t)(t < L ? t : L - 1) * kD, xnext, lane);
+  const int tile0 = (blockIdx.x * 4 + wv) * tpw;
+  constexpr int NT = kApplyNT;
+  floatx4 xnext[NT][2];  // the next group's tokens, loaded while this group computes
+#pragma unroll
+  for (int p = 0; p < NT; ++p) {
+    const int t = (tile0 + p) * 16 + (lane & 15);
+    if (p < tpw) load_token_frag(xv + (size_t)(t < L ? t : L - 1) * kD, xnext[p], lane);
   }
 #pragma unroll 1
-  for (int it = 0; it < kApplyTilesPerWave; it += kApplyNT) {
+  for (int it = 0; it < tpw; it += NT) {
     if ((tile0 + it) * 16 >= L) break;  // wave-uniform
-    constexpr int NT = kApplyNT;
     int salt = 0;  // opaque offset: fragment reads stay in the loop (not hoisted back into VGPRs)
     asm volatile("" : "+v"(salt));
     const float* fr = frag + salt;
+    const float* vb = vec + salt;
     float* row[NT];
     bool ok[NT];
     floatx4 xs[NT][2];
-    {
-      const int t = (tile0 + it) * 16 + (lane & 15);
-      ok[0] = t < L;
-      row[0] = xv + (size_t)(ok[0] ? t : L - 1) * kD;
-      xs[0][0] = xnext[0];
-      xs[0][1] = xnext[1];
-      if (it + 1 < kApplyTilesPerWave && (tile0 + it + 1) * 16 < L) {
-        const int tn = t + 16;
-        load_token_frag(xv + (size_t)(tn < L ? tn : L - 1) * kD, xnext, lane);
-      }
+#pragma unroll
+    for (int p = 0; p < NT; ++p) {
+      const int t = (tile0 + it + p) * 16 + (lane & 15);
+      ok[p] = t < L && it + p < tpw;
+      row[p] = xv + (size_t)(t < L ? t : L - 1) * kD;
+      xs[p][0] = xnext[p][0];
+      xs[p][1] = xnext[p][1];
+      const int tn = t + 16 * NT;
+      if (it + NT + p < tpw) load_token_frag(xv + (size_t)(tn < L ? tn : L - 1) * kD, xnext[p], lane);
     }
     floatx4 q[NT][2], msg[NT][2];
     mfma_linear_lds<32, 32, NT>(fr, xs, q, lane);
@@ -423,7 +427,7 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
         const int h = 4 * mb + g;
         float qe[4];
 #pragma unroll
-        for (int d = 0; d < 4; ++d) qe[d] = elu1(q[p][mb][d] + w[TMVS_ENC_BQ + 4 * h + d]);
+        for (int d = 0; d < 4; ++d) qe[d] = elu1(q[p][mb][d] + vb[4 * h + d]);
         float den = 0.f;
 #pragma unroll
         for (int d = 0; d < 4; ++d) den = fmaf(qe[d], kvs[128 + h * 4 + d], den);
@@ -443,8 +447,8 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xs[p][mb][r] = xs[p][mb][r] + (a[p][mb][r] + w[TMVS_ENC_BO + 16 * mb + 4 * g + r]);
-      layer_norm_frag(xs[p], vec, vec + kD, lane);
+        for (int r = 0; r < 4; ++r) xs[p][mb][r] = xs[p][mb][r] + (a[p][mb][r] + vb[32 + 16 * mb + 4 * g + r]);
+      layer_norm_frag(xs[p], vb + kVLN, vb + kVLN + kD, lane);
     }
     floatx4 hdn[NT][4], ff[NT][2];
     mfma_linear_lds<64, 32, NT>(fr + 2048, xs, hdn, lane);
@@ -453,15 +457,15 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) hdn[p][mb][r] = relu(hdn[p][mb][r] + w[TMVS_ENC_B1 + 16 * mb + 4 * g + r]);
+        for (int r = 0; r < 4; ++r) hdn[p][mb][r] = relu(hdn[p][mb][r] + vb[64 + 16 * mb + 4 * g + r]);
     mfma_linear_lds<32, 64, NT>(fr + 4096, hdn, ff, lane);
 #pragma unroll
     for (int p = 0; p < NT; ++p) {
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xs[p][mb][r] = xs[p][mb][r] + (ff[p][mb][r] + w[TMVS_ENC_B2 + 16 * mb + 4 * g + r]);
-      layer_norm_frag(xs[p], vec + 2 * kD, vec + 3 * kD, lane);
+        for (int r = 0; r < 4; ++r) xs[p][mb][r] = xs[p][mb][r] + (ff[p][mb][r] + vb[kVB2 + 16 * mb + 4 * g + r]);
+      layer_norm_frag(xs[p], vb + kVLN + 2 * kD, vb + kVLN + 3 * kD, lane);
       if (ok[p]) {
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb)
@@ -472,22 +476,48 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
   }
 }
 
-// Tiles per wave: as many as possible (small partial slabs, short combine) while the launch still
-// has >= 2048 waves (2 per SIMD); the one-view cross-attention K/V otherwise runs at 0.1 waves/SIMD.
-#ifndef TMVS_KV_MIN_WAVES
-#define TMVS_KV_MIN_WAVES 2048
-#endif
+// Resident 4-wave blocks of `kernel` on the whole GPU (its occupancy at 256 threads: VGPRs, LDS)
+template <typename K>
+static long block_slots(K kernel) {
+  int dev = 0, cus = 0, per = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess || per <= 0) per = 4;
+  return (long)(cus > 0 ? cus : 256) * per;
+}
+static int wave_slots_kv() {
+  static long slots = 0;
+  if (!slots) slots = 4 * block_slots(fmt_kv_partial_kernel);
+  return (int)slots;
+}
+static int wave_slots_apply() {
+  static long slots = 0;
+  if (!slots) slots = 4 * block_slots(fmt_apply_kernel);
+  return (int)slots;
+}
+
+// Tiles per wave: the launch in ONE round of resident waves (each wave's tiles are a dependent
+// chain, so a launch lasts about tpw tile-latencies): 2.4 waves/SIMD at 8 tiles per wave for the
+// 5-view self-attention K/V (r05f); 2 to kKvTilesPerWave (1 measured slower for the one-view K/V:
+// twice the partial slabs for the combine).
 static int kv_tiles_per_wave(int nv, int S) {
-  const int tiles = (S + 15) / 16;
-  int tpw = kKvTilesPerWave;
-  while (tpw > 2 && (long)nv * ((tiles + tpw - 1) / tpw) < TMVS_KV_MIN_WAVES) tpw >>= 1;
-  return tpw;
+  const long tiles = (long)nv * ((S + 15) / 16);
+  return (int)std::min<long>(kKvTilesPerWave, std::max<long>(2, (tiles + wave_slots_kv() - 1) / wave_slots_kv()));
 }
 static int kv_nblk(int nv, int S) {
   const int per = 16 * 4 * kv_tiles_per_wave(nv, S);
   return (S + per - 1) / per;
 }
-static int apply_nblk(int L) { return (L + 16 * 4 * kApplyTilesPerWave - 1) / (16 * 4 * kApplyTilesPerWave); }
+// Tiles per wave for the apply: the whole launch in ONE round of resident waves (5 per SIMD at its
+// 92 VGPRs since the bias vectors moved to LDS): with a fixed 4 tiles per wave the C2 grid (5 x 3888
+// tiles = 4.75 waves per SIMD at 4/SIMD) ran as a full round plus a 3/4-empty second one (2.4
+// waves/SIMD on average, r05f).
+static int apply_tiles_per_wave(int nv, int L) {
+  const long tiles = (long)nv * ((L + 15) / 16);
+  const long tpw = std::max<long>(1, (tiles + wave_slots_apply() - 1) / wave_slots_apply());
+  return (int)((tpw + kApplyNT - 1) / kApplyNT * kApplyNT);  // whole groups of kApplyNT tiles
+}
+static int apply_nblk(int L, int tpw) { return (L + 16 * 4 * tpw - 1) / (16 * 4 * tpw); }
 
 }  // namespace tmvs
 
@@ -525,8 +555,9 @@ extern "C" int tmvs_fmt_kv(const float* source, int nv, int s_tokens, const floa
 extern "C" int tmvs_fmt_apply(float* x, int nv, int l_tokens, const float* kv, long kv_view_stride,
                               const float* enc_w, void* stream) {
   if (!x || !kv || !enc_w || nv <= 0 || l_tokens <= 0 || kv_view_stride < 0) return TMVS_ERR_ARG;
-  hipLaunchKernelGGL(fmt_apply_kernel, dim3(apply_nblk(l_tokens), nv), dim3(256), 0, (hipStream_t)stream, x,
-                     l_tokens, kv, kv_view_stride, enc_w);
+  const int tpw = apply_tiles_per_wave(nv, l_tokens);
+  hipLaunchKernelGGL(fmt_apply_kernel, dim3(apply_nblk(l_tokens, tpw), nv), dim3(256), 0, (hipStream_t)stream, x,
+                     l_tokens, kv, kv_view_stride, enc_w, tpw);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
