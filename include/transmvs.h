@@ -363,6 +363,19 @@ int tmvs_bn_relu_train(const float* z, long nvox, int channels, const float* mea
 int tmvs_bn_relu_backward(const float* dy, const float* z, long nvox, int channels, const float* mean,
                           const float* var, const float* gamma, const float* beta, float eps, void* workspace,
                           size_t workspace_bytes, float* dz, float* dgamma, float* dbeta, void* stream);
+/* The same over `groups` consecutive [nvox][C] slabs with statistics per group (FeatureNet's BatchNorm2d
+ * runs once per view: models/TransMVSNet.py:165-166 calls FeatureNet per view) in one launch each:
+ * mean / var [groups][C]; dgamma / dbeta are the per-group sums added over the groups in order.   */
+size_t tmvs_bn_train_workspace_grouped(int groups, long nvox, int channels);
+int tmvs_bn_stats_grouped(const float* z, int groups, long nvox, int channels, void* workspace, size_t workspace_bytes,
+                          float* mean, float* var, void* stream);
+int tmvs_bn_relu_train_grouped(const float* z, int groups, long nvox, int channels, const float* mean,
+                               const float* var, const float* gamma, const float* beta, float eps, const float* skip,
+                               float* out, void* stream);
+int tmvs_bn_relu_backward_grouped(const float* dy, const float* z, int groups, long nvox, int channels,
+                                  const float* mean, const float* var, const float* gamma, const float* beta,
+                                  float eps, void* workspace, size_t workspace_bytes, float* dz, float* dgamma,
+                                  float* dbeta, void* stream);
 
 /* ------------------------------------------------------------------ FeatureNet heads
  * Modulated deformable convolution of DCN.forward (models/dcn.py:66-80; torchvision.ops.deform_conv2d,

@@ -616,3 +616,34 @@ def test_training_loop_reduces_loss():
     assert all(np.isfinite(losses)), losses
     assert losses[-1] < 0.9 * losses[0], losses
     assert not torch.equal(model.cost_regularization[0].conv0.bn.running_mean, rm0)
+
+
+def test_bn_grouped_matches_per_group():
+    """tmvs_bn_*_grouped (FeatureNet's per-view BatchNorm2d in one launch per pass) against torch
+    autograd of relu(batch_norm(training=True)) applied to each group separately, with the parameter
+    gradients summed over the groups. Bar: 1e-5 of each quantity's max |value|."""
+    import torch.nn.functional as F
+    from transmvsnet_amd import ops
+    torch.manual_seed(3)
+    g, h, w, c = 4, 23, 37, 16
+    z = torch.randn(g, h, w, c) * 2 + 0.3
+    dy = torch.randn(g, h, w, c)
+    gamma = torch.rand(c) + 0.5
+    beta = torch.randn(c) * 0.2
+    gm, gb = gamma.clone().requires_grad_(), beta.clone().requires_grad_()
+    zr = z.clone().requires_grad_()
+    ys = []
+    for v in range(g):
+        x = zr[v].permute(2, 0, 1).unsqueeze(0)
+        ys.append(F.relu(F.batch_norm(x, None, None, gm, gb, True, 0.1, 1e-5))[0].permute(1, 2, 0))
+    y = torch.stack(ys)
+    (y * dy).sum().backward()
+    zd = z.to(DEV)
+    mean, var = ops.bn_stats_grouped(zd)
+    yd = ops.bn_relu_train_grouped(zd, mean, var, gamma.to(DEV), beta.to(DEV), 1e-5)
+    dz, dg, db = ops.bn_relu_backward_grouped(dy.to(DEV), zd, mean, var, gamma.to(DEV), beta.to(DEV), 1e-5)
+    for v in range(g):
+        assert _rel(mean[v], z[v].reshape(-1, c).mean(0)) < 1e-6
+        assert _rel(var[v], z[v].reshape(-1, c).var(0, unbiased=False)) < 1e-5
+    for got, ref, tag in ((yd, y, "y"), (dz, zr.grad, "dz"), (dg, gm.grad, "dgamma"), (db, gb.grad, "dbeta")):
+        assert _rel(got, ref) < 1e-5, tag

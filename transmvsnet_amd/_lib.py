@@ -83,6 +83,10 @@ SIGNATURES = {
     "tmvs_bn_stats": (I, [P, L, I, P, S, P, P, P]),
     "tmvs_bn_relu_train": (I, [P, L, I, P, P, P, P, F, P, P, P]),
     "tmvs_bn_relu_backward": (I, [P, P, L, I, P, P, P, P, F, P, S, P, P, P, P]),
+    "tmvs_bn_train_workspace_grouped": (S, [I, L, I]),
+    "tmvs_bn_stats_grouped": (I, [P, I, L, I, P, S, P, P, P]),
+    "tmvs_bn_relu_train_grouped": (I, [P, I, L, I, P, P, P, P, F, P, P, P]),
+    "tmvs_bn_relu_backward_grouped": (I, [P, P, I, L, I, P, P, P, P, F, P, S, P, P, P, P]),
     "tmvs_conv2d_generic": (I, [P, I, I, I, I, P, P, I, I, I, I, I, I, I, P, P]),
     "tmvs_conv2d_wgrad_workspace": (S, [I, I, I, I, I, I]),
     "tmvs_conv2d_wgrad": (I, [P, I, I, I, I, P, I, I, I, I, I, I, P, S, P, P]),

@@ -469,9 +469,12 @@ __global__ __launch_bounds__(kTrainBlock) void sum_partials_kernel(const double*
 // ---------------------------------------------------------------- BatchNorm3d, train mode
 // Per-block fp64 partials of (sum z, sum z^2) per channel: thread t handles channel t % C of
 // rows t / C, t / C + 256/C, ... (C divides 256).
+// (grid.y = group: independent statistics of `groups` consecutive [nvox][C] slabs)
 __global__ __launch_bounds__(kTrainBlock) void bn_stats_partial_kernel(const float* __restrict__ z, long nvox, int C,
                                                                        long vpb, double* __restrict__ partial) {
   __shared__ double red[2][kTrainBlock];
+  z += (size_t)blockIdx.y * nvox * C;
+  partial += (size_t)blockIdx.y * gridDim.x * 2 * C;
   const int c = threadIdx.x % C, r0 = threadIdx.x / C, rs = kTrainBlock / C;
   const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
   double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};  // 4 independent chains
@@ -511,6 +514,8 @@ __global__ __launch_bounds__(kTrainBlock) void sum_double_partials_kernel(const 
                                                                           int K, double* __restrict__ out) {
   __shared__ double red[kTrainBlock];
   const int k = blockIdx.x;
+  partial += (size_t)blockIdx.y * nblk * K;  // grid.y = group
+  out += (size_t)blockIdx.y * K;
   double a = 0.0;
   for (int j = threadIdx.x; j < nblk; j += kTrainBlock) a += partial[(size_t)j * K + k];
   red[threadIdx.x] = a;
@@ -527,6 +532,9 @@ __global__ void bn_stats_finalize_kernel(const double* __restrict__ sums, int C,
                                          float* __restrict__ var) {
   const int c = threadIdx.x;
   if (c >= C) return;
+  sums += (size_t)blockIdx.x * 2 * C;  // grid = groups
+  mean += (size_t)blockIdx.x * C;
+  var += (size_t)blockIdx.x * C;
   const double m = sums[c] / (double)nvox;
   const double v = sums[C + c] / (double)nvox - m * m;
   mean[c] = (float)m;
@@ -538,8 +546,8 @@ __device__ __forceinline__ void bn_affine(float mean, float var, float g, float 
   sh = fmaf(-mean, al, bt);
 }
 
-// out = relu(fmaf(z, alpha, shift)) [+ skip]
-__global__ __launch_bounds__(kTrainBlock) void bn_relu_apply_kernel(const float* __restrict__ z, long n, int C,
+// out = relu(fmaf(z, alpha, shift)) [+ skip]; group i / per uses statistics [group][C]
+__global__ __launch_bounds__(kTrainBlock) void bn_relu_apply_kernel(const float* __restrict__ z, long n, long per, int C,
                                                                     const float* __restrict__ mean,
                                                                     const float* __restrict__ var,
                                                                     const float* __restrict__ gamma,
@@ -549,8 +557,9 @@ __global__ __launch_bounds__(kTrainBlock) void bn_relu_apply_kernel(const float*
   const long i = (long)blockIdx.x * kTrainBlock + threadIdx.x;
   if (i >= n) return;
   const int c = (int)(i % C);
+  const long gc = (i / per) * C + c;
   float al, sh;
-  bn_affine(mean[c], var[c], gamma[c], beta[c], eps, al, sh);
+  bn_affine(mean[gc], var[gc], gamma[c], beta[c], eps, al, sh);
   float y = relu(fmaf(z[i], al, sh));
   if (skip) y = skip[i] + y;
   out[i] = y;
@@ -563,6 +572,11 @@ __global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_partial_kernel(
     double* __restrict__ partial) {
   __shared__ double red[2][kTrainBlock];
   const int c = threadIdx.x % C, r0 = threadIdx.x / C, rs = kTrainBlock / C;
+  dy += (size_t)blockIdx.y * nvox * C;  // grid.y = group
+  z += (size_t)blockIdx.y * nvox * C;
+  partial += (size_t)blockIdx.y * gridDim.x * 2 * C;
+  mean += (size_t)blockIdx.y * C;
+  var += (size_t)blockIdx.y * C;
   float al, sh;
   bn_affine(mean[c], var[c], gamma[c], beta[c], eps, al, sh);
   const float m = mean[c], rstd = 1.f / sqrtf(var[c] + eps);
@@ -603,13 +617,19 @@ __global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_partial_kernel(
   }
 }
 
-// dbeta = sum g, dgamma = sum g*xhat (fp32) from the summed partials
-__global__ void bn_relu_bwd_finalize_kernel(const double* __restrict__ sums, int C, float* __restrict__ dgamma,
-                                            float* __restrict__ dbeta) {
+// dbeta = sum g, dgamma = sum g*xhat from the summed partials: per group in fp32, then added over the
+// groups in order (as autograd accumulates the per-view gradients of a module called per view)
+__global__ void bn_relu_bwd_finalize_kernel(const double* __restrict__ sums, int C, int groups,
+                                            float* __restrict__ dgamma, float* __restrict__ dbeta) {
   const int c = threadIdx.x;
   if (c >= C) return;
-  dbeta[c] = (float)sums[c];
-  dgamma[c] = (float)sums[C + c];
+  float b = (float)sums[c], g = (float)sums[C + c];
+  for (int k = 1; k < groups; ++k) {
+    b = b + (float)sums[(size_t)k * 2 * C + c];
+    g = g + (float)sums[(size_t)k * 2 * C + C + c];
+  }
+  dbeta[c] = b;
+  dgamma[c] = g;
 }
 
 // pass 2: dz = gamma*rstd/N * (N*g - sum g - xhat * sum g*xhat)
@@ -620,14 +640,17 @@ __global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_apply_kernel(
   const long i = (long)blockIdx.x * kTrainBlock + threadIdx.x;
   if (i >= n) return;
   const int c = (int)(i % C);
+  const long grp = i / (nvox * C);  // statistics and sums of element i's group
+  const long gc = grp * C + c;
+  const double* sg = sums + (size_t)grp * 2 * C;
   float al, sh;
-  bn_affine(mean[c], var[c], gamma[c], beta[c], eps, al, sh);
+  bn_affine(mean[gc], var[gc], gamma[c], beta[c], eps, al, sh);
   const float zz = z[i];
-  const float rstd = 1.f / sqrtf(var[c] + eps);
-  const float xhat = (zz - mean[c]) * rstd;
+  const float rstd = 1.f / sqrtf(var[gc] + eps);
+  const float xhat = (zz - mean[gc]) * rstd;
   const float g = fmaf(zz, al, sh) > 0.f ? dy[i] : 0.f;
   const double inv_n = 1.0 / (double)nvox;
-  const float mg = (float)(sums[c] * inv_n), mgx = (float)(sums[C + c] * inv_n);
+  const float mg = (float)(sg[c] * inv_n), mgx = (float)(sg[C + c] * inv_n);
   dz[i] = (gamma[c] * rstd) * ((g - mg) - xhat * mgx);
 }
 
@@ -746,28 +769,52 @@ extern "C" int tmvs_conv3d_wgrad(const float* direct, int a_ch, int batch, int p
   return TMVS_ERR_SHAPE;
 }
 
-extern "C" size_t tmvs_bn_train_workspace(long nvox, int channels) {
+static size_t bn_group_ws(long nvox, int channels) {
   const long vpb = bn_vpb(nvox);
   return (size_t)((nvox + vpb - 1) / vpb) * 2 * channels * sizeof(double) + 2 * channels * sizeof(double);
 }
 
-extern "C" int tmvs_bn_stats(const float* z, long nvox, int channels, void* workspace, size_t workspace_bytes,
-                             float* mean, float* var, void* stream) {
-  if (!z || !workspace || !mean || !var || nvox <= 0) return TMVS_ERR_ARG;
+extern "C" size_t tmvs_bn_train_workspace(long nvox, int channels) { return bn_group_ws(nvox, channels); }
+extern "C" size_t tmvs_bn_train_workspace_grouped(int groups, long nvox, int channels) {
+  return groups > 0 ? (size_t)groups * bn_group_ws(nvox, channels) : 0;
+}
+
+// workspace: [groups][nblk][2][C] partials, then [groups][2][C] sums
+extern "C" int tmvs_bn_stats_grouped(const float* z, int groups, long nvox, int channels, void* workspace,
+                                     size_t workspace_bytes, float* mean, float* var, void* stream) {
+  if (!z || !workspace || !mean || !var || nvox <= 0 || groups <= 0) return TMVS_ERR_ARG;
   if (channels <= 0 || kTrainBlock % channels) return TMVS_ERR_SHAPE;
-  if (workspace_bytes < tmvs_bn_train_workspace(nvox, channels)) return TMVS_ERR_ARG;
+  if (workspace_bytes < tmvs_bn_train_workspace_grouped(groups, nvox, channels)) return TMVS_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   const long vpb = bn_vpb(nvox);
   const int nblk = (int)((nvox + vpb - 1) / vpb);
   double* part = (double*)workspace;
-  hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(nblk), dim3(kTrainBlock), 0, st, z, nvox, channels, vpb, part);
+  hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(nblk, groups), dim3(kTrainBlock), 0, st, z, nvox, channels, vpb,
+                     part);
   TMVS_CHECK_LAUNCH();
-  double* sums = part + (size_t)nblk * 2 * channels;
-  hipLaunchKernelGGL(sum_double_partials_kernel, dim3(2 * channels), dim3(kTrainBlock), 0, st, (const double*)part,
-                     nblk, 2 * channels, sums);
+  double* sums = part + (size_t)groups * nblk * 2 * channels;
+  hipLaunchKernelGGL(sum_double_partials_kernel, dim3(2 * channels, groups), dim3(kTrainBlock), 0, st,
+                     (const double*)part, nblk, 2 * channels, sums);
   TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(1), dim3(64), 0, st, (const double*)sums, channels, nvox, mean,
-                     var);
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(groups), dim3(64), 0, st, (const double*)sums, channels, nvox,
+                     mean, var);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+extern "C" int tmvs_bn_stats(const float* z, long nvox, int channels, void* workspace, size_t workspace_bytes,
+                             float* mean, float* var, void* stream) {
+  return tmvs_bn_stats_grouped(z, 1, nvox, channels, workspace, workspace_bytes, mean, var, stream);
+}
+
+extern "C" int tmvs_bn_relu_train_grouped(const float* z, int groups, long nvox, int channels, const float* mean,
+                                          const float* var, const float* gamma, const float* beta, float eps,
+                                          const float* skip, float* out, void* stream) {
+  if (!z || !mean || !var || !gamma || !beta || !out || nvox <= 0 || channels <= 0 || groups <= 0)
+    return TMVS_ERR_ARG;
+  const long per = nvox * channels, n = per * groups;
+  hipLaunchKernelGGL(bn_relu_apply_kernel, dim3((unsigned)((n + kTrainBlock - 1) / kTrainBlock)), dim3(kTrainBlock), 0,
+                     (hipStream_t)stream, z, n, per, channels, mean, var, gamma, beta, eps, skip, out);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -775,10 +822,35 @@ extern "C" int tmvs_bn_stats(const float* z, long nvox, int channels, void* work
 extern "C" int tmvs_bn_relu_train(const float* z, long nvox, int channels, const float* mean, const float* var,
                                   const float* gamma, const float* beta, float eps, const float* skip, float* out,
                                   void* stream) {
-  if (!z || !mean || !var || !gamma || !beta || !out || nvox <= 0 || channels <= 0) return TMVS_ERR_ARG;
-  const long n = nvox * channels;
-  hipLaunchKernelGGL(bn_relu_apply_kernel, dim3((unsigned)((n + kTrainBlock - 1) / kTrainBlock)), dim3(kTrainBlock), 0,
-                     (hipStream_t)stream, z, n, channels, mean, var, gamma, beta, eps, skip, out);
+  return tmvs_bn_relu_train_grouped(z, 1, nvox, channels, mean, var, gamma, beta, eps, skip, out, stream);
+}
+
+extern "C" int tmvs_bn_relu_backward_grouped(const float* dy, const float* z, int groups, long nvox, int channels,
+                                             const float* mean, const float* var, const float* gamma,
+                                             const float* beta, float eps, void* workspace, size_t workspace_bytes,
+                                             float* dz, float* dgamma, float* dbeta, void* stream) {
+  if (!dy || !z || !mean || !var || !gamma || !beta || !workspace || !dz || !dgamma || !dbeta || nvox <= 0 ||
+      groups <= 0)
+    return TMVS_ERR_ARG;
+  if (channels <= 0 || kTrainBlock % channels) return TMVS_ERR_SHAPE;
+  if (workspace_bytes < tmvs_bn_train_workspace_grouped(groups, nvox, channels)) return TMVS_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const long vpb = bn_vpb(nvox);
+  const int nblk = (int)((nvox + vpb - 1) / vpb);
+  double* part = (double*)workspace;
+  double* sums = part + (size_t)groups * nblk * 2 * channels;
+  hipLaunchKernelGGL(bn_relu_bwd_partial_kernel, dim3(nblk, groups), dim3(kTrainBlock), 0, st, dy, z, nvox, channels,
+                     mean, var, gamma, beta, eps, vpb, part);
+  TMVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sum_double_partials_kernel, dim3(2 * channels, groups), dim3(kTrainBlock), 0, st,
+                     (const double*)part, nblk, 2 * channels, sums);
+  TMVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_relu_bwd_finalize_kernel, dim3(1), dim3(64), 0, st, (const double*)sums, channels, groups,
+                     dgamma, dbeta);
+  TMVS_CHECK_LAUNCH();
+  const long n = nvox * channels * groups;
+  hipLaunchKernelGGL(bn_relu_bwd_apply_kernel, dim3((unsigned)((n + kTrainBlock - 1) / kTrainBlock)), dim3(kTrainBlock),
+                     0, st, dy, z, n, channels, nvox, mean, var, gamma, beta, eps, (const double*)sums, dz);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -787,27 +859,6 @@ extern "C" int tmvs_bn_relu_backward(const float* dy, const float* z, long nvox,
                                      const float* var, const float* gamma, const float* beta, float eps,
                                      void* workspace, size_t workspace_bytes, float* dz, float* dgamma, float* dbeta,
                                      void* stream) {
-  if (!dy || !z || !mean || !var || !gamma || !beta || !workspace || !dz || !dgamma || !dbeta || nvox <= 0)
-    return TMVS_ERR_ARG;
-  if (channels <= 0 || kTrainBlock % channels) return TMVS_ERR_SHAPE;
-  if (workspace_bytes < tmvs_bn_train_workspace(nvox, channels)) return TMVS_ERR_ARG;
-  hipStream_t st = (hipStream_t)stream;
-  const long vpb = bn_vpb(nvox);
-  const int nblk = (int)((nvox + vpb - 1) / vpb);
-  double* part = (double*)workspace;
-  double* sums = part + (size_t)nblk * 2 * channels;
-  hipLaunchKernelGGL(bn_relu_bwd_partial_kernel, dim3(nblk), dim3(kTrainBlock), 0, st, dy, z, nvox, channels, mean, var,
-                     gamma, beta, eps, vpb, part);
-  TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(sum_double_partials_kernel, dim3(2 * channels), dim3(kTrainBlock), 0, st, (const double*)part,
-                     nblk, 2 * channels, sums);
-  TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_relu_bwd_finalize_kernel, dim3(1), dim3(64), 0, st, (const double*)sums, channels, dgamma,
-                     dbeta);
-  TMVS_CHECK_LAUNCH();
-  const long n = nvox * channels;
-  hipLaunchKernelGGL(bn_relu_bwd_apply_kernel, dim3((unsigned)((n + kTrainBlock - 1) / kTrainBlock)), dim3(kTrainBlock),
-                     0, st, dy, z, n, channels, nvox, mean, var, gamma, beta, eps, (const double*)sums, dz);
-  TMVS_CHECK_LAUNCH();
-  return TMVS_OK;
+  return tmvs_bn_relu_backward_grouped(dy, z, 1, nvox, channels, mean, var, gamma, beta, eps, workspace,
+                                       workspace_bytes, dz, dgamma, dbeta, stream);
 }

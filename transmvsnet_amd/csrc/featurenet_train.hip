@@ -358,19 +358,35 @@ constexpr long kMaxAdds = (long)TY * TX * 9;
 }  // namespace dbw
 
 // max |x| over n floats of two tensors -> atomicMax on the bit patterns (non-negative floats order as
-// unsigned): mx[0] over a (n_a), mx[1] over b (n_b)
+// unsigned): mx[0] over a (n_a), mx[1] over b (n_b). One atomic per block (a per-wave atomic on one
+// word from ~30K waves serialised to 0.6 ms).
 __global__ __launch_bounds__(kBlk) void absmax2_kernel(const float* __restrict__ a, long n_a,
                                                        const float* __restrict__ b, long n_b,
                                                        unsigned* __restrict__ mx) {
-  const float* x = blockIdx.y ? b : a;
-  const long n = blockIdx.y ? n_b : n_a;  // a multiple of 4 (16-byte aligned tensors)
-  float m = 0.f;
-  for (long i = (long)blockIdx.x * kBlk + threadIdx.x; 4 * i < n; i += (long)gridDim.x * kBlk) {
-    const float4 v = reinterpret_cast<const float4*>(x)[i];
-    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  __shared__ float red[kBlk / 64];
+  const float4* x = reinterpret_cast<const float4*>(blockIdx.y ? b : a);
+  const long n4 = (blockIdx.y ? n_b : n_a) / 4;  // a multiple of 4 floats (16-byte aligned tensors)
+  const long stride = (long)gridDim.x * kBlk;
+  float m0 = 0.f, m1 = 0.f;
+  long i = (long)blockIdx.x * kBlk + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {  // two independent loads in flight per thread
+    const float4 u = x[i], v = x[i + stride];
+    m0 = fmaxf(m0, fmaxf(fmaxf(fabsf(u.x), fabsf(u.y)), fmaxf(fabsf(u.z), fabsf(u.w))));
+    m1 = fmaxf(m1, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
   }
+  if (i < n4) {
+    const float4 u = x[i];
+    m0 = fmaxf(m0, fmaxf(fmaxf(fabsf(u.x), fabsf(u.y)), fmaxf(fabsf(u.z), fabsf(u.w))));
+  }
+  float m = fmaxf(m0, m1);
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) atomicMax(mx + blockIdx.y, __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = red[0];
+    for (int w = 1; w < kBlk / 64; ++w) t = fmaxf(t, red[w]);
+    atomicMax(mx + blockIdx.y, __float_as_uint(t));
+  }
 }
 
 // the window's fixed-point exponent: a contribution m * w_bilinear * dcol_c has magnitude at most
@@ -754,7 +770,7 @@ extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, 
   float* scratch = (float*)((char*)workspace + dcn_partials_bytes(batch, cout, height, width));
   unsigned* absmax = (unsigned*)((char*)scratch + dcn_scratch_bytes(batch, height, width));
   if (hipMemsetAsync(absmax, 0, 2 * sizeof(unsigned), st) != hipSuccess) return TMVS_ERR_HIP;
-  hipLaunchKernelGGL(absmax2_kernel, dim3((unsigned)std::min<long>(8192, (np * cout / 4 + kBlk - 1) / kBlk), 2),
+  hipLaunchKernelGGL(absmax2_kernel, dim3((unsigned)std::min<long>(512, (np * cout / 4 + kBlk - 1) / kBlk), 2),
                      dim3(kBlk), 0, st, dy_nhwc, np * cout, w_taps, 9L * cout * 32, absmax);
   TMVS_CHECK_LAUNCH();
 #define TMVS_DCNB(CO)                                                                                             \

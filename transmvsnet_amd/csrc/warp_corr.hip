@@ -683,7 +683,12 @@ static int dispatch_mode(bool pw, bool partial, int D, const float* ref, const f
 // the forward, incl. TMVS_WARP_ROT_PLAIN).
 // max |x| over n floats -> atomicMax on its bit pattern (non-negative floats order as unsigned);
 // a non-finite element sets the flag (the host raises: the gradient is unusable)
-__global__ void absmax_kernel(const float* __restrict__ x, long n, unsigned* __restrict__ out, int* __restrict__ flag) {
+// (one atomic per block: per-wave atomics on one word serialise)
+__global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, long n, unsigned* __restrict__ out,
+                                                     int* __restrict__ flag) {
+  __shared__ float red[4];
+  __shared__ int anybad;
+  if (threadIdx.x == 0) anybad = 0;
   float m = 0.f;
   bool bad = false;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -692,8 +697,14 @@ __global__ void absmax_kernel(const float* __restrict__ x, long n, unsigned* __r
     m = fmaxf(m, a);
   }
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
-  if (bad) atomicOr(flag, 1);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  if (bad) anybad = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+    if (anybad) atomicOr(flag, 1);
+  }
 }
 
 // the per-call fixed-point exponent: contributions are scaled by 2^k (see above)

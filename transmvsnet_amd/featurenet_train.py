@@ -11,9 +11,9 @@ differentiable w.r.t. every FeatureNet parameter (the image needs no gradient).
 Forward: the inference kernels without their folded BatchNorm -- tmvs_conv2d_bn_relu (trunk and the
 stage-1 head's 1x1), tmvs_conv3x3_nhwc (stage-2/3 heads' 3x3), tmvs_fpn_merge, and each DCN as ONE
 tmvs_dcn_forward_train launch (offset/mask conv + deformable conv, also writing the offset/mask
-tensor for the backward) -- then tmvs_bn_stats / tmvs_bn_relu_train per view.
+tensor for the backward) -- then tmvs_bn_stats_grouped / tmvs_bn_relu_train_grouped (group = view).
 Backward (csrc/featurenet_train.hip + the BatchNorm kernels of costreg_train.hip): per layer in
-reverse, tmvs_bn_relu_backward per view, weight gradients tmvs_conv2d_wgrad, data gradients
+reverse, tmvs_bn_relu_backward_grouped (group = view), weight gradients tmvs_conv2d_wgrad, data gradients
 tmvs_conv2d_generic (transposed gathers), the DCN by tmvs_dcn_backward (dcol, d offsets / d mask
 logits, dW, the bilinear scatter into dx) followed by its offset/mask conv's gradients, bias
 gradients tmvs_colsum, the FPN merges' nearest x2 adjoint tmvs_nearest_up2_backward_nhwc.
@@ -90,27 +90,17 @@ class _Tape:
 
 
 def _bn_relu_views(tape, z, bn):
-    """relu(BatchNorm_train(z)) with statistics per view (z [N,h,w,C] NHWC)."""
-    y = torch.empty_like(z)
-    per = []
-    for v in range(tape.n):
-        mean, var = ops.bn_stats(z[v])
-        ops.bn_relu_train(z[v], mean, var, bn.weight.detach(), bn.bias.detach(), bn.eps, out=y[v])
-        per.append((mean, var))
-    tape.stats.append((bn, per, z.shape[1] * z.shape[2]))
-    return y, per
+    """relu(BatchNorm_train(z)) with statistics per view (z [N,h,w,C] NHWC): one grouped launch each
+    for the statistics and the normalisation (group = view)."""
+    mean, var = ops.bn_stats_grouped(z)
+    y = ops.bn_relu_train_grouped(z, mean, var, bn.weight.detach(), bn.bias.detach(), bn.eps)
+    tape.stats.append((bn, [(mean[v], var[v]) for v in range(tape.n)], z.shape[1] * z.shape[2]))
+    return y, (mean, var)
 
 
 def _bn_relu_views_backward(dy, z, per, bn):
-    dz = torch.empty_like(z)
-    dy = dy.contiguous()
-    dg = db = None
-    for v, (mean, var) in enumerate(per):
-        _, dgv, dbv = ops.bn_relu_backward(dy[v], z[v], mean, var, bn.weight.detach(), bn.bias.detach(), bn.eps,
-                                           dz=dz[v])
-        dg = dgv if dg is None else dg + dgv
-        db = dbv if db is None else db + dbv
-    return dz, dg, db
+    mean, var = per
+    return ops.bn_relu_backward_grouped(dy.contiguous(), z, mean, var, bn.weight.detach(), bn.bias.detach(), bn.eps)
 
 
 # ------------------------------------------------------------------------- layers: forward records

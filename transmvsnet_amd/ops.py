@@ -671,6 +671,51 @@ def bn_relu_backward(dy, z, mean, var, gamma, beta, eps, dz=None):
     return dz, dg, db
 
 
+def bn_stats_grouped(z):
+    """tmvs_bn_stats_grouped: z [G, ..., C] -> (mean [G, C], biased variance [G, C]), statistics per group."""
+    _dev(z, "z")
+    g, c = z.shape[0], z.shape[-1]
+    nvox = z.numel() // (g * c)
+    ws = torch.empty(_lib_h().tmvs_bn_train_workspace_grouped(g, nvox, c) // 4 + 64, device=z.device)
+    mean = torch.empty(g, c, device=z.device)
+    var = torch.empty(g, c, device=z.device)
+    with _Span("tmvs_bn_stats_grouped"):
+        _lib.check(_lib_h().tmvs_bn_stats_grouped(_ptr(z), g, nvox, c, _ptr(ws), ws.numel() * 4, _ptr(mean), _ptr(var),
+                                                  _stream()), "tmvs_bn_stats_grouped")
+    return mean, var
+
+
+def bn_relu_train_grouped(z, mean, var, gamma, beta, eps):
+    """tmvs_bn_relu_train_grouped: relu(BN_batch(z)) per group, z [G, ..., C], mean / var [G, C]."""
+    for t, n in ((z, "z"), (mean, "mean"), (var, "var"), (gamma, "gamma"), (beta, "beta")):
+        _dev(t, n)
+    g, c = z.shape[0], z.shape[-1]
+    out = torch.empty_like(z)
+    with _Span("tmvs_bn_relu_train_grouped"):
+        _lib.check(_lib_h().tmvs_bn_relu_train_grouped(_ptr(z), g, z.numel() // (g * c), c, _ptr(mean), _ptr(var),
+                                                       _ptr(gamma), _ptr(beta), ctypes.c_float(eps), None, _ptr(out),
+                                                       _stream()), "tmvs_bn_relu_train_grouped")
+    return out
+
+
+def bn_relu_backward_grouped(dy, z, mean, var, gamma, beta, eps):
+    """tmvs_bn_relu_backward_grouped -> (dz, dgamma, dbeta), dgamma / dbeta summed over the groups in order."""
+    for t, n in ((dy, "dy"), (z, "z"), (mean, "mean"), (var, "var"), (gamma, "gamma"), (beta, "beta")):
+        _dev(t, n)
+    g, c = z.shape[0], z.shape[-1]
+    nvox = z.numel() // (g * c)
+    ws = torch.empty(_lib_h().tmvs_bn_train_workspace_grouped(g, nvox, c) // 4 + 64, device=z.device)
+    dz = torch.empty_like(z)
+    dg = torch.empty(c, device=z.device)
+    db = torch.empty(c, device=z.device)
+    with _Span("tmvs_bn_relu_backward_grouped"):
+        _lib.check(_lib_h().tmvs_bn_relu_backward_grouped(_ptr(dy), _ptr(z), g, nvox, c, _ptr(mean), _ptr(var),
+                                                          _ptr(gamma), _ptr(beta), ctypes.c_float(eps), _ptr(ws),
+                                                          ws.numel() * 4, _ptr(dz), _ptr(dg), _ptr(db), _stream()),
+                   "tmvs_bn_relu_backward_grouped")
+    return dz, dg, db
+
+
 def warp_corr_backward(ref_nhwc, src_nhwc, proj12, hyp, dsim, rot_order="auto"):
     """tmvs_warp_corr_backward: one sample, ref [H,W,C], src [V,H,W,C] NHWC, proj12 HOST [V,12],
     hyp [D,H,W], dsim [V,D,H,W] -> (dref [H,W,C], dsrc [V,H,W,C], overflow flag tensor [1] int32)."""
@@ -916,7 +961,8 @@ def adam_step(param_flat, grad_flat, exp_avg, exp_avg_sq, lr, betas, eps, weight
                                            float(weight_decay), int(step), _stream()), "tmvs_adam_step")
 
 
-for _name in ("conv3d_generic", "conv3d_mfma", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn_relu_backward", "warp_corr_backward",
+for _name in ("conv3d_generic", "conv3d_mfma", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn_relu_backward", "bn_stats_grouped", "bn_relu_train_grouped",
+              "bn_relu_backward_grouped", "warp_corr_backward",
               "upsample2_add_nhwc", "upsample2_backward_nhwc", "pixelwise_train_forward", "aggregate_train", "aggregate_train_backward", "pixelwise_train_backward",
               "token_linear", "token_wgrad", "layer_norm_fwd", "layer_norm_bwd", "linattn_fwd", "linattn_bwd_q",
               "linattn_bwd_kv", "adam_step"):
