@@ -36,7 +36,7 @@ def _newer(src_paths, dst):
 def _compile(src, force):
     s = os.path.join(CSRC, src)
     o = os.path.join(OBJ, src.replace(".hip", ".o"))
-    deps = [s, os.path.join(CSRC, "common.h"), os.path.join(ROOT, "include", "transmvs.h")]
+    deps = [s, os.path.join(ROOT, "include", "transmvs.h")] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     if not force and not _newer(deps, o):
         return o, None
     cmd = [HIPCC, *CFLAGS, "-c", s, "-o", o]

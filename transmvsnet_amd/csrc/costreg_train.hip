@@ -23,6 +23,7 @@
 // Bounds: the convolutions are fp32 FMA work (VALU; 3 x 3,456 MAC per voxel for forward + both
 // gradients), the BN passes HBM (2-3 reads of z per pass).
 #include "common.h"
+#include "reduce_mfma.h"
 
 namespace tmvs {
 
@@ -184,14 +185,31 @@ template <int A, int BC>
 __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_tile_kernel(
     const float* __restrict__ direct, const float* __restrict__ gath, int B, int Pd, int Ph, int Pw, int Gd, int Gh,
     int Gw, int stride, long vpb, double* __restrict__ partial) {
+  const int k = blockIdx.y;
+  const int kd = k / 9, kh = (k / 3) % 3, kw = k % 3;
+  if constexpr (A % 8 == 0 && BC % 8 == 0) {  // on the matrix cores (reduce_mfma.h)
+    const long nv = (long)B * Pd * Ph * Pw;
+    const long u0 = (long)blockIdx.x * vpb, u1 = u0 + vpb < nv ? u0 + vpb : nv;
+    auto la = [&](long v, int q) { return *reinterpret_cast<const float4*>(direct + v * A + 4 * q); };
+    auto lb = [&](long v, int q) {
+      const int pw = (int)(v % Pw);
+      long t = v / Pw;
+      const int ph = (int)(t % Ph);
+      t /= Ph;
+      const int pd = (int)(t % Pd), b = (int)(t / Pd);
+      const int gd = pd * stride - 1 + kd, gh = ph * stride - 1 + kh, gw = pw * stride - 1 + kw;
+      if (gd < 0 || gh < 0 || gw < 0 || gd >= Gd || gh >= Gh || gw >= Gw) return make_float4(0.f, 0.f, 0.f, 0.f);
+      return *reinterpret_cast<const float4*>(gath + ((((size_t)b * Gd + gd) * Gh + gh) * Gw + gw) * BC + 4 * q);
+    };
+    tile_reduce_mfma<A, BC>(u0, u1, la, lb, partial + ((size_t)blockIdx.x * 27 + k) * A * BC);
+    return;
+  }
   constexpr int CH = 64, TA = A / 8, TB = BC / 8, SA = A + 4, SB = BC + 4;
   static_assert(A >= 8 && BC >= 8, "tile kernel needs 8 x 8 lanes");
   static_assert(CH * (SA + SB) * 4 >= A * BC * 8, "combine buffer fits the staging LDS");
   __shared__ __attribute__((aligned(16))) float lds[CH * (SA + SB)];
   float* sd = lds;
   float* sg = lds + CH * SA;
-  const int k = blockIdx.y;
-  const int kd = k / 9, kh = (k / 3) % 3, kw = k % 3;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ci = lane & 7, ai = lane >> 3;
   const long nvox = (long)B * Pd * Ph * Pw;

@@ -27,6 +27,7 @@
 // texel in a fixed block order; only corners beyond the window (offsets over R px) go to global
 // memory with fp32 atomics, as torchvision's deformable_col2im adds every contribution with atomicAdd.
 #include "common.h"
+#include "reduce_mfma.h"
 
 namespace tmvs {
 namespace {
@@ -187,6 +188,15 @@ __device__ __forceinline__ void tile_reduce(long v0, long v1, LoadA load_a, Load
       for (int j = 0; j < TB; ++j) out[(ai * TA + i) * BC + ci * TB + j] = acc[i][j];
 }
 
+// the matrix-core form (reduce_mfma.h) wherever both sides have >= 8 channels
+template <int A, int BC, typename LoadA, typename LoadB>
+__device__ __forceinline__ void tile_reduce_any(long v0, long v1, LoadA load_a, LoadB load_b, double* __restrict__ out) {
+  if constexpr (A % 8 == 0 && BC % 8 == 0)
+    tile_reduce_mfma<A, BC>(v0, v1, load_a, load_b, out);
+  else
+    tile_reduce<A, BC>(v0, v1, load_a, load_b, out);
+}
+
 __device__ __forceinline__ float4 load_row4(const float* __restrict__ base, long v, int ch, int q) {
   // 4 channels 4q..4q+3 of row v of a [.][ch] tensor, zero past ch (ch = 27 rows are not 16-B aligned)
   const float* r = base + (size_t)v * ch;
@@ -214,7 +224,7 @@ __global__ __launch_bounds__(kBlk) void conv2d_wgrad_kernel(const float* __restr
     if (gh < 0 || gw < 0 || gh >= Gh || gw >= Gw) return make_float4(0.f, 0.f, 0.f, 0.f);
     return *reinterpret_cast<const float4*>(gath + (((size_t)b * Gh + gh) * Gw + gw) * BC + 4 * q);
   };
-  tile_reduce<AP, BC>(v0, v1, la, lb, partial + ((size_t)blockIdx.x * K * K + k) * AP * BC);
+  tile_reduce_any<AP, BC>(v0, v1, la, lb, partial + ((size_t)blockIdx.x * K * K + k) * AP * BC);
 }
 
 // few channels on the gathered side (the image: 3): thread t owns pairs t, t+256, .. of a x b,
@@ -593,7 +603,7 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_weight_kernel(const float* __res
     return make_float4(blend(v4[0].x, v4[1].x, v4[2].x, v4[3].x), blend(v4[0].y, v4[1].y, v4[2].y, v4[3].y),
                        blend(v4[0].z, v4[1].z, v4[2].z, v4[3].z), blend(v4[0].w, v4[1].w, v4[2].w, v4[3].w));
   };
-  tile_reduce<CO, 32>(v0, v1, la, lb, partial + ((size_t)blockIdx.x * 9 + k) * CO * 32);
+  tile_reduce_any<CO, 32>(v0, v1, la, lb, partial + ((size_t)blockIdx.x * 9 + k) * CO * 32);
 }
 
 // ---------------------------------------------------------------- small backward pieces
