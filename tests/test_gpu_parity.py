@@ -346,6 +346,39 @@ def test_e2e_cascade_48_32_8(sd):
     print("e2e cascade", _e2e_check(out, vw, g))
 
 
+def test_e2e_hip_graph_replay_is_bitwise_eager(sd):
+    """bench.py's step as one captured HIP graph (FMT, the pathway's side stream, 3 stages) replays
+    to exactly the eager forward's outputs, also after the inputs are overwritten in place."""
+    m = TransMVSNet().eval()
+    m.load_state_dict(sd, strict=True)
+    m = m.to(DEV)
+    H, W, N = 256, 320, 3
+    feats = synthetic.stacked_features(N, H, W, seed=2)
+    feats = {k: v.to(DEV) for k, v in feats.items()}
+    proj = synthetic.synthetic_cameras(N, H, W, seed=1)
+    dv = synthetic.synthetic_depth_values(1).to(DEV)
+    with torch.no_grad():
+        ref = m.forward_features(feats, proj, dv, (H, W))
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = m.forward_features(feats, proj, dv, (H, W))
+        graph.replay()
+        torch.cuda.synchronize()
+        for s in (1, 2, 3):
+            for k in ("depth", "prob_volume", "photo_confidence"):
+                assert torch.equal(out[f"stage{s}"][k], ref[f"stage{s}"][k]), (s, k)
+        feats2 = synthetic.stacked_features(N, H, W, seed=7)
+        for k in feats:
+            feats[k].copy_(feats2[k].to(DEV))
+        ref2 = m.forward_features(feats, proj, dv, (H, W))
+        graph.replay()
+        torch.cuda.synchronize()
+        assert not torch.equal(ref2["stage3"]["depth"], ref["stage3"]["depth"])
+        for s in (1, 2, 3):
+            assert torch.equal(out[f"stage{s}"]["depth"], ref2[f"stage{s}"]["depth"]), s
+
+
 def test_e2e_cascade_view_sharded_path(sd):
     """transmvsnet_amd.distributed on one rank: partial cost volume + finalize + replicated CostRegNet."""
     from transmvsnet_amd.distributed import ViewShard

@@ -74,21 +74,45 @@ __device__ __forceinline__ void layer_norm(float (&x)[kD], const float* __restri
   for (int i = 0; i < kD; ++i) x[i] = fmaf(fmaf(x[i], rstd, bias), g[i], b[i]);
 }
 
+// tokens[v][p][c] = feat[v][c][p] + pe[c][y][x]: a block transposes 64 pixels x 32 channels through
+// LDS for every view (coalesced 256-B channel rows in, 8 KB of contiguous token rows out), reading
+// its positional-encoding tile once for all views.
 __global__ __launch_bounds__(256) void fmt_embed_kernel(const float* __restrict__ feat, long view_stride,
                                                         const float* __restrict__ pe, int pe_h, int pe_w, int H, int W,
-                                                        float* __restrict__ tokens) {
+                                                        int nv, float* __restrict__ tokens) {
+  __shared__ float tile[64][kD + 1];
   const int HW = H * W;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= HW) return;
-  const int v = blockIdx.y;
-  const int y = p / W, x = p - y * W;
-  const float* f = feat + (size_t)v * view_stride + p;
-  float t[kD];
+  const int p0 = blockIdx.x * 64;
+  const int px = threadIdx.x & 63, c0 = threadIdx.x >> 6;  // loads: pixel px, channels c0 + 4k
+  const int p = p0 + px;
+  const bool in = p < HW;
+  const int y = in ? p / W : 0, x = in ? p - y * W : 0;
+  float pv[kD / 4];
 #pragma unroll
-  for (int c = 0; c < kD; ++c) t[c] = f[(size_t)c * HW] + pe[((size_t)c * pe_h + y) * pe_w + x];
-  float4* o = reinterpret_cast<float4*>(tokens + ((size_t)v * HW + p) * kD);
+  for (int k = 0; k < kD / 4; ++k) pv[k] = in ? pe[((size_t)(c0 + 4 * k) * pe_h + y) * pe_w + x] : 0.f;
+  const int tp = threadIdx.x >> 3, q = threadIdx.x & 7;  // stores: token tp (and tp + 32), channel quad q
+  float t[kD / 4];
+  auto load = [&](int v) {
+    const float* f = feat + (size_t)v * view_stride;
 #pragma unroll
-  for (int c4 = 0; c4 < kD / 4; ++c4) o[c4] = make_float4(t[4 * c4], t[4 * c4 + 1], t[4 * c4 + 2], t[4 * c4 + 3]);
+    for (int k = 0; k < kD / 4; ++k) t[k] = in ? f[(size_t)(c0 + 4 * k) * HW + p] : 0.f;
+  };
+  load(0);
+#pragma unroll 1
+  for (int v = 0; v < nv; ++v) {
+    __syncthreads();  // the previous view's tile has been stored
+#pragma unroll
+    for (int k = 0; k < kD / 4; ++k) tile[px][c0 + 4 * k] = t[k] + pv[k];
+    __syncthreads();
+    if (v + 1 < nv) load(v + 1);  // in flight during this view's stores
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = tp + 32 * h;
+      if (p0 + r < HW)
+        *reinterpret_cast<float4*>(tokens + ((size_t)v * HW + p0 + r) * kD + 4 * q) =
+            make_float4(tile[r][4 * q], tile[r][4 * q + 1], tile[r][4 * q + 2], tile[r][4 * q + 3]);
+    }
+  }
 }
 
 // ============================================================================ MFMA formulation
@@ -528,8 +552,8 @@ extern "C" int tmvs_fmt_embed(const float* feat, long feat_view_stride, const fl
   if (!feat || !pe || !tokens || nv <= 0 || height <= 0 || width <= 0) return TMVS_ERR_ARG;
   if (channels != kD || height > pe_h || width > pe_w) return TMVS_ERR_SHAPE;
   const int HW = height * width;
-  hipLaunchKernelGGL(fmt_embed_kernel, dim3((HW + 255) / 256, nv), dim3(256), 0, (hipStream_t)stream, feat,
-                     feat_view_stride, pe, pe_h, pe_w, height, width, tokens);
+  hipLaunchKernelGGL(fmt_embed_kernel, dim3((HW + 63) / 64), dim3(256), 0, (hipStream_t)stream, feat,
+                     feat_view_stride, pe, pe_h, pe_w, height, width, nv, tokens);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }

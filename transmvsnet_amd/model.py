@@ -406,10 +406,12 @@ class TransMVSNet(nn.Module):
             done = torch.cuda.Event()
             done.record(side)
             # allocator bookkeeping: st2/st3 are consumed on the main stream, st1/s2/s3 read on side
-            lateral["st2"].record_stream(main)
-            lateral["st3"].record_stream(main)
-            for t in (st1, s2, s3):
-                t.record_stream(side)
+            # (inside a HIP-graph capture the graph's private pool keeps every block alive instead)
+            if not torch.cuda.is_current_stream_capturing():
+                lateral["st2"].record_stream(main)
+                lateral["st3"].record_stream(main)
+                for t in (st1, s2, s3):
+                    t.record_stream(side)
             lateral["done"] = done
 
         if not overlap:
