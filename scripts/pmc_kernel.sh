@@ -11,7 +11,7 @@ i=0
 for ctrs in "$@"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $ctrs --kernel-include-regex "$REGEX" -T -d $OUT/pmc_$i -o run \
-      --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --profile-steps 0 --e2e-steps 0 --train-steps 0 \
+      --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --profile-steps 0 --e2e-steps 0 --train-steps 0 --no-graph \
       > $OUT/pmc_$i.log 2>&1
   rc=$?
   echo "pass $i ($ctrs) rc=$rc"
