@@ -24,6 +24,7 @@ import numpy as np
 import torch
 
 from . import ops
+from .bn_running import update_running_stats
 
 BN_MOMENTUM = 0.1
 _PACK_INDEX = {}
@@ -86,7 +87,7 @@ class _Tape:
 
     def __init__(self, n_views):
         self.n = n_views
-        self.stats = []  # (bn module, [(mean, var)] per view, pixels per view)
+        self.stats = []  # (bn module, (mean [N, C], var [N, C]) per view, pixels per view)
 
 
 def _bn_relu_views(tape, z, bn):
@@ -94,7 +95,7 @@ def _bn_relu_views(tape, z, bn):
     for the statistics and the normalisation (group = view)."""
     mean, var = ops.bn_stats_grouped(z)
     y = ops.bn_relu_train_grouped(z, mean, var, bn.weight.detach(), bn.bias.detach(), bn.eps)
-    tape.stats.append((bn, [(mean[v], var[v]) for v in range(tape.n)], z.shape[1] * z.shape[2]))
+    tape.stats.append((bn, (mean, var), z.shape[1] * z.shape[2]))
     return y, (mean, var)
 
 
@@ -299,10 +300,6 @@ def featurenet_train(fnet, imgs):
     params = list(fnet.parameters())
     with torch.cuda.device(imgs.device):
         s1, s2, s3 = _FeatureNetTrain.apply(imgs, fnet, tape, *params)
-        with torch.no_grad():
-            for bn, per, n in tape.stats:
-                for mean, var in per:  # views in order, as the reference's per-view calls
-                    bn.running_mean.mul_(1.0 - BN_MOMENTUM).add_(mean, alpha=BN_MOMENTUM)
-                    bn.running_var.mul_(1.0 - BN_MOMENTUM).add_(var * (n / max(n - 1, 1)), alpha=BN_MOMENTUM)
-                    bn.num_batches_tracked.add_(1)
+        # views in order, as the reference's per-view calls (closed form, bn_running.py)
+        update_running_stats([(bn, mean, var, n) for bn, (mean, var), n in tape.stats], BN_MOMENTUM)
     return s1, s2, s3

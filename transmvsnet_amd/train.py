@@ -40,6 +40,7 @@ import torch
 import torch.nn.functional as F
 
 from . import ops
+from .bn_running import update_running_stats
 
 # (name, stride, transposed, skip source) in forward order; channels from the module
 _LAYERS = (("conv0", 1, False, None), ("conv1", 2, False, None), ("conv2", 1, False, None),
@@ -427,12 +428,8 @@ def costregnet_train(module, x):
     stats = []
     with torch.cuda.device(x.device):
         logits = _CostRegNetTrain.apply(x.float(), eps, stats, *params)
-        with torch.no_grad():
-            for (name, _, _, _), (mean, var, n) in zip(_LAYERS, stats):
-                bn = getattr(module, name).bn
-                bn.running_mean.mul_(1.0 - BN_MOMENTUM).add_(mean, alpha=BN_MOMENTUM)
-                bn.running_var.mul_(1.0 - BN_MOMENTUM).add_(var * (n / max(n - 1, 1)), alpha=BN_MOMENTUM)
-                bn.num_batches_tracked.add_(1)
+        update_running_stats([(getattr(module, name).bn, mean[None], var[None], n)
+                              for (name, _, _, _), (mean, var, n) in zip(_LAYERS, stats)], BN_MOMENTUM)
     return logits
 
 
@@ -485,12 +482,9 @@ def aggregate_train(sims, model, vw_given=None, vw_shift=0):
     sim, vw = _AggregateTrain.apply(sims, _pw_params(pw), vw_given, vw_shift, stats)
     if stats:
         n = sims.shape[1] * sims.shape[2] * sims.shape[3]
-        with torch.no_grad():
-            for st in stats[0]:  # views in order
-                for bn, m, v in ((pw.conv0.bn, st[0:16], st[16:32]), (pw.conv1.bn, st[32:40], st[40:48])):
-                    bn.running_mean.mul_(1.0 - bn.momentum).add_(m, alpha=bn.momentum)
-                    bn.running_var.mul_(1.0 - bn.momentum).add_(v * (n / max(n - 1, 1)), alpha=bn.momentum)
-                    bn.num_batches_tracked.add_(1)
+        st = torch.stack(list(stats[0]))  # [views, 48], views in order
+        update_running_stats([(pw.conv0.bn, st[:, 0:16], st[:, 16:32], n), (pw.conv1.bn, st[:, 32:40], st[:, 40:48], n)],
+                             pw.conv0.bn.momentum)
     return sim, vw
 
 
