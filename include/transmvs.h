@@ -249,7 +249,9 @@ int tmvs_conv3d_generic(const float* x, int batch, int cin, int d_in, int h_in, 
  * the dgrad of the stride-2 Conv3d layers, whose weight read as ConvTranspose [Co][Ci] is the
  * adjoint), skip (nullable, transposed only, must not alias y) added. wpk [27][cout][cin].
  * Shapes: the inference layers' (cin, cout) pairs -- stride 1: 16->16, 32->32, 64->64; stride 2:
- * 8->16, 16->32, 32->64; transposed: 64->32, 32->16, 16->8 -- else TMVS_ERR_SHAPE.            */
+ * 8->16, 16->32, 32->64; transposed: 64->32, 32->16, 16->8 -- else TMVS_ERR_SHAPE; and conv0's and
+ * prob's VALU kernels, stride 1: 1->8 (wpk [27][8]) and 8->1 (wpk in the prob packing of
+ * TmvsCostRegWeights.w[10], [3][72]).                                                           */
 int tmvs_conv3d_mfma(const float* x, int batch, int cin, int d, int h, int w, const float* wpk, int cout, int stride,
                      int transposed, const float* skip, float* y, void* stream);
 

@@ -86,10 +86,12 @@ def test_costregnet_train_forward_backward(shape):
 
 @pytest.mark.parametrize("cin,cout,stride,transposed", [(16, 16, 1, False), (32, 32, 1, False), (64, 64, 1, False),
                                                          (8, 16, 2, False), (16, 32, 2, False), (32, 64, 2, False),
-                                                         (64, 32, 2, True), (32, 16, 2, True), (16, 8, 2, True)])
+                                                         (64, 32, 2, True), (32, 16, 2, True), (16, 8, 2, True),
+                                                         (1, 8, 1, False), (8, 1, 1, False)])
 @pytest.mark.parametrize("dims", [(4, 10, 20), (1, 6, 37)])
 def test_conv3d_mfma_raw_vs_torch(cin, cout, stride, transposed, dims):
-    """tmvs_conv3d_mfma (the inference layers' MFMA kernels with the raw epilogue) against torch's
+    """tmvs_conv3d_mfma (the inference layers' MFMA kernels, and conv0's / prob's VALU kernels, with the
+    raw epilogue) against torch's
     fp32 conv3d / conv_transpose3d (k3 p1, op1), incl. ragged H/W and depth 1, negative outputs kept
     (no ReLU) and the transposed form's skip add. Bar: 2e-6 of max|y| (K = 27 cin fp32 terms)."""
     import torch.nn.functional as F
@@ -105,7 +107,10 @@ def test_conv3d_mfma_raw_vs_torch(cin, cout, stride, transposed, dims):
     else:
         ref = F.conv3d(x, w, stride=stride, padding=1)
         skip = None
-    got = ops.conv3d_mfma(x.permute(0, 2, 3, 4, 1).contiguous().to(DEV), _pack_fwd(w, transposed).to(DEV), cout,
+    pk = _pack_fwd(w, transposed)
+    if (cin, cout) == (8, 1):
+        pk = ops.prob_pack(pk)
+    got = ops.conv3d_mfma(x.permute(0, 2, 3, 4, 1).contiguous().to(DEV), pk.to(DEV), cout,
                           stride, transposed,
                           skip=None if skip is None else skip.permute(0, 2, 3, 4, 1).contiguous().to(DEV))
     got = got.permute(0, 4, 1, 2, 3).cpu()

@@ -515,7 +515,7 @@ __device__ __forceinline__ float lane_from_right(float v) {  // lane l <- lane l
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, float* __restrict__ y, int D, int H,
                                                     int W, const float* __restrict__ wt,
                                                     const float* __restrict__ alpha,
-                                                    const float* __restrict__ shift) {
+                                                    const float* __restrict__ shift, float lo) {
   const int HW = H * W;
   const int nseg = (W + kProbCols - 1) / kProbCols, nrow = (H + 3) / 4, ndc = (D + kDChunk - 1) / kDChunk;
   int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -577,8 +577,8 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
     float o[8];
 #pragma unroll
     for (int cp = 0; cp < 4; ++cp) {
-      o[2 * cp] = relu(fmaf(a[cp].x, al[2 * cp], sh[2 * cp]));
-      o[2 * cp + 1] = relu(fmaf(a[cp].y, al[2 * cp + 1], sh[2 * cp + 1]));
+      o[2 * cp] = act(fmaf(a[cp].x, al[2 * cp], sh[2 * cp]), lo);
+      o[2 * cp + 1] = act(fmaf(a[cp].y, al[2 * cp + 1], sh[2 * cp + 1]), lo);
     }
     if (writes) {
       float4* q = reinterpret_cast<float4*>(yp + (size_t)d * HW * 8);
@@ -1362,6 +1362,10 @@ extern "C" int tmvs_deconv3d_bn_relu_add(const float* x, int batch, int cin, int
   return deconv_dispatch(x, batch, cin, d, h, w, wpk, alpha, shift, cout, skip, y, (hipStream_t)stream);
 }
 
+static dim3 prob_grid(int batch, int D, int H, int W, int dchunk) {
+  return dim3((unsigned)(((W + kProbCols - 1) / kProbCols) * ((H + 3) / 4) * batch * ((D + dchunk - 1) / dchunk)));
+}
+
 // alpha = 1, shift = 0 for the raw (training) form of the MFMA layers (64 = the widest layer)
 __device__ float kUnitAlpha[64] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f,
                                    1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f,
@@ -1388,6 +1392,19 @@ extern "C" int tmvs_conv3d_mfma(const float* x, int batch, int cin, int d, int h
   const float *al = unit[dev][0], *sh = unit[dev][1];
   const float lo = -__builtin_huge_valf();
   hipStream_t st = (hipStream_t)stream;
+  if (!transposed && stride == 1 && cin == 1 && cout == 8) {  // conv0's VALU kernel, raw epilogue
+    if ((long long)d * h * w * 32 >= (1LL << 31)) return TMVS_ERR_SHAPE;
+    const dim3 grid((unsigned)(((w + kProbCols - 1) / kProbCols) * ((h + 3) / 4) * batch * ((d + kDChunk - 1) / kDChunk)));
+    hipLaunchKernelGGL(conv0_kernel, grid, dim3(256), 0, st, x, y, d, h, w, wpk, al, sh, lo);
+    TMVS_CHECK_LAUNCH();
+    return TMVS_OK;
+  }
+  if (!transposed && stride == 1 && cin == 8 && cout == 1) {  // prob's VALU kernel (prob packing)
+    if ((long long)d * h * w * 32 >= (1LL << 31)) return TMVS_ERR_SHAPE;
+    hipLaunchKernelGGL(prob_kernel, prob_grid(batch, d, h, w, kDChunk), dim3(256), 0, st, x, y, d, h, w, wpk);
+    TMVS_CHECK_LAUNCH();
+    return TMVS_OK;
+  }
   if (transposed) return deconv_dispatch(x, batch, cin, d, h, w, wpk, al, sh, cout, skip, y, st, lo);
   return conv_dispatch(x, batch, cin, d, h, w, wpk, al, sh, cout, stride, y, st, lo);
 }
@@ -1450,7 +1467,8 @@ static int costregnet_trunk(const float* x, int batch, int depth, int height, in
   const int D3 = D2 / 2, H3 = H2 / 2, W3 = W2 / 2;
   int rc;
   const dim3 g0x((unsigned)(((W0 + kProbCols - 1) / kProbCols) * ((H0 + 3) / 4) * batch * ((D0 + kDChunk - 1) / kDChunk)));
-  hipLaunchKernelGGL(conv0_kernel, g0x, dim3(256), 0, st, x, c0, D0, H0, W0, w->w[0], w->alpha[0], w->shift[0]);
+  hipLaunchKernelGGL(conv0_kernel, g0x, dim3(256), 0, st, x, c0, D0, H0, W0, w->w[0], w->alpha[0], w->shift[0],
+                     0.f);
   TMVS_CHECK_LAUNCH();
   if ((rc = conv_dispatch(c0, batch, c, D0, H0, W0, w->w[1], w->alpha[1], w->shift[1], 2 * c, 2, c1, st))) return rc;
   if ((rc = conv_dispatch(c1, batch, 2 * c, D1, H1, W1, w->w[2], w->alpha[2], w->shift[2], 2 * c, 1, c2, st)))
@@ -1474,9 +1492,6 @@ static int costregnet_trunk(const float* x, int batch, int depth, int height, in
   return TMVS_OK;
 }
 
-static dim3 prob_grid(int batch, int D, int H, int W, int dchunk) {
-  return dim3((unsigned)(((W + kProbCols - 1) / kProbCols) * ((H + 3) / 4) * batch * ((D + dchunk - 1) / dchunk)));
-}
 
 extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height, int width,
                                const TmvsCostRegWeights* w, void* workspace, size_t workspace_bytes, float* logits,

@@ -581,8 +581,17 @@ def conv3d_generic(x, w_packed, cout, out_dhw, stride, transposed=False, out=Non
 
 
 # (cin, cout, stride) of the inference layers' MFMA kernels (tmvs_conv3d_mfma); transposed: (cin, cout)
-MFMA_CONV = {(16, 16, 1), (32, 32, 1), (64, 64, 1), (8, 16, 2), (16, 32, 2), (32, 64, 2)}
+MFMA_CONV = {(16, 16, 1), (32, 32, 1), (64, 64, 1), (8, 16, 2), (16, 32, 2), (32, 64, 2), (1, 8, 1), (8, 1, 1)}
 MFMA_DECONV = {(64, 32), (32, 16), (16, 8)}
+
+
+def prob_pack(w27):
+    """[27][1][8] (tap = kd*9 + kh*3 + kw) -> prob_kernel's [3][72] packing (model.CostRegNet.packed):
+    per kh, the {kd=1, kd=2} pairs in (kw, c) order, then kd=0 in (kw, c) order."""
+    pw = w27.reshape(3, 3, 3, 8).permute(3, 0, 1, 2)  # [c][kd][kh][kw]
+    pairs = pw[:, 1:3].permute(2, 3, 0, 1).reshape(3, -1)
+    single = pw[:, 0].permute(1, 2, 0).reshape(3, -1)
+    return torch.cat([pairs, single], 1).contiguous()
 
 
 def conv3d_mfma(x, w_packed, cout, stride, transposed=False, skip=None):
@@ -600,7 +609,10 @@ def conv3d_mfma(x, w_packed, cout, stride, transposed=False, skip=None):
     y = torch.empty(b, *dims, cout, device=x.device)
     if skip is not None and (tuple(skip.shape) != tuple(y.shape) or not skip.is_contiguous()):
         raise ValueError("conv3d_mfma: skip must be a contiguous tensor of the output's shape")
-    if tuple(w_packed.shape) != (27, cout, cin):
+    if (cin, cout) == (8, 1):
+        if tuple(w_packed.shape) != (3, 72):
+            raise ValueError("conv3d_mfma: the 8 -> 1 conv takes the prob packing [3, 72] (prob_pack)")
+    elif tuple(w_packed.shape) != (27, cout, cin):
         raise ValueError("conv3d_mfma: w_packed must be [27, cout, cin]")
     with _Span("tmvs_conv3d_mfma"):
         _lib.check(_lib_h().tmvs_conv3d_mfma(_ptr(x.contiguous()), b, cin, d, h, w, _ptr(w_packed), cout, stride,

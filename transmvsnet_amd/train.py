@@ -305,7 +305,8 @@ def _conv_fwd(x, w, cout, odims, stride, transposed):
     Cin = 1)."""
     cin = x.shape[-1]
     if (cin, cout) in ops.MFMA_DECONV if transposed else (cin, cout, stride) in ops.MFMA_CONV:
-        return ops.conv3d_mfma(x, _pack_fwd(w, transposed), cout, stride, transposed)
+        pk = _pack_fwd(w, transposed)
+        return ops.conv3d_mfma(x, ops.prob_pack(pk) if (cin, cout) == (8, 1) else pk, cout, stride, transposed)
     return ops.conv3d_generic(x, _pack_fwd(w, transposed), cout, odims, stride, transposed)
 
 
@@ -322,7 +323,8 @@ def _conv_dgrad(dz, w, cin, idims, stride, transposed, acc):
     elif not transposed and stride == 2 and (cout, cin) in ops.MFMA_DECONV:
         return ops.conv3d_mfma(dz, pk, cin, 2, transposed=True, skip=acc)
     elif not transposed and stride == 1 and (cout, cin, 1) in ops.MFMA_CONV:
-        dx = ops.conv3d_mfma(dz, pk.flip(0).contiguous(), cin, 1)
+        fl = pk.flip(0).contiguous()
+        dx = ops.conv3d_mfma(dz, ops.prob_pack(fl) if (cout, cin) == (8, 1) else fl, cin, 1)
     elif transposed:  # strided gather of dz
         return ops.conv3d_generic(dz, pk, cin, idims, 2, False, out=acc)
     else:  # transposed gather of dz
@@ -363,7 +365,7 @@ class _CostRegNetTrain(torch.autograd.Function):
             stats.append((mean, var, z.numel() // z.shape[-1]))
             acts[name] = (y, odims)
             cur, dims = y, odims
-        logits = ops.conv3d_generic(cur, _pack_fwd(wprob.detach(), False), 1, dims, 1, False)
+        logits = _conv_fwd(cur, wprob.detach(), 1, dims, 1, False)
         ctx.eps = eps
         ctx.layer_io = saved
         ctx.u11 = cur
@@ -381,8 +383,7 @@ class _CostRegNetTrain(torch.autograd.Function):
         grads = [None] * len(params)
         grads[-1] = _unpack_wgrad(ops.conv3d_wgrad(g, ctx.u11, 1), wprob.shape)
         # gradient w.r.t. each layer's output, filled as the backward reaches it
-        dout = {"conv11": ops.conv3d_generic(g, _pack_dgrad(wprob.detach(), False), ctx.u11.shape[-1], (d, h, w), 1,
-                                             transposed=True)}
+        dout = {"conv11": _conv_dgrad(g, wprob.detach(), ctx.u11.shape[-1], (d, h, w), 1, False, None)}
         for i in range(len(_LAYERS) - 1, -1, -1):
             name, stride, transposed, skip = _LAYERS[i]
             wt, gm, bt = ws[3 * i], ws[3 * i + 1], ws[3 * i + 2]
