@@ -658,20 +658,25 @@ class FlatAdam:
         if self._gathered:
             return
         slices = [self._is_slice(p, off) for p, (off, _) in zip(self.params, self._segs)]
-        if not any(slices):
-            parts = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=self.flat.device)
-                     for p in self.params]
-            torch.cat(parts, out=self.grad_flat)
-        else:
-            # gradient accumulation over several backwards, or step() twice: the .grad views already
-            # live in grad_flat; copy only the parameters whose gradient autograd replaced
-            for p, (off, k), inside in zip(self.params, self._segs, slices):
-                if inside:
-                    continue
-                if p.grad is None:
-                    self.grad_flat[off:off + k].zero_()
-                else:
-                    self.grad_flat[off:off + k].copy_(p.grad.reshape(-1))
+        # a .grad that is not already its grad_flat view (after a first backward: all of them; with
+        # gradient accumulation over several backwards: only those autograd replaced) is copied in
+        # with multi-tensor launches; parameters without a gradient get zeros
+        dst, src, none = [], [], []
+        for p, (off, k), inside in zip(self.params, self._segs, slices):
+            if inside:
+                continue
+            if p.grad is None:
+                none.append(self.grad_flat[off:off + k])
+            else:
+                dst.append(self.grad_flat[off:off + k])
+                src.append(p.grad.reshape(-1))
+        if none:
+            if not any(slices) and len(none) > 8:
+                self.grad_flat.zero_()
+            else:
+                torch._foreach_zero_(none)
+        if dst:
+            torch._foreach_copy_(dst, src)
         for p, (off, k) in zip(self.params, self._segs):
             p.grad = self.grad_flat[off:off + k].view_as(p)
         self._gathered = True
