@@ -237,12 +237,14 @@ __device__ __forceinline__ void layer_norm_frag(floatx4 (&x)[2], const float* __
   const float rstd = 1.f / sqrtf(token_sum(v) / (float)kD + 1e-5f);
   const float bias = -rstd * mean;
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
+  for (int mb = 0; mb < 2; ++mb) {
+    // features 16 mb + 4 (lane >> 4) + r, r < 4: one 16-byte read each of gamma and beta (aligned)
+    const float4 g4 = *reinterpret_cast<const float4*>(g + 16 * mb + 4 * (lane >> 4));
+    const float4 b4 = *reinterpret_cast<const float4*>(b + 16 * mb + 4 * (lane >> 4));
+    const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int f = 16 * mb + 4 * (lane >> 4) + r;
-      x[mb][r] = fmaf(fmaf(x[mb][r], rstd, bias), g[f], b[f]);
-    }
+    for (int r = 0; r < 4; ++r) x[mb][r] = fmaf(fmaf(x[mb][r], rstd, bias), gg[r], bb[r]);
+  }
 }
 
 __device__ __forceinline__ void load_token_frag(const float* __restrict__ row, floatx4 (&x)[2], int lane) {
@@ -394,12 +396,12 @@ __global__ __launch_bounds__(1024) void fmt_kv_combine_kernel(const float* __res
 constexpr int kApplyNT = TMVS_APPLY_NT;
 __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, int L, const float* __restrict__ kvg,
                                                         long kv_stride, const float* __restrict__ w, int tpw) {
-  __shared__ float kvs[kKV];
+  __shared__ __attribute__((aligned(16))) float kvs[kKV];
   // the per-feature vectors, read from LDS in the tile loop: a global load there is a full memory
   // latency, and its vmcnt(0) wait also drains the next tile's token prefetch
   // [0, 32) BQ  [32, 64) BO  [64, 128) B1  [128, 160) B2  [160, 288) LN1G LN1B LN2G LN2B
   constexpr int kVB2 = 128, kVLN = 160;
-  __shared__ float vec[288];
+  __shared__ __attribute__((aligned(16))) float vec[288];
   const int v = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4;
@@ -449,18 +451,26 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb) {
         const int h = 4 * mb + g;
+        // head h's K/V summary, bias and Ksum as 16-byte LDS reads issued together
+        const float4 bq = *reinterpret_cast<const float4*>(vb + 4 * h);
+        const float4 ks4 = *reinterpret_cast<const float4*>(kvs + 128 + h * 4);
+        float4 kv4[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) kv4[m] = *reinterpret_cast<const float4*>(kvs + h * 16 + m * 4);
+        const float bqa[4] = {bq.x, bq.y, bq.z, bq.w}, ksa[4] = {ks4.x, ks4.y, ks4.z, ks4.w};
         float qe[4];
 #pragma unroll
-        for (int d = 0; d < 4; ++d) qe[d] = elu1(q[p][mb][d] + vb[4 * h + d]);
+        for (int d = 0; d < 4; ++d) qe[d] = elu1(q[p][mb][d] + bqa[d]);
         float den = 0.f;
 #pragma unroll
-        for (int d = 0; d < 4; ++d) den = fmaf(qe[d], kvs[128 + h * 4 + d], den);
+        for (int d = 0; d < 4; ++d) den = fmaf(qe[d], ksa[d], den);
         const float z = 1.f / (den + 1e-6f);
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
+          const float kva[4] = {kv4[m].x, kv4[m].y, kv4[m].z, kv4[m].w};
           float num = 0.f;
 #pragma unroll
-          for (int d = 0; d < 4; ++d) num = fmaf(qe[d], kvs[h * 16 + m * 4 + d], num);
+          for (int d = 0; d < 4; ++d) num = fmaf(qe[d], kva[d], num);
           msg[p][mb][m] = num * z;
         }
       }
@@ -470,8 +480,12 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
     for (int p = 0; p < NT; ++p) {
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
+      {
+        const float4 b4 = *reinterpret_cast<const float4*>(vb + 32 + 16 * mb + 4 * g);
+        const float bo[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xs[p][mb][r] = xs[p][mb][r] + (a[p][mb][r] + vb[32 + 16 * mb + 4 * g + r]);
+        for (int r = 0; r < 4; ++r) xs[p][mb][r] = xs[p][mb][r] + (a[p][mb][r] + bo[r]);
+      }
       layer_norm_frag(xs[p], vb + kVLN, vb + kVLN + kD, lane);
     }
     floatx4 hdn[NT][4], ff[NT][2];
@@ -480,15 +494,23 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
     for (int p = 0; p < NT; ++p)
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb)
+      {
+        const float4 b4 = *reinterpret_cast<const float4*>(vb + 64 + 16 * mb + 4 * g);
+        const float b1[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) hdn[p][mb][r] = relu(hdn[p][mb][r] + vb[64 + 16 * mb + 4 * g + r]);
+        for (int r = 0; r < 4; ++r) hdn[p][mb][r] = relu(hdn[p][mb][r] + b1[r]);
+      }
     mfma_linear_lds<32, 64, NT>(fr + 4096, hdn, ff, lane);
 #pragma unroll
     for (int p = 0; p < NT; ++p) {
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
+      {
+        const float4 b4 = *reinterpret_cast<const float4*>(vb + kVB2 + 16 * mb + 4 * g);
+        const float b2[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xs[p][mb][r] = xs[p][mb][r] + (ff[p][mb][r] + vb[kVB2 + 16 * mb + 4 * g + r]);
+        for (int r = 0; r < 4; ++r) xs[p][mb][r] = xs[p][mb][r] + (ff[p][mb][r] + b2[r]);
+      }
       layer_norm_frag(xs[p], vb + kVLN + 2 * kD, vb + kVLN + 3 * kD, lane);
       if (ok[p]) {
 #pragma unroll
