@@ -213,3 +213,24 @@ def test_dcn_backward_vs_autograd(cout, h, w, scale):
         ops.dcn_backward(x32.permute(0, 2, 3, 1).contiguous().to(DEV), om32.contiguous().to(DEV),
                          _taps(w32).to(DEV), dy.float().permute(0, 2, 3, 1).contiguous().to(DEV), dx2)
         assert torch.equal(dx, dx2)
+
+
+@pytest.mark.parametrize("a,bc,k,stride,h,w", [(32, 32, 3, 1, 37, 70), (27, 32, 3, 1, 20, 33), (16, 16, 3, 1, 9, 40),
+                                               (16, 8, 3, 2, 24, 30), (32, 16, 1, 1, 13, 17)])
+def test_conv2d_wgrad_vs_torch(a, bc, k, stride, h, w):
+    """tmvs_conv2d_wgrad (dW[k][a][b] = sum_p dz[p][a] x[p*s - pad + k][b]) against torch's fp64 conv2d
+    weight gradient, incl. the all-taps 3x3 kernel (32 x 32, ragged tiles) and the 27-row offset conv.
+    Bar: 1e-5 of max |dW| (fp32 products summed over <= 10^4 pixels per tile, fp64 across tiles)."""
+    from torch.nn.grad import conv2d_weight
+    torch.manual_seed(a + bc + k + h)
+    pad = k // 2
+    b = 3
+    x = torch.randn(b, bc, h, w, dtype=torch.float64)
+    ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+    dz = torch.randn(b, a, ho, wo, dtype=torch.float64)
+    ref = conv2d_weight(x, (a, bc, k, k), dz, stride=stride, padding=pad)  # [a][bc][k][k]
+    dw = ops.conv2d_wgrad(dz.float().permute(0, 2, 3, 1).contiguous().to(DEV),
+                          x.float().permute(0, 2, 3, 1).contiguous().to(DEV), k, stride, pad)  # [k*k][a][bc]
+    got = dw.double().cpu().reshape(k, k, a, bc).permute(2, 3, 0, 1)
+    err = float((got - ref).abs().max() / ref.abs().max())
+    assert err < 1e-5, err
