@@ -227,80 +227,6 @@ __global__ __launch_bounds__(kBlk) void conv2d_wgrad_kernel(const float* __restr
   tile_reduce_any<AP, BC>(v0, v1, la, lb, partial + ((size_t)blockIdx.x * K * K + k) * AP * BC);
 }
 
-// 3x3, stride 1, pad 1, all 9 taps per workgroup on the matrix cores: the tap-per-block form above
-// reads both operands once per tap (9x; at C5 full resolution 4 GB per call). Here a workgroup walks
-// 4 x 32-pixel tiles: the direct tile [128][AP] and the gathered tile with its 1-pixel halo
-// [6][34][BC] are staged once in LDS, and wave w owns output tile w of the (AP/16) x (BC/16) grid
-// for all 9 taps (9 accumulators): dW[k] += direct^T (16 a x 4 px) . gathered shifted by tap k
-// (4 px x 16 b), 32 MFMA k-steps per tap and tile. fp32 within a tile, fp64 across tiles; block
-// partials [nblk][9][AP][BC] (the tap-per-block form's layout and combine).
-namespace w9 {
-constexpr int TH = 4, TW = 32, NP = TH * TW, GH = TH + 2, GW = TW + 2;  // 64 KB of LDS: 2 workgroups / CU
-}
-template <int AP, int BC>
-__global__ __launch_bounds__(kBlk) void conv2d_wgrad9_kernel(const float* __restrict__ direct, int a_ch,
-                                                            const float* __restrict__ gath, int B, int H, int W,
-                                                            double* __restrict__ partial) {
-  using namespace w9;
-  static_assert((AP / 16) * (BC / 16) == 4, "one 16 x 16 output tile per wave");
-  constexpr int SA = AP + 16, SG = BC + 16;  // row strides: the 4 k-row groups of a read in disjoint banks
-  __shared__ __attribute__((aligned(16))) float sd[NP * SA];
-  __shared__ __attribute__((aligned(16))) float sg[GH * GW * SG];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int col = lane & 15, kg = lane >> 4;
-  const int ma = wv / (BC / 16), nb = wv % (BC / 16);
-  const int ntw = (W + TW - 1) / TW, nth = (H + TH - 1) / TH;
-  const long ntiles = (long)B * nth * ntw;
-  double acc[9][4];
-#pragma unroll
-  for (int k = 0; k < 9; ++k)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc[k][r] = 0.0;
-#pragma unroll 1
-  for (long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int tw = (int)(t % ntw);
-    const long t2 = t / ntw;
-    const int th = (int)(t2 % nth), b = (int)(t2 / nth);
-    const int y0 = th * TH, x0 = tw * TW;
-    __syncthreads();  // the previous tile's reads are done
-    for (int i = threadIdx.x; i < NP * AP / 4; i += kBlk) {
-      const int p = i / (AP / 4), q = i % (AP / 4);
-      const int y = y0 + p / TW, x = x0 + p % TW;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (y < H && x < W) v = load_row4(direct, ((long)b * H + y) * W + x, a_ch, q);
-      *reinterpret_cast<float4*>(sd + p * SA + 4 * q) = v;
-    }
-    for (int i = threadIdx.x; i < GH * GW * BC / 4; i += kBlk) {
-      const int p = i / (BC / 4), q = i % (BC / 4);
-      const int y = y0 - 1 + p / GW, x = x0 - 1 + p % GW;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (y >= 0 && x >= 0 && y < H && x < W)
-        v = *reinterpret_cast<const float4*>(gath + (((size_t)b * H + y) * W + x) * BC + 4 * q);
-      *reinterpret_cast<float4*>(sg + p * SG + 4 * q) = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {  // unrolled: acc[k] stays in registers
-      const int kh = k / 3, kw = k % 3;
-      floatx4_t d = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-      for (int s = 0; s < NP / 4; ++s) {
-        const int p = 4 * s + kg;  // pixel (row p / TW, column p % TW) of the tile
-        const int gp = (p / TW + kh) * GW + p % TW + kw;
-        d = __builtin_amdgcn_mfma_f32_16x16x4f32(sd[p * SA + 16 * ma + col], sg[gp * SG + 16 * nb + col], d, 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[k][r] += (double)d[r];
-    }
-  }
-  // lane (col, kg) holds dW[k][16 ma + 4 kg + r][16 nb + col]
-#pragma unroll
-  for (int k = 0; k < 9; ++k)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      partial[(((size_t)blockIdx.x * 9 + k) * AP + 16 * ma + 4 * kg + r) * BC + 16 * nb + col] = acc[k][r];
-}
-
 // few channels on the gathered side (the image: 3): thread t owns pairs t, t+256, .. of a x b,
 // straight from global memory (L1 hits), fp32 over a block's pixels in 8 interleaved chains, fp64 after
 template <int A, int BC>
@@ -778,11 +704,6 @@ extern "C" int tmvs_conv2d_wgrad(const float* direct, int a_ch, int batch, int p
     hipLaunchKernelGGL((conv2d_wgrad_kernel<AP, BC>), dim3(nblk, k * k), dim3(kBlk), 0, st, direct, a_ch, gathered, \
                        batch, ph, pw, gh, gw, k, stride, pad, ppb, part);                                        \
     done = true;                                                                                                 \
-  }
-  if (k == 3 && stride == 1 && pad == 1 && gh == ph && gw == pw && ap == 32 && b_ch == 32) {  // all taps per block
-    hipLaunchKernelGGL((conv2d_wgrad9_kernel<32, 32>), dim3(nblk), dim3(kBlk), 0, st, direct, a_ch, gathered, batch,
-                       ph, pw, part);
-    done = true;
   }
   TMVS_WG2(8, 8) TMVS_WG2(16, 8) TMVS_WG2(16, 16) TMVS_WG2(32, 8) TMVS_WG2(32, 16) TMVS_WG2(32, 32)
 #undef TMVS_WG2
