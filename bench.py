@@ -266,7 +266,8 @@ def run(args, world, rank, local):
         ospans = otimer.durations()
 
         e2e = end_to_end(model, args.e2e_steps, proj, dv_dev, dev) if args.e2e_steps > 0 and shard is None else None
-    train = train_timing(args.train_steps, dev, world) if args.train_steps > 0 and shard is None else None
+    train = (train_timing(args.train_steps, dev, world, use_graph=not args.no_graph)
+             if args.train_steps > 0 and shard is None else None)
 
     maps_per_step = 1 if args.mode == "views" else world
     value = maps_per_step * args.steps / elapsed
@@ -431,7 +432,7 @@ def _train_setup(dev):
           for s in range(3)}
     mask = {k: torch.ones_like(v) for k, v in gt.items()}
     dint = float(dv[0, 1] - dv[0, 0])  # the sample's depth_interval (finetune.py:159)
-    interval = torch.tensor([dint], device=dev)
+    interval = torch.tensor([dint])  # host: focal_loss_bld reads it as a number (no device sync in the step)
     opt = FlatAdam(list(m.parameters()), lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4)  # finetune.py:27,29,324
 
     def full_step():
@@ -463,7 +464,7 @@ def train_steps(dev):
     return _train_setup(dev)
 
 
-def train_timing(steps, dev, world):
+def train_timing(steps, dev, world, use_graph=True):
     """C5 training step (BlendedMVS 768x576, N=4, 48/32/8, one sample per rank): the reference's
     train_sample body (finetune.py:144-168) on the drop-in model -- model.train(); zero_grad;
     outputs = model(imgs, proj, depth_values) (FeatureNet + DCN, FMT, pathway, 3 DepthNet stages, all
@@ -490,12 +491,44 @@ def train_timing(steps, dev, world):
             ms = float(t.item())
         return ms
 
-    ms = timed(full_step)
-    ms_feat = timed(features_step)
+    def graphed(fn):
+        """fn captured as one HIP graph (forward, autograd backward, gradient gather, Adam with its step
+        counter on the device; the warp backwards' overflow flags are checked after the replays) and
+        replayed; None when the capture fails (then the step is timed eagerly)."""
+        if world > 1 or not use_graph:
+            return None
+        try:
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                fn()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fn()
+            torch.cuda.synchronize()
+            return g.replay
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line, the eager timing stands
+            launch_notes.append(f"{getattr(fn, '__name__', 'step')}: capture failed ({type(e).__name__}: {str(e)[:120]})")
+            torch.cuda.synchronize()
+            return None
+
+    from transmvsnet_amd import train as _train
+    launch_notes = []
+    ms_eager = timed(full_step)
+    ms_feat_eager = timed(features_step)
+    g_full, g_feat = graphed(full_step), graphed(features_step)
+    ms = timed(g_full) if g_full else ms_eager
+    ms_feat = timed(g_feat) if g_feat else ms_feat_eager
+    if g_full or g_feat:
+        _train.check_graph_flags()
     nbytes = sum(p.numel() for p in m.parameters()) * 4
     return {"ms_per_sample": round(ms, 3), "samples_per_s": round(world * 1e3 / ms, 3), "ranks": world,
             "grad_allreduce_bytes": nbytes if world > 1 else 0,
             "ms_per_sample_from_features": round(ms_feat, 3),
+            "launch": ("hip_graph replay" if g_full else "eager") + "; eager: "
+                      f"{round(ms_eager, 3)} / {round(ms_feat_eager, 3)} ms" + (f"; {'; '.join(launch_notes)}" if launch_notes else ""),
             "workload": "BlendedMVS 768x576, N=4, 48/32/8, 1 sample per rank: finetune.py:144-168's train_sample "
                         "body on the drop-in model -- model.train(); optimizer.zero_grad(); outputs = model(imgs, "
                         "proj, depth_values); focal_loss_bld(..., dlossw 1,1,1); loss.backward(); optimizer.step() -- "

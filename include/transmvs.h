@@ -352,6 +352,11 @@ int tmvs_linattn_bwd_kv(const float* k, const float* v, long tokens, long tokens
  * Scalars are doubles, as the Python floats torch receives (1 - beta is formed before rounding).  */
 int tmvs_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, double lr,
                    double beta1, double beta2, double eps, double weight_decay, int step, void* stream);
+/* The same with the step number on the device (a captured HIP graph replays it): *step_counter
+ * (int, device) is advanced by the launch itself; scalars: 2 device floats of scratch.          */
+int tmvs_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, double lr,
+                       double beta1, double beta2, double eps, double weight_decay, int* step_counter, float* scalars,
+                       void* stream);
 
 /* BatchNorm3d in train mode over z [nvox][C] (C divides 256): batch mean and biased variance
  * (fp64 partials, fixed-order combine); y = relu(fmaf(z, a, b)) [+ skip] with a = gamma /

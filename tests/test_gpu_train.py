@@ -584,6 +584,44 @@ def test_flat_adam_matches_torch_adam():
     assert worst < 2e-6, worst
 
 
+def test_flat_adam_graph_replay_equals_eager_steps():
+    """A FlatAdam step captured in a HIP graph (tmvs_adam_step_dev: the step number advanced on the
+    device per replay) gives bitwise the same parameters and moments as eager steps (host step
+    number), after 2 eager steps and 3 replays vs 5 eager steps with the same gradients."""
+    from transmvsnet_amd.train import FlatAdam
+    torch.manual_seed(5)
+    shapes = [(8, 1, 3, 3, 3), (16,), (64, 32)]
+    init = [torch.randn(s) for s in shapes]
+    grads = [torch.randn(s).to(DEV) * 0.1 for s in shapes]
+    pa = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+    pb = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+    oa = FlatAdam(pa, lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4)
+    ob = FlatAdam(pb, lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4)
+    for _ in range(5):
+        oa.zero_grad()
+        for p, gr in zip(pa, grads):
+            p.grad = gr.clone()
+        oa.step()
+
+    def step_b():
+        ob.zero_grad()
+        for p, gr in zip(pb, grads):
+            p.grad = gr.clone()
+        ob.step()
+    for _ in range(2):
+        step_b()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step_b()  # captured: its launches run only on replay
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert int(ob._step_dev.item()) == 5
+    assert torch.equal(oa.flat, ob.flat)
+    assert torch.equal(oa.exp_avg, ob.exp_avg) and torch.equal(oa.exp_avg_sq, ob.exp_avg_sq)
+
+
 def test_training_loop_reduces_loss():
     """A C5-style loop on one fixed synthetic sample (128x160, N=3, 8/8/8): FMT -> pathway -> DepthNet
     stages -> focal_loss_bld (dlossw 1,1,1) -> backward -> FlatAdam.step, 8 iterations, all HIP. The

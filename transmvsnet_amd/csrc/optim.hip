@@ -42,3 +42,45 @@ extern "C" int tmvs_adam_step(float* param, const float* grad, float* exp_avg, f
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
+
+// The same step with the step counter on the device (HIP-graph replays): a one-thread kernel advances
+// *step and writes lr / (1 - beta1^step) and sqrt(1 - beta2^step) (double, as the host form) into
+// scal[0..1], which adam_kernel_dev reads.
+__global__ void adam_prep_kernel(int* __restrict__ step, float* __restrict__ scal, double lr, double beta1,
+                                 double beta2) {
+  const int s = ++step[0];
+  scal[0] = (float)(lr / (1.0 - pow(beta1, (double)s)));
+  scal[1] = (float)sqrt(1.0 - pow(beta2, (double)s));
+}
+
+__global__ __launch_bounds__(256) void adam_kernel_dev(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ m, float* __restrict__ v, long n, float omb1,
+                                                       float beta2, float omb2, float eps, float wd,
+                                                       const float* __restrict__ scal) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float step_size = scal[0], bc2_sqrt = scal[1];
+  const float pv = p[i];
+  const float gr = wd != 0.f ? fmaf(wd, pv, g[i]) : g[i];
+  const float mv = m[i];
+  const float mn = fmaf(omb1, gr - mv, mv);
+  const float vn = fmaf(omb2, gr * gr, beta2 * v[i]);
+  const float denom = sqrtf(vn) / bc2_sqrt + eps;
+  m[i] = mn;
+  v[i] = vn;
+  p[i] = fmaf(-step_size, mn / denom, pv);
+}
+
+extern "C" int tmvs_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n,
+                                  double lr, double beta1, double beta2, double eps, double weight_decay,
+                                  int* step_counter, float* scalars, void* stream) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq || !step_counter || !scalars || n <= 0) return TMVS_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, st, step_counter, scalars, lr, beta1, beta2);
+  TMVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(adam_kernel_dev, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, param, grad, exp_avg,
+                     exp_avg_sq, n, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
+                     (float)weight_decay, (const float*)scalars);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}

@@ -973,11 +973,25 @@ def adam_step(param_flat, grad_flat, exp_avg, exp_avg_sq, lr, betas, eps, weight
                                            float(weight_decay), int(step), _stream()), "tmvs_adam_step")
 
 
+def adam_step_dev(param_flat, grad_flat, exp_avg, exp_avg_sq, lr, betas, eps, weight_decay, step_counter, scalars):
+    """tmvs_adam_step_dev: adam_step with the step number advanced on the device (graph-replayable)."""
+    for t, n in ((param_flat, "param"), (grad_flat, "grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq"),
+                 (scalars, "scalars")):
+        _dev(t, n)
+    if step_counter.dtype != torch.int32 or not step_counter.is_cuda:
+        raise RuntimeError("step_counter must be a device int32 tensor")
+    with _Span("tmvs_adam_step"):
+        _lib.check(_lib_h().tmvs_adam_step_dev(_ptr(param_flat), _ptr(grad_flat), _ptr(exp_avg), _ptr(exp_avg_sq),
+                                               param_flat.numel(), float(lr), float(betas[0]), float(betas[1]),
+                                               float(eps), float(weight_decay), _ptr(step_counter), _ptr(scalars),
+                                               _stream()), "tmvs_adam_step_dev")
+
+
 for _name in ("conv3d_generic", "conv3d_mfma", "conv3d_wgrad", "bn_stats", "bn_relu_train", "bn_relu_backward", "bn_stats_grouped", "bn_relu_train_grouped",
               "bn_relu_backward_grouped", "warp_corr_backward",
               "upsample2_add_nhwc", "upsample2_backward_nhwc", "pixelwise_train_forward", "aggregate_train", "aggregate_train_backward", "pixelwise_train_backward",
               "token_linear", "token_wgrad", "layer_norm_fwd", "layer_norm_bwd", "linattn_fwd", "linattn_bwd_q",
-              "linattn_bwd_kv", "adam_step"):
+              "linattn_bwd_kv", "adam_step", "adam_step_dev"):
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name
 

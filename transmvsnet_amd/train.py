@@ -71,12 +71,20 @@ class _WarpCorrViews(torch.autograd.Function):
         dref, dsrc, flag = ops.warp_corr_backward(ref, src, ctx.proj12, hyp, dsims.contiguous(), ctx.rot_order)
         if _DEFERRED_FLAGS is not None:  # inside depth_stages_train: one host sync after the whole backward
             _DEFERRED_FLAGS.append(flag.clone())
+        elif torch.cuda.is_current_stream_capturing():  # a HIP-graph capture: checked after the replays
+            GRAPH_FLAGS.append(flag)
         else:
             _check_overflow([flag])
         return dref, dsrc, None, None, None
 
 
 _DEFERRED_FLAGS = None
+GRAPH_FLAGS = []  # overflow flags of backwards captured in a HIP graph (check_graph_flags after replaying)
+
+
+def check_graph_flags():
+    """The overflow check of the warp backwards inside a captured training-step graph (one host sync)."""
+    _check_overflow(GRAPH_FLAGS)
 
 
 def _check_overflow(flags):
@@ -583,7 +591,10 @@ def depth_stages_train(model, stage_features, proj_matrix, depth_values, depth_g
             flags = _DEFERRED_FLAGS
         finally:
             _DEFERRED_FLAGS = None
-        _check_overflow(flags)
+        if torch.cuda.is_current_stream_capturing():
+            GRAPH_FLAGS.extend(flags)
+        else:
+            _check_overflow(flags)
     return total, outputs
 
 
@@ -640,6 +651,10 @@ class FlatAdam:
         self.exp_avg_sq = torch.zeros(n, device=dev)
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.step_count = 0
+        # the step number on the device as well, for a step captured in a HIP graph (tmvs_adam_step_dev
+        # advances it per replay); eager steps keep it equal to step_count
+        self._step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._scal_dev = torch.zeros(2, device=dev)
         self._gathered = False
 
     def zero_grad(self):
@@ -692,8 +707,13 @@ class FlatAdam:
     def step(self, lr=None):
         self._gather()
         self.step_count += 1
-        ops.adam_step(self.flat, self.grad_flat, self.exp_avg, self.exp_avg_sq, self.lr if lr is None else lr,
-                      self.betas, self.eps, self.weight_decay, self.step_count)
+        if torch.cuda.is_current_stream_capturing():
+            ops.adam_step_dev(self.flat, self.grad_flat, self.exp_avg, self.exp_avg_sq, self.lr if lr is None else lr,
+                              self.betas, self.eps, self.weight_decay, self._step_dev, self._scal_dev)
+        else:
+            ops.adam_step(self.flat, self.grad_flat, self.exp_avg, self.exp_avg_sq, self.lr if lr is None else lr,
+                          self.betas, self.eps, self.weight_decay, self.step_count)
+            self._step_dev.fill_(self.step_count)
         # the launch wrote the parameters through a raw pointer: bump their version counters so the
         # inference caches keyed on them (TransMVSNet._param_key, FeatureNet's packed weights) rebuild
         with torch.no_grad():
