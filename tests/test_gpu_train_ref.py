@@ -277,3 +277,54 @@ def test_flat_adam_accumulates_two_backwards_and_invalidates_inference_cache():
     assert torch.equal(a["prob_volume"], b["prob_volume"])
     assert torch.equal(c["prob_volume"], d["prob_volume"])
     assert not torch.equal(a["prob_volume"], c["prob_volume"])
+
+
+def test_train_sample_hip_graph_replay_equals_eager(gold):
+    """The same train_sample body captured once as a HIP graph (bench.py's training timing) and
+    replayed: two replays after one eager step leave the parameters, Adam moments and BatchNorm
+    running statistics where three eager steps leave them (within 1e-5 of each quantity's max: the
+    DCN's beyond-window corners use fp32 atomics, so not bitwise)."""
+    from transmvsnet_amd import loss as hip_loss
+    from transmvsnet_amd import synthetic
+    from transmvsnet_amd import train as tr
+    imgs = synthetic.synthetic_images(N, H, H * 5 // 4, seed=0).to(DEV)
+    proj = synthetic.synthetic_cameras(N, H, H * 5 // 4, seed=1)
+    dv = synthetic.synthetic_depth_values(1).to(DEV)
+    depth_gt_ms, mask_ms = _targets(gold)
+    interval = torch.tensor([float(gold["i_interval"])])  # host (no device read inside the graph)
+    runs = []
+    for graphed in (False, True):
+        model = _model()
+        opt = tr.FlatAdam([p for p in model.parameters()], lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4)
+
+        def body():
+            model.train()
+            opt.zero_grad()
+            outputs = model(imgs, proj, dv)
+            loss = hip_loss.focal_loss_bld(outputs, depth_gt_ms, mask_ms, interval, dlossw=[1.0, 1.0, 1.0])[0]
+            loss.backward()
+            opt.step()
+        with golden_rot(model):
+            body()
+            torch.cuda.synchronize()
+            if graphed:
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    body()  # captured, not run
+                for _ in range(2):
+                    graph.replay()
+                torch.cuda.synchronize()
+                tr.check_graph_flags()
+            else:
+                for _ in range(2):
+                    body()
+        torch.cuda.synchronize()
+        bufs = {n: b.detach().clone() for n, b in model.named_buffers() if "running" in n}
+        runs.append((opt.flat.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), bufs))
+    (fa, ma, va, ba), (fb, mb, vb, bb) = runs
+    for a, b, tag in ((fa, fb, "params"), (ma, mb, "exp_avg"), (va, vb, "exp_avg_sq")):
+        err = float((a - b).abs().max() / a.abs().max())
+        assert err < 1e-5, (tag, err)
+    for n in ba:
+        err = float((ba[n] - bb[n]).abs().max() / max(float(ba[n].abs().max()), 1e-30))
+        assert err < 1e-5, (n, err)

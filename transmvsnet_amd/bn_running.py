@@ -12,6 +12,16 @@ from __future__ import annotations
 import torch
 
 
+_COEF = {}  # (calls, momentum, device) -> the per-call weights m (1 - m)^(G-1-v) (made once: no copy in a graph)
+
+
+def _coef(g, m, dev):
+    key = (g, m, str(dev))
+    if key not in _COEF:
+        _COEF[key] = torch.tensor([m * (1.0 - m) ** (g - 1 - v) for v in range(g)], device=dev, dtype=torch.float32)
+    return _COEF[key]
+
+
 def update_running_stats(items, momentum):
     """items: [(bn, mean [G, C], var [G, C] (biased, per call, in call order), n elements per call)]."""
     if not items:
@@ -23,7 +33,7 @@ def update_running_stats(items, momentum):
         for g, group in by_g.items():
             dev = group[0][1].device
             m = float(momentum)
-            coef = torch.tensor([m * (1.0 - m) ** (g - 1 - v) for v in range(g)], device=dev, dtype=torch.float32)
+            coef = _coef(g, m, dev)
             rms = [bn.running_mean for bn, _, _, _ in group]
             rvs = [bn.running_var for bn, _, _, _ in group]
             cms = [torch.mv(mean.t(), coef) for _, mean, _, _ in group]
