@@ -1,5 +1,7 @@
 """Run ONE kind of the bench's C5 training step alone (for rocprofv3 --kernel-trace --stats):
-    python scripts/diag/train_prof.py full|features STEPS   (1 warm-up step first; diagnostic, GPU box)"""
+    python scripts/diag/train_prof.py full|features STEPS [graph]
+(1 warm-up step first; with `graph` the step is captured once and replayed STEPS times; diagnostic,
+GPU box)"""
 import os
 import sys
 
@@ -9,9 +11,17 @@ import torch
 import bench
 
 kind, steps = sys.argv[1], int(sys.argv[2])
-full_step, features_step, _ = bench.train_steps(torch.device("cuda", 0))
+dev = torch.device("cuda", 0)
+full_step, features_step, _ = bench.train_steps(dev)
 fn = full_step if kind == "full" else features_step
-for i in range(steps + 1):
+fn()
+torch.cuda.synchronize()
+if len(sys.argv) > 3 and sys.argv[3] == "graph":
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    fn = g.replay
+for i in range(steps):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     fn()
