@@ -14,7 +14,8 @@ architecture (key-seeded, transmvsnet_amd.synthetic). FeatureNet (SURVEY.md 8f, 
 is outside the timed step. Multi-GPU:
   replica (default) -- every rank computes its own depth maps, no collective ("weak");
   views             -- the 4 source views are sharded over ranks, one RCCL all-reduce of
-                       (sum w*sim, sum w) per stage (transmvsnet_amd.distributed).
+                       (sum w*sim, sum w) per stage (transmvsnet_amd.distributed); with more
+                       ranks than source views, replicas x view-shard groups (8 ranks: 2 x 4).
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -190,8 +191,9 @@ def run(args, world, rank, local):
     dv_dev = dv.to(dev)
     shard = None
     if args.mode == "views" and world > 1:
-        from transmvsnet_amd.distributed import ViewShard
-        shard = ViewShard(rank, world, NVIEWS - 1)
+        # replica x view-shard groups: more ranks than source views run several view-sharded groups
+        from transmvsnet_amd.distributed import make_view_shard
+        shard = make_view_shard(rank, world, NVIEWS - 1)
 
     def step():
         return model.forward_features(feats, proj, dv_dev, (H, W), view_shard=shard)
@@ -269,7 +271,7 @@ def run(args, world, rank, local):
     train = (train_timing(args.train_steps, dev, world, use_graph=not args.no_graph)
              if args.train_steps > 0 and shard is None else None)
 
-    maps_per_step = 1 if args.mode == "views" else world
+    maps_per_step = shard.replicas if shard is not None else (1 if args.mode == "views" else world)
     value = maps_per_step * args.steps / elapsed
     per_kernel = {}
     for n, ms in spans:

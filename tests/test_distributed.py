@@ -192,3 +192,54 @@ def test_flat_adam_views():
     assert ps[1].grad.data_ptr() == opt.grad_flat[12:].data_ptr()
     opt.zero_grad()
     assert all(p.grad is None for p in ps)
+
+
+def test_view_groups_layout():
+    from transmvsnet_amd.distributed import view_groups
+    assert view_groups(8, 4) == (4, 2)
+    assert view_groups(4, 4) == (4, 1)
+    assert view_groups(2, 4) == (2, 1)
+    assert view_groups(6, 4) == (3, 2)
+    assert view_groups(5, 4) == (1, 5)
+    assert view_groups(16, 10) == (8, 2)
+
+
+def _hybrid_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from transmvsnet_amd.distributed import make_view_shard
+        torch.set_num_threads(1)
+        sd = golden_state_dict()
+        feats, proj, dv = _inputs()
+        feats, proj = feats[:3], proj[:, :3]  # 2 source views
+        part = _oracle_partial(sd, feats, proj)
+        shard = make_view_shard(rank, world, 2, finalize_fn=_finalize)
+        shard._partial = lambda *a, **k: part(*a, views=shard.src_views)
+        sim, _ = shard.cost_volume(None, None, dv, 0, None, None)
+        ref_sim, _ = oracle.build_cost_volume(sd, feats, proj, dv)
+        q.put((rank, shard.replica, shard.replicas, shard.src_views, float((sim - ref_sim[:, 0]).abs().max())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_replica_by_view_shard_groups_gloo():
+    """World 4 over 2 source views: 2 replica groups x 2 view shards (the layout bench.py
+    --mode views uses when ranks outnumber source views); each group's all-reduce stays inside it and
+    every rank gets the full aggregate."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hybrid_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = 2
+    for rank, replica, replicas, views, err in res:
+        assert replicas == world // g and replica == rank // g
+        assert views == [rank % g], (rank, views)
+        assert err <= 1e-6, (rank, err)

@@ -34,6 +34,29 @@ def partition_views(n_src: int, world: int, rank: int) -> List[int]:
     return list(range(start, start + count))
 
 
+def view_groups(world: int, n_src: int) -> tuple:
+    """Replica x view-shard layout of `world` ranks for n_src source views: the view-shard group size g
+    is the largest divisor of world that is <= n_src (more ranks than source views would leave some
+    idle), so world = replicas x g; group r holds ranks r*g .. r*g + g - 1 and computes its own depth
+    maps. -> (g, replicas)."""
+    g = max(d for d in range(1, min(world, n_src) + 1) if world % d == 0)
+    return g, world // g
+
+
+def make_view_shard(rank: int, world: int, n_src: int, **kw) -> "ViewShard":
+    """This rank's ViewShard in the replica x view-shard layout (view_groups). Every rank creates every
+    group (torch.distributed.new_group is collective), in the same order."""
+    g, replicas = view_groups(world, n_src)
+    group = None
+    if replicas > 1:
+        groups = [dist.new_group(list(range(r * g, (r + 1) * g))) for r in range(replicas)]
+        group = groups[rank // g]
+    shard = ViewShard(rank % g, g, n_src, group=group, **kw)
+    shard.replica = rank // g
+    shard.replicas = replicas
+    return shard
+
+
 class ViewShard:
     """Source-view sharding for TransMVSNet.forward_features(view_shard=...).
 
@@ -50,6 +73,7 @@ class ViewShard:
         self.src_views = partition_views(n_src, world, rank)
         self._partial = partial_fn or _hip_partial
         self._finalize = finalize_fn or _hip_finalize
+        self.replica, self.replicas = 0, 1  # make_view_shard: this rank's replica group, and their count
         self.timer = None       # optional begin(name)/end(token) around each collective (bench.py)
         self.comm_bytes = []    # bytes of each all-reduce issued, in order (3 per forward)
 
