@@ -531,24 +531,22 @@ static long block_slots(K kernel) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess || per <= 0) per = 4;
   return (long)(cus > 0 ? cus : 256) * per;
 }
-static int wave_slots_kv() {
-  static long slots = 0;
-  if (!slots) slots = 4 * block_slots(fmt_kv_partial_kernel);
-  return (int)slots;
-}
 static int wave_slots_apply() {
   static long slots = 0;
   if (!slots) slots = 4 * block_slots(fmt_apply_kernel);
   return (int)slots;
 }
 
-// Tiles per wave: the launch in ONE round of resident waves (each wave's tiles are a dependent
-// chain, so a launch lasts about tpw tile-latencies): 2.4 waves/SIMD at 8 tiles per wave for the
-// 5-view self-attention K/V (r05f); 2 to kKvTilesPerWave (1 measured slower for the one-view K/V:
-// twice the partial slabs for the combine).
+// Tiles per wave: as many as possible (small partial slabs, short combine) while the launch still
+// has >= 2048 waves (2 per SIMD); the one-view cross-attention K/V otherwise runs at 0.1 waves/SIMD.
+// (Sizing it from the occupancy like the apply measured 28.6 -> 26.4 us for the 5-view launch, but it
+// changes the partial sums' grouping -- the K/V bits -- and with them a C2 near-tie at stage 2 whose
+// flip then moves stage 3's hypotheses (tests/test_gpu_fullsize.py, r11g): kept as before.)
 static int kv_tiles_per_wave(int nv, int S) {
-  const long tiles = (long)nv * ((S + 15) / 16);
-  return (int)std::min<long>(kKvTilesPerWave, std::max<long>(2, (tiles + wave_slots_kv() - 1) / wave_slots_kv()));
+  const int tiles = (S + 15) / 16;
+  int tpw = kKvTilesPerWave;
+  while (tpw > 2 && (long)nv * ((tiles + tpw - 1) / tpw) < 2048) tpw >>= 1;
+  return tpw;
 }
 static int kv_nblk(int nv, int S) {
   const int per = 16 * 4 * kv_tiles_per_wave(nv, S);
