@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TMVS_ABI_VERSION 6
+#define TMVS_ABI_VERSION 7
 
 #define TMVS_OK 0
 #define TMVS_ERR_ARG (-1)    /* null pointer / non-positive size / bad enum        */
@@ -87,6 +87,7 @@ int tmvs_stage_hypotheses(const float* depth_values, int n_values, const float* 
  *            V*H*W*C*4 < 2^30 bytes per sample (32-bit buffer offsets); H, W <= 32766.      */
 #define TMVS_WARP_PARTIAL 1
 #define TMVS_WARP_ROT_PLAIN 2
+#define TMVS_WARP_BWD_PLANES 4 /* tmvs_warp_corr_backward: hyp[d] is one depth per plane (stage 1) */
 #define TMVS_PW_NPARAMS 201 /* w0[16] a0[16] s0[16] w1[8][16] a1[8] s1[8] w2[8] b2 */
 int tmvs_warp_corr(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,
                    const float* view_w_in, int vw_shift, int vw_offset, int vw_total, const float* pw_params,
@@ -273,7 +274,12 @@ int tmvs_conv3d_wgrad(const float* direct, int a_ch, int batch, int pd, int ph, 
  * max|dsim| and max|ref| so that no texel's sum can overflow (ABI 5; it was a fixed 2^-40). The
  * workspace's int after the buffer is set to 1 when dsim or ref holds a non-finite value. One
  * thread per (pixel, view, chunk of 8 planes); dref is the fixed-order sum of those partials.
- * ABI 3: the workspace size takes ndepth (the d ref partials live in it).                      */
+ * ABI 3: the workspace size takes ndepth (the d ref partials live in it).
+ * flags & TMVS_WARP_BWD_PLANES (ABI 7; hyp[d][p] = hyp[d][0] for every p, i.e. fronto-parallel
+ * depth planes, D <= 64): dsrc is GATHERED instead -- per source texel, the reference pixels in the
+ * preimage of its tap square under the plane homography, re-projected with the forward's rounding --
+ * in fp32 with a fixed order, no atomics; a pixel whose hyp differs from its plane's sets bit 2 of
+ * the workspace flag int.                                                                        */
 size_t tmvs_warp_corr_backward_workspace(int n_src, int channels, int height, int width, int ndepth);
 int tmvs_warp_corr_backward(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,
                             const float* dsim, int n_src, int channels, int ndepth, int height, int width, int flags,

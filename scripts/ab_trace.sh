@@ -9,7 +9,7 @@ for v in "$@"; do
   mkdir -p $OUT
   if [ "$v" = base ]; then unset TMVS_LIB_PATH; else export TMVS_LIB_PATH=$PWD/variants/$v/libtransmvs_hip.so; fi
   timeout -k 10 300 rocprofv3 --kernel-trace -T -d $OUT/trace -o run --output-format csv -- \
-      python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --profile-steps 0 > $OUT/trace.log 2>&1 || exit $?
+      python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --profile-steps 0 --e2e-steps 0 --train-steps 0 > $OUT/trace.log 2>&1 || exit $?
   python3 scripts/trace_table.py $OUT/trace/run_kernel_trace.csv > $OUT/trace_table.txt
   echo "== $v"
   grep -E "$REGEX" $OUT/trace_table.txt

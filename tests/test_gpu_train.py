@@ -160,6 +160,71 @@ def test_warp_corr_views_forward_backward(c, d, h, w, nv, scale):
     assert rep["sim"] < 2e-5 and rep["dref"] < 1e-5 and rep["dsrc"] < 1e-5, rep
 
 
+@pytest.mark.parametrize("c,d,h,w,nv,scale,zoom", [(32, 48, 144, 192, 3, 1.0, False), (8, 8, 24, 32, 3, 1.0, False),
+                                                   (32, 48, 144, 192, 3, 1e-7, False), (16, 32, 288, 384, 3, 1.0, False),
+                                                   (32, 48, 144, 192, 3, 1.0, True), (32, 16, 61, 83, 2, 1.0, True)])
+def test_warp_corr_views_backward_planes(c, d, h, w, nv, scale, zoom):
+    """The stage-1 backward with fronto-parallel depth planes (TMVS_WARP_BWD_PLANES: d src gathered per
+    source texel from the preimage of its tap square under the plane homography, no atomics) against
+    torch autograd through the oracle (CPU fp32), and against the fixed-point scatter of the same
+    call without the flag. zoom: source views with 2x and 0.5x focal lengths (a preimage box of
+    ~1 and ~4 pixels per side) and planes from 300 mm, partly off-image."""
+    from transmvsnet_amd import ops, synthetic
+    from transmvsnet_amd.train import warp_corr_views
+    g = torch.Generator().manual_seed(c + d + h + int(zoom))
+    feats = [torch.randn(1, c, h, w, generator=g) for _ in range(nv + 1)]
+    proj = synthetic.synthetic_cameras(nv + 1, h * 4, w * 4, seed=3)["stage1"].clone()
+    lo = 425.0
+    if zoom:
+        for v, f in ((1, 2.0), (2, 0.5)):
+            proj[0, v, 1, 0, 0] *= f
+            proj[0, v, 1, 1, 1] *= f
+        lo = 300.0
+    hyp = torch.linspace(lo, 935.0, d).view(1, d, 1, 1).expand(1, d, h, w).contiguous()
+    dsim = torch.randn(nv, d, h, w, generator=g) * scale
+    rows = ops.proj_rows(proj)[0]
+    grads = {}
+    for planes in (True, False):
+        ref_g = feats[0][0].permute(1, 2, 0).contiguous().to(DEV).requires_grad_()
+        src_g = torch.stack([f[0].permute(1, 2, 0) for f in feats[1:]]).contiguous().to(DEV).requires_grad_()
+        sims = warp_corr_views(ref_g, src_g, hyp[0].to(DEV), rows, planes=planes)
+        sims.backward(dsim.to(DEV))
+        torch.cuda.synchronize()
+        grads[planes] = (ref_g.grad.cpu(), src_g.grad.cpu())
+    xs = [f.clone().requires_grad_() for f in feats]
+    projs = torch.unbind(proj, 1)
+    ref_sims = []
+    for i in range(nv):
+        warped = oracle.homo_warping(xs[1 + i], oracle.compose_proj(projs[1 + i]), oracle.compose_proj(projs[0]), hyp)
+        ref_sims.append((warped * xs[0].unsqueeze(2)).mean(1))
+    torch.cat(ref_sims, 0).backward(dsim)
+    dref, dsrc = grads[True]
+    rep = {"dref": _rel(dref.permute(2, 0, 1), xs[0].grad[0]),
+           "dsrc": max(_rel(dsrc[i].permute(2, 0, 1), xs[1 + i].grad[0]) for i in range(nv)),
+           "dsrc_vs_scatter": max(_rel(dsrc[i], grads[False][1][i]) for i in range(nv)),
+           "dref_vs_scatter": float((dref - grads[False][0]).abs().max())}
+    print((c, d, h, w, nv, scale, zoom), rep)
+    assert rep["dref"] < 1e-5 and rep["dsrc"] < 1e-5 and rep["dsrc_vs_scatter"] < 1e-5, rep
+    assert rep["dref_vs_scatter"] == 0.0, rep  # the same gather kernel (without its scatter half)
+
+
+def test_warp_corr_backward_planes_flags_nonplanar():
+    """planes=True on hypotheses that are not one depth per plane sets flag bit 2 (the backward raises)."""
+    from transmvsnet_amd import ops, synthetic
+    c, d, h, w, nv = 8, 8, 24, 32, 2
+    g = torch.Generator().manual_seed(5)
+    ref = torch.randn(h, w, c, generator=g).to(DEV)
+    src = torch.randn(nv, h, w, c, generator=g).to(DEV)
+    rows = ops.proj_rows(synthetic.synthetic_cameras(nv + 1, h * 4, w * 4, seed=3)["stage1"])[0]
+    hyp = torch.linspace(425.0, 935.0, d).view(d, 1, 1).expand(d, h, w).contiguous()
+    dsim = torch.randn(nv, d, h, w, generator=g).to(DEV)
+    _, _, flag = ops.warp_corr_backward(ref, src, rows, hyp.to(DEV), dsim, planes=True)
+    assert int(flag.item()) == 0
+    hyp2 = hyp.clone()
+    hyp2[3, 7, 9] += 1.0
+    _, _, flag = ops.warp_corr_backward(ref, src, rows, hyp2.to(DEV), dsim, planes=True)
+    assert int(flag.item()) & 2
+
 
 def test_depth_stages_training_step():
     """A training step's three DepthNet stages (hypotheses, cost volume + its backward, view aggregation,

@@ -100,12 +100,13 @@ SIGNATURES = {
     "tmvs_softmax_backward": (I, [P, P, I, I, I, I, P, P]),
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 PW_NPARAMS = 201
 ENC_NPARAMS = 8544
 KV_NFLOATS = 160
 WARP_PARTIAL = 1
 WARP_ROT_PLAIN = 2
+WARP_BWD_PLANES = 4
 CONV_TRANSPOSED = 1
 CONV_ACCUMULATE = 2
 

@@ -259,7 +259,11 @@ constexpr int kKvTilesPerWave = 8;     // kv: at most this many tiles per wave (
 
 // (KV, Ksum) partial sums: per wave, tiles of 16 source tokens; K, V by MFMA; per lane the
 // two heads it owns are accumulated over its tokens, then summed over the 16 token lanes.
-__global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __restrict__ src, int S,
+#ifndef TMVS_KV_WAVES
+#define TMVS_KV_WAVES 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_KV_WAVES)))
+void fmt_kv_partial_kernel(const float* __restrict__ src, int S,
                                                               const float* __restrict__ w,
                                                               float* __restrict__ partial, int tpw) {
   __shared__ float red[4][kKV];
@@ -394,7 +398,11 @@ __global__ __launch_bounds__(1024) void fmt_kv_combine_kernel(const float* __res
 #define TMVS_APPLY_NT 1
 #endif
 constexpr int kApplyNT = TMVS_APPLY_NT;
-__global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, int L, const float* __restrict__ kvg,
+#ifndef TMVS_APPLY_WAVES
+#define TMVS_APPLY_WAVES 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_APPLY_WAVES)))
+void fmt_apply_kernel(float* __restrict__ x, int L, const float* __restrict__ kvg,
                                                         long kv_stride, const float* __restrict__ w, int tpw) {
   __shared__ __attribute__((aligned(16))) float kvs[kKV];
   // the per-feature vectors, read from LDS in the tile loop: a global load there is a full memory

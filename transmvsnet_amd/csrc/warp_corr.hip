@@ -716,7 +716,7 @@ __device__ inline int fix_shift(const unsigned* mx, int C, long count) {
   return 62 - e;
 }
 
-template <int C>
+template <int C, bool SCATTER>
 __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restrict__ ref,
                                                             const float* __restrict__ src,
                                                             const float* __restrict__ hyp,
@@ -816,6 +816,7 @@ __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restr
       // scatter coefficients w_tap * g, summed per source pixel across consecutive planes: the 4 taps
       // of a plane occupy the 4 (x, y) parity classes, so slot (X&1, Y&1) holds the latest tap of its
       // class and its running coefficient; a slot is flushed (C atomics) only when its tap changes
+      if constexpr (SCATTER)
 #pragma unroll
       for (int sl = 0; sl < 4; ++sl) {
         const int X = x0 + ((x0 ^ sl) & 1), Y = y0 + ((y0 ^ (sl >> 1)) & 1);
@@ -831,8 +832,9 @@ __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restr
         if (act && inside) scoef[sl] = fmaf(wgt, g, scoef[sl]);
       }
     }
+    if constexpr (SCATTER)
 #pragma unroll
-    for (int sl = 0; sl < 4; ++sl) flush(sl, true);
+      for (int sl = 0; sl < 4; ++sl) flush(sl, true);
   }
   if (live) {
     float* dref = dref_part + ((size_t)(v * gridDim.z + blockIdx.z) * HW + p) * C;
@@ -840,6 +842,153 @@ __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restr
     for (int c4 = 0; c4 < C / 4; ++c4)
       *reinterpret_cast<float4*>(dref + 4 * c4) =
           make_float4(dr[4 * c4], dr[4 * c4 + 1], dr[4 * c4 + 2], dr[4 * c4 + 3]);
+  }
+}
+
+// d src as a GATHER, for fronto-parallel hypotheses (hyp[d][p] = hyp[d][0] for every p: stage 1's
+// depth planes). On plane d the forward maps reference pixel p to X = A_d (p, 1) with
+// A_d = z_d R + t e3^T (project(): ix = X/Z), a homography; source texel q is one of p's 4 bilinear
+// taps iff ix(p) lies in [qx-1, qx+1) x [qy-1, qy+1). So q's contributors are the integer pixels in
+// the preimage of that square under A_d: while the square is in front of the source camera (the
+// third coordinate of A_d^-1 (c, 1), = 1/Z, positive at its 4 corners -- it is affine in c) that
+// preimage is the quadrilateral of the 4 mapped corners; otherwise (the plane's horizon crosses the
+// square) every pixel is a candidate. Each candidate is re-projected with project() -- the forward's
+// own rounding -- and contributes w_tap * dsim/C * ref[p] exactly when the forward sampled q with
+// weight w_tap, so no atomics and no fixed point: a texel's sum has a fixed order (planes ascending
+// within each of the 4 waves' plane quarters, then (w0 + w1) + (w2 + w3)). The square is widened by
+// 0.02 px before mapping to cover the difference between the exact and the forward-rounded ix.
+// Block = 64 texels x 4 plane quarters (one wave each); a thread whose own hyp[d][q] differs from
+// hyp[d][0] sets flag bit 2 (the hypotheses were not planes: the result is unusable).
+constexpr int kPlanesMaxD = 64;
+template <int C>
+__global__ __launch_bounds__(256) void warp_bwd_src_planes_kernel(const float* __restrict__ ref,
+                                                                  const float* __restrict__ hyp,
+                                                                  const float* __restrict__ dsim, int D, int H, int W,
+                                                                  WarpArgs args, float* __restrict__ dsrc,
+                                                                  int* __restrict__ flag) {
+  __shared__ float ainv[kPlanesMaxD][9];
+  __shared__ float plane[kPlanesMaxD];
+  __shared__ float red[3][64][C + 1];
+  const int HW = H * W;
+  const int v = blockIdx.y;
+  const float* R = args.proj[v];
+  if (threadIdx.x < D) {
+    const double z = hyp[(size_t)threadIdx.x * HW];
+    plane[threadIdx.x] = (float)z;
+    const double a0 = z * R[0], a1 = z * R[1], a2 = z * R[2] + R[3];
+    const double a3 = z * R[4], a4 = z * R[5], a5 = z * R[6] + R[7];
+    const double a6 = z * R[8], a7 = z * R[9], a8 = z * R[10] + R[11];
+    const double c0 = a4 * a8 - a5 * a7, c1 = a2 * a7 - a1 * a8, c2 = a1 * a5 - a2 * a4;
+    const double det = a0 * c0 + a3 * c1 + a6 * c2;
+    float* o = ainv[threadIdx.x];
+    if (det != 0.0 && isfinite(det)) {
+      const double r = 1.0 / det;
+      o[0] = (float)(c0 * r);
+      o[1] = (float)(c1 * r);
+      o[2] = (float)(c2 * r);
+      o[3] = (float)((a5 * a6 - a3 * a8) * r);
+      o[4] = (float)((a0 * a8 - a2 * a6) * r);
+      o[5] = (float)((a2 * a3 - a0 * a5) * r);
+      o[6] = (float)((a3 * a7 - a4 * a6) * r);
+      o[7] = (float)((a1 * a6 - a0 * a7) * r);
+      o[8] = (float)((a0 * a4 - a1 * a3) * r);
+    } else {
+      for (int k = 0; k < 9; ++k) o[k] = 0.f;  // third coordinate 0: every pixel is a candidate
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int q = blockIdx.x * 64 + lane;
+  const bool live = q < HW;
+  const int qq = live ? q : HW - 1;
+  const int qy = qq / W, qx = qq - qy * W;
+  const float halfw = (float)(W - 1) / 2.f, halfh = (float)(H - 1) / 2.f;
+  const float* dv = dsim + (size_t)v * D * HW;
+  float acc[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) acc[c] = 0.f;
+  const int per = (D + 3) / 4, d0 = wv * per, d1 = d0 + per < D ? d0 + per : D;
+  bool nonplanar = false;
+  constexpr float kPad = 1.02f;
+#pragma unroll 1
+  for (int d = d0; d < d1; ++d) {
+    const float dep = plane[d];
+    nonplanar |= live && hyp[(size_t)d * HW + qq] != dep;
+    const float* A = ainv[d];
+    float mnx = 3.0e38f, mxx = -3.0e38f, mny = 3.0e38f, mxy = -3.0e38f;
+    bool unb = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float cx = (float)qx + ((k & 1) ? kPad : -kPad), cy = (float)qy + ((k & 2) ? kPad : -kPad);
+      const float hz = fmaf(A[6], cx, fmaf(A[7], cy, A[8]));
+      if (!(hz > 0.f)) {
+        unb = true;
+      } else {
+        const float px = fmaf(A[0], cx, fmaf(A[1], cy, A[2])) / hz;
+        const float py = fmaf(A[3], cx, fmaf(A[4], cy, A[5])) / hz;
+        mnx = fminf(mnx, px);
+        mxx = fmaxf(mxx, px);
+        mny = fminf(mny, py);
+        mxy = fmaxf(mxy, py);
+      }
+    }
+    int bx0 = 0, bx1 = W - 1, by0 = 0, by1 = H - 1;
+    if (!unb) {  // clamp in float first (a far-away preimage must not overflow the int conversion)
+      bx0 = (int)fminf(fmaxf(floorf(mnx), 0.f), (float)W);
+      bx1 = (int)fmaxf(fminf(ceilf(mxx), (float)(W - 1)), -1.f);
+      by0 = (int)fminf(fmaxf(floorf(mny), 0.f), (float)H);
+      by1 = (int)fmaxf(fminf(ceilf(mxy), (float)(H - 1)), -1.f);
+    }
+    if (!live) bx1 = bx0 - 1;
+    const float* gd = dv + (size_t)d * HW;
+#pragma unroll 1
+    for (int py = by0; py <= by1; ++py) {
+      const float fyp = (float)py;
+#pragma unroll 1
+      for (int px = bx0; px <= bx1; ++px) {
+        const float fxp = (float)px;
+        const float rx = rot_row(R, fxp, fyp, args.rot_plain);
+        const float ry = rot_row(R + 4, fxp, fyp, args.rot_plain);
+        const float rz = rot_row(R + 8, fxp, fyp, args.rot_plain);
+        int x0, y0;
+        float fx, fy;
+        project(rx, ry, rz, R[3], R[7], R[11], dep, halfw, halfh, x0, y0, fx, fy);
+        const int dx = qx - x0, dy = qy - y0;
+        if ((unsigned)dx > 1u || (unsigned)dy > 1u) continue;
+        const int p = py * W + px;
+        const float g = gd[p] * (1.f / (float)C);  // C = 2^n: exact
+        const float wgt = (dy == 0 ? 1.f - fy : fy) * (dx == 0 ? 1.f - fx : fx);
+        const float coef = wgt * g;
+        const float* rp = ref + (size_t)p * C;
+#pragma unroll
+        for (int c4 = 0; c4 < C / 4; ++c4) {
+          const float4 r4 = *reinterpret_cast<const float4*>(rp + 4 * c4);
+          acc[4 * c4 + 0] = fmaf(coef, r4.x, acc[4 * c4 + 0]);
+          acc[4 * c4 + 1] = fmaf(coef, r4.y, acc[4 * c4 + 1]);
+          acc[4 * c4 + 2] = fmaf(coef, r4.z, acc[4 * c4 + 2]);
+          acc[4 * c4 + 3] = fmaf(coef, r4.w, acc[4 * c4 + 3]);
+        }
+      }
+    }
+  }
+  if (nonplanar) atomicOr(flag, 2);
+  if (wv > 0) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) red[wv - 1][lane][c] = acc[c];
+  }
+  __syncthreads();
+  if (wv == 0 && live) {
+    float* o = dsrc + ((size_t)v * HW + q) * C;
+#pragma unroll
+    for (int c4 = 0; c4 < C / 4; ++c4) {
+      float t[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = 4 * c4 + e;
+        t[e] = (acc[c] + red[0][lane][c]) + (red[1][lane][c] + red[2][lane][c]);
+      }
+      *reinterpret_cast<float4*>(o + 4 * c4) = make_float4(t[0], t[1], t[2], t[3]);
+    }
   }
 }
 
@@ -974,7 +1123,9 @@ extern "C" int tmvs_warp_corr_backward(const float* ref_fea, const float* src_fe
   unsigned long long* fix = (unsigned long long*)workspace;
   int* ovf = (int*)((char*)workspace + (size_t)n * sizeof(unsigned long long));
   unsigned* absmax = (unsigned*)(ovf + 1);
-  if (hipMemsetAsync(workspace, 0, (size_t)n * sizeof(unsigned long long) + 3 * sizeof(int), st) != hipSuccess)
+  if ((flags & TMVS_WARP_BWD_PLANES) ? hipMemsetAsync(ovf, 0, 3 * sizeof(int), st) != hipSuccess
+                                      : hipMemsetAsync(workspace, 0, (size_t)n * sizeof(unsigned long long) + 3 * sizeof(int),
+                                                       st) != hipSuccess)
     return TMVS_ERR_HIP;
   const int HW = height * width;
   const long nd = (long)n_src * ndepth * HW, nr = (long)HW * channels;
@@ -986,29 +1137,38 @@ extern "C" int tmvs_warp_corr_backward(const float* ref_fea, const float* src_fe
   const int dchunk = bwd_dchunk(ndepth), nch = (ndepth + dchunk - 1) / dchunk;
   float* part = (float*)((char*)workspace + (size_t)n * sizeof(unsigned long long) + 256);
   const dim3 grid((HW + 255) / 256, n_src, nch);
+  const bool planes = (flags & TMVS_WARP_BWD_PLANES) != 0;
+  if (planes && ndepth > kPlanesMaxD) return TMVS_ERR_SHAPE;
+  const dim3 pgrid((HW + 63) / 64, n_src);
+#define TMVS_BWD_CASE(CC)                                                                                              \
+  case CC:                                                                                                             \
+    if (planes) {                                                                                                      \
+      hipLaunchKernelGGL((warp_corr_bwd_kernel<CC, false>), grid, dim3(256), 0, st, ref_fea, src_fea, hyp, dsim, n_src, \
+                         ndepth, height, width, dchunk, a, part, fix, absmax);                                          \
+      hipLaunchKernelGGL(warp_bwd_src_planes_kernel<CC>, pgrid, dim3(256), 0, st, ref_fea, hyp, dsim, ndepth, height,   \
+                         width, a, dsrc, ovf);                                                                          \
+    } else {                                                                                                           \
+      hipLaunchKernelGGL((warp_corr_bwd_kernel<CC, true>), grid, dim3(256), 0, st, ref_fea, src_fea, hyp, dsim, n_src,  \
+                         ndepth, height, width, dchunk, a, part, fix, absmax);                                          \
+    }                                                                                                                  \
+    break;
   switch (channels) {
-    case 8:
-      hipLaunchKernelGGL(warp_corr_bwd_kernel<8>, grid, dim3(256), 0, st, ref_fea, src_fea, hyp, dsim, n_src, ndepth,
-                         height, width, dchunk, a, part, fix, absmax);
-      break;
-    case 16:
-      hipLaunchKernelGGL(warp_corr_bwd_kernel<16>, grid, dim3(256), 0, st, ref_fea, src_fea, hyp, dsim, n_src, ndepth,
-                         height, width, dchunk, a, part, fix, absmax);
-      break;
-    case 32:
-      hipLaunchKernelGGL(warp_corr_bwd_kernel<32>, grid, dim3(256), 0, st, ref_fea, src_fea, hyp, dsim, n_src, ndepth,
-                         height, width, dchunk, a, part, fix, absmax);
-      break;
+    TMVS_BWD_CASE(8)
+    TMVS_BWD_CASE(16)
+    TMVS_BWD_CASE(32)
     default:
       return TMVS_ERR_SHAPE;
   }
+#undef TMVS_BWD_CASE
   TMVS_CHECK_LAUNCH();
   const long nref = (long)HW * channels;
   hipLaunchKernelGGL(sum_dref_parts_kernel, dim3((unsigned)((nref + 255) / 256)), dim3(256), 0, st, (const float*)part,
                      n_src * nch, nref, dref);
   TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(fix_to_float_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (const unsigned long long*)fix,
-                     n, (const unsigned*)absmax, channels, (long)ndepth * HW, dsrc);
-  TMVS_CHECK_LAUNCH();
+  if (!planes) {
+    hipLaunchKernelGGL(fix_to_float_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       (const unsigned long long*)fix, n, (const unsigned*)absmax, channels, (long)ndepth * HW, dsrc);
+    TMVS_CHECK_LAUNCH();
+  }
   return TMVS_OK;
 }

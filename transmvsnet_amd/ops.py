@@ -728,9 +728,11 @@ def bn_relu_backward_grouped(dy, z, mean, var, gamma, beta, eps):
     return dz, dg, db
 
 
-def warp_corr_backward(ref_nhwc, src_nhwc, proj12, hyp, dsim, rot_order="auto"):
+def warp_corr_backward(ref_nhwc, src_nhwc, proj12, hyp, dsim, rot_order="auto", planes=False):
     """tmvs_warp_corr_backward: one sample, ref [H,W,C], src [V,H,W,C] NHWC, proj12 HOST [V,12],
-    hyp [D,H,W], dsim [V,D,H,W] -> (dref [H,W,C], dsrc [V,H,W,C], overflow flag tensor [1] int32)."""
+    hyp [D,H,W], dsim [V,D,H,W] -> (dref [H,W,C], dsrc [V,H,W,C], flag tensor [1] int32: bit 0 a
+    non-finite dsim / ref, bit 1 non-planar hyp under planes=True). planes=True (TMVS_WARP_BWD_PLANES:
+    hyp[d] is one depth per plane, stage 1) gathers dsrc per source texel instead of scattering it."""
     for t, n in ((ref_nhwc, "ref"), (src_nhwc, "src"), (hyp, "hyp"), (dsim, "dsim")):
         _dev(t, n)
     v, h, w, c = src_nhwc.shape
@@ -744,7 +746,8 @@ def warp_corr_backward(ref_nhwc, src_nhwc, proj12, hyp, dsim, rot_order="auto"):
     dsrc = torch.empty_like(src_nhwc)
     with _Span("tmvs_warp_corr_backward"):
         _lib.check(_lib_h().tmvs_warp_corr_backward(_ptr(ref_nhwc), _ptr(src_nhwc), proj.ctypes.data, _ptr(hyp), _ptr(dsim),
-                                                    v, c, d, h, w, warp_flags(rot_order, h * w), _ptr(ws),
+                                                    v, c, d, h, w,
+                                                    warp_flags(rot_order, h * w) | (_lib.WARP_BWD_PLANES if planes else 0), _ptr(ws),
                                                     ws.numel() * 4, _ptr(dref), _ptr(dsrc), _stream()),
                    "tmvs_warp_corr_backward")
     flag = ws.view(torch.int32)[2 * v * h * w * c: 2 * v * h * w * c + 1]

@@ -52,7 +52,7 @@ BN_MOMENTUM = 0.1
 
 class _WarpCorrViews(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ref, src, hyp, proj12, rot_order):
+    def forward(ctx, ref, src, hyp, proj12, rot_order, planes):
         v, h, w, c = src.shape
         d = hyp.shape[0]
         sims = torch.empty(v, d, h, w, device=src.device)
@@ -62,20 +62,21 @@ class _WarpCorrViews(torch.autograd.Function):
             ops.warp_corr(ref[None], src[i:i + 1][None], proj12[None, i:i + 1], hyp[None], view_w_in=ones, vw_shift=0,
                           vw_total=1, partial=True, sim_out=sims[i:i + 1], wsum_out=wsum, rot_order=rot_order)
         ctx.save_for_backward(ref, src, hyp)
-        ctx.proj12, ctx.rot_order = proj12, rot_order
+        ctx.proj12, ctx.rot_order, ctx.planes = proj12, rot_order, planes
         return sims
 
     @staticmethod
     def backward(ctx, dsims):
         ref, src, hyp = ctx.saved_tensors
-        dref, dsrc, flag = ops.warp_corr_backward(ref, src, ctx.proj12, hyp, dsims.contiguous(), ctx.rot_order)
+        dref, dsrc, flag = ops.warp_corr_backward(ref, src, ctx.proj12, hyp, dsims.contiguous(), ctx.rot_order,
+                                                  planes=ctx.planes)
         if _DEFERRED_FLAGS is not None:  # inside depth_stages_train: one host sync after the whole backward
             _DEFERRED_FLAGS.append(flag.clone())
         elif torch.cuda.is_current_stream_capturing():  # a HIP-graph capture: checked after the replays
             GRAPH_FLAGS.append(flag)
         else:
             _check_overflow([flag])
-        return dref, dsrc, None, None, None
+        return dref, dsrc, None, None, None, None
 
 
 _DEFERRED_FLAGS = None
@@ -88,17 +89,23 @@ def check_graph_flags():
 
 
 def _check_overflow(flags):
-    if flags and int(torch.stack([f.reshape(()) for f in flags]).sum().item()):
-        raise RuntimeError("warp_corr_backward: non-finite d similarity or reference features (the fixed-point "
-                           "scatter needs finite values)")
+    if not flags:
+        return
+    bits = int(torch.stack([f.reshape(()) for f in flags]).max().item())  # flag words are 0 when clean
+    if bits:
+        raise RuntimeError("warp_corr_backward: non-finite d similarity or reference features (bit 1: the "
+                           "fixed-point scatter needs finite values) or non-planar hypotheses under planes=True "
+                           f"(bit 2); flag {bits}")
 
 
-def warp_corr_views(ref_nhwc, src_nhwc, hyp, proj12, rot_order="auto"):
+def warp_corr_views(ref_nhwc, src_nhwc, hyp, proj12, rot_order="auto", planes=False):
     """Per-view similarity volumes sim_v [V, D, H, W] for ONE sample (ref [H,W,C], src [V,H,W,C] NHWC,
-    hyp [D,H,W], proj12 HOST [V,12] from ops.proj_rows), differentiable w.r.t. ref and src."""
+    hyp [D,H,W], proj12 HOST [V,12] from ops.proj_rows), differentiable w.r.t. ref and src. planes:
+    hyp[d] holds one depth per plane (stage 1), so the backward gathers d src (TMVS_WARP_BWD_PLANES)."""
     if not src_nhwc.is_cuda:
         raise RuntimeError("warp_corr_views runs on the GPU only (no CPU fallback)")
-    return _WarpCorrViews.apply(ref_nhwc.contiguous(), src_nhwc.contiguous(), hyp.contiguous(), proj12, rot_order)
+    return _WarpCorrViews.apply(ref_nhwc.contiguous(), src_nhwc.contiguous(), hyp.contiguous(), proj12, rot_order,
+                                planes)
 
 
 def _pack2d(w, transpose_io=False, flip=False):
@@ -540,7 +547,8 @@ def depth_stages_forward_train(model, stage_features, proj_matrix, depth_values,
             hyp = ops.stage_hypotheses(dv, prev_raw, model.ndepths[s], model.depth_interals_ratio[s], img_hw,
                                        STAGE_SCALES[s])
             rows = ops.proj_rows(proj_matrix[name])[0]
-            sims = warp_corr_views(f[0], f[1:], hyp[0], rows, rot_order=model.warp_rot_order)  # [V,D,h,w]
+            sims = warp_corr_views(f[0], f[1:], hyp[0], rows, rot_order=model.warp_rot_order,
+                                   planes=prev_raw is None)  # [V,D,h,w]; stage 1: depth planes
             if s == 0:  # TransMVSNet.py:107 returns the stage-1 view weights detached
                 sim, vw_det = aggregate_train(sims, model)
             else:       # nearest x2 per stage (:194) = reading the stage-1 map at (y >> s, x >> s)
