@@ -6,7 +6,7 @@ reduction protocol: every rank must end with the full-view aggregate of oracle.b
 Tolerance: 1e-6 abs on O(1e-1) similarities (partial sums re-associate the view sum).
 """
 import os
-import socket
+import tempfile
 
 import pytest
 import torch
@@ -76,8 +76,7 @@ def _finalize(sim_sum, w_sum):
 
 
 def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         torch.set_num_threads(1)
         sd = golden_state_dict()
@@ -97,9 +96,8 @@ def _worker(rank, world, port, q):
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A file:// rendezvous in a fresh directory (no TCP port to race for when test files run in parallel)."""
+    return "file://" + os.path.join(tempfile.mkdtemp(prefix="tmvs_gloo_"), "store")
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -121,8 +119,7 @@ def test_view_sharded_cost_volume_gloo(world):
 
 
 def _grad_worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         from transmvsnet_amd.train import allreduce_gradients
         g = torch.Generator().manual_seed(100 + rank)
@@ -205,8 +202,7 @@ def test_view_groups_layout():
 
 
 def _hybrid_worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         from transmvsnet_amd.distributed import make_view_shard
         torch.set_num_threads(1)

@@ -108,27 +108,14 @@ def warp_corr_views(ref_nhwc, src_nhwc, hyp, proj12, rot_order="auto", planes=Fa
                                 planes)
 
 
-def _pack2d(w, transpose_io=False, flip=False):
-    """A Conv2d weight [Co][Ci][k][k] (k = 1 or 3) as the kd = 1 plane of a [27][Co'][Ci'] block for the
-    depth-1 generic 3-D conv (other taps zero); transpose_io swaps Co/Ci (data gradient)."""
-    co, ci, k, _ = w.shape
-    blk = torch.zeros(27, ci if transpose_io else co, co if transpose_io else ci, device=w.device)
-    ww = w.detach().float()
-    if transpose_io:
-        ww = ww.transpose(0, 1)
-    if k == 1:
-        blk[13] = ww[:, :, 0, 0]
-    else:
-        blk[9:18] = ww.permute(2, 3, 0, 1).reshape(9, ww.shape[0], ww.shape[1])
-    return blk.contiguous()
-
-
 class _PathwayStep(torch.autograd.Function):
     """One FMT_with_pathway lateral step (models/FMT.py:201-209, 221-228) with its backward:
     out = smooth(up2(reduce(coarse)) + lateral). coarse [N,h,w,cc] NHWC, lateral [N,cf,2h,2w] NCHW ->
-    out [N,2h,2w,cf] NHWC. Forward: the fused inference kernel (tmvs_fmt_pathway); backward: the
-    smoothing's data / weight gradients (depth-1 generic conv, transposed gather / wgrad), the
-    interpolation's adjoint (tmvs_upsample2_backward_nhwc), the 1x1 reduction's gradients."""
+    out [N,2h,2w,cf] NHWC. Forward: the fused inference kernel (tmvs_fmt_pathway); backward on the 2-D
+    training convs of FeatureNet: the smoothing's data gradient as a forward conv of the flipped,
+    transposed weight on the MFMA kernels (featurenet_train.dgrad_same), its weight gradient
+    (tmvs_conv2d_wgrad), the interpolation's adjoint (tmvs_upsample2_backward_nhwc), the 1x1
+    reduction's gradients (tmvs_conv2d_generic / tmvs_conv2d_wgrad)."""
 
     @staticmethod
     def forward(ctx, coarse, lateral, w_reduce, w_smooth):
@@ -141,24 +128,22 @@ class _PathwayStep(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        from .featurenet_train import _taps, _taps_t, _untaps, dgrad_same
         coarse, lateral, w_reduce, w_smooth = ctx.saved_tensors
         n, h, w, cc = coarse.shape
         cf = w_reduce.shape[0]
         dout = dout.contiguous()
-        c5 = coarse.contiguous().view(n, 1, h, w, cc)
+        coarse = coarse.contiguous()
         # recompute u = up2(reduce(coarse)) + lateral (the fused forward keeps no intermediate)
-        r = ops.conv3d_generic(c5, _pack2d(w_reduce), cf, (1, h, w), 1, False)
-        u = ops.upsample2_add_nhwc(r.view(n, h, w, cf), lateral.contiguous())
-        d5 = dout.view(n, 1, 2 * h, 2 * w, cf)
-        du = ops.conv3d_generic(d5, _pack2d(w_smooth, transpose_io=True), cf, (1, 2 * h, 2 * w), 1, True)
-        dws = ops.conv3d_wgrad(d5, u.view(n, 1, 2 * h, 2 * w, cf), 1)[9:18]           # [9][co][ci]
-        dws = dws.permute(1, 2, 0).reshape(cf, cf, 3, 3).contiguous()
-        dlat = du.view(n, 2 * h, 2 * w, cf).permute(0, 3, 1, 2).contiguous()
-        dr = ops.upsample2_backward_nhwc(du.view(n, 2 * h, 2 * w, cf))
-        dr5 = dr.view(n, 1, h, w, cf)
-        dcoarse = ops.conv3d_generic(dr5, _pack2d(w_reduce, transpose_io=True), cc, (1, h, w), 1, True)
-        dwr = ops.conv3d_wgrad(dr5, c5, 1)[13].reshape(cf, cc, 1, 1).contiguous()
-        return dcoarse.view(n, h, w, cc), dlat, dwr, dws
+        r = ops.conv2d_generic(coarse, _taps(w_reduce), cf, (h, w), 1, 1, 0)
+        u = ops.upsample2_add_nhwc(r, lateral.contiguous())
+        du = dgrad_same(dout, w_smooth, (2 * h, 2 * w))
+        dws = _untaps(ops.conv2d_wgrad(dout, u.view(n, 2 * h, 2 * w, cf), 3, 1, 1), w_smooth.shape)
+        dlat = du.permute(0, 3, 1, 2).contiguous()
+        dr = ops.upsample2_backward_nhwc(du)
+        dcoarse = ops.conv2d_generic(dr, _taps_t(w_reduce), cc, (h, w), 1, 1, 0)
+        dwr = _untaps(ops.conv2d_wgrad(dr, coarse, 1, 1, 0), w_reduce.shape)
+        return dcoarse, dlat, dwr, dws
 
 
 def pathway_train(model, stage1_nhwc, stage2_nchw, stage3_nchw):
