@@ -216,7 +216,8 @@ def test_dcn_backward_vs_autograd(cout, h, w, scale):
 
 
 @pytest.mark.parametrize("a,bc,k,stride,h,w", [(32, 32, 3, 1, 37, 70), (27, 32, 3, 1, 20, 33), (16, 16, 3, 1, 9, 40),
-                                               (16, 8, 3, 2, 24, 30), (32, 16, 1, 1, 13, 17)])
+                                               (16, 8, 3, 2, 24, 30), (32, 16, 1, 1, 13, 17), (16, 32, 1, 1, 36, 48),
+                                               (8, 16, 1, 1, 72, 96), (8, 8, 3, 1, 144, 192)])
 def test_conv2d_wgrad_vs_torch(a, bc, k, stride, h, w):
     """tmvs_conv2d_wgrad (dW[k][a][b] = sum_p dz[p][a] x[p*s - pad + k][b]) against torch's fp64 conv2d
     weight gradient, incl. the all-taps 3x3 kernel (32 x 32, ragged tiles) and the 27-row offset conv.

@@ -705,7 +705,8 @@ extern "C" int tmvs_conv2d_wgrad(const float* direct, int a_ch, int batch, int p
                        batch, ph, pw, gh, gw, k, stride, pad, ppb, part);                                        \
     done = true;                                                                                                 \
   }
-  TMVS_WG2(8, 8) TMVS_WG2(16, 8) TMVS_WG2(16, 16) TMVS_WG2(32, 8) TMVS_WG2(32, 16) TMVS_WG2(32, 32)
+  TMVS_WG2(8, 8) TMVS_WG2(8, 16) TMVS_WG2(8, 32) TMVS_WG2(16, 8) TMVS_WG2(16, 16) TMVS_WG2(16, 32) TMVS_WG2(32, 8)
+  TMVS_WG2(32, 16) TMVS_WG2(32, 32)
 #undef TMVS_WG2
   if (!done && a_ch == 8 && b_ch == 3) {
     hipLaunchKernelGGL((conv2d_wgrad_small_kernel<8, 3>), dim3(nblk, k * k), dim3(kBlk), 0, st, direct, gathered,
