@@ -12,34 +12,25 @@ from __future__ import annotations
 import torch
 
 
-_COEF = {}  # (calls, momentum, device) -> the per-call weights m (1 - m)^(G-1-v) (made once: no copy in a graph)
-
-
-def _coef(g, m, dev):
-    key = (g, m, str(dev))
-    if key not in _COEF:
-        _COEF[key] = torch.tensor([m * (1.0 - m) ** (g - 1 - v) for v in range(g)], device=dev, dtype=torch.float32)
-    return _COEF[key]
-
-
 def update_running_stats(items, momentum):
-    """items: [(bn, mean [G, C], var [G, C] (biased, per call, in call order), n elements per call)]."""
+    """items: [(bn, mean [G, C], var [G, C] (biased, per call, in call order), n elements per call)].
+    Multi-tensor launches only (no per-BatchNorm kernels): per group of modules with the same G, one
+    scale of the running buffers, then per call v one weighted add of that call's statistics."""
     if not items:
         return
     with torch.no_grad():
         by_g = {}
         for bn, mean, var, n in items:
             by_g.setdefault(int(mean.shape[0]), []).append((bn, mean, var, n))
+        m = float(momentum)
         for g, group in by_g.items():
-            dev = group[0][1].device
-            m = float(momentum)
-            coef = _coef(g, m, dev)
             rms = [bn.running_mean for bn, _, _, _ in group]
             rvs = [bn.running_var for bn, _, _, _ in group]
-            cms = [torch.mv(mean.t(), coef) for _, mean, _, _ in group]
-            cvs = [torch.mv(var.t(), coef * (n / max(n - 1, 1))) for _, _, var, n in group]
             torch._foreach_mul_(rms, (1.0 - m) ** g)
             torch._foreach_mul_(rvs, (1.0 - m) ** g)
-            torch._foreach_add_(rms, cms)
-            torch._foreach_add_(rvs, cvs)
+            for v in range(g):
+                c = m * (1.0 - m) ** (g - 1 - v)
+                torch._foreach_add_(rms, [mean[v] for _, mean, _, _ in group], alpha=c)
+                torch._foreach_add_(rvs, torch._foreach_mul([var[v] for _, _, var, _ in group],
+                                                            [c * n / max(n - 1, 1) for _, _, _, n in group]))
             torch._foreach_add_([bn.num_batches_tracked for bn, _, _, _ in group], g)
