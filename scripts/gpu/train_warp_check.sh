@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_train.py -k "$K" \
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread ${FILES:-tests/test_gpu_train.py} -k "$K" \
   > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
 tail -3 $OUT/pytest.log
 bash scripts/diag/ab_train.sh > $OUT/train_times.txt 2>&1 || exit $?

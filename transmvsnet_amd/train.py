@@ -41,6 +41,7 @@ import torch.nn.functional as F
 
 from . import ops
 from .bn_running import update_running_stats
+from .packing import gather_packs
 
 # (name, stride, transposed, skip source) in forward order; channels from the module
 _LAYERS = (("conv0", 1, False, None), ("conv1", 2, False, None), ("conv2", 1, False, None),
@@ -221,7 +222,8 @@ class _FMTTrain(torch.autograd.Function):
     def forward(ctx, s1, pe, *params):
         nv, c, h, w = s1.shape
         L = h * w
-        enc = [_pack_enc(params[16 * i:16 * i + 16]) for i in range(8)]
+        enc = gather_packs(list(params), [(tuple(range(16 * i, 16 * i + 16)), lambda *p: _pack_enc(p))
+                                          for i in range(8)], "fmt_enc")  # one gather (packing.py)
         tokens = torch.empty(nv, L, c, device=s1.device)
         ops.fmt_embed(s1.contiguous(), pe, tokens)
         saved = []
@@ -299,32 +301,51 @@ def _pack_dgrad(w, transposed):
     return w.reshape(co, ci, 27).permute(2, 1, 0).contiguous()
 
 
-def _conv_fwd(x, w, cout, odims, stride, transposed):
-    """A CostRegNet layer's raw convolution (before train-mode BN): the inference layers' MFMA kernels
-    (tmvs_conv3d_mfma) where they cover the (cin, cout, stride), else tmvs_conv3d_generic (conv0's
-    Cin = 1)."""
+def _fwd_pack_fn(cin, cout, stride, transposed):
+    """The packing _conv_fwd's kernel reads: [27][Co][Ci], prob_kernel's [3][72] for the 8 -> 1 conv."""
+    def fn(w):
+        pk = _pack_fwd(w, transposed)
+        return ops.prob_pack(pk) if not transposed and (cin, cout, stride) == (8, 1, 1) else pk
+    return fn
+
+
+def _dgrad_pack_fn(cin, cout, stride, transposed):
+    """The packing _conv_dgrad's kernel reads (cin, cout: the forward layer's): [27][Ci][Co], its taps
+    reversed for a stride-1 conv on the MFMA kernels (prob_kernel's packing for conv0's 8 -> 1)."""
+    def fn(w):
+        pk = _pack_dgrad(w, transposed)
+        if not transposed and stride == 1 and (cout, cin, 1) in ops.MFMA_CONV:
+            pk = pk.flip(0)
+            if (cout, cin) == (8, 1):
+                pk = ops.prob_pack(pk)
+        return pk
+    return fn
+
+
+def _conv_fwd(x, pk, cout, odims, stride, transposed):
+    """A CostRegNet layer's raw convolution (before train-mode BN) with pk = _fwd_pack_fn's packing: the
+    inference layers' MFMA kernels (tmvs_conv3d_mfma) where they cover the (cin, cout, stride), else
+    tmvs_conv3d_generic."""
     cin = x.shape[-1]
     if (cin, cout) in ops.MFMA_DECONV if transposed else (cin, cout, stride) in ops.MFMA_CONV:
-        pk = _pack_fwd(w, transposed)
-        return ops.conv3d_mfma(x, ops.prob_pack(pk) if (cin, cout) == (8, 1) else pk, cout, stride, transposed)
-    return ops.conv3d_generic(x, _pack_fwd(w, transposed), cout, odims, stride, transposed)
+        return ops.conv3d_mfma(x, pk, cout, stride, transposed)
+    return ops.conv3d_generic(x, pk, cout, odims, stride, transposed)
 
 
-def _conv_dgrad(dz, w, cin, idims, stride, transposed, acc):
-    """d input of a layer (+ acc, the gradient already gathered for that tensor through a skip):
+def _conv_dgrad(dz, pk, cin, idims, stride, transposed, acc):
+    """d input of a layer (+ acc, the gradient already gathered for that tensor through a skip), pk =
+    _dgrad_pack_fn's packing:
       ConvTranspose3d -> Conv3d stride 2 of dz with the same weight tensor read as [Ci_t][Co_t];
       Conv3d stride 2 -> ConvTranspose3d of dz with the weight read as ConvTranspose [Co][Ci];
       Conv3d stride 1 -> Conv3d of dz with the taps reversed and [Co][Ci] transposed.
     On the MFMA kernels where they cover the shape, else the generic gathers."""
     cout = dz.shape[-1]
-    pk = _pack_dgrad(w, transposed)  # [27][Ci][Co]
     if transposed and (cout, cin, 2) in ops.MFMA_CONV:
         dx = ops.conv3d_mfma(dz, pk, cin, 2)
     elif not transposed and stride == 2 and (cout, cin) in ops.MFMA_DECONV:
         return ops.conv3d_mfma(dz, pk, cin, 2, transposed=True, skip=acc)
     elif not transposed and stride == 1 and (cout, cin, 1) in ops.MFMA_CONV:
-        fl = pk.flip(0).contiguous()
-        dx = ops.conv3d_mfma(dz, ops.prob_pack(fl) if (cout, cin) == (8, 1) else fl, cin, 1)
+        dx = ops.conv3d_mfma(dz, pk, cin, 1)
     elif transposed:  # strided gather of dz
         return ops.conv3d_generic(dz, pk, cin, idims, 2, False, out=acc)
     else:  # transposed gather of dz
@@ -332,6 +353,11 @@ def _conv_dgrad(dz, w, cin, idims, stride, transposed, acc):
     if acc is None:
         return dx
     return acc.add_(dx)
+
+
+def _layer_channels(w, transposed):
+    """(cin, cout) of a Conv3d [Co][Ci][..] / ConvTranspose3d [Ci][Co][..] weight."""
+    return (w.shape[0], w.shape[1]) if transposed else (w.shape[1], w.shape[0])
 
 
 def _unpack_wgrad(dw27, shape):
@@ -349,6 +375,13 @@ class _CostRegNetTrain(torch.autograd.Function):
         b, d, h, w = x.shape
         ws = params[:-1]
         wprob = params[-1]
+        # every layer's forward and data-gradient packings in one gather (packing.py)
+        weights = [ws[3 * i] for i in range(len(_LAYERS))] + [wprob]
+        geo = [(i, *_layer_channels(weights[i], tr), st, tr) for i, (_, st, tr, _) in enumerate(_LAYERS)]
+        geo.append((len(_LAYERS), 8, 1, 1, False))
+        packs = gather_packs(weights, [(i, _fwd_pack_fn(ci, co, st, tr)) for i, ci, co, st, tr in geo] +
+                             [(i, _dgrad_pack_fn(ci, co, st, tr)) for i, ci, co, st, tr in geo], "costregnet")
+        fwd_pk, ctx.dgrad_pk = packs[:len(geo)], packs[len(geo):]
         acts = {"input": (x.contiguous().view(b, d, h, w, 1), (d, h, w))}
         saved = []
         cur, dims = acts["input"]
@@ -357,7 +390,7 @@ class _CostRegNetTrain(torch.autograd.Function):
             wt, g, bt = ws[3 * i], ws[3 * i + 1], ws[3 * i + 2]
             cout = wt.shape[1] if transposed else wt.shape[0]
             odims = tuple(2 * n for n in dims) if transposed else (dims if stride == 1 else _down(dims))
-            z = _conv_fwd(cur, wt.detach(), cout, odims, stride, transposed)
+            z = _conv_fwd(cur, fwd_pk[i], cout, odims, stride, transposed)
             mean, var = ops.bn_stats(z)
             y = ops.bn_relu_train(z, mean, var, g.detach(), bt.detach(), eps,
                                   skip=acts[skip][0] if skip is not None else None)
@@ -365,7 +398,7 @@ class _CostRegNetTrain(torch.autograd.Function):
             stats.append((mean, var, z.numel() // z.shape[-1]))
             acts[name] = (y, odims)
             cur, dims = y, odims
-        logits = _conv_fwd(cur, wprob.detach(), 1, dims, 1, False)
+        logits = _conv_fwd(cur, fwd_pk[-1], 1, dims, 1, False)
         ctx.eps = eps
         ctx.layer_io = saved
         ctx.u11 = cur
@@ -381,9 +414,10 @@ class _CostRegNetTrain(torch.autograd.Function):
         b, d, h, w = dlogits.shape
         g = dlogits.contiguous().view(b, d, h, w, 1)
         grads = [None] * len(params)
-        grads[-1] = _unpack_wgrad(ops.conv3d_wgrad(g, ctx.u11, 1), wprob.shape)
+        dws = [None] * (len(_LAYERS) + 1)
+        dws[-1] = ops.conv3d_wgrad(g, ctx.u11, 1)
         # gradient w.r.t. each layer's output, filled as the backward reaches it
-        dout = {"conv11": _conv_dgrad(g, wprob.detach(), ctx.u11.shape[-1], (d, h, w), 1, False, None)}
+        dout = {"conv11": _conv_dgrad(g, ctx.dgrad_pk[-1], ctx.u11.shape[-1], (d, h, w), 1, False, None)}
         for i in range(len(_LAYERS) - 1, -1, -1):
             name, stride, transposed, skip = _LAYERS[i]
             wt, gm, bt = ws[3 * i], ws[3 * i + 1], ws[3 * i + 2]
@@ -397,12 +431,20 @@ class _CostRegNetTrain(torch.autograd.Function):
                 dw = ops.conv3d_wgrad(xin, dz, 2)
             else:
                 dw = ops.conv3d_wgrad(dz, xin, stride)
-            grads[3 * i] = _unpack_wgrad(dw, wt.shape)
+            dws[i] = dw
             grads[3 * i + 1], grads[3 * i + 2] = dgam, dbet
             prev = _LAYERS[i - 1][0] if i > 0 else "input"
             cin = xin.shape[-1]
             acc = dout.get(prev)
-            dout[prev] = _conv_dgrad(dz, wt.detach(), cin, idims, stride, transposed, acc)
+            dout[prev] = _conv_dgrad(dz, ctx.dgrad_pk[i], cin, idims, stride, transposed, acc)
+        # the weight gradients back to the torch layouts, one gather for all layers
+        shapes = [ws[3 * i].shape for i in range(len(_LAYERS))] + [wprob.shape]
+        unp = gather_packs(dws, [(i, (lambda t, s=s_: _unpack_wgrad(t, s))) for i, s_ in enumerate(shapes)],
+                           "costregnet_wgrad")
+        for i in range(len(_LAYERS)):
+            grads[3 * i] = unp[i]
+        grads[-1] = unp[-1]
+        ctx.dgrad_pk = None
         dx = dout["input"].view(b, d, h, w)
         return (dx, None, None, *grads)
 
