@@ -305,100 +305,104 @@ __global__ __launch_bounds__(kTB) void layer_norm_bwd_kernel(const float* __rest
         (red[threadIdx.x][0] + red[threadIdx.x][1]) + (red[threadIdx.x][2] + red[threadIdx.x][3]);
 }
 
+// Thread layout of the three token kernels below: thread = (token slot, head) with head = threadIdx & 7, so
+// a wave's 64 lanes cover 8 consecutive tokens x 8 heads and each 16-byte head quad load/store of the wave
+// is one contiguous 1 KiB span (the former token-per-thread loop over heads read 128-B-strided quads).
+constexpr int kTokPerBlock = kTB / 8;
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
 // msg[t][h*4+m] = (sum_d Q[h,d] KV[h][m][d]) / (sum_d Q[h,d] Ks[h][d] + eps); tokens of group gi use kv[gi*kvs]
 __global__ __launch_bounds__(kTB) void linattn_fwd_kernel(const float* __restrict__ q, long T, long tpg,
                                                           const float* __restrict__ kv, long kv_stride,
                                                           float* __restrict__ msg) {
-  const long t = (long)blockIdx.x * kTB + threadIdx.x;
+  const int h = threadIdx.x & 7;
+  const long t = (long)blockIdx.x * kTokPerBlock + (threadIdx.x >> 3);
   if (t >= T) return;
   const float* K = kv + (t / tpg) * kv_stride;
+  const float4 q4 = ld4(q + t * 32 + h * 4);
+  const float Q[4] = {elu1f(q4.x), elu1f(q4.y), elu1f(q4.z), elu1f(q4.w)};
+  float den = 0.f;
 #pragma unroll
-  for (int h = 0; h < 8; ++h) {
-    float Q[4];
+  for (int d = 0; d < 4; ++d) den = fmaf(Q[d], K[128 + h * 4 + d], den);
+  const float z = 1.f / (den + kAttnEps);
+  float o[4];
 #pragma unroll
-    for (int d = 0; d < 4; ++d) Q[d] = elu1f(q[t * 32 + h * 4 + d]);
-    float den = 0.f;
+  for (int m = 0; m < 4; ++m) {
+    float num = 0.f;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) den = fmaf(Q[d], K[128 + h * 4 + d], den);
-    const float z = 1.f / (den + kAttnEps);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      float num = 0.f;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) num = fmaf(Q[d], K[h * 16 + m * 4 + d], num);
-      msg[t * 32 + h * 4 + m] = num * z;
-    }
+    for (int d = 0; d < 4; ++d) num = fmaf(Q[d], K[h * 16 + m * 4 + d], num);
+    o[m] = num * z;
   }
+  *reinterpret_cast<float4*>(msg + t * 32 + h * 4) = make_float4(o[0], o[1], o[2], o[3]);
 }
 
 // query side: dq, and per block partial dKV (128) + dKs (32) -- blocks never straddle a K/V group.
-// One head at a time (20 accumulators per thread, then an fp64 block reduction of those 20).
+// Thread (slot, head) walks the block's tokens slot, slot + 32, ... for its head (20 fp32 accumulators),
+// then per head a fixed fp64 reduction: xor 8, 16, 32 within the wave, then the 4 waves in order.
 __global__ __launch_bounds__(kTB) void linattn_bwd_q_kernel(const float* __restrict__ q, const float* __restrict__ dmsg,
                                                             long T, long tpg, long tpb, const float* __restrict__ kv,
                                                             long kv_stride, float* __restrict__ dq,
                                                             double* __restrict__ partial) {
-  __shared__ double red[20][kTB / 64];
+  __shared__ double red[kTB / 64][160];
   const long t0 = (long)blockIdx.x * tpb, t1 = t0 + tpb < T ? t0 + tpb : T;
   const float* K = kv + (t0 / tpg) * kv_stride;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll 1
-  for (int h = 0; h < 8; ++h) {
-    float kvh[16], ksh[4];
+  const int h = threadIdx.x & 7;
+  float kvh[16], ksh[4];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) kvh[i] = K[h * 16 + i];
+  for (int i = 0; i < 16; ++i) kvh[i] = K[h * 16 + i];
 #pragma unroll
-    for (int d = 0; d < 4; ++d) ksh[d] = K[128 + h * 4 + d];
-    float acc[20];
+  for (int d = 0; d < 4; ++d) ksh[d] = K[128 + h * 4 + d];
+  float acc[20];
 #pragma unroll
-    for (int i = 0; i < 20; ++i) acc[i] = 0.f;
-    for (long t = t0 + threadIdx.x; t < t1; t += kTB) {
-      float qr[4], Q[4], dm[4];
+  for (int i = 0; i < 20; ++i) acc[i] = 0.f;
+  for (long t = t0 + (threadIdx.x >> 3); t < t1; t += kTokPerBlock) {
+    const float4 q4 = ld4(q + t * 32 + h * 4), d4 = ld4(dmsg + t * 32 + h * 4);
+    const float qr[4] = {q4.x, q4.y, q4.z, q4.w}, dm[4] = {d4.x, d4.y, d4.z, d4.w};
+    float Q[4];
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        qr[d] = q[t * 32 + h * 4 + d];
-        Q[d] = elu1f(qr[d]);
-        dm[d] = dmsg[t * 32 + h * 4 + d];
-      }
-      float den = 0.f;
+    for (int d = 0; d < 4; ++d) Q[d] = elu1f(qr[d]);
+    float den = 0.f;
 #pragma unroll
-      for (int d = 0; d < 4; ++d) den = fmaf(Q[d], ksh[d], den);
-      const float z = 1.f / (den + kAttnEps);
-      float dz = 0.f;
+    for (int d = 0; d < 4; ++d) den = fmaf(Q[d], ksh[d], den);
+    const float z = 1.f / (den + kAttnEps);
+    float dz = 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      float nm = 0.f;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) nm = fmaf(Q[d], kvh[m * 4 + d], nm);
+      dz = fmaf(dm[m], nm, dz);
+    }
+    const float dden = -dz * z * z;
+    float o[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      float dQ = dden * ksh[d];
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        float nm = 0.f;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) nm = fmaf(Q[d], kvh[m * 4 + d], nm);
-        dz = fmaf(dm[m], nm, dz);
+        const float dn = dm[m] * z;
+        dQ = fmaf(dn, kvh[m * 4 + d], dQ);
+        acc[m * 4 + d] = fmaf(dn, Q[d], acc[m * 4 + d]);
       }
-      const float dden = -dz * z * z;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        float dQ = dden * ksh[d];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const float dn = dm[m] * z;
-          dQ = fmaf(dn, kvh[m * 4 + d], dQ);
-          acc[m * 4 + d] = fmaf(dn, Q[d], acc[m * 4 + d]);
-        }
-        acc[16 + d] = fmaf(dden, Q[d], acc[16 + d]);
-        dq[t * 32 + h * 4 + d] = dQ * elu1_grad(qr[d]);
-      }
+      acc[16 + d] = fmaf(dden, Q[d], acc[16 + d]);
+      o[d] = dQ * elu1_grad(qr[d]);
     }
+    *reinterpret_cast<float4*>(dq + t * 32 + h * 4) = make_float4(o[0], o[1], o[2], o[3]);
+  }
 #pragma unroll
-    for (int i = 0; i < 20; ++i) {
-      double val = (double)acc[i];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off, 64);
-      if (lane == 0) red[i][wv] = val;
-    }
-    __syncthreads();
-    if (threadIdx.x < 20) {
-      const int i = threadIdx.x;
-      const double v = (red[i][0] + red[i][1]) + (red[i][2] + red[i][3]);
-      partial[(size_t)blockIdx.x * 160 + (i < 16 ? h * 16 + i : 128 + h * 4 + (i - 16))] = v;
-    }
-    __syncthreads();
+  for (int i = 0; i < 20; ++i) {
+    double val = (double)acc[i];
+    val += __shfl_xor(val, 8, 64);
+    val += __shfl_xor(val, 16, 64);
+    val += __shfl_xor(val, 32, 64);
+    if (lane < 8) red[wv][i < 16 ? h * 16 + i : 128 + h * 4 + (i - 16)] = val;
+  }
+  __syncthreads();
+  if (threadIdx.x < 160) {
+    const int i = threadIdx.x;
+    partial[(size_t)blockIdx.x * 160 + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
   }
 }
 
@@ -422,33 +426,31 @@ __global__ void linattn_group_combine_kernel(const double* __restrict__ partial,
 __global__ __launch_bounds__(kTB) void linattn_bwd_kv_kernel(const float* __restrict__ k, const float* __restrict__ v,
                                                              long S, long spg, const float* __restrict__ dkv,
                                                              float* __restrict__ dk, float* __restrict__ dv) {
-  const long s = (long)blockIdx.x * kTB + threadIdx.x;
+  const int h = threadIdx.x & 7;
+  const long s = (long)blockIdx.x * kTokPerBlock + (threadIdx.x >> 3);
   if (s >= S) return;
   const float* G = dkv + (s / spg) * 160;
+  const float4 k4 = ld4(k + s * 32 + h * 4), v4 = ld4(v + s * 32 + h * 4);
+  const float kr[4] = {k4.x, k4.y, k4.z, k4.w}, V[4] = {v4.x, v4.y, v4.z, v4.w};
+  float Kf[4], ok[4], ov[4];
 #pragma unroll
-  for (int h = 0; h < 8; ++h) {
-    float kr[4], Kf[4], V[4];
+  for (int d = 0; d < 4; ++d) Kf[d] = elu1f(kr[d]);
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      kr[d] = k[s * 32 + h * 4 + d];
-      Kf[d] = elu1f(kr[d]);
-      V[d] = v[s * 32 + h * 4 + d];
-    }
+  for (int d = 0; d < 4; ++d) {
+    float g = G[128 + h * 4 + d];
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      float g = G[128 + h * 4 + d];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) g = fmaf(G[h * 16 + m * 4 + d], V[m], g);
-      dk[s * 32 + h * 4 + d] = g * elu1_grad(kr[d]);
-    }
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      float g = 0.f;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) g = fmaf(G[h * 16 + m * 4 + d], Kf[d], g);
-      dv[s * 32 + h * 4 + m] = g;
-    }
+    for (int m = 0; m < 4; ++m) g = fmaf(G[h * 16 + m * 4 + d], V[m], g);
+    ok[d] = g * elu1_grad(kr[d]);
   }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    float g = 0.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) g = fmaf(G[h * 16 + m * 4 + d], Kf[d], g);
+    ov[m] = g;
+  }
+  *reinterpret_cast<float4*>(dk + s * 32 + h * 4) = make_float4(ok[0], ok[1], ok[2], ok[3]);
+  *reinterpret_cast<float4*>(dv + s * 32 + h * 4) = make_float4(ov[0], ov[1], ov[2], ov[3]);
 }
 
 static long tok_chunk(long T, long maxblk, long c = 1024) {
@@ -540,7 +542,7 @@ extern "C" int tmvs_layer_norm_bwd(const float* dy, const float* x, long tokens,
 extern "C" int tmvs_linattn_fwd(const float* q, long tokens, long tokens_per_group, const float* kv, long kv_stride,
                                 float* msg, void* stream) {
   if (!q || !kv || !msg || tokens <= 0 || tokens_per_group <= 0) return TMVS_ERR_ARG;
-  hipLaunchKernelGGL(linattn_fwd_kernel, dim3((unsigned)((tokens + kTB - 1) / kTB)), dim3(kTB), 0,
+  hipLaunchKernelGGL(linattn_fwd_kernel, dim3((unsigned)((tokens + kTokPerBlock - 1) / kTokPerBlock)), dim3(kTB), 0,
                      (hipStream_t)stream, q, tokens, tokens_per_group, kv, kv_stride, msg);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
@@ -548,7 +550,7 @@ extern "C" int tmvs_linattn_fwd(const float* q, long tokens, long tokens_per_gro
 
 // blocks of tpb tokens that never straddle a group: tpb divides tokens_per_group
 static long group_chunk(long tpg) {
-  long c = 256;  // one token per thread per head: ~4 blocks per CU at the C5 size
+  long c = 128;  // 4 tokens per (slot, head) thread: ~3 blocks per CU at the C5 size
   while (c > 1 && tpg % c) c >>= 1;
   while (tpg / c > 512 && tpg % (2 * c) == 0) c *= 2;
   return c;
@@ -579,7 +581,7 @@ extern "C" int tmvs_linattn_bwd_q(const float* q, const float* dmsg, long tokens
 extern "C" int tmvs_linattn_bwd_kv(const float* k, const float* v, long tokens, long tokens_per_group,
                                    const float* dkv, float* dk, float* dv, void* stream) {
   if (!k || !v || !dkv || !dk || !dv || tokens <= 0 || tokens_per_group <= 0) return TMVS_ERR_ARG;
-  hipLaunchKernelGGL(linattn_bwd_kv_kernel, dim3((unsigned)((tokens + kTB - 1) / kTB)), dim3(kTB), 0,
+  hipLaunchKernelGGL(linattn_bwd_kv_kernel, dim3((unsigned)((tokens + kTokPerBlock - 1) / kTokPerBlock)), dim3(kTB), 0,
                      (hipStream_t)stream, k, v, tokens, tokens_per_group, dkv, dk, dv);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
