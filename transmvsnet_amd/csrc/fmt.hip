@@ -259,11 +259,7 @@ constexpr int kKvTilesPerWave = 8;     // kv: at most this many tiles per wave (
 
 // (KV, Ksum) partial sums: per wave, tiles of 16 source tokens; K, V by MFMA; per lane the
 // two heads it owns are accumulated over its tokens, then summed over the 16 token lanes.
-#ifndef TMVS_KV_WAVES
-#define TMVS_KV_WAVES 4
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_KV_WAVES)))
-void fmt_kv_partial_kernel(const float* __restrict__ src, int S,
+__global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __restrict__ src, int S,
                                                               const float* __restrict__ w,
                                                               float* __restrict__ partial, int tpw) {
   __shared__ float red[4][kKV];
@@ -398,11 +394,9 @@ __global__ __launch_bounds__(1024) void fmt_kv_combine_kernel(const float* __res
 #define TMVS_APPLY_NT 1
 #endif
 constexpr int kApplyNT = TMVS_APPLY_NT;
-#ifndef TMVS_APPLY_WAVES
-#define TMVS_APPLY_WAVES 4
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_APPLY_WAVES)))
-void fmt_apply_kernel(float* __restrict__ x, int L, const float* __restrict__ kvg,
+// (amdgpu_waves_per_eu(5) fits it in 94 VGPRs without AGPRs, 5 waves/SIMD instead of 4: the 8 applies
+// measured 456.6 vs 448.1 us per step, 6 waves (80 VGPRs + scratch) 472.0 -- profiles/r11n: not kept)
+__global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, int L, const float* __restrict__ kvg,
                                                         long kv_stride, const float* __restrict__ w, int tpw) {
   __shared__ __attribute__((aligned(16))) float kvs[kKV];
   // the per-feature vectors, read from LDS in the tile loop: a global load there is a full memory
