@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TMVS_ABI_VERSION 8
+#define TMVS_ABI_VERSION 7
 
 #define TMVS_OK 0
 #define TMVS_ERR_ARG (-1)    /* null pointer / non-positive size / bad enum        */
@@ -93,19 +93,6 @@ int tmvs_warp_corr(const float* ref_fea, const float* src_fea, const float* proj
                    const float* view_w_in, int vw_shift, int vw_offset, int vw_total, const float* pw_params,
                    int batch, int n_src, int channels, int ndepth, int height, int width, int flags,
                    float* sim_out, float* wsum_out, float* view_w_out, void* stream);
-
-/* tmvs_warp_corr with a workspace (ABI 8): stage 1 (view_w_in NULL: PixelwiseNet weights, C = 32,
- * D % 8 == 0, D <= 64) reads its bilinear taps from LDS source windows (warp_win_kernel: per 8x4
- * reference tile and chunk of 8 planes the bounding box of the tile's tap footprint is staged in LDS)
- * and writes the per-view similarities [n_src][H][W][ndepth] into the workspace; PixelwiseNet and the
- * view aggregation follow in a second pass. Same outputs, bit for bit, as tmvs_warp_corr. With a
- * workspace smaller than tmvs_warp_corr_workspace(...) (0 for shapes without the window path) it is
- * tmvs_warp_corr.                                                                                   */
-size_t tmvs_warp_corr_workspace(int n_src, int channels, int ndepth, int height, int width, int pixelwise);
-int tmvs_warp_corr_ws(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,
-                      const float* view_w_in, int vw_shift, int vw_offset, int vw_total, const float* pw_params,
-                      int batch, int n_src, int channels, int ndepth, int height, int width, int flags, float* sim_out,
-                      float* wsum_out, float* view_w_out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* sim = sim_sum / (1e-5 + w_sum) after a cross-rank all-reduce of both (TransMVSNet.py:72,93). */
 int tmvs_aggregate_finalize(float* sim_sum, const float* w_sum, int batch, int ndepth, int height, int width,

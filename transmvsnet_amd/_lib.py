@@ -24,8 +24,6 @@ SIGNATURES = {
     "tmvs_bn_fold": (I, [P, P, P, P, I, F, P, P]),
     "tmvs_stage_hypotheses": (I, [P, I, P, I, I, I, I, F, I, I, I, P, P]),
     "tmvs_warp_corr": (I, [P, P, P, P, P, I, I, I, P, I, I, I, I, I, I, I, P, P, P, P]),
-    "tmvs_warp_corr_workspace": (S, [I, I, I, I, I, I]),
-    "tmvs_warp_corr_ws": (I, [P, P, P, P, P, I, I, I, P, I, I, I, I, I, I, I, P, P, P, P, S, P]),
     "tmvs_aggregate_finalize": (I, [P, P, I, I, I, I, P]),
     "tmvs_homo_warping": (I, [P, P, P, I, I, I, I, I, I, P, P]),
     "tmvs_costregnet_workspace": (S, [I, I, I, I, I]),
@@ -102,7 +100,7 @@ SIGNATURES = {
     "tmvs_softmax_backward": (I, [P, P, I, I, I, I, P, P]),
 }
 
-ABI_VERSION = 8
+ABI_VERSION = 7
 PW_NPARAMS = 201
 ENC_NPARAMS = 8544
 KV_NFLOATS = 160

@@ -608,273 +608,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   if (PARTIAL && k == 0) wsum_out[p] = wsum;
 }
 
-// ---------------------------------------------------------------- stage 1 from LDS source windows
-// Stage 1's hypotheses are fronto-parallel planes, so a block's 8x8 reference pixels project, for one
-// chunk of 8 consecutive planes, into a compact source region: the convex hull of its 4 corner pixels'
-// projections at the chunk's first and last plane (a homography maps the tile to a convex quad; along
-// the chunk a pixel moves monotonically on its epipolar line). Per (view, chunk) the block stages that
-// region's bounding box (+1 texel of margin, out-of-image texels as 0 = grid_sample's zero padding)
-// into LDS with coalesced 16-byte row loads, and the lane groups read their bilinear taps from LDS
-// instead of gathering them through the vector L1 (the address unit that bounds warp_corr_kernel).
-// A tap quad outside the staged box (a box over kWinMax texels, or a rounding outlier) is read from
-// global memory as in warp_corr_kernel, so the result never depends on the box being right.
-// Lane layout, plane rounds, combine() and the reduce-scatter are warp_corr_kernel's: the per-view
-// similarities are bit-identical. They are written as sims [V][HW][D]; PixelwiseNet, the view weights
-// and the aggregation follow in warp_pw_agg_kernel (same op order as warp_corr_kernel's PW path).
-constexpr int kWinT = 8;      // kWinT x kWinTH reference pixels per block
-#ifndef TMVS_WIN_TH
-#define TMVS_WIN_TH 4
-#endif
-constexpr int kWinTH = TMVS_WIN_TH;
-#ifndef TMVS_WIN_MAX
-#define TMVS_WIN_MAX 256
-#endif
-constexpr int kWinMax = TMVS_WIN_MAX;  // texels per staged box (C = 32: 32 KB per buffer, two buffers)
-#ifndef TMVS_WIN_N
-#define TMVS_WIN_N 2
-#endif
-constexpr int kWinN = TMVS_WIN_N;  // plane rounds per batch of LDS reads (2 or 4)
-
-template <int C>
-__device__ __forceinline__ void fetch_win(const float* __restrict__ win, int bx, int by, int bw, int bh,
-                                          const __amdgpu_buffer_rsrc_t rsrc, unsigned vbase, unsigned rowb, int W,
-                                          int H, const Geom& g, int k, floatx4 (&val)[4], float (&w)[4]) {
-  const int wx = g.x0 - bx, wy = g.y0 - by;
-  if (wx >= 0 && wy >= 0 && wx < bw - 1 && wy < bh - 1) {  // (bw = bh = 0: no window)
-    const float we = g.fx, n = g.fy;
-    const float ea = 1.f - we, s = 1.f - n;
-    w[0] = s * ea;
-    w[1] = s * we;
-    w[2] = n * ea;
-    w[3] = n * we;
-    const float* b = win + (wy * bw + wx) * C + 4 * k;
-    const float4 a0 = *reinterpret_cast<const float4*>(b);
-    const float4 a1 = *reinterpret_cast<const float4*>(b + C);
-    const float4 a2 = *reinterpret_cast<const float4*>(b + bw * C);
-    const float4 a3 = *reinterpret_cast<const float4*>(b + bw * C + C);
-    val[0] = floatx4{a0.x, a0.y, a0.z, a0.w};
-    val[1] = floatx4{a1.x, a1.y, a1.z, a1.w};
-    val[2] = floatx4{a2.x, a2.y, a2.z, a2.w};
-    val[3] = floatx4{a3.x, a3.y, a3.z, a3.w};
-  } else {
-    fetch_full<C>(rsrc, vbase, rowb, W, H, g, val, w);
-  }
-}
-
-template <int C, int R0, int N>
-__device__ __forceinline__ void win_rounds(const float* __restrict__ win, int bx, int by, int bw, int bh,
-                                           const __amdgpu_buffer_rsrc_t rsrc, unsigned vbase, unsigned rowb, int W,
-                                           int H, const Geom& own, const float4& r4, int k, float* part) {
-  floatx4 v[N][4];
-  float w[N][4];
-#define TMVS_WFETCH(I) \
-  fetch_win<C>(win, bx, by, bw, bh, rsrc, vbase, rowb, W, H, geom_bcast<C / 4, R0 + I>(own), k, v[I], w[I]);
-  TMVS_WFETCH(0)
-  if constexpr (N > 1) { TMVS_WFETCH(1) }
-  if constexpr (N > 2) { TMVS_WFETCH(2) }
-  if constexpr (N > 3) { TMVS_WFETCH(3) }
-#undef TMVS_WFETCH
-#pragma unroll
-  for (int i = 0; i < N; ++i) part[R0 + i] = combine(v[i], w[i], r4);
-}
-
-// zero texel for the LDS-DMA of out-of-image window texels (grid_sample's zero padding)
-__device__ __attribute__((aligned(16))) float kWinZero[4] = {0.f, 0.f, 0.f, 0.f};
-
-// 16-byte LDS-DMA: lane l's 16 bytes from g land at lds + 16 l (lds wave-uniform)
-__device__ __forceinline__ void glds16(const float* g, float* lds) { __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0); }
-
-#ifndef TMVS_WIN_WAVES
-#define TMVS_WIN_WAVES 2
-#endif
-// Double-buffered: while the block computes chunk n from one LDS buffer, chunk n+1's box is copied into
-// the other by LDS-DMA (global_load_lds_dwordx4: element e = texel * C/4 + quad lands at byte 16 e, so a
-// wave's 64 consecutive elements are one lane-linear 1 KiB write); the barrier that ends chunk n drains
-// it. The compute phase issues no ordinary global load (the hypotheses are staged in LDS up front), so
-// nothing waits on the DMA early. Corner taps run 3 chunks ahead in a ring of 4.
-template <int C, int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_WIN_WAVES))) void warp_win_kernel(
-    const float* __restrict__ ref, const float* __restrict__ src, const float* __restrict__ hyp,
-    float* __restrict__ sims, int V, int H, int W, WarpArgs args) {
-  constexpr int LPS = C / 4, NCH = D / LPS, GROUPS = 256 / LPS, NPIX = kWinT * kWinTH;
-  static_assert(LPS == 8 && D % LPS == 0 && NPIX == GROUPS, "stage-1 layout: C = 32, one pixel per lane group");
-  __shared__ __attribute__((aligned(16))) float win[2][kWinMax * C];
-  __shared__ float dep[D][NPIX];
-  __shared__ int cor[4][8][2];
-  const int tid = threadIdx.x, lane = tid & 63, k = lane % LPS, grp = tid / LPS;
-  const int HW = H * W, NN = V * NCH;
-  const int tw = (W + kWinT - 1) / kWinT, nt = tw * ((H + kWinTH - 1) / kWinTH);
-  const int tile = xcd_remap(blockIdx.x, nt);
-  const int tx0 = (tile % tw) * kWinT, ty0 = (tile / tw) * kWinTH;
-  const float halfw = (float)(W - 1) / 2.f, halfh = (float)(H - 1) / 2.f;
-  const int px = tx0 + grp % kWinT, py = ty0 + grp / kWinT;
-  const bool act = px < W && py < H;
-  const int pxc = px < W ? px : W - 1, pyc = py < H ? py : H - 1;
-  const int pp = pyc * W + pxc;
-  const float fxp = (float)pxc, fyp = (float)pyc;
-  const float4 r4 = *reinterpret_cast<const float4*>(ref + (size_t)pp * C + 4 * k);
-  for (int e = tid; e < D * NPIX; e += 256) {
-    const int d = e / NPIX, g = e % NPIX;
-    const int gx = min(tx0 + g % kWinT, W - 1), gy = min(ty0 + g / kWinT, H - 1);
-    dep[d][g] = hyp[(size_t)d * HW + gy * W + gx];
-  }
-  auto corners = [&](int n) {  // tile corners (clamped to the image) at the chunk's first / last plane
-    if (tid < 8 && n < NN) {
-      const int v = n / NCH, j = n % NCH;
-      const float* R = args.proj[v];
-      const int cx = (tid & 1) ? min(tx0 + kWinT - 1, W - 1) : tx0;
-      const int cy = (tid & 2) ? min(ty0 + kWinTH - 1, H - 1) : ty0;
-      const int d = j * LPS + ((tid & 4) ? LPS - 1 : 0);
-      const float fx = (float)cx, fy = (float)cy;
-      Geom g;
-      project(rot_row(R, fx, fy, args.rot_plain), rot_row(R + 4, fx, fy, args.rot_plain),
-              rot_row(R + 8, fx, fy, args.rot_plain), R[3], R[7], R[11], dep[d][(cy - ty0) * kWinT + (cx - tx0)],
-              halfw, halfh, g.x0, g.y0, g.fx, g.fy);  // (the staged depths: no global load while a DMA is in flight)
-      cor[n & 3][tid][0] = g.x0;
-      cor[n & 3][tid][1] = g.y0;
-    }
-  };
-  // chunk n's box: the corner taps' bounding box + 1 texel each side (bw = bh = 0: not staged)
-  auto box = [&](int n, int& bx, int& by, int& bw, int& bh) {
-    int mnx = cor[n & 3][0][0], mxx = mnx, mny = cor[n & 3][0][1], mxy = mny;
-#pragma unroll
-    for (int q = 1; q < 8; ++q) {
-      mnx = min(mnx, cor[n & 3][q][0]);
-      mxx = max(mxx, cor[n & 3][q][0]);
-      mny = min(mny, cor[n & 3][q][1]);
-      mxy = max(mxy, cor[n & 3][q][1]);
-    }
-    bx = mnx - 1;
-    by = mny - 1;
-    bw = mxx - mnx + 4;
-    bh = mxy - mny + 4;
-    if (bw * bh > kWinMax || bw > 1024 || bh > 1024) bw = bh = 0;
-  };
-  auto stage = [&](int n) {  // LDS-DMA of chunk n's box into win[n & 1]
-    if (n >= NN) return;
-    int bx, by, bw, bh;
-    box(n, bx, by, bw, bh);
-    const float* sv = src + (size_t)(n / NCH) * HW * C;
-    const int ne = bw * bh * (C / 4);
-    for (int e0 = (tid & ~63); e0 < ne; e0 += 256) {
-      const int e = e0 + lane;
-      if (e < ne) {
-        const int t = e / (C / 4), q = e % (C / 4);
-        const int X = bx + t % bw, Y = by + t / bw;
-        const bool in = (unsigned)X < (unsigned)W && (unsigned)Y < (unsigned)H;
-        const float* g = in ? sv + ((size_t)Y * W + X) * C + 4 * q : kWinZero;
-        glds16(g, win[n & 1] + e0 * 4);
-      }
-    }
-  };
-  const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, V * HW * C * 4, kRsrcWord3);
-  const unsigned rowb = (unsigned)W * C * 4;
-  __syncthreads();  // dep is staged
-  corners(0);
-  corners(1);
-  corners(2);
-  __syncthreads();
-  stage(0);
-  __syncthreads();
-  float rx = 0.f, ry = 0.f, rz = 0.f;
-#pragma unroll 1
-  for (int n = 0; n < NN; ++n) {
-    const int v = n / NCH, j = n % NCH;
-    const float* R = args.proj[v];
-    if (j == 0) {
-      rx = rot_row(R, fxp, fyp, args.rot_plain);
-      ry = rot_row(R + 4, fxp, fyp, args.rot_plain);
-      rz = rot_row(R + 8, fxp, fyp, args.rot_plain);
-    }
-    stage(n + 1);    // in flight during this chunk
-    corners(n + 3);  // ring slot (n + 3) & 3 was last read in chunk n - 1
-    int bx, by, bw, bh;
-    box(n, bx, by, bw, bh);
-    const float* wb = win[n & 1];
-    const unsigned vbase = (unsigned)(v * HW * C * 4) + 16 * k;
-    const int d = j * LPS + k;
-    Geom own;
-    project(rx, ry, rz, R[3], R[7], R[11], dep[d][grp], halfw, halfh, own.x0, own.y0, own.fx, own.fy);
-    float part[LPS];
-    win_rounds<C, 0, kWinN>(wb, bx, by, bw, bh, rsrc, vbase, rowb, W, H, own, r4, k, part);
-    win_rounds<C, kWinN, kWinN>(wb, bx, by, bw, bh, rsrc, vbase, rowb, W, H, own, r4, k, part);
-    if constexpr (kWinN == 2) {
-      win_rounds<C, 4, 2>(wb, bx, by, bw, bh, rsrc, vbase, rowb, W, H, own, r4, k, part);
-      win_rounds<C, 6, 2>(wb, bx, by, bw, bh, rsrc, vbase, rowb, W, H, own, r4, k, part);
-    }
-    const float sim = reduce_scatter<LPS>(part, k) * (1.f / (float)C);  // C = 2^n: == / C
-    if (act) sims[((size_t)v * HW + pp) * D + d] = sim;
-    __syncthreads();  // chunk n + 1's box has landed (the barrier drains the DMA); win[n & 1] is free
-  }
-}
-
-// PixelwiseNet view weights and the view aggregation from warp_win_kernel's sims [V][HW][D] in
-// warp_corr_kernel's PW lane layout and op order: 8 lanes per pixel, lane k owns planes j*8 + k;
-// w_v = max over the group of each lane's running max of sigmoid(pixelwise_logit(sim)),
-// acc[j] = acc[j] + sim * w_v over views in order, wsum = (1e-5 or 0) + w_0 + w_1 + ...
-template <int D, bool PARTIAL>
-__global__ __launch_bounds__(256) void warp_pw_agg_kernel(const float* __restrict__ sims, float* __restrict__ sim_out,
-                                                          float* __restrict__ wsum_out, float* __restrict__ vw_out,
-                                                          int V, int HW, int vw_offset, WarpArgs args) {
-  constexpr int LPS = 8, DPT = D / LPS;
-  __shared__ __attribute__((aligned(16))) float pw_lds[TMVS_PW_NPARAMS + 3];
-  __shared__ float sim_lds[DPT][256];
-  if (threadIdx.x < TMVS_PW_NPARAMS) pw_lds[threadIdx.x] = args.pw[threadIdx.x];
-  __syncthreads();
-  const int tid = threadIdx.x, k = tid % LPS;
-  const int p0 = (blockIdx.x * 256 + tid) / LPS;
-  const bool active = p0 < HW;
-  const int p = active ? p0 : HW - 1;
-  float acc[DPT];
-#pragma unroll
-  for (int j = 0; j < DPT; ++j) acc[j] = 0.f;
-  float wsum = PARTIAL ? 0.f : 1e-5f;
-#pragma unroll 1
-  for (int v = 0; v < V; ++v) {
-    const float* sv = sims + ((size_t)v * HW + p) * D + k;
-#pragma unroll
-    for (int j = 0; j < DPT; ++j) sim_lds[j][tid] = sv[j * LPS];
-    float wm = 0.f;
-#pragma unroll 1
-    for (int j = 0; j < DPT; ++j) {
-      int salt = 0;  // opaque offset: keeps the parameter reads from being hoisted into VGPRs
-      asm volatile("" : "+v"(salt));
-      const float lg = pixelwise_logit(sim_lds[j][tid], pw_lds + salt);
-      wm = fmaxf(wm, 1.f / (1.f + expf(-lg)));
-    }
-    const float w = group_max<LPS>(wm);
-    if (active && k == 0) vw_out[(size_t)(vw_offset + v) * HW + p] = w;
-#pragma unroll
-    for (int j = 0; j < DPT; ++j) acc[j] = acc[j] + sim_lds[j][tid] * w;
-    wsum = wsum + w;
-  }
-  if (!active) return;
-#pragma unroll
-  for (int j = 0; j < DPT; ++j) sim_out[(size_t)(j * LPS + k) * HW + p] = PARTIAL ? acc[j] : acc[j] / wsum;
-  if (PARTIAL && k == 0) wsum_out[p] = wsum;
-}
-
-// the window path's sims buffer [V][HW][D] (0: the shape takes warp_corr_kernel)
-static size_t win_workspace(int C, int D, int V, int H, int W, bool pw) {
-  return (pw && C == 32 && D % 8 == 0 && D <= 64) ? (size_t)V * H * W * D * sizeof(float) : 0;
-}
-
 template <int C, int D, bool PW, bool PARTIAL>
 static int launch_warp(const float* ref, const float* src, const float* hyp, const float* vw_in, float* sim,
                        float* wsum, float* vw_out, int V, int H, int W, int vw_shift, int vw_offset, int vw_total,
-                       const WarpArgs& args, hipStream_t st, float* ws = nullptr) {
-  if constexpr (C == 32 && PW && D % 8 == 0) {
-    if (ws) {
-      const int nt = ((W + kWinT - 1) / kWinT) * ((H + kWinTH - 1) / kWinTH);
-      hipLaunchKernelGGL((warp_win_kernel<C, D>), dim3(nt), dim3(256), 0, st, ref, src, hyp, ws, V, H, W, args);
-      TMVS_CHECK_LAUNCH();
-      hipLaunchKernelGGL((warp_pw_agg_kernel<D, PARTIAL>), dim3((H * W + 31) / 32), dim3(256), 0, st, ws, sim, wsum,
-                         vw_out, V, H * W, vw_offset, args);
-      TMVS_CHECK_LAUNCH();
-      return TMVS_OK;
-    }
-  }
+                       const WarpArgs& args, hipStream_t st) {
   if constexpr ((C == 8 || C == 16) && !PW) {
     constexpr int PIXP = 4 * (64 / (C / 2));
     const int nblk = (H * W + PIXP - 1) / PIXP;
@@ -894,11 +631,11 @@ static int launch_warp(const float* ref, const float* src, const float* hyp, con
 template <int C, bool PW, bool PARTIAL>
 static int dispatch_depth(int D, const float* ref, const float* src, const float* hyp, const float* vw_in, float* sim,
                           float* wsum, float* vw_out, int V, int H, int W, int vw_shift, int vw_offset, int vw_total,
-                          const WarpArgs& a, hipStream_t st, float* ws) {
+                          const WarpArgs& a, hipStream_t st) {
 #define TMVS_WARP_CASE(DD)                                                                                        \
   if (D == DD)                                                                                                    \
     return launch_warp<C, DD, PW, PARTIAL>(ref, src, hyp, vw_in, sim, wsum, vw_out, V, H, W, vw_shift, vw_offset, \
-                                           vw_total, a, st, ws);
+                                           vw_total, a, st);
   TMVS_WARP_CASE(48)
   TMVS_WARP_CASE(32)
   TMVS_WARP_CASE(16)
@@ -912,18 +649,18 @@ static int dispatch_depth(int D, const float* ref, const float* src, const float
 template <int C>
 static int dispatch_mode(bool pw, bool partial, int D, const float* ref, const float* src, const float* hyp,
                          const float* vw_in, float* sim, float* wsum, float* vw_out, int V, int H, int W, int vw_shift,
-                         int vw_offset, int vw_total, const WarpArgs& a, hipStream_t st, float* ws) {
+                         int vw_offset, int vw_total, const WarpArgs& a, hipStream_t st) {
   if (pw && partial)
     return dispatch_depth<C, true, true>(D, ref, src, hyp, vw_in, sim, wsum, vw_out, V, H, W, vw_shift, vw_offset,
-                                         vw_total, a, st, ws);
+                                         vw_total, a, st);
   if (pw)
     return dispatch_depth<C, true, false>(D, ref, src, hyp, vw_in, sim, wsum, vw_out, V, H, W, vw_shift, vw_offset,
-                                          vw_total, a, st, ws);
+                                          vw_total, a, st);
   if (partial)
     return dispatch_depth<C, false, true>(D, ref, src, hyp, vw_in, sim, wsum, vw_out, V, H, W, vw_shift, vw_offset,
-                                          vw_total, a, st, nullptr);
+                                          vw_total, a, st);
   return dispatch_depth<C, false, false>(D, ref, src, hyp, vw_in, sim, wsum, vw_out, V, H, W, vw_shift, vw_offset,
-                                         vw_total, a, st, nullptr);
+                                         vw_total, a, st);
 }
 
 
@@ -1274,10 +1011,11 @@ __global__ void fix_to_float_kernel(const unsigned long long* __restrict__ in, l
 
 using namespace tmvs;
 
-static int warp_corr_impl(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,
-                          const float* view_w_in, int vw_shift, int vw_offset, int vw_total, const float* pw_params,
-                          int batch, int n_src, int channels, int ndepth, int height, int width, int flags,
-                          float* sim_out, float* wsum_out, float* view_w_out, float* ws, void* stream) {
+extern "C" int tmvs_warp_corr(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,
+                              const float* view_w_in, int vw_shift, int vw_offset, int vw_total,
+                              const float* pw_params, int batch, int n_src, int channels, int ndepth, int height,
+                              int width, int flags, float* sim_out, float* wsum_out, float* view_w_out,
+                              void* stream) {
   if (!ref_fea || !src_fea || !proj || !hyp || !sim_out) return TMVS_ERR_ARG;
   if (batch <= 0 || n_src <= 0 || n_src > TMVS_MAX_VIEWS || height <= 0 || width <= 0 || ndepth <= 0)
     return TMVS_ERR_ARG;
@@ -1312,15 +1050,15 @@ static int warp_corr_impl(const float* ref_fea, const float* src_fea, const floa
     switch (channels) {
       case 32:
         rc = dispatch_mode<32>(pw, partial, ndepth, rb, sb, hb, vib, sob, wob, vob, n_src, height, width, vw_shift,
-                               vw_offset, vw_total, a, st, ws);
+                               vw_offset, vw_total, a, st);
         break;
       case 16:
         rc = dispatch_mode<16>(pw, partial, ndepth, rb, sb, hb, vib, sob, wob, vob, n_src, height, width, vw_shift,
-                               vw_offset, vw_total, a, st, ws);
+                               vw_offset, vw_total, a, st);
         break;
       case 8:
         rc = dispatch_mode<8>(pw, partial, ndepth, rb, sb, hb, vib, sob, wob, vob, n_src, height, width, vw_shift,
-                              vw_offset, vw_total, a, st, ws);
+                              vw_offset, vw_total, a, st);
         break;
       default:
         return TMVS_ERR_SHAPE;
@@ -1328,31 +1066,6 @@ static int warp_corr_impl(const float* ref_fea, const float* src_fea, const floa
     if (rc != TMVS_OK) return rc;
   }
   return TMVS_OK;
-}
-
-extern "C" int tmvs_warp_corr(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,
-                              const float* view_w_in, int vw_shift, int vw_offset, int vw_total,
-                              const float* pw_params, int batch, int n_src, int channels, int ndepth, int height,
-                              int width, int flags, float* sim_out, float* wsum_out, float* view_w_out,
-                              void* stream) {
-  return warp_corr_impl(ref_fea, src_fea, proj, hyp, view_w_in, vw_shift, vw_offset, vw_total, pw_params, batch, n_src,
-                        channels, ndepth, height, width, flags, sim_out, wsum_out, view_w_out, nullptr, stream);
-}
-
-extern "C" size_t tmvs_warp_corr_workspace(int n_src, int channels, int ndepth, int height, int width, int pw) {
-  if (n_src <= 0 || ndepth <= 0 || height <= 0 || width <= 0) return 0;
-  return win_workspace(channels, ndepth, n_src, height, width, pw != 0);
-}
-
-extern "C" int tmvs_warp_corr_ws(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,
-                                 const float* view_w_in, int vw_shift, int vw_offset, int vw_total,
-                                 const float* pw_params, int batch, int n_src, int channels, int ndepth, int height,
-                                 int width, int flags, float* sim_out, float* wsum_out, float* view_w_out,
-                                 void* workspace, size_t workspace_bytes, void* stream) {
-  const size_t need = tmvs_warp_corr_workspace(n_src, channels, ndepth, height, width, view_w_in == nullptr);
-  float* ws = (need > 0 && workspace && workspace_bytes >= need) ? (float*)workspace : nullptr;
-  return warp_corr_impl(ref_fea, src_fea, proj, hyp, view_w_in, vw_shift, vw_offset, vw_total, pw_params, batch, n_src,
-                        channels, ndepth, height, width, flags, sim_out, wsum_out, view_w_out, ws, stream);
 }
 
 extern "C" int tmvs_aggregate_finalize(float* sim_sum, const float* w_sum, int batch, int ndepth, int height,

@@ -8,7 +8,6 @@ reference does it so the warp coordinates match bit for bit.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -196,21 +195,13 @@ def warp_corr(ref_nhwc, src_nhwc, proj12, hyp, view_w_in=None, vw_shift=0, vw_of
         pw_ptr = pw.ctypes.data
     else:
         pw_ptr = None
-    # stage 1 (PixelwiseNet weights): the LDS-window kernel needs its per-view similarity buffer
-    nws = _lib_h().tmvs_warp_corr_workspace(v, c, d, h, w, int(view_w_in is None)) if WARP_WINDOW else 0
-    ws = torch.empty(nws // 4 + 64, device=hyp.device) if nws else None
     with _Span("tmvs_warp_corr"):
-        _lib.check(_lib_h().tmvs_warp_corr_ws(_ptr(ref_nhwc), _ptr(src_nhwc), proj.ctypes.data, _ptr(hyp),
-                                              _ptr(view_w_in), vw_shift, vw_offset, vw_total, pw_ptr, b, v, c, d, h, w,
-                                              (_lib.WARP_PARTIAL if partial else 0) | warp_flags(rot_order, h * w),
-                                              _ptr(sim), _ptr(wsum), _ptr(view_w_out if view_w_in is None else None),
-                                              _ptr(ws), 0 if ws is None else ws.numel() * 4, _stream()),
-                   "tmvs_warp_corr")
+        _lib.check(_lib_h().tmvs_warp_corr(_ptr(ref_nhwc), _ptr(src_nhwc), proj.ctypes.data, _ptr(hyp), _ptr(view_w_in),
+                                           vw_shift, vw_offset, vw_total, pw_ptr, b, v, c, d, h, w,
+                                           (_lib.WARP_PARTIAL if partial else 0) | warp_flags(rot_order, h * w),
+                                           _ptr(sim), _ptr(wsum),
+                                           _ptr(view_w_out if view_w_in is None else None), _stream()), "tmvs_warp_corr")
     return sim, wsum, (view_w_out if view_w_in is None else None)
-
-
-# stage 1 from LDS source windows (tmvs_warp_corr_ws); TMVS_WARP_WINDOW=0 keeps warp_corr_kernel (A/B)
-WARP_WINDOW = os.environ.get("TMVS_WARP_WINDOW", "1") != "0"
 
 
 def aggregate_finalize(sim_sum, w_sum):
