@@ -526,49 +526,37 @@ __global__ __launch_bounds__(kTrainBlock) void bn_stats_partial_kernel(const flo
   }
 }
 
-// One block for all groups: the per-block partials [groups][nblk][2C] summed per value -- lane l of a wave
-// takes rows l, l + 64, ... (fixed order), then a fixed xor tree -- into sums [groups][2C] (LDS and, for
-// the backward's apply pass, global), then
-//   STATS: mean, biased var (fp32) of every group;
-//   BWD:   dbeta = sum g, dgamma = sum g*xhat, per group in fp32 then over the groups in order.
-// (Replaces sum_double_partials + bn_stats_finalize / bn_relu_bwd_finalize: one launch instead of two.)
-template <bool BWD>
-__global__ __launch_bounds__(kTrainBlock) void bn_combine_kernel(const double* __restrict__ partial, int nblk, int C,
-                                                                 int groups, long nvox, double* __restrict__ sums_out,
-                                                                 float* __restrict__ out0, float* __restrict__ out1) {
-  extern __shared__ double tot[];  // [groups][2C]
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, K = 2 * C;
-  for (int gk = wv; gk < groups * K; gk += kTrainBlock / 64) {
-    const int g = gk / K, k = gk % K;
-    const double* p = partial + (size_t)g * nblk * K + k;
-    double a = 0.0;
-    for (int j = lane; j < nblk; j += 64) a += p[(size_t)j * K];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
-    if (lane == 0) {
-      tot[gk] = a;
-      if (BWD) sums_out[gk] = a;
-    }
-  }
+// out[k] = sum_j partial[j][k] (K values per block row): block k, threads stride j, then a fixed
+// LDS tree -- deterministic, and parallel over the (up to 4096) partial rows
+__global__ __launch_bounds__(kTrainBlock) void sum_double_partials_kernel(const double* __restrict__ partial, int nblk,
+                                                                          int K, double* __restrict__ out) {
+  __shared__ double red[kTrainBlock];
+  const int k = blockIdx.x;
+  partial += (size_t)blockIdx.y * nblk * K;  // grid.y = group
+  out += (size_t)blockIdx.y * K;
+  double a = 0.0;
+  for (int j = threadIdx.x; j < nblk; j += kTrainBlock) a += partial[(size_t)j * K + k];
+  red[threadIdx.x] = a;
   __syncthreads();
+  for (int st = kTrainBlock / 2; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[k] = red[0];
+}
+
+// mean, biased var (fp32) from the summed (sum z, sum z^2)
+__global__ void bn_stats_finalize_kernel(const double* __restrict__ sums, int C, long nvox, float* __restrict__ mean,
+                                         float* __restrict__ var) {
   const int c = threadIdx.x;
   if (c >= C) return;
-  if (BWD) {
-    float b = (float)tot[c], gm = (float)tot[C + c];
-    for (int g = 1; g < groups; ++g) {
-      b = b + (float)tot[(size_t)g * K + c];
-      gm = gm + (float)tot[(size_t)g * K + C + c];
-    }
-    out1[c] = b;   // dbeta
-    out0[c] = gm;  // dgamma
-  } else {
-    for (int g = 0; g < groups; ++g) {
-      const double m = tot[(size_t)g * K + c] / (double)nvox;
-      const double v = tot[(size_t)g * K + C + c] / (double)nvox - m * m;
-      out0[(size_t)g * C + c] = (float)m;
-      out1[(size_t)g * C + c] = (float)(v > 0.0 ? v : 0.0);
-    }
-  }
+  sums += (size_t)blockIdx.x * 2 * C;  // grid = groups
+  mean += (size_t)blockIdx.x * C;
+  var += (size_t)blockIdx.x * C;
+  const double m = sums[c] / (double)nvox;
+  const double v = sums[C + c] / (double)nvox - m * m;
+  mean[c] = (float)m;
+  var[c] = (float)(v > 0.0 ? v : 0.0);
 }
 
 __device__ __forceinline__ void bn_affine(float mean, float var, float g, float bt, float eps, float& al, float& sh) {
@@ -647,6 +635,21 @@ __global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_partial_kernel(
   }
 }
 
+// dbeta = sum g, dgamma = sum g*xhat from the summed partials: per group in fp32, then added over the
+// groups in order (as autograd accumulates the per-view gradients of a module called per view)
+__global__ void bn_relu_bwd_finalize_kernel(const double* __restrict__ sums, int C, int groups,
+                                            float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  float b = (float)sums[c], g = (float)sums[C + c];
+  for (int k = 1; k < groups; ++k) {
+    b = b + (float)sums[(size_t)k * 2 * C + c];
+    g = g + (float)sums[(size_t)k * 2 * C + C + c];
+  }
+  dbeta[c] = b;
+  dgamma[c] = g;
+}
+
 // pass 2: dz = gamma*rstd/N * (N*g - sum g - xhat * sum g*xhat)
 __global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_apply_kernel(
     const float* __restrict__ dy, const float* __restrict__ z, long n, int C, long nvox, const float* __restrict__ mean,
@@ -715,9 +718,9 @@ static int launch_wgrad(const float* direct, const float* gath, int B, int Pd, i
 
 static bool valid_ch(int c) { return c == 1 || c == 8 || c == 16 || c == 32 || c == 64; }
 
-static long bn_vpb(long nvox) {  // at most 512 partial rows (bn_combine_kernel: 8 per lane)
+static long bn_vpb(long nvox) {
   long vpb = 1024;
-  while ((nvox + vpb - 1) / vpb > 512) vpb *= 2;
+  while ((nvox + vpb - 1) / vpb > 4096) vpb *= 2;
   return vpb;
 }
 
@@ -807,8 +810,12 @@ extern "C" int tmvs_bn_stats_grouped(const float* z, int groups, long nvox, int 
   hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(nblk, groups), dim3(kTrainBlock), 0, st, z, nvox, channels, vpb,
                      part);
   TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_combine_kernel<false>, dim3(1), dim3(kTrainBlock), groups * 2 * channels * sizeof(double), st,
-                     (const double*)part, nblk, channels, groups, nvox, nullptr, mean, var);
+  double* sums = part + (size_t)groups * nblk * 2 * channels;
+  hipLaunchKernelGGL(sum_double_partials_kernel, dim3(2 * channels, groups), dim3(kTrainBlock), 0, st,
+                     (const double*)part, nblk, 2 * channels, sums);
+  TMVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(groups), dim3(64), 0, st, (const double*)sums, channels, nvox,
+                     mean, var);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -853,8 +860,11 @@ extern "C" int tmvs_bn_relu_backward_grouped(const float* dy, const float* z, in
   hipLaunchKernelGGL(bn_relu_bwd_partial_kernel, dim3(nblk, groups), dim3(kTrainBlock), 0, st, dy, z, nvox, channels,
                      mean, var, gamma, beta, eps, vpb, part);
   TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_combine_kernel<true>, dim3(1), dim3(kTrainBlock), groups * 2 * channels * sizeof(double), st,
-                     (const double*)part, nblk, channels, groups, nvox, sums, dgamma, dbeta);
+  hipLaunchKernelGGL(sum_double_partials_kernel, dim3(2 * channels, groups), dim3(kTrainBlock), 0, st,
+                     (const double*)part, nblk, 2 * channels, sums);
+  TMVS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_relu_bwd_finalize_kernel, dim3(1), dim3(64), 0, st, (const double*)sums, channels, groups,
+                     dgamma, dbeta);
   TMVS_CHECK_LAUNCH();
   const long n = nvox * channels * groups;
   hipLaunchKernelGGL(bn_relu_bwd_apply_kernel, dim3((unsigned)((n + kTrainBlock - 1) / kTrainBlock)), dim3(kTrainBlock),
