@@ -127,7 +127,7 @@ def _grad_worker(rank, world, port, q):
         for p in params:
             p.grad = torch.randn(p.shape, generator=g)
         allreduce_gradients(params, bucket_bytes=1024)  # forces several buckets
-        got = [p.grad.clone() for p in params]
+        got = [p.grad.numpy().copy() for p in params]  # plain arrays: a queued tensor is shared by fd and dies with this process
         # the same sync on FlatAdam's single flat gradient buffer (its parameters are views of one buffer)
         from transmvsnet_amd.train import FlatAdam
         g = torch.Generator().manual_seed(100 + rank)
@@ -136,7 +136,7 @@ def _grad_worker(rank, world, port, q):
         for p in params2:
             p.grad = torch.randn(p.shape, generator=g)
         opt.allreduce()
-        q.put((rank, got, [p.grad.clone() for p in params2]))
+        q.put((rank, got, [p.grad.numpy().copy() for p in params2]))
     finally:
         dist.destroy_process_group()
 
@@ -166,9 +166,9 @@ def test_allreduce_gradients_is_the_rank_mean():
         expect.append(acc / world)
     for r in range(world):
         for got, exp in zip(res[r], expect):
-            torch.testing.assert_close(got, exp, rtol=1e-6, atol=1e-6)
+            torch.testing.assert_close(torch.from_numpy(got), exp, rtol=1e-6, atol=1e-6)
         for got, exp in zip(res_flat[r], expect):
-            torch.testing.assert_close(got, exp, rtol=1e-6, atol=1e-6)
+            torch.testing.assert_close(torch.from_numpy(got), exp, rtol=1e-6, atol=1e-6)
 
 
 def test_flat_adam_views():
