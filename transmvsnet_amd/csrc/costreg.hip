@@ -66,7 +66,7 @@ __device__ __forceinline__ float act(float v, float lo) { return v > lo ? v : lo
 // its NBW = TD*TH/4 rows through the 27 taps: A (weights) from global/L2, requested two taps
 // ahead, B from LDS. The next chunk's tile is fetched into registers during the current
 // chunk's MFMAs.
-template <int CIN, int COUT, int S, int TD, int TH, int MBB>
+template <int CIN, int COUT, int S, int TD, int TH, int MBB, bool KDSKIP = false>
 #ifndef TMVS_LDS_WPE
 #define TMVS_LDS_WPE 3
 #endif
@@ -134,6 +134,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
       if (idx < NVOX * PL) *reinterpret_cast<float4*>(tile + vox * VST + 4 * qs) = pf[k];
     }
   };
+  // KDSKIP (launched only for output depth <= 2, where every wave has one): the kd slices whose
+  // input plane lies wholly in the depth padding of the wave's output slice are not run (their
+  // products are exact zeros). The taps then run as a loop over the kept slices (9 unrolled taps
+  // each); the full-depth instance keeps the straight 27-tap schedule.
+  static_assert(!KDSKIP || TH % NBW == 0, "KDSKIP needs one output slice per wave");
+  int kd_lo = 0, kd_hi = 2;
+  if constexpr (KDSKIP) {
+    const int od = od0 + (__builtin_amdgcn_readfirstlane(wv) * NBW) / TH;
+    const int id_base = od * S - 1;  // input slice of kd = 0
+    kd_lo = id_base < 0 ? -id_base : 0;
+    kd_hi = g.Di - 1 - id_base < 2 ? g.Di - 1 - id_base : 2;
+    if (od >= g.Do) kd_hi = -1;  // rows past the volume: nothing to compute
+  }
   fetch(0);
   commit();
   __syncthreads();
@@ -152,6 +165,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
       }
     };
     VecN<PL> aw[3][MBB];
+    // one tap: B fragments from the LDS tile, NBW x MBB x PL MFMAs
+    auto tap_mfma = [&](int kd, int kh, int kw, const VecN<PL>* a) {
+      VecN<PL> b[NBW];
+#pragma unroll
+      for (int r = 0; r < NBW; ++r) {
+        const int rr = wv * NBW + r;
+        const int odl = rr / TH, ohl = rr - odl * TH;
+        const int lvox = ((odl * S + kd) * LH + ohl * S + kh) * LW + col * S + kw;
+        const int qs = SWZ ? (kgrp ^ ((lvox >> 1) & 3)) : kgrp;
+        b[r].load(tile + lvox * VST + qs * PL);
+      }
+#pragma unroll
+      for (int j = 0; j < PL; ++j)
+#pragma unroll
+        for (int r = 0; r < NBW; ++r)
+#pragma unroll
+          for (int m = 0; m < MBB; ++m)
+            acc[r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b[r].v[j], acc[r][m], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // keep the 2-tap-ahead schedule (and the VGPR budget)
+    };
+    if constexpr (KDSKIP) {
+      if (kd_lo <= kd_hi) {
+        wload(kd_lo * 9, aw[0]);
+        wload(kd_lo * 9 + 1, aw[1]);
+      }
+#pragma unroll 1
+      for (int kd = kd_lo; kd <= kd_hi; ++kd)
+#pragma unroll
+        for (int k9 = 0; k9 < 9; ++k9) {
+          if (k9 + 2 < 9 || kd < kd_hi) wload(kd * 9 + k9 + 2, aw[(k9 + 2) % 3]);
+          tap_mfma(kd, k9 / 3, k9 % 3, aw[k9 % 3]);
+        }
+    } else {
     wload(0, aw[0]);
     wload(1, aw[1]);
 #pragma unroll
@@ -176,6 +222,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
           for (int m = 0; m < MBB; ++m)
             acc[r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b[r].v[j], acc[r][m], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);  // keep the 2-tap-ahead schedule (and the VGPR budget)
+    }
     }
     if (ch + 1 < NCH) {
       __syncthreads();
@@ -1051,13 +1098,21 @@ static int launch_conv_s2c8_tile(const float* x, const float* w, const float* al
 }
 
 // ---------------------------------------------------------------- launchers
+#ifndef TMVS_KDSKIP_MAX_DO
+#define TMVS_KDSKIP_MAX_DO 2
+#endif
 template <int CIN, int COUT, int S, int TD, int TH, int MBB>
 static int launch_conv(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
                        const Geo& g, hipStream_t st) {
   constexpr int MG = ((COUT + 15) / 16) / MBB;
   const long nblk = (long)B * ((g.Do + TD - 1) / TD) * ((g.Ho + TH - 1) / TH) * ((g.Wo + 15) / 16) * MG;
-  hipLaunchKernelGGL((conv3d_lds_kernel<CIN, COUT, S, TD, TH, MBB>), dim3((unsigned)nblk), dim3(256), 0, st, x, w, al,
-                     sh, y, g);
+  // output depth <= 2 (the coarse levels of a D = 8 stage): every wave has a depth-padding kd slice
+  if (g.Do <= TMVS_KDSKIP_MAX_DO)
+    hipLaunchKernelGGL((conv3d_lds_kernel<CIN, COUT, S, TD, TH, MBB, true>), dim3((unsigned)nblk), dim3(256), 0, st, x,
+                       w, al, sh, y, g);
+  else
+    hipLaunchKernelGGL((conv3d_lds_kernel<CIN, COUT, S, TD, TH, MBB>), dim3((unsigned)nblk), dim3(256), 0, st, x, w, al,
+                       sh, y, g);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
