@@ -257,6 +257,30 @@ __device__ __forceinline__ void load_token_frag(const float* __restrict__ row, f
 
 constexpr int kKvTilesPerWave = 8;     // kv: at most this many tiles per wave (see kv_tiles_per_wave)
 
+// x + x[lane ^ 1], then ^2, ^4, ^8: the butterfly sum over a 16-lane row. The partner values move by
+// DPP (quad_perm for 1 and 2; row_half_mirror = ^7 and row_mirror = ^15 composed with a quad_perm /
+// half mirror for 4 and 8), not by ds_bpermute through the LDS unit: the same values in the same
+// additions, so the sums are bitwise those of __shfl_xor.
+#ifndef TMVS_KV_DPP
+#define TMVS_KV_DPP 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ float dppf(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float xor_sum16(float x) {
+#if TMVS_KV_DPP
+  x += dppf<0xB1>(x);               // quad_perm [1,0,3,2]: lane ^ 1
+  x += dppf<0x4E>(x);               // quad_perm [2,3,0,1]: lane ^ 2
+  x += dppf<0x1B>(dppf<0x141>(x));  // half mirror (^7) then quad_perm [3,2,1,0] (^3): lane ^ 4
+  x += dppf<0x141>(dppf<0x140>(x)); // row mirror (^15) then half mirror (^7): lane ^ 8
+#else
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) x += __shfl_xor(x, off, 64);
+#endif
+  return x;
+}
+
 // (KV, Ksum) partial sums: per wave, tiles of 16 source tokens; K, V by MFMA; per lane the
 // two heads it owns are accumulated over its tokens, then summed over the 16 token lanes.
 __global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __restrict__ src, int S,
@@ -336,19 +360,9 @@ __global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __rest
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float x = kv[mb][i];
+    for (int i = 0; i < 16; ++i) kv[mb][i] = xor_sum16(kv[mb][i]);
 #pragma unroll
-      for (int off = 1; off < 16; off <<= 1) x += __shfl_xor(x, off, 64);
-      kv[mb][i] = x;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float x = ks[mb][i];
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) x += __shfl_xor(x, off, 64);
-      ks[mb][i] = x;
-    }
+    for (int i = 0; i < 4; ++i) ks[mb][i] = xor_sum16(ks[mb][i]);
   }
   if ((lane & 15) == 0) {
 #pragma unroll

@@ -584,10 +584,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const float rz = rot_row(R + 8, fxp, fyp, args.rot_plain);
     const unsigned vbase = (unsigned)(v * HW * C * 4 + 16 * q);
     const float w = wv[(size_t)v * Hs * Ws];
-#ifndef TMVS_PAIR_JUNROLL
-#define TMVS_PAIR_JUNROLL 1
-#endif
-#pragma unroll ((C == 8) ? TMVS_PAIR_JUNROLL : 1)
+#pragma unroll 1
     for (int j = 0; j < DPT; ++j) {
       Geom own;
       project(rx, ry, rz, R[3], R[7], R[11], dep_lds[j][tid], halfw, halfh, own.x0, own.y0, own.fx, own.fy);
