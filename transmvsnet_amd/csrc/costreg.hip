@@ -1383,11 +1383,13 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
   if (cin == CI && cout == CO && stride == 2) return launch_conv_direct<CI, CO, 2, NBW, MBW>(x, wpk, al, sh, y, B, g, st);
   TMVS_CONV_DIRECT(8, 16, 4, 1)
   TMVS_CONV_DIRECT(16, 32, 4, 1)
-#ifndef TMVS_C5_NBW
-#define TMVS_C5_NBW 2  // conv5 (r12r): 1 row per wave measured 61.9 / 36.6 / 28.5 vs 57.4 / 28.6 / 25.9 us
-#define TMVS_C5_MBW 1
-#endif
-  TMVS_CONV_DIRECT(32, 64, TMVS_C5_NBW, TMVS_C5_MBW)
+  // conv5: 2 rows x 2 output blocks per wave (half the waves, each weight fragment used twice as
+  // often) on the stage-2/3 grids (15.5 K output voxels): 58.1 -> 51.4 / 29.8 -> 27.0 us; the
+  // stage-1 grid (5.8 K voxels) is faster at 2 x 1 (26.6 vs 35.3 us). 1 x 1 and 4 x 1 measured slower
+  // (r12r, r12s). Both tilings keep every output's accumulation order.
+  if (cin == 32 && cout == 64 && stride == 2 && (long)g.Do * g.Ho * g.Wo >= 8192)
+    return launch_conv_direct<32, 64, 2, 2, 2>(x, wpk, al, sh, y, B, g, st);
+  TMVS_CONV_DIRECT(32, 64, 2, 1)
 #undef TMVS_CONV_DIRECT
   return TMVS_ERR_SHAPE;
 }
