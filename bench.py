@@ -199,7 +199,9 @@ def run(args, world, rank, local):
         return model.forward_features(feats, proj, dv_dev, (H, W), view_shard=shard)
 
     eager_step = step
-    graphed = shard is None and not args.no_graph
+    # a view-sharded step replays as one graph too: RCCL all-reduces are captured on the step's stream
+    # (gloo's CPU-side collectives cannot be captured)
+    graphed = not args.no_graph and (shard is None or args.dist_backend == "nccl")
     with torch.no_grad():
         for _ in range(args.warmup):
             out = step()
@@ -506,10 +508,9 @@ def train_timing(steps, dev, world, use_graph=True):
                 fn()
             torch.cuda.current_stream(dev).wait_stream(side)
             torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                fn()
+            g = _train.TrainStepGraph(fn, m)  # per-graph overflow flags; replay() re-keys the inference caches
             torch.cuda.synchronize()
+            graphs.append(g)
             return g.replay
         except Exception as e:  # noqa: BLE001 -- reported in the JSON line, the eager timing stands
             launch_notes.append(f"{getattr(fn, '__name__', 'step')}: capture failed ({type(e).__name__}: {str(e)[:120]})")
@@ -517,14 +518,14 @@ def train_timing(steps, dev, world, use_graph=True):
             return None
 
     from transmvsnet_amd import train as _train
-    launch_notes = []
+    launch_notes, graphs = [], []
     ms_eager = timed(full_step)
     ms_feat_eager = timed(features_step)
     g_full, g_feat = graphed(full_step), graphed(features_step)
     ms = timed(g_full) if g_full else ms_eager
     ms_feat = timed(g_feat) if g_feat else ms_feat_eager
-    if g_full or g_feat:
-        _train.check_graph_flags()
+    for g in graphs:
+        g.check_flags()
     nbytes = sum(p.numel() for p in m.parameters()) * 4
     return {"ms_per_sample": round(ms, 3), "samples_per_s": round(world * 1e3 / ms, 3), "ranks": world,
             "grad_allreduce_bytes": nbytes if world > 1 else 0,

@@ -652,7 +652,8 @@ def test_flat_adam_matches_torch_adam():
 def test_flat_adam_graph_replay_equals_eager_steps():
     """A FlatAdam step captured in a HIP graph (tmvs_adam_step_dev: the step number advanced on the
     device per replay) gives bitwise the same parameters and moments as eager steps (host step
-    number), after 2 eager steps and 3 replays vs 5 eager steps with the same gradients."""
+    number), after 2 eager steps and 3 replays vs 5 eager steps with the same gradients; and an
+    eager step after the replays is step 6 (the capture does not count as a step, the replays do)."""
     from transmvsnet_amd.train import FlatAdam
     torch.manual_seed(5)
     shapes = [(8, 1, 3, 3, 3), (16,), (64, 32)]
@@ -682,7 +683,16 @@ def test_flat_adam_graph_replay_equals_eager_steps():
     for _ in range(3):
         graph.replay()
     torch.cuda.synchronize()
-    assert int(ob._step_dev.item()) == 5
+    assert int(ob._step_dev.item()) == 5 and ob.step_count == 5
+    assert torch.equal(oa.flat, ob.flat)
+    assert torch.equal(oa.exp_avg, ob.exp_avg) and torch.equal(oa.exp_avg_sq, ob.exp_avg_sq)
+    oa.zero_grad()
+    for p, gr in zip(pa, grads):
+        p.grad = gr.clone()
+    oa.step()
+    step_b()  # eager, after the capture
+    torch.cuda.synchronize()
+    assert oa.step_count == 6 and ob.step_count == 6
     assert torch.equal(oa.flat, ob.flat)
     assert torch.equal(oa.exp_avg, ob.exp_avg) and torch.equal(oa.exp_avg_sq, ob.exp_avg_sq)
 

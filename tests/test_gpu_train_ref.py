@@ -280,10 +280,14 @@ def test_flat_adam_accumulates_two_backwards_and_invalidates_inference_cache():
 
 
 def test_train_sample_hip_graph_replay_equals_eager(gold):
-    """The same train_sample body captured once as a HIP graph (bench.py's training timing) and
-    replayed: two replays after one eager step leave the parameters, Adam moments and BatchNorm
-    running statistics where three eager steps leave them (within 1e-5 of each quantity's max: the
-    DCN's beyond-window corners use fp32 atomics, so not bitwise)."""
+    """The same train_sample body captured once as a HIP graph (train.TrainStepGraph, bench.py's
+    training timing) and replayed: one eager step, an eval forward (builds the inference caches), two
+    replays, an eval forward, and one more eager step leave the parameters, Adam moments and BatchNorm
+    running statistics where four eager steps leave them (within 1e-5 of each quantity's max: the
+    DCN's beyond-window corners use fp32 atomics, so not bitwise). Also: Adam's step number after
+    the replays is 4 (the eager step after a capture uses the device counter), and the eval forward
+    after the replays equals a fresh model's built from the same state_dict bit for bit (the replays
+    invalidated the inference caches keyed on parameter versions)."""
     from transmvsnet_amd import loss as hip_loss
     from transmvsnet_amd import synthetic
     from transmvsnet_amd import train as tr
@@ -304,21 +308,31 @@ def test_train_sample_hip_graph_replay_equals_eager(gold):
             loss = hip_loss.focal_loss_bld(outputs, depth_gt_ms, mask_ms, interval, dlossw=[1.0, 1.0, 1.0])[0]
             loss.backward()
             opt.step()
+
+        def eval_prob(m):
+            m.eval()
+            with torch.no_grad(), golden_rot(m):
+                return m(imgs, proj, dv)["stage3"]["prob_volume"].clone()
         with golden_rot(model):
             body()
+            eval_prob(model)  # the inference caches now hold step 1's weights
             torch.cuda.synchronize()
             if graphed:
-                graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(graph):
-                    body()  # captured, not run
+                graph = tr.TrainStepGraph(body, model)  # captured, not run
                 for _ in range(2):
                     graph.replay()
                 torch.cuda.synchronize()
-                tr.check_graph_flags()
+                graph.check_flags()
             else:
                 for _ in range(2):
                     body()
+            ev = eval_prob(model)
+            fresh = _model()
+            fresh.load_state_dict(model.state_dict())
+            assert torch.equal(ev, eval_prob(fresh)), "eval forward used stale packed weights"
+            body()  # an eager step after the replays: Adam step 4
         torch.cuda.synchronize()
+        assert opt.step_count == 4, opt.step_count
         bufs = {n: b.detach().clone() for n, b in model.named_buffers() if "running" in n}
         runs.append((opt.flat.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), bufs))
     (fa, ma, va, ba), (fb, mb, vb, bb) = runs

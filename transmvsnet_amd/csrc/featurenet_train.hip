@@ -402,10 +402,14 @@ __global__ __launch_bounds__(kBlk) void absmax2_kernel(const float* __restrict__
 // the window's fixed-point exponent: a contribution m * w_bilinear * dcol_c has magnitude at most
 // CO max|dy| max|W| (m, w_bilinear <= 1), a cell at most kMaxAdds of them: with 2^e above that
 // bound, units of 2^-(62 - e) keep every cell's int64 sum in range, at a resolution 2^-40 or finer
-// relative to the largest possible contribution
+// relative to the largest possible contribution. A non-finite max|dy| or max|W| (an inf/NaN
+// upstream gradient) returns kFixBad: the window is then written as NaN, so dx propagates the NaN
+// as torch's deform_conv2d backward would, instead of converting inf/NaN to garbage integers.
+constexpr int kFixBad = -100000;
 __device__ __forceinline__ int dcn_fix_shift(const unsigned* __restrict__ mx, int CO) {
   const double bound = (double)__uint_as_float(mx[0]) * (double)__uint_as_float(mx[1]) * CO * (double)dbw::kMaxAdds;
-  if (!(bound > 0.0) || !(bound < 1e300)) return 0;
+  if (!(bound < 1e300)) return kFixBad;  // inf or NaN (finite floats bound it far below 1e300)
+  if (!(bound > 0.0)) return 0;          // every contribution is 0
   int e;
   frexp(bound, &e);
   return 62 - e;
@@ -509,7 +513,7 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
 #pragma unroll
             for (int c = 0; c < CC; ++c)
               atomicAdd(wp + c * (WR * WC),
-                        (unsigned long long)__double2ll_rn(ldexp((double)(f * dc[c]), kfix)));
+                        (unsigned long long)(kfix == kFixBad ? 0ll : __double2ll_rn(ldexp((double)(f * dc[c]), kfix))));
           } else {  // an offset beyond the window: straight to global memory
             float* gp = dxb + ((size_t)cy * W + cx) * 32 + cc * CC;
 #pragma unroll
@@ -522,7 +526,8 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
     float* sb = scratch + (size_t)blockIdx.x * (WR * WC) * 32 + cc * CC;
     for (int i = tid; i < WR * WC * CC; i += kBlk) {
       const int cell = i / CC, c = i - cell * CC;  // 8 lanes = one cell's 32-byte channel chunk
-      sb[(size_t)cell * 32 + c] = (float)ldexp((double)(long long)win[c * (WR * WC) + cell], -kfix);
+      sb[(size_t)cell * 32 + c] =
+          kfix == kFixBad ? __builtin_nanf("") : (float)ldexp((double)(long long)win[c * (WR * WC) + cell], -kfix);
     }
     __syncthreads();
   }

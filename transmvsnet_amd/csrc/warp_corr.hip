@@ -481,7 +481,7 @@ __device__ __forceinline__ Geom geom_round(const Geom& own, int t) {
 // batch are issued before any is consumed.
 template <int C, int R0, int N>
 __device__ __forceinline__ void pair_rounds(const __amdgpu_buffer_rsrc_t rsrc, unsigned vbase, unsigned rowb, int W,
-                                            int H, const Geom& own, const float4& r4, int tx, float* part) {
+                                            int H, const Geom& own, const float4* r4, int tx, float* part) {
   constexpr int LPS = C / 2;
   floatx4 top[N], bot[N];
   float wt[N], wb[N];
@@ -501,11 +501,12 @@ __device__ __forceinline__ void pair_rounds(const __amdgpu_buffer_rsrc_t rsrc, u
   }
 #pragma unroll
   for (int i = 0; i < N; ++i) {
+    const float4 r = r4[R0 + i];
     float acc = 0.f;
-    acc = acc + fmaf(bot[i][0], wb[i], top[i][0] * wt[i]) * r4.x;
-    acc = acc + fmaf(bot[i][1], wb[i], top[i][1] * wt[i]) * r4.y;
-    acc = acc + fmaf(bot[i][2], wb[i], top[i][2] * wt[i]) * r4.z;
-    acc = acc + fmaf(bot[i][3], wb[i], top[i][3] * wt[i]) * r4.w;
+    acc = acc + fmaf(bot[i][0], wb[i], top[i][0] * wt[i]) * r.x;
+    acc = acc + fmaf(bot[i][1], wb[i], top[i][1] * wt[i]) * r.y;
+    acc = acc + fmaf(bot[i][2], wb[i], top[i][2] * wt[i]) * r.z;
+    acc = acc + fmaf(bot[i][3], wb[i], top[i][3] * wt[i]) * r.w;
     part[R0 + i] = acc;
   }
 }
@@ -540,6 +541,20 @@ __device__ __forceinline__ float reduce_scatter(const float* p, int k) {
   return q[0];
 }
 
+// Which samples share a load instruction (TMVS_WARP_PMAJOR, default 1). The address path pays per
+// distinct cache line an instruction touches (≈2 cycles each past the 16-cycle floor of a 64-lane
+// 16-byte load), not per byte. A pixel's consecutive depth planes project ≈0.7 px apart on its
+// epipolar line, so their taps share lines, while different pixels' taps (per-pixel hypotheses)
+// do not. Pixel-major rounds: in round t the wave's SPW groups sample PPR = SPW/LPS pixels ×
+// LPS consecutive planes each (stage 3: 4 pixels × 4 planes, stage 2: 1 pixel × 8 planes)
+// instead of SPW pixels × one plane. Group g's round-t sample is owned by its lane t (geometry
+// broadcast as before), so lane (g, k) owns pixel k·PPR + g/LPS at planes j·LPS + g%LPS, and
+// holds the reference quads of the LPS pixels its rounds visit. Each sample's arithmetic (lane
+// roles, channel order, reduce-scatter) is unchanged: the outputs are bit-identical.
+#ifndef TMVS_WARP_PMAJOR
+#define TMVS_WARP_PMAJOR 1
+#endif
+
 template <int C, int D, bool PARTIAL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void warp_pair_kernel(
     const float* __restrict__ ref, const float* __restrict__ src, const float* __restrict__ hyp,
@@ -548,8 +563,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   constexpr int NQ = C / 4;             // channel quads
   constexpr int LPS = 2 * NQ;           // lanes per pixel: (tap column, quad)
   constexpr int SPW = 64 / LPS, PIX = 4 * SPW, DPT = D / LPS;
+  constexpr int PPR = TMVS_WARP_PMAJOR ? SPW / LPS : SPW;  // pixels per round
   static_assert(C == 8 || C == 16, "row-pair layout for 8 or 16 channels");
   static_assert(D % LPS == 0, "D must be a multiple of the lanes per pixel");
+  static_assert(!TMVS_WARP_PMAJOR || PPR * LPS == SPW, "pixel-major rounds: LPS^2 must divide 64");
   __shared__ float dep_lds[DPT][256];
   __shared__ float acc_lds[DPT][256];
   const int tid = threadIdx.x;
@@ -557,16 +574,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const int nblk = (HW + PIX - 1) / PIX;
   const int tile = xcd_remap(blockIdx.x, nblk);
   const int lane = tid & 63;
-  const int k = lane % LPS, tx = k / NQ, q = k % NQ;
-  int p = tile * PIX + (tid >> 6) * SPW + lane / LPS;
+  const int k = lane % LPS, tx = k / NQ, q = k % NQ, g = lane / LPS;
+  const int wbase = tile * PIX + (tid >> 6) * SPW;
+  // owned samples: pixel `p`, planes j·LPS + dsub (pixel-major) or j·LPS + k (plane-major)
+  const int pix_own = TMVS_WARP_PMAJOR ? k * PPR + g / LPS : g;
+  const int dsub = TMVS_WARP_PMAJOR ? g % LPS : k;
+  int p = wbase + pix_own;
   const bool active = p < HW;
   if (!active) p = HW - 1;
   const int py = p / W, px = p - py * W;
   const float fxp = (float)px, fyp = (float)py;
-  const float4 r4 = *reinterpret_cast<const float4*>(ref + (size_t)p * C + 4 * q);
+  float4 r4[LPS];  // reference quad q of the pixel round t samples
+#pragma unroll
+  for (int t = 0; t < LPS; ++t) {
+    const int pt = TMVS_WARP_PMAJOR ? min(wbase + t * PPR + g / LPS, HW - 1) : p;
+    r4[t] = *reinterpret_cast<const float4*>(ref + (size_t)pt * C + 4 * q);
+  }
 #pragma unroll
   for (int j = 0; j < DPT; ++j) {
-    dep_lds[j][tid] = hyp[(size_t)(j * LPS + k) * HW + p];
+    dep_lds[j][tid] = hyp[(size_t)(j * LPS + dsub) * HW + p];
     acc_lds[j][tid] = 0.f;
   }
   const float halfw = (float)(W - 1) / 2.f;
@@ -602,10 +628,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   if (!active) return;
 #pragma unroll 4
   for (int j = 0; j < DPT; ++j) {
-    const size_t o = (size_t)(j * LPS + k) * HW + p;
+    const size_t o = (size_t)(j * LPS + dsub) * HW + p;
     sim_out[o] = PARTIAL ? acc_lds[j][tid] : acc_lds[j][tid] / wsum;
   }
-  if (PARTIAL && k == 0) wsum_out[p] = wsum;
+  if (PARTIAL && dsub == 0) wsum_out[p] = wsum;
 }
 
 template <int C, int D, bool PW, bool PARTIAL>

@@ -66,7 +66,8 @@ class ViewShard:
     """
 
     def __init__(self, rank: int, world: int, n_src: int, group=None,
-                 partial_fn: Optional[Callable] = None, finalize_fn: Optional[Callable] = None):
+                 partial_fn: Optional[Callable] = None, finalize_fn: Optional[Callable] = None,
+                 always_reduce: bool = False):
         if not 0 <= rank < world:
             raise ValueError(f"rank {rank} outside world {world}")
         self.rank, self.world, self.n_src, self.group = rank, world, n_src, group
@@ -75,6 +76,9 @@ class ViewShard:
         self._finalize = finalize_fn or _hip_finalize
         self.replica, self.replicas = 0, 1  # make_view_shard: this rank's replica group, and their count
         self.timer = None       # optional begin(name)/end(token) around each collective (bench.py)
+        # issue the all-reduce even at world 1 (a one-rank group: the collective is a copy) -- tests use
+        # it to capture the collective in a HIP graph on a single GPU
+        self.always_reduce = always_reduce
         self.comm_bytes = []    # bytes of each all-reduce issued, in order (3 per forward)
 
     @property
@@ -113,7 +117,10 @@ class ViewShard:
         return sim, (new_vw if stage == 0 else view_w)
 
     def allreduce(self, buf: torch.Tensor) -> None:
-        if self.world > 1:
+        """The stage's one collective. Graph-capturable on RCCL: `bench.py --mode views` captures the
+        whole view-sharded step (FMT, pathway, partial volumes, these all-reduces, finalize,
+        CostRegNet) as one HIP graph and replays it per step, like replica mode."""
+        if self.world > 1 or self.always_reduce:
             tok = self.timer.begin("rccl_all_reduce") if self.timer is not None else None
             dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
             if tok is not None:

@@ -36,6 +36,10 @@ def _pack_index(kind, cout, cin, k, device):
     zero (index cout*cin*k*k = a padding slot), so training packs on the device with no host sync."""
     key = (kind, cout, cin, k, str(device))
     if key not in _PACK_INDEX:
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            # the host-to-device copy below cannot run inside a capture (and would cache garbage)
+            raise RuntimeError(f"featurenet_train: pack index {key[:4]} not built yet inside a HIP-graph "
+                               "capture; run the step once eagerly before capturing it")
         zero = cout * cin * k * k
         if kind == "dcn":  # [tap][m-tile][half][lane][e] <- W[16m + (l & 15)][16h + 4 (l >> 4) + e][tap]
             mt = (cout + 15) // 16

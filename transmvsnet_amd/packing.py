@@ -25,6 +25,11 @@ def gather_packs(tensors, specs, key):
     full_key = (key, tuple(tuple(t.shape) for t in tensors), str(dev))
     ent = _IDX.get(full_key)
     if ent is None:
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            # inside a capture the index kernels would only be recorded, and the uninitialised index
+            # tensor cached for every later eager call
+            raise RuntimeError(f"gather_packs: index for {key!r} not built yet inside a HIP-graph capture; "
+                               "run the step once eagerly before capturing it")
         offs, off = [], 1
         for t in tensors:
             offs.append(off)

@@ -74,7 +74,7 @@ class _WarpCorrViews(torch.autograd.Function):
         if _DEFERRED_FLAGS is not None:  # inside depth_stages_train: one host sync after the whole backward
             _DEFERRED_FLAGS.append(flag.clone())
         elif torch.cuda.is_current_stream_capturing():  # a HIP-graph capture: checked after the replays
-            GRAPH_FLAGS.append(flag)
+            GRAPH_FLAGS.append(flag.clone())  # a graph-owned copy, not a view into the warp workspace
         else:
             _check_overflow([flag])
         return dref, dsrc, None, None, None, None
@@ -85,8 +85,12 @@ GRAPH_FLAGS = []  # overflow flags of backwards captured in a HIP graph (check_g
 
 
 def check_graph_flags():
-    """The overflow check of the warp backwards inside a captured training-step graph (one host sync)."""
-    _check_overflow(GRAPH_FLAGS)
+    """The overflow check of the warp backwards captured outside a TrainStepGraph (one host sync); the
+    flags are dropped after the check, so a later capture is checked on its own flags only."""
+    try:
+        _check_overflow(GRAPH_FLAGS)
+    finally:
+        GRAPH_FLAGS.clear()
 
 
 def _check_overflow(flags):
@@ -685,9 +689,10 @@ class FlatAdam:
         self.exp_avg = torch.zeros(n, device=dev)
         self.exp_avg_sq = torch.zeros(n, device=dev)
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
-        self.step_count = 0
+        self._host_steps = 0
+        self._graphed = False
         # the step number on the device as well, for a step captured in a HIP graph (tmvs_adam_step_dev
-        # advances it per replay); eager steps keep it equal to step_count
+        # advances it per replay); eager steps before any capture keep it equal to the host count
         self._step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self._scal_dev = torch.zeros(2, device=dev)
         self._gathered = False
@@ -739,22 +744,73 @@ class FlatAdam:
             dist.all_reduce(self.grad_flat, op=dist.ReduceOp.SUM, group=group)
             self.grad_flat.div_(dist.get_world_size(group))
 
+    @property
+    def step_count(self):
+        """Adam's step number. Once a step has been captured in a HIP graph, replays advance only the
+        device counter, so that counter is the only count from then on (one host sync to read)."""
+        return int(self._step_dev.item()) if self._graphed else self._host_steps
+
     def step(self, lr=None):
         self._gather()
-        self.step_count += 1
-        if torch.cuda.is_current_stream_capturing():
-            ops.adam_step_dev(self.flat, self.grad_flat, self.exp_avg, self.exp_avg_sq, self.lr if lr is None else lr,
-                              self.betas, self.eps, self.weight_decay, self._step_dev, self._scal_dev)
+        lr = self.lr if lr is None else lr
+        if torch.cuda.is_current_stream_capturing() or self._graphed:
+            # captured (the launch runs once per replay) or any step after a capture: the step number
+            # lives on the device (tmvs_adam_step_dev advances it per launch); the host count is not
+            # touched, so eager steps interleaved with replays use the right bias correction
+            self._graphed = True
+            ops.adam_step_dev(self.flat, self.grad_flat, self.exp_avg, self.exp_avg_sq, lr, self.betas, self.eps,
+                              self.weight_decay, self._step_dev, self._scal_dev)
         else:
-            ops.adam_step(self.flat, self.grad_flat, self.exp_avg, self.exp_avg_sq, self.lr if lr is None else lr,
-                          self.betas, self.eps, self.weight_decay, self.step_count)
-            self._step_dev.fill_(self.step_count)
+            self._host_steps += 1
+            ops.adam_step(self.flat, self.grad_flat, self.exp_avg, self.exp_avg_sq, lr, self.betas, self.eps,
+                          self.weight_decay, self._host_steps)
+            self._step_dev.fill_(self._host_steps)
         # the launch wrote the parameters through a raw pointer: bump their version counters so the
         # inference caches keyed on them (TransMVSNet._param_key, FeatureNet's packed weights) rebuild
-        with torch.no_grad():
-            for p in self.params:
-                torch.autograd.graph.increment_version(p)
+        # (a replay bumps nothing: TrainStepGraph.replay does it)
+        bump_versions(self.params)
         self._gathered = False  # the next backward adds into the current .grad views unless zero_grad runs
+
+
+def bump_versions(tensors):
+    """Advance the in-place version counter of every tensor (after a raw-pointer write or a graph replay
+    that wrote them), so caches keyed on `_version` rebuild."""
+    with torch.no_grad():
+        for t in tensors:
+            torch.autograd.graph.increment_version(t)
+
+
+class TrainStepGraph:
+    """A training step captured once as a HIP graph and replayed (finetune.py:144-168's body per replay).
+
+    * The overflow flags of the warp backwards captured in this graph are kept per graph (cloned into
+      graph-owned buffers at capture) and checked by `check_flags`, so one graph's overflow never
+      blocks another's check, and no flag keeps a freed graph's workspace alive.
+    * `replay` bumps the version counters of the model's parameters and buffers (the replay's Adam step
+      and BatchNorm running-statistic updates wrote them without Python seeing it), so an eval forward
+      after replays rebuilds the inference caches (TransMVSNet._param_key, FeatureNet's packed
+      weights) instead of running on the weights of the last eager step.
+    Index caches that a step fills lazily (packing.gather_packs, featurenet_train's pack indices) must
+    be warm before capture: run the step once eagerly first (capture raises otherwise)."""
+
+    def __init__(self, fn, model, stream=None):
+        self.model = model
+        self.graph = torch.cuda.CUDAGraph()
+        n0 = len(GRAPH_FLAGS)
+        with torch.cuda.graph(self.graph, stream=stream):
+            self.out = fn()
+        self.flags = GRAPH_FLAGS[n0:]
+        del GRAPH_FLAGS[n0:]
+        self._tensors = list(model.parameters()) + list(model.buffers())
+
+    def replay(self):
+        self.graph.replay()
+        bump_versions(self._tensors)
+        return self.out
+
+    def check_flags(self):
+        """One host sync: raise if any captured warp backward overflowed in the replays so far."""
+        _check_overflow(self.flags)
 
 
 def allreduce_gradients(params, group=None, bucket_bytes=64 << 20):
