@@ -25,6 +25,9 @@ ORACLE's previous-stage depth ("fed"), so a near-tie flip upstream (which moves 
 hypotheses) is separated from the stage's own arithmetic. The C4 shape is additionally checked by
 properties (probabilities, clamp, WTA consistency, the view-sharded path).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -118,6 +121,15 @@ def _cascade_report(out, ref, allowed):
     return report
 
 
+def _write_report(tag, report):
+    """Per-config parity report as JSON (TMVS_REPORT_DIR, default gpurun_out/fullsize): a GPU run pulls
+    it back, and the round's measurement copies it to profiles/<run>/fullsize.json."""
+    out = os.path.join(os.environ.get("TMVS_REPORT_DIR", os.path.join("gpurun_out", "fullsize")), f"{tag}.json")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out, "w") as f:
+        json.dump(report, f, indent=1, default=lambda o: o.tolist() if hasattr(o, "tolist") else str(o))
+
+
 def _pyramid(model, feats_dev):
     """The GPU FMT + pathway features (NHWC, reference view first), as TransMVSNet._forward_one."""
     prep = model._prepared(torch.device(DEV, torch.cuda.current_device()))
@@ -153,6 +165,7 @@ def _full_size_parity(model, sd, n_views, H, W):
             report[f"fed_stage{s + 1}"].pop("_diff")
     torch.cuda.synchronize()
     print(f"\nN={n_views} {H}x{W}:", report)
+    _write_report(f"N{n_views}_{H}x{W}", report)
     for k in ("cascade_stage1", "cascade_stage2", "cascade_stage3", "fed_stage2", "fed_stage3"):
         assert not report[k]["unexplained"], (k, report)
     for k in ("fed_stage2", "fed_stage3"):
@@ -172,6 +185,8 @@ def test_c2_dtu_full_forward_parity(model, sd):
 def test_c3_dtu_11_views_full_forward_parity(model, sd):
     """C3's shape on one GPU: DTU 864x1152, N=11 (10 source views)."""
     rep = _full_size_parity(model, sd, 11, 864, 1152)
+    # the cascade (not only the fed stages) meets the north-star bar, as at C2
+    assert rep["cascade_stage3"]["mean_abs_mm"] <= 1e-4, rep
     assert rep["fed_stage3"]["mean_abs_mm"] <= 1e-4, rep
 
 

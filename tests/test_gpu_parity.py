@@ -148,6 +148,33 @@ def test_warp_corr_incoherent_depth_and_degenerate_planes(sd):
     _close(to_np(vw), to_np(vw_ref), 5e-7, "incoherent view weights")
 
 
+@pytest.mark.parametrize("c,d,interval,scale", [(16, 32, 2.5, "stage2"), (8, 8, 1.25, "stage3"),
+                                                (16, 16, 2.5, "stage2"), (8, 64, 1.0, "stage3")])
+def test_warp_corr_stage23_segments(c, d, interval, scale):
+    """Stages 2/3 (given view weights) with the forward's kind of hypotheses: per pixel D increasing
+    planes `interval` mm apart around a random centre, so each pixel-view's taps lie on a short
+    epipolar segment (warp_dot_kernel's per-pixel tap window). Mixed in: a patch of pixels whose
+    planes span 400 mm (segments longer than the window), a patch with one plane behind the camera,
+    and a patch with decreasing planes -- those pixels take the per-lane gather path. Against the
+    oracle's build_cost_volume."""
+    torch.manual_seed(11 + d)
+    n, h, w = 5, 48, 80
+    feats = [torch.randn(1, c, h, w) for _ in range(n)]
+    mult = 2 if scale == "stage2" else 4
+    proj = synthetic.synthetic_cameras(n, h * 4 // mult, w * 4 // mult, seed=2)[scale]
+    centre = torch.rand(1, 1, h, w) * 450 + 450
+    hyp = centre + (torch.arange(d, dtype=torch.float32) - d / 2).view(1, d, 1, 1) * interval
+    hyp[:, :, 4:10, 4:20] = torch.linspace(450.0, 850.0, d).view(1, d, 1, 1)
+    hyp[0, d // 2, 20:24, 30:40] = -30.0
+    hyp[:, :, 30:36, 50:70] = hyp[:, :, 30:36, 50:70].flip(1)
+    vw = torch.rand(1, n - 1, h, w)
+    sim_ref, _ = oracle.build_cost_volume({}, feats, proj, hyp, view_weights=vw)
+    nh = [_nhwc(f).to(DEV) for f in feats]
+    src = torch.stack([x[0] for x in nh[1:]], 0).unsqueeze(0).contiguous()
+    sim, _, _ = ops.warp_corr(nh[0], src, ops.proj_rows(proj), hyp.to(DEV), view_w_in=vw.to(DEV), vw_shift=0)
+    _close(to_np(sim)[:, None], to_np(sim_ref), 5e-7, f"segments c{c} d{d}")
+
+
 def test_e2e_eleven_views_tnt_aspect(sd):
     """Whole hot path at N=11 on a Tanks&Temples-shaped (1056x1920 / 4) frame vs the oracle."""
     m = TransMVSNet().eval()

@@ -634,10 +634,238 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   if (PARTIAL && dsub == 0) wsum_out[p] = wsum;
 }
 
+// ---------------------------------------------------------------- stages 2/3: "dot first" over unique taps
+// The row-pair kernel above gathers every (pixel, plane, view) tap through the vector-memory address
+// unit, 16 B per lane, and runs at 0.6-0.8 of that unit's rate. A pixel's D hypotheses
+// project onto a short segment of its epipolar line (≈0.7 px apart on the synthetic DTU rig), so its
+// D·4 taps hold only ≈1.5·D distinct texels (48 of 128 at stage 2, 14 of 32 at stage 3), and the
+// similarity factors over them:
+//   sim(p, d) = (1/C) Σ_c ref_c · Σ_tap w_tap(d) src_tap,c = (1/C) Σ_tap w_tap(d) · dot(p, tap),
+// dot(p, T) = Σ_c ref_c src_T,c. warp_dot_kernel loads each distinct texel of a pixel-view once,
+// reduces it to its dot with the reference features, parks the dot in a per-pixel LDS window, and
+// forms each plane's bilinear sample from 4 window reads.
+//
+// Lanes: a wave holds NPW = 64/D pixels × D planes; lane (p, d) owns plane d of pixel p (one sample per
+// view; its accumulator is a register). Per view:
+//  1. each lane projects its plane (project(): the forward's rounding) -> block (x0, y0) of 2×2 taps; a
+//     block with no tap inside the image is dead (sim 0: the reference's zero padding);
+//  2. the taps of its block not in plane d-1's block are new (hypotheses increase with d, so a pixel's
+//     blocks walk monotonically along the segment and each texel is new once); the wave's new texels
+//     are listed in LDS (byte offset, window slot) at a ballot prefix sum;
+//  3. load rounds: C/4 lanes per listed texel (a channel quad each; buffer loads, out-of-image texels
+//     read 0), dot with the pixel's reference quad, quad sum by DPP, store into the window;
+//  4. each lane reads its 4 taps' dots and forms sim = fma chain in grid_sample's order (nw, ne, sw, se)
+//     × 1/C; acc += sim · w_view as in the other kernels.
+// Window: MX × kWinRows floats per pixel, addressed along the segment: u = major − lo (major = the axis
+// the segment advances most along; lo from the end samples, planes 0 and D-1), v = minor −
+// floor(line(major)) + 3 with line() through the end samples: every tap lies within 2 texels of it, so
+// v ∈ [1, 6]. Each lane checks its own taps' slots; a pixel with any tap outside the window (a segment
+// longer than ≈MX − 4, hypotheses not increasing, a camera behind a plane) is gathered per lane (its 4
+// taps, same dot and quad-sum order: the same bits, without the reuse).
+// Numerics: the channel sum runs before the bilinear sum (the reference samples every channel, then
+// takes the channel mean), so similarities differ from the product form by a few ulps (5e-7 bar,
+// tests/test_gpu_parity.py).
+constexpr int kWinRows = 8;
+
+template <int D>
+struct DotCfg {
+  static constexpr int MX = D <= 8 ? 16 : D <= 16 ? 32 : D <= 32 ? 64 : 128;
+};
+
+// window slot of texel (X, Y) for the pixel's line (xmaj, lo, m0, M0, b); -1 when outside the window
+__device__ __forceinline__ int win_slot(int X, int Y, bool xmaj, int lo, float m0, float M0, float b, int MX) {
+  const int M = xmaj ? X : Y, m = xmaj ? Y : X;
+  const int u = M - lo;
+  const int v = m - (int)floorf(m0 + b * ((float)M - M0)) + 3;
+  return ((unsigned)u < (unsigned)MX && (unsigned)v < (unsigned)kWinRows) ? u * kWinRows + v : -1;
+}
+
+// dot of a texel's channel quad with the reference quad: serial FMA chain (the gather path and the load
+// rounds must agree bit for bit)
+__device__ __forceinline__ float quad_dot(const float4& r, const floatx4& s) {
+  float a = r.x * s[0];
+  a = fmaf(r.y, s[1], a);
+  a = fmaf(r.z, s[2], a);
+  return fmaf(r.w, s[3], a);
+}
+
+template <int C, int D, bool PARTIAL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void warp_dot_kernel(
+    const float* __restrict__ ref, const float* __restrict__ src, const float* __restrict__ hyp,
+    const float* __restrict__ vw_in, float* __restrict__ sim_out, float* __restrict__ wsum_out, int V, int H, int W,
+    int vw_shift, int vw_offset, WarpArgs args) {
+  constexpr int NPW = 64 / D;             // pixels per wave
+  constexpr int LPT = C / 4;              // lanes per texel (channel quads)
+  constexpr int TPR = 64 / LPT;           // texels per load round
+  constexpr int MX = DotCfg<D>::MX;
+  constexpr int WIN = MX * kWinRows;      // window floats per pixel
+  constexpr int NB = 2;                   // load rounds in flight
+  static_assert(64 % D == 0 && (C == 8 || C == 16), "warp_dot_kernel: D divides 64, C in {8, 16}");
+  __shared__ float win_lds[4][NPW * WIN];
+  __shared__ uint2 list_lds[4][4 * 64];
+  __shared__ float4 ref_lds[4][NPW * LPT];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int p = lane / D, d = lane % D;
+  const int q = lane % LPT;
+  const int HW = H * W;
+  const int nblk = (HW + 4 * NPW - 1) / (4 * NPW);
+  const int tile = xcd_remap(blockIdx.x, nblk);
+  const int wbase = tile * 4 * NPW + wave * NPW;
+  int pix = wbase + p;
+  const bool active = pix < HW;
+  if (!active) pix = HW - 1;
+  float* win = win_lds[wave];
+  uint2* list = list_lds[wave];
+  const float4* refq = ref_lds[wave];
+  if (lane < NPW * LPT) {
+    const int pp = min(wbase + lane / LPT, HW - 1);
+    ref_lds[wave][lane] = *reinterpret_cast<const float4*>(ref + (size_t)pp * C + 4 * (lane % LPT));
+  }
+  const int py = pix / W, px = pix - py * W;
+  const float fxp = (float)px, fyp = (float)py;
+  const float dep = hyp[(size_t)d * HW + pix];
+  const float halfw = (float)(W - 1) / 2.f;
+  const float halfh = (float)(H - 1) / 2.f;
+  const int Ws = W >> vw_shift, Hs = H >> vw_shift;
+  const float* wv = vw_in + (size_t)vw_offset * Hs * Ws + (py >> vw_shift) * Ws + (px >> vw_shift);
+  float acc = 0.f;
+  float wsum = PARTIAL ? 0.f : 1e-5f;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, V * HW * C * 4, kRsrcWord3);
+  const unsigned rowb = (unsigned)W * C * 4;
+  const unsigned long long lanes_below = (1ull << lane) - 1ull;
+  const unsigned long long pix_mask = D == 64 ? ~0ull : ((1ull << D) - 1ull);
+  for (int v = 0; v < V; ++v) {
+    const float* R = args.proj[v];
+    const float rx = rot_row(R, fxp, fyp, args.rot_plain);
+    const float ry = rot_row(R + 4, fxp, fyp, args.rot_plain);
+    const float rz = rot_row(R + 8, fxp, fyp, args.rot_plain);
+    const float w = wv[(size_t)v * Hs * Ws];
+    const unsigned vbase = (unsigned)(v * HW * C * 4);
+    // 1. this lane's plane, and the pixel's segment line from its end samples
+    int x0, y0;
+    float fx, fy;
+    project(rx, ry, rz, R[3], R[7], R[11], dep, halfw, halfh, x0, y0, fx, fy);
+    float ix, iy;  // unclamped sample position; NaN behind the camera (the pixel is then gathered)
+    {
+      const float Z = rz * dep + R[11];  // (x/z normalised and unnormalised again = x/z, up to rounding)
+      ix = Z < 1e-6f ? __builtin_nanf("") : (rx * dep + R[3]) / Z;
+      iy = Z < 1e-6f ? __builtin_nanf("") : (ry * dep + R[7]) / Z;
+    }
+    const bool live = x0 >= -1 && x0 < W && y0 >= -1 && y0 < H;
+    const float e0x = __shfl(ix, p * D), e0y = __shfl(iy, p * D);
+    const float e1x = __shfl(ix, p * D + D - 1), e1y = __shfl(iy, p * D + D - 1);
+    const bool xmaj = fabsf(e1x - e0x) >= fabsf(e1y - e0y);
+    const float M0 = xmaj ? e0x : e0y, m0 = xmaj ? e0y : e0x;
+    const float dM = xmaj ? e1x - e0x : e1y - e0y, dm = xmaj ? e1y - e0y : e1x - e0x;
+    const float b = dM != 0.f ? dm / dM : 0.f;  // |b| <= 1
+    const float Mlo = fminf(M0, M0 + dM);
+    const bool line_ok = Mlo == Mlo && b == b && m0 == m0 && fabsf(Mlo) < 1e6f && fabsf(m0) < 1e6f;
+    const int lo = line_ok ? (int)floorf(Mlo) - 1 : 0;
+    int s4[4];  // window slots of nw, ne, sw, se
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s4[k] = win_slot(x0 + (k & 1), y0 + (k >> 1), xmaj, lo, m0, M0, b, MX);
+    const bool bad = live && (!line_ok || (s4[0] | s4[1] | s4[2] | s4[3]) < 0);
+    const bool gather = ((__ballot(bad) >> (p * D)) & pix_mask) != 0ull;
+    const bool fast = live && !gather;
+    // 2. list the taps not in plane d-1's block (plane d-1 dead, gathered or another pixel: all four)
+    const unsigned me = fast ? (unsigned)(x0 + 2) | ((unsigned)(y0 + 2) << 16) : 0xFFFFFFFFu;
+    const unsigned prev = __shfl(me, lane - 1);
+    const bool chain = d > 0 && prev != 0xFFFFFFFFu;
+    const int xp = (int)(prev & 0xFFFFu) - 2, yp = (int)(prev >> 16) - 2;
+    unsigned nb = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int X = x0 + (k & 1), Y = y0 + (k >> 1);
+      const bool seen = chain && (unsigned)(X - xp) <= 1u && (unsigned)(Y - yp) <= 1u;
+      nb |= (fast && !seen) ? (1u << k) : 0u;
+    }
+    const int cnt = __builtin_popcount(nb);
+    const unsigned long long c0 = __ballot(cnt & 1), c1 = __ballot(cnt & 2), c2 = __ballot(cnt & 4);
+    const int total = __popcll(c0) + 2 * __popcll(c1) + 4 * __popcll(c2);
+    {
+      int o = __popcll(c0 & lanes_below) + 2 * __popcll(c1 & lanes_below) + 4 * __popcll(c2 & lanes_below);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (nb & (1u << k)) {
+          const int X = x0 + (k & 1), Y = y0 + (k >> 1);
+          const bool in = (unsigned)X < (unsigned)W && (unsigned)Y < (unsigned)H;
+          list[o] = make_uint2(in ? (unsigned)Y * rowb + (unsigned)X * (unsigned)(C * 4) : kOffOut,
+                               (unsigned)(p * WIN + s4[k]));
+          ++o;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // 3. load rounds: texel t = round·TPR + lane/LPT, channel quad q
+    const unsigned vq = vbase + 16u * (unsigned)q;
+    for (int t0 = 0; t0 < total; t0 += NB * TPR) {
+      floatx4 val[NB];
+      uint2 e[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int t = t0 + i * TPR + lane / LPT;
+        e[i] = list[min(t, 4 * 64 - 1)];
+        if (t >= total) e[i] = make_uint2(kOffOut, 0xFFFFFFFFu);
+        val[i] = buf_load_f32x4(rsrc, e[i].x + vq);  // out of range (kOffOut): no request, reads 0
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const unsigned sl = e[i].y;
+        float part = quad_dot(refq[(sl == 0xFFFFFFFFu ? 0u : sl / WIN) * LPT + q], val[i]);
+        if constexpr (LPT >= 2) part = part + lane_xor_f<1>(part);
+        if constexpr (LPT >= 4) part = part + lane_xor_f<2>(part);
+        if (q == 0 && sl != 0xFFFFFFFFu) win[sl] = part;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // 4. this lane's sample
+    float dt[4] = {0.f, 0.f, 0.f, 0.f};
+    if (fast) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dt[k] = win[p * WIN + s4[k]];
+    } else if (live) {  // gathered pixel: its 4 taps straight from memory, the same dot / quad-sum order
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int X = x0 + (k & 1), Y = y0 + (k >> 1);
+        const bool in = (unsigned)X < (unsigned)W && (unsigned)Y < (unsigned)H;
+        const unsigned off = in ? vbase + (unsigned)Y * rowb + (unsigned)X * (unsigned)(C * 4) : kOffOut;
+        float qs[LPT];
+#pragma unroll
+        for (int qq = 0; qq < LPT; ++qq) qs[qq] = quad_dot(refq[p * LPT + qq], buf_load_f32x4(rsrc, off + 16u * qq));
+        dt[k] = LPT == 2 ? qs[0] + qs[1] : (qs[0] + qs[1]) + (qs[LPT - 2] + qs[LPT - 1]);
+      }
+    }
+    const float ea = 1.f - fx, s = 1.f - fy;
+    const float sim = fmaf(dt[3], fy * fx, fmaf(dt[2], fy * ea, fmaf(dt[1], s * fx, dt[0] * (s * ea))));
+    acc = acc + (sim * (1.f / (float)C)) * w;
+    wsum = wsum + w;
+    __builtin_amdgcn_wave_barrier();  // the window and list are rewritten by the next view
+  }
+  if (!active) return;
+  sim_out[(size_t)d * HW + pix] = PARTIAL ? acc : acc / wsum;
+  if (PARTIAL && d == 0) wsum_out[pix] = wsum;
+}
+
 template <int C, int D, bool PW, bool PARTIAL>
 static int launch_warp(const float* ref, const float* src, const float* hyp, const float* vw_in, float* sim,
                        float* wsum, float* vw_out, int V, int H, int W, int vw_shift, int vw_offset, int vw_total,
                        const WarpArgs& args, hipStream_t st) {
+#ifndef TMVS_WARP_DOT
+#define TMVS_WARP_DOT 1
+#endif
+  if constexpr (TMVS_WARP_DOT && (C == 8 || C == 16) && !PW && 64 % D == 0) {
+    constexpr int PIXD = 4 * (64 / D);
+    const int nblk = (H * W + PIXD - 1) / PIXD;
+    hipLaunchKernelGGL((warp_dot_kernel<C, D, PARTIAL>), dim3(nblk), dim3(256), 0, st, ref, src, hyp, vw_in, sim,
+                       wsum, V, H, W, vw_shift, vw_offset, args);
+    TMVS_CHECK_LAUNCH();
+    return TMVS_OK;
+  }
   if constexpr ((C == 8 || C == 16) && !PW) {
     constexpr int PIXP = 4 * (64 / (C / 2));
     const int nblk = (H * W + PIXP - 1) / PIXP;
