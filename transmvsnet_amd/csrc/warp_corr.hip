@@ -104,6 +104,33 @@ __device__ __forceinline__ void project(const float rx, const float ry, const fl
   y0i = (int)fminf(fmaxf(y0, -2.f), 32766.f);
 }
 
+// project() that also returns the unnormalised sample position (ix, iy) before the floor, NaN when
+// the point is behind the camera (z < 1e-6); (x0, y0, fx, fy) are project()'s bits
+__device__ __forceinline__ void project_pos(const float rx, const float ry, const float rz, const float tx,
+                                            const float ty, const float tz, const float dep, const float halfw,
+                                            const float halfh, int& x0i, int& y0i, float& fx, float& fy, float& ixo,
+                                            float& iyo) {
+  const float X = rx * dep + tx;
+  const float Y = ry * dep + ty;
+  const float Z = rz * dep + tz;
+  float xn = (X / Z) / halfw - 1.f;
+  float yn = (Y / Z) / halfh - 1.f;
+  const bool behind = Z < 1e-6f;
+  if (behind) {
+    xn = -99.f;
+    yn = -99.f;
+  }
+  const float ix = (xn + 1.f) * halfw;
+  const float iy = (yn + 1.f) * halfh;
+  const float x0 = floorf(ix), y0 = floorf(iy);
+  fx = ix - x0;
+  fy = iy - y0;
+  x0i = (int)fminf(fmaxf(x0, -2.f), 32766.f);
+  y0i = (int)fminf(fmaxf(y0, -2.f), 32766.f);
+  ixo = behind ? __builtin_nanf("") : ix;
+  iyo = behind ? __builtin_nanf("") : iy;
+}
+
 // x from lane (lane ^ R) inside an aligned group of 8 (R compile-time)
 template <int R>
 __device__ __forceinline__ int lane_xor(int x) {
@@ -666,11 +693,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 // takes the channel mean), so similarities differ from the product form by a few ulps (5e-7 bar,
 // tests/test_gpu_parity.py).
 constexpr int kWinRows = 8;
+// LDS list entry: texel index y*W + x (kTexOut: outside the image) << kSlotBits | window slot
+constexpr int kSlotBits = 11;
+constexpr unsigned kTexOut = (1u << (32 - kSlotBits)) - 1u;
 
 template <int D>
 struct DotCfg {
   static constexpr int MX = D <= 8 ? 16 : D <= 16 ? 32 : D <= 32 ? 64 : 128;
 };
+
+// Cross-lane hand-offs through the wave's private LDS (list, window): the LDS executes one wave's
+// DS instructions in issue order, so a read issued after a write (by any lane of the wave) sees it;
+// only the compiler must not reorder them.
+__device__ __forceinline__ void lds_order() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 
 // window slot of texel (X, Y) for the pixel's line (xmaj, lo, m0, M0, b); -1 when outside the window
 __device__ __forceinline__ int win_slot(int X, int Y, bool xmaj, int lo, float m0, float M0, float b, int MX) {
@@ -689,6 +727,17 @@ __device__ __forceinline__ float quad_dot(const float4& r, const floatx4& s) {
   return fmaf(r.w, s[3], a);
 }
 
+// One lane's view of one plane (phase 1's output, consumed one pipeline step later)
+struct DotLane {
+  int x0, y0;
+  float fx, fy, w;
+  int s[4];  // slots of the taps nw, ne, sw, se
+  bool live;
+};
+
+#ifndef TMVS_DOT_NB
+#define TMVS_DOT_NB 6
+#endif
 template <int C, int D, bool PARTIAL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void warp_dot_kernel(
     const float* __restrict__ ref, const float* __restrict__ src, const float* __restrict__ hyp,
@@ -699,10 +748,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   constexpr int TPR = 64 / LPT;           // texels per load round
   constexpr int MX = DotCfg<D>::MX;
   constexpr int WIN = MX * kWinRows;      // window floats per pixel
-  constexpr int NB = 2;                   // load rounds in flight
+  constexpr int NWIN = NPW * WIN;         // window slots of the wave; then 256 direct slots (lane*4 + tap)
+  constexpr int NB = TMVS_DOT_NB;         // load rounds issued one view ahead
   static_assert(64 % D == 0 && (C == 8 || C == 16), "warp_dot_kernel: D divides 64, C in {8, 16}");
-  __shared__ float win_lds[4][NPW * WIN];
-  __shared__ uint2 list_lds[4][4 * 64];
+  static_assert(NWIN + 256 <= (1 << kSlotBits), "slots must fit the list entry");
+  __shared__ float slot_lds[4][NWIN + 256];
+  __shared__ unsigned list_lds[4][2][256];
   __shared__ float4 ref_lds[4][NPW * LPT];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int p = lane / D, d = lane % D;
@@ -714,8 +765,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   int pix = wbase + p;
   const bool active = pix < HW;
   if (!active) pix = HW - 1;
-  float* win = win_lds[wave];
-  uint2* list = list_lds[wave];
+  float* slot = slot_lds[wave];
   const float4* refq = ref_lds[wave];
   if (lane < NPW * LPT) {
     const int pp = min(wbase + lane / LPT, HW - 1);
@@ -728,123 +778,156 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const float halfh = (float)(H - 1) / 2.f;
   const int Ws = W >> vw_shift, Hs = H >> vw_shift;
   const float* wv = vw_in + (size_t)vw_offset * Hs * Ws + (py >> vw_shift) * Ws + (px >> vw_shift);
-  float acc = 0.f;
-  float wsum = PARTIAL ? 0.f : 1e-5f;
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, V * HW * C * 4, kRsrcWord3);
   const unsigned rowb = (unsigned)W * C * 4;
   const unsigned long long lanes_below = (1ull << lane) - 1ull;
   const unsigned long long pix_mask = D == 64 ? ~0ull : ((1ull << D) - 1ull);
-  for (int v = 0; v < V; ++v) {
-    const float* R = args.proj[v];
-    const float rx = rot_row(R, fxp, fyp, args.rot_plain);
-    const float ry = rot_row(R + 4, fxp, fyp, args.rot_plain);
-    const float rz = rot_row(R + 8, fxp, fyp, args.rot_plain);
-    const float w = wv[(size_t)v * Hs * Ws];
-    const unsigned vbase = (unsigned)(v * HW * C * 4);
-    // 1. this lane's plane, and the pixel's segment line from its end samples
-    int x0, y0;
-    float fx, fy;
-    project(rx, ry, rz, R[3], R[7], R[11], dep, halfw, halfh, x0, y0, fx, fy);
-    float ix, iy;  // unclamped sample position; NaN behind the camera (the pixel is then gathered)
-    {
-      const float Z = rz * dep + R[11];  // (x/z normalised and unnormalised again = x/z, up to rounding)
-      ix = Z < 1e-6f ? __builtin_nanf("") : (rx * dep + R[3]) / Z;
-      iy = Z < 1e-6f ? __builtin_nanf("") : (ry * dep + R[7]) / Z;
-    }
-    const bool live = x0 >= -1 && x0 < W && y0 >= -1 && y0 < H;
+  const int rot_plain = args.rot_plain;
+
+  // phase 1 (view v): project, window slots, list the new texels -> number listed (wave-uniform)
+  auto geometry = [&](int v, DotLane& L) -> int {
+    float R[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) R[k] = args.proj[v][k];
+    const float rx = rot_row(R, fxp, fyp, rot_plain);
+    const float ry = rot_row(R + 4, fxp, fyp, rot_plain);
+    const float rz = rot_row(R + 8, fxp, fyp, rot_plain);
+    L.w = wv[(size_t)v * Hs * Ws];
+    float ix, iy;
+    project_pos(rx, ry, rz, R[3], R[7], R[11], dep, halfw, halfh, L.x0, L.y0, L.fx, L.fy, ix, iy);
+    const int x0 = L.x0, y0 = L.y0;
+    const bool inx0 = (unsigned)x0 < (unsigned)W, inx1 = (unsigned)(x0 + 1) < (unsigned)W;
+    const bool iny0 = (unsigned)y0 < (unsigned)H, iny1 = (unsigned)(y0 + 1) < (unsigned)H;
+    L.live = (inx0 || inx1) && (iny0 || iny1);
     const float e0x = __shfl(ix, p * D), e0y = __shfl(iy, p * D);
     const float e1x = __shfl(ix, p * D + D - 1), e1y = __shfl(iy, p * D + D - 1);
     const bool xmaj = fabsf(e1x - e0x) >= fabsf(e1y - e0y);
     const float M0 = xmaj ? e0x : e0y, m0 = xmaj ? e0y : e0x;
     const float dM = xmaj ? e1x - e0x : e1y - e0y, dm = xmaj ? e1y - e0y : e1x - e0x;
-    const float b = dM != 0.f ? dm / dM : 0.f;  // |b| <= 1
+    const float b = dM != 0.f ? dm * __builtin_amdgcn_rcpf(dM) : 0.f;  // |b| <= 1 (up to the rcp's ulp)
     const float Mlo = fminf(M0, M0 + dM);
     const bool line_ok = Mlo == Mlo && b == b && m0 == m0 && fabsf(Mlo) < 1e6f && fabsf(m0) < 1e6f;
     const int lo = line_ok ? (int)floorf(Mlo) - 1 : 0;
-    int s4[4];  // window slots of nw, ne, sw, se
-#pragma unroll
-    for (int k = 0; k < 4; ++k) s4[k] = win_slot(x0 + (k & 1), y0 + (k >> 1), xmaj, lo, m0, M0, b, MX);
-    const bool bad = live && (!line_ok || (s4[0] | s4[1] | s4[2] | s4[3]) < 0);
-    const bool gather = ((__ballot(bad) >> (p * D)) & pix_mask) != 0ull;
-    const bool fast = live && !gather;
-    // 2. list the taps not in plane d-1's block (plane d-1 dead, gathered or another pixel: all four)
-    const unsigned me = fast ? (unsigned)(x0 + 2) | ((unsigned)(y0 + 2) << 16) : 0xFFFFFFFFu;
-    const unsigned prev = __shfl(me, lane - 1);
-    const bool chain = d > 0 && prev != 0xFFFFFFFFu;
-    const int xp = (int)(prev & 0xFFFFu) - 2, yp = (int)(prev >> 16) - 2;
-    unsigned nb = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int X = x0 + (k & 1), Y = y0 + (k >> 1);
-      const bool seen = chain && (unsigned)(X - xp) <= 1u && (unsigned)(Y - yp) <= 1u;
-      nb |= (fast && !seen) ? (1u << k) : 0u;
+    // the block's 2 major-axis lines (x-major: columns x0, x0+1; else rows y0, y0+1), each holding 2
+    // consecutive window rows: slot(major i, minor j) = (u + i)·kWinRows + v_i + j
+    const int Mb = xmaj ? x0 : y0, mb = xmaj ? y0 : x0;
+    const int u = Mb - lo;
+    const int v0 = mb - (int)floorf(m0 + b * ((float)Mb - M0)) + 3;
+    const int v1 = mb - (int)floorf(m0 + b * ((float)(Mb + 1) - M0)) + 3;
+    const bool fits = line_ok && (unsigned)u < (unsigned)(MX - 1) && (unsigned)v0 < (unsigned)(kWinRows - 1) &&
+                      (unsigned)v1 < (unsigned)(kWinRows - 1);
+    const bool direct = ((__ballot(L.live && !fits) >> (p * D)) & pix_mask) != 0ull;
+    {
+      const int w0 = p * WIN + u * kWinRows + v0, w1 = p * WIN + (u + 1) * kWinRows + v1;
+      const int dbase = NWIN + 4 * lane;
+      // taps nw (x0,y0), ne (x0+1,y0), sw (x0,y0+1), se (x0+1,y0+1)
+      L.s[0] = direct ? dbase : w0;
+      L.s[1] = direct ? dbase + 1 : (xmaj ? w1 : w0 + 1);
+      L.s[2] = direct ? dbase + 2 : (xmaj ? w0 + 1 : w1);
+      L.s[3] = direct ? dbase + 3 : w1 + 1;
     }
+    // the taps not in plane d-1's block (window pixels); every tap of a direct pixel's plane
+    const bool chainable = L.live && !direct;
+    const unsigned me = chainable ? (unsigned)(x0 + 2) | ((unsigned)(y0 + 2) << 16) : 0xFFFFFFFFu;
+    const unsigned prev = __shfl(me, lane - 1);
+    const bool chain = chainable && d > 0 && prev != 0xFFFFFFFFu;
+    const int ddx = x0 - ((int)(prev & 0xFFFFu) - 2), ddy = y0 - ((int)(prev >> 16) - 2);
+    const bool c0s = chain && (unsigned)ddx <= 1u, c1s = chain && (unsigned)(ddx + 1) <= 1u;  // column x0 / x0+1 seen
+    const bool r0s = (unsigned)ddy <= 1u, r1s = (unsigned)(ddy + 1) <= 1u;                   // row y0 / y0+1 seen
+    unsigned nb = 0;
+    nb |= (L.live && !(c0s && r0s)) ? 1u : 0u;
+    nb |= (L.live && !(c1s && r0s)) ? 2u : 0u;
+    nb |= (L.live && !(c0s && r1s)) ? 4u : 0u;
+    nb |= (L.live && !(c1s && r1s)) ? 8u : 0u;
     const int cnt = __builtin_popcount(nb);
     const unsigned long long c0 = __ballot(cnt & 1), c1 = __ballot(cnt & 2), c2 = __ballot(cnt & 4);
-    const int total = __popcll(c0) + 2 * __popcll(c1) + 4 * __popcll(c2);
-    {
-      int o = __popcll(c0 & lanes_below) + 2 * __popcll(c1 & lanes_below) + 4 * __popcll(c2 & lanes_below);
+    unsigned* list = list_lds[wave][v & 1];
+    int o = __popcll(c0 & lanes_below) + 2 * __popcll(c1 & lanes_below) + 4 * __popcll(c2 & lanes_below);
+    const unsigned tb = (unsigned)(y0 * W + x0);
+    const bool in4[4] = {inx0 && iny0, inx1 && iny0, inx0 && iny1, inx1 && iny1};
+    const unsigned to4[4] = {0u, 1u, (unsigned)W, (unsigned)W + 1u};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (nb & (1u << k)) {
-          const int X = x0 + (k & 1), Y = y0 + (k >> 1);
-          const bool in = (unsigned)X < (unsigned)W && (unsigned)Y < (unsigned)H;
-          list[o] = make_uint2(in ? (unsigned)Y * rowb + (unsigned)X * (unsigned)(C * 4) : kOffOut,
-                               (unsigned)(p * WIN + s4[k]));
-          ++o;
-        }
+    for (int k = 0; k < 4; ++k) {
+      if (nb & (1u << k)) {
+        list[o] = ((in4[k] ? tb + to4[k] : kTexOut) << kSlotBits) | (unsigned)L.s[k];
+        ++o;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // 3. load rounds: texel t = round·TPR + lane/LPT, channel quad q
-    const unsigned vq = vbase + 16u * (unsigned)q;
-    for (int t0 = 0; t0 < total; t0 += NB * TPR) {
-      floatx4 val[NB];
-      uint2 e[NB];
+    return __popcll(c0) + 2 * __popcll(c1) + 4 * __popcll(c2);
+  };
+  // phase 2 (view v): the first NB load rounds (texel t = round·TPR + lane/LPT, channel quad q)
+  auto issue = [&](int v, int total, unsigned (&e)[NB], floatx4 (&val)[NB]) {
+    const unsigned* list = list_lds[wave][v & 1];
+    const unsigned vq = (unsigned)(v * HW * C * 4) + 16u * (unsigned)q;
 #pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const int t = t0 + i * TPR + lane / LPT;
-        e[i] = list[min(t, 4 * 64 - 1)];
-        if (t >= total) e[i] = make_uint2(kOffOut, 0xFFFFFFFFu);
-        val[i] = buf_load_f32x4(rsrc, e[i].x + vq);  // out of range (kOffOut): no request, reads 0
-      }
-#pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const unsigned sl = e[i].y;
-        float part = quad_dot(refq[(sl == 0xFFFFFFFFu ? 0u : sl / WIN) * LPT + q], val[i]);
-        if constexpr (LPT >= 2) part = part + lane_xor_f<1>(part);
-        if constexpr (LPT >= 4) part = part + lane_xor_f<2>(part);
-        if (q == 0 && sl != 0xFFFFFFFFu) win[sl] = part;
-      }
+    for (int i = 0; i < NB; ++i) {
+      const int t = i * TPR + lane / LPT;
+      const unsigned ent = list[t];
+      e[i] = t < total ? ent : 0xFFFFFFFFu;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // 4. this lane's sample
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const unsigned tex = e[i] >> kSlotBits;
+      val[i] = buf_load_f32x4(rsrc, tex >= kTexOut ? kOffOut : tex * (unsigned)(C * 4) + vq);  // kOffOut: reads 0
+    }
+  };
+  // dot of a loaded texel quad with its pixel's reference quad, quad sum, into its slot
+  auto deposit = [&](unsigned ent, const float4& r, const floatx4& val) {
+    float part = quad_dot(r, val);
+    if constexpr (LPT >= 2) part = part + lane_xor_f<1>(part);
+    if constexpr (LPT >= 4) part = part + lane_xor_f<2>(part);
+    if (q == 0 && ent != 0xFFFFFFFFu) slot[ent & ((1u << kSlotBits) - 1u)] = part;
+  };
+  auto ref_of = [&](unsigned ent) -> float4 {
+    const unsigned sl = ent & ((1u << kSlotBits) - 1u);
+    const unsigned pp = sl < (unsigned)NWIN ? sl / WIN : ((sl - NWIN) >> 2) / D;
+    return refq[(pp % NPW) * LPT + q];
+  };
+
+  float acc = 0.f;
+  float wsum = PARTIAL ? 0.f : 1e-5f;
+  DotLane cur, nxt;
+  int tot_cur = geometry(0, cur), tot_nxt = 0;
+  lds_order();
+  unsigned e[NB];
+  floatx4 val[NB];
+  issue(0, tot_cur, e, val);
+  for (int v = 0; v < V; ++v) {
+    if (v + 1 < V) tot_nxt = geometry(v + 1, nxt);  // while view v's loads are in flight
+    float4 rr[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) rr[i] = ref_of(e[i]);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) deposit(e[i], rr[i], val[i]);
+    // rounds past NB (long segments, many direct pixels): not pipelined
+    const unsigned* list = list_lds[wave][v & 1];
+    const unsigned vq = (unsigned)(v * HW * C * 4) + 16u * (unsigned)q;
+    for (int t0 = NB * TPR; t0 < tot_cur; t0 += TPR) {
+      const int t = t0 + lane / LPT;
+      const unsigned ent = t < tot_cur ? list[t] : 0xFFFFFFFFu;
+      const unsigned tex = ent >> kSlotBits;
+      const floatx4 x = buf_load_f32x4(rsrc, tex >= kTexOut ? kOffOut : tex * (unsigned)(C * 4) + vq);
+      deposit(ent, ref_of(ent), x);
+    }
+    lds_order();
+    // this lane's sample: sim = fma chain over the taps in grid_sample's order, / C
     float dt[4] = {0.f, 0.f, 0.f, 0.f};
-    if (fast) {
+    if (cur.live) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) dt[k] = win[p * WIN + s4[k]];
-    } else if (live) {  // gathered pixel: its 4 taps straight from memory, the same dot / quad-sum order
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int X = x0 + (k & 1), Y = y0 + (k >> 1);
-        const bool in = (unsigned)X < (unsigned)W && (unsigned)Y < (unsigned)H;
-        const unsigned off = in ? vbase + (unsigned)Y * rowb + (unsigned)X * (unsigned)(C * 4) : kOffOut;
-        float qs[LPT];
-#pragma unroll
-        for (int qq = 0; qq < LPT; ++qq) qs[qq] = quad_dot(refq[p * LPT + qq], buf_load_f32x4(rsrc, off + 16u * qq));
-        dt[k] = LPT == 2 ? qs[0] + qs[1] : (qs[0] + qs[1]) + (qs[LPT - 2] + qs[LPT - 1]);
-      }
+      for (int k = 0; k < 4; ++k) dt[k] = slot[cur.s[k]];
     }
-    const float ea = 1.f - fx, s = 1.f - fy;
-    const float sim = fmaf(dt[3], fy * fx, fmaf(dt[2], fy * ea, fmaf(dt[1], s * fx, dt[0] * (s * ea))));
-    acc = acc + (sim * (1.f / (float)C)) * w;
-    wsum = wsum + w;
-    __builtin_amdgcn_wave_barrier();  // the window and list are rewritten by the next view
+    const float ea = 1.f - cur.fx, sy = 1.f - cur.fy;
+    const float sim =
+        fmaf(dt[3], cur.fy * cur.fx, fmaf(dt[2], cur.fy * ea, fmaf(dt[1], sy * cur.fx, dt[0] * (sy * ea))));
+    acc = acc + (sim * (1.f / (float)C)) * cur.w;
+    wsum = wsum + cur.w;
+    lds_order();  // the slots are rewritten by the next view
+    if (v + 1 < V) {
+      cur = nxt;
+      tot_cur = tot_nxt;
+      issue(v + 1, tot_cur, e, val);
+    }
   }
   if (!active) return;
   sim_out[(size_t)d * HW + pix] = PARTIAL ? acc : acc / wsum;
@@ -858,7 +941,8 @@ static int launch_warp(const float* ref, const float* src, const float* hyp, con
 #ifndef TMVS_WARP_DOT
 #define TMVS_WARP_DOT 1
 #endif
-  if constexpr (TMVS_WARP_DOT && (C == 8 || C == 16) && !PW && 64 % D == 0) {
+  // warp_dot_kernel's list entries hold a texel index below kTexOut (= 2^21 - 1)
+  if constexpr (TMVS_WARP_DOT && (C == 8 || C == 16) && !PW && 64 % D == 0) if ((long long)H * W < (long long)kTexOut) {
     constexpr int PIXD = 4 * (64 / D);
     const int nblk = (H * W + PIXD - 1) / PIXD;
     hipLaunchKernelGGL((warp_dot_kernel<C, D, PARTIAL>), dim3(nblk), dim3(256), 0, st, ref, src, hyp, vw_in, sim,
