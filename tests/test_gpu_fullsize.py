@@ -88,7 +88,12 @@ def _classify(depth_gpu, ref_stage, allowed=frozenset(), explained=None):
     diff = np.abs(g - r) > 1e-3
     casc = np.zeros_like(diff) if explained is None else np.broadcast_to(explained, diff.shape)
     other = [(int(y), int(x)) for _, y, x in np.argwhere(diff & ~near & ~casc)]
-    return {"mean_abs_mm": float(np.abs(g - r).mean()), "differing": int(diff.sum()),
+    absd = np.abs(g - r)
+    outside = ~casc
+    return {"mean_abs_mm": float(absd.mean()), "differing": int(diff.sum()),
+            "differing_pixels": [(int(y), int(x)) for _, y, x in np.argwhere(diff)[:64]],
+            "footprint_pixels": int(casc[0].sum()),
+            "mean_abs_mm_outside_footprint": float(absd[outside].mean()) if outside.any() else 0.0,
             "near_tie_flips": int((diff & near).sum()), "cascade_explained": int((diff & ~near & casc).sum()),
             "other_flips": len(other), "max_flip_margin": float(marg[diff].max()) if diff.any() else 0.0,
             "unexplained": [p for p in other if p not in allowed], "exact_arithmetic_picks": [p for p in other if p in allowed],

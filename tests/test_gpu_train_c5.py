@@ -1,0 +1,148 @@
+"""C5 at full size on one GPU: BlendedMVS 768x576, N=4, 48/32/8 -- finetune.py:144-170's train_sample
+body on the drop-in model, with bench.py's C5 inputs (bench._train_setup: key-seeded weights with
+logit sharpening, synthetic images / cameras, random ground truth). Needs an MI355X (-m gpu).
+
+    model.train(); optimizer.zero_grad(); outputs = model(imgs, proj, dv)
+    loss = focal_loss_bld(outputs, depth_gt_ms, mask_ms, interval, dlossw=[1, 1, 1])[0]
+    loss.backward(); optimizer.step()
+
+Checked (the 8-GPU DDP part of C5 is covered by tests/test_gpu_distributed.py and the gloo tests):
+  * every loss term and all parameter gradients finite; a parameter's gradient is zero only where it
+    is zero in exact arithmetic (conv biases feeding a train-mode BatchNorm: the batch mean removes
+    them) or where nothing reaches it;
+  * against the fp32 oracle run from the same FeatureNet outputs (oracle.forward_from_features in
+    train mode + oracle/loss_ref.focal_loss_bld: the reference's op sequence on the CPU; FeatureNet's
+    own forward/backward is judged by test_gpu_featurenet.py / test_gpu_train_ref.py):
+      - loss terms within 1e-4 relative (a near-tie argmax flip moves EPE / less1 / less3 by a pixel);
+      - WTA depth of every stage identical outside the 1e-4 near-tie margin;
+      - the gradients of the three prob convs (cost_regularization.{s}.prob.weight: d loss / d logits
+        through softmax and the loss, contracted with conv11's output) within 2e-3 of their max;
+      - the running statistics of PixelwiseNet and the three CostRegNets within 1e-4 of the oracle's;
+  * a HIP-graph replay of the step (train.TrainStepGraph) leaves parameters, Adam moments and the
+    running statistics within 1e-5 of eager steps (as tests/test_gpu_train_ref.py at C1).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+H5, W5, N5 = 576, 768, 4
+
+
+def _setup():
+    import bench
+    full_step, _, m = bench._train_setup(torch.device(DEV, 0))
+    return full_step, m
+
+
+def test_c5_train_sample_full_size_vs_oracle():
+    from oracle import loss_ref
+    from oracle import transmvs_ref as oracle
+    from transmvsnet_amd import loss as hip_loss
+    from transmvsnet_amd import synthetic
+    from transmvsnet_amd.featurenet_train import featurenet_train
+    from transmvsnet_amd.train import FlatAdam
+    from transmvsnet_amd import TransMVSNet
+    model = TransMVSNet()
+    sd0 = synthetic.synthetic_state_dict(synthetic.state_dict_shapes(model), seed=0, sharpen=100.0)
+    model.load_state_dict(sd0)
+    model = model.to(DEV)
+    imgs = synthetic.synthetic_images(N5, H5, W5, seed=8).to(DEV)
+    proj = synthetic.synthetic_cameras(N5, H5, W5, seed=6)
+    dv = synthetic.synthetic_depth_values(1)
+    g = torch.Generator().manual_seed(7)
+    gt = {f"stage{s + 1}": 425.0 + 500.0 * torch.rand(1, H5 >> (2 - s), W5 >> (2 - s), generator=g) for s in range(3)}
+    mask = {k: torch.ones_like(v) for k, v in gt.items()}
+    interval = torch.tensor([float(dv[0, 1] - dv[0, 0])])
+    # the FeatureNet outputs the GPU step sees (same weights, same kernels; its own BN statistics)
+    fnet = TransMVSNet()
+    fnet.load_state_dict(sd0)
+    fnet = fnet.to(DEV)
+    fnet.train()
+    with torch.no_grad():
+        f1, f2, f3 = featurenet_train(fnet.feature, imgs)
+    feats = [{"stage1": f1[i:i + 1].cpu(), "stage2": f2[i:i + 1].cpu(), "stage3": f3[i:i + 1].cpu()} for i in range(N5)]
+    del fnet
+    # the GPU step
+    opt = FlatAdam(list(model.parameters()), lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4)
+    model.train()
+    opt.zero_grad()
+    outputs = model(imgs, proj, dv.to(DEV))
+    terms = hip_loss.focal_loss_bld(outputs, {k: v.to(DEV) for k, v in gt.items()},
+                                    {k: v.to(DEV) for k, v in mask.items()}, interval, dlossw=[1.0, 1.0, 1.0])
+    terms[0].backward()
+    torch.cuda.synchronize()
+    grads = {n: p.grad.detach().cpu().numpy() for n, p in model.named_parameters() if p.grad is not None}
+    gpu_terms = [float(t) for t in terms]
+    assert all(np.isfinite(gpu_terms)), gpu_terms
+    bad = [n for n, v in grads.items() if not np.isfinite(v).all()]
+    assert not bad, bad[:8]
+    names = [n for n, _ in model.named_parameters()]
+    zero = [n for n in names if n not in grads or not np.any(grads[n])]
+    # exactly zero in exact arithmetic: a conv bias followed by a train-mode BatchNorm; the DCN offset/mask
+    # conv's weight and bias are zero-initialised (models/dcn.py:62-64) but do receive gradients
+    allowed_zero = {n for n in zero if n.endswith(".bias") and "conv_offset_mask" not in n}
+    assert set(zero) <= allowed_zero, sorted(set(zero) - allowed_zero)[:8]
+    # the fp32 oracle from the same features: forward, loss, prob-conv gradients, running statistics
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    sd = {k: v.clone() for k, v in sd0.items()}
+    probw = [f"cost_regularization.{s}.prob.weight" for s in range(3)]
+    for k in probw:
+        sd[k].requires_grad_(True)
+    out_ref = oracle.forward_from_features(sd, feats, proj, dv, (H5, W5), training=True)
+    res = loss_ref.focal_loss_bld(out_ref, gt, mask, interval, dlossw=[1.0, 1.0, 1.0])
+    res[0].backward()
+    ref_terms = [float(t) for t in res]
+    rep = {"loss_terms_gpu": gpu_terms, "loss_terms_ref": ref_terms}
+    for gv, rv, name in zip(gpu_terms, ref_terms, ("loss", "depth_loss", "epe", "less1", "less3")):
+        assert abs(gv - rv) <= 1e-4 * max(abs(rv), 1.0), (name, gv, rv)
+    for s in (1, 2, 3):
+        prob = out_ref[f"stage{s}"]["prob_volume"].detach().numpy().astype(np.float64)
+        srt = np.sort(prob, axis=1)
+        near = (np.log(np.maximum(srt[:, -1], 1e-30)) - np.log(np.maximum(srt[:, -2], 1e-30))) < 1e-4
+        diff = np.abs(outputs[f"stage{s}"]["depth"].detach().cpu().numpy().astype(np.float64)
+                      - out_ref[f"stage{s}"]["depth"].detach().numpy()) > 1e-3
+        rep[f"stage{s}_flips"] = (int(diff.sum()), int((diff & ~near).sum()))
+        assert not (diff & ~near).any(), (s, rep)
+    for k in probw:
+        ref = sd[k].grad.numpy().astype(np.float64)
+        err = float(np.abs(grads[k] - ref).max() / np.abs(ref).max())
+        rep[k] = err
+        assert err <= 2e-3, (k, err)
+    bufs = dict(model.named_buffers())
+    worst = 0.0
+    for k, v in sd.items():
+        if k.startswith(("cost_regularization.", "DepthNet.")) and k.endswith(("running_mean", "running_var")):
+            worst = max(worst, float(np.abs(bufs[k].cpu().numpy() - v.numpy()).max()))
+    rep["running_stats"] = worst
+    print("C5 full size vs fp32 oracle:", rep)
+    assert worst <= 1e-4, rep
+
+
+def test_c5_train_step_graph_replay_equals_eager():
+    """Two eager steps vs one eager step + a captured step replayed once (train.TrainStepGraph, as
+    bench.py times it), at full C5 size."""
+    from transmvsnet_amd import train as tr
+    runs = []
+    for graphed in (False, True):
+        step, m = _setup()
+        step()  # warm-up / first step: fills the lazily built index caches (capture needs them)
+        torch.cuda.synchronize()
+        if graphed:
+            g = tr.TrainStepGraph(step, m)
+            g.replay()
+            torch.cuda.synchronize()
+            g.check_flags()
+        else:
+            step()
+        torch.cuda.synchronize()
+        params = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+        bufs = {n: b.detach().clone() for n, b in m.named_buffers() if "running" in n}
+        runs.append((params, bufs))
+    (pa, ba), (pb, bb) = runs
+    err = float((pa - pb).abs().max() / pa.abs().max())
+    assert err < 1e-5, err
+    for n in ba:
+        e = float((ba[n] - bb[n]).abs().max() / max(float(ba[n].abs().max()), 1e-30))
+        assert e < 1e-5, (n, e)

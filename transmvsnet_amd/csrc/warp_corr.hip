@@ -699,7 +699,7 @@ constexpr unsigned kTexOut = (1u << (32 - kSlotBits)) - 1u;
 
 template <int D>
 struct DotCfg {
-  static constexpr int MX = D <= 8 ? 16 : D <= 16 ? 32 : D <= 32 ? 64 : 128;
+  static constexpr int MX = D <= 8 ? 16 : D <= 16 ? 32 : D <= 32 ? 48 : 96;
 };
 
 // Cross-lane hand-offs through the wave's private LDS (list, window): the LDS executes one wave's
@@ -738,8 +738,17 @@ struct DotLane {
 #ifndef TMVS_DOT_NB
 #define TMVS_DOT_NB 6
 #endif
+#ifndef TMVS_DOT_PIPE
+#define TMVS_DOT_PIPE 0
+#endif
+#ifndef TMVS_DOT_NBL
+#define TMVS_DOT_NBL 4
+#endif
+#ifndef TMVS_DOT_WAVES
+#define TMVS_DOT_WAVES 6
+#endif
 template <int C, int D, bool PARTIAL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void warp_dot_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_DOT_WAVES, TMVS_DOT_WAVES))) void warp_dot_kernel(
     const float* __restrict__ ref, const float* __restrict__ src, const float* __restrict__ hyp,
     const float* __restrict__ vw_in, float* __restrict__ sim_out, float* __restrict__ wsum_out, int V, int H, int W,
     int vw_shift, int vw_offset, WarpArgs args) {
@@ -749,11 +758,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   constexpr int MX = DotCfg<D>::MX;
   constexpr int WIN = MX * kWinRows;      // window floats per pixel
   constexpr int NWIN = NPW * WIN;         // window slots of the wave; then 256 direct slots (lane*4 + tap)
-  constexpr int NB = TMVS_DOT_NB;         // load rounds issued one view ahead
+  constexpr int NB = TMVS_DOT_NB;         // load rounds issued one view ahead (TMVS_DOT_PIPE)
+  constexpr int NBL = TMVS_DOT_NBL;       // load rounds in flight otherwise
   static_assert(64 % D == 0 && (C == 8 || C == 16), "warp_dot_kernel: D divides 64, C in {8, 16}");
   static_assert(NWIN + 256 <= (1 << kSlotBits), "slots must fit the list entry");
   __shared__ float slot_lds[4][NWIN + 256];
-  __shared__ unsigned list_lds[4][2][256];
+  __shared__ unsigned list_lds[4][TMVS_DOT_PIPE ? 2 : 1][256];
   __shared__ float4 ref_lds[4][NPW * LPT];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int p = lane / D, d = lane % D;
@@ -780,7 +790,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const float* wv = vw_in + (size_t)vw_offset * Hs * Ws + (py >> vw_shift) * Ws + (px >> vw_shift);
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, V * HW * C * 4, kRsrcWord3);
-  const unsigned rowb = (unsigned)W * C * 4;
   const unsigned long long lanes_below = (1ull << lane) - 1ull;
   const unsigned long long pix_mask = D == 64 ? ~0ull : ((1ull << D) - 1ull);
   const int rot_plain = args.rot_plain;
@@ -842,7 +851,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     nb |= (L.live && !(c1s && r1s)) ? 8u : 0u;
     const int cnt = __builtin_popcount(nb);
     const unsigned long long c0 = __ballot(cnt & 1), c1 = __ballot(cnt & 2), c2 = __ballot(cnt & 4);
-    unsigned* list = list_lds[wave][v & 1];
+    unsigned* list = list_lds[wave][TMVS_DOT_PIPE ? v & 1 : 0];
     int o = __popcll(c0 & lanes_below) + 2 * __popcll(c1 & lanes_below) + 4 * __popcll(c2 & lanes_below);
     const unsigned tb = (unsigned)(y0 * W + x0);
     const bool in4[4] = {inx0 && iny0, inx1 && iny0, inx0 && iny1, inx1 && iny1};
@@ -857,8 +866,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     return __popcll(c0) + 2 * __popcll(c1) + 4 * __popcll(c2);
   };
   // phase 2 (view v): the first NB load rounds (texel t = round·TPR + lane/LPT, channel quad q)
-  auto issue = [&](int v, int total, unsigned (&e)[NB], floatx4 (&val)[NB]) {
-    const unsigned* list = list_lds[wave][v & 1];
+  [[maybe_unused]] auto issue = [&](int v, int total, unsigned (&e)[NB], floatx4 (&val)[NB]) {
+    const unsigned* list = list_lds[wave][TMVS_DOT_PIPE ? v & 1 : 0];
     const unsigned vq = (unsigned)(v * HW * C * 4) + 16u * (unsigned)q;
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
@@ -887,28 +896,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 
   float acc = 0.f;
   float wsum = PARTIAL ? 0.f : 1e-5f;
+#if TMVS_DOT_PIPE
   DotLane cur, nxt;
   int tot_cur = geometry(0, cur), tot_nxt = 0;
   lds_order();
   unsigned e[NB];
   floatx4 val[NB];
   issue(0, tot_cur, e, val);
+#endif
   for (int v = 0; v < V; ++v) {
+#if TMVS_DOT_PIPE
     if (v + 1 < V) tot_nxt = geometry(v + 1, nxt);  // while view v's loads are in flight
     float4 rr[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) rr[i] = ref_of(e[i]);
 #pragma unroll
     for (int i = 0; i < NB; ++i) deposit(e[i], rr[i], val[i]);
-    // rounds past NB (long segments, many direct pixels): not pipelined
-    const unsigned* list = list_lds[wave][v & 1];
+    const int t_rest = NB * TPR;
+#else
+    DotLane cur;
+    const int tot_cur = geometry(v, cur);
+    lds_order();
+    const int t_rest = 0;
+#endif
+    // load rounds not issued ahead (all of them without the pipeline)
+    const unsigned* list = list_lds[wave][TMVS_DOT_PIPE ? v & 1 : 0];
     const unsigned vq = (unsigned)(v * HW * C * 4) + 16u * (unsigned)q;
-    for (int t0 = NB * TPR; t0 < tot_cur; t0 += TPR) {
-      const int t = t0 + lane / LPT;
-      const unsigned ent = t < tot_cur ? list[t] : 0xFFFFFFFFu;
-      const unsigned tex = ent >> kSlotBits;
-      const floatx4 x = buf_load_f32x4(rsrc, tex >= kTexOut ? kOffOut : tex * (unsigned)(C * 4) + vq);
-      deposit(ent, ref_of(ent), x);
+    for (int t0 = t_rest; t0 < tot_cur; t0 += NBL * TPR) {
+      unsigned el[NBL];
+      floatx4 xl[NBL];
+#pragma unroll
+      for (int i = 0; i < NBL; ++i) {
+        const int t = t0 + i * TPR + lane / LPT;
+        const unsigned ent = list[min(t, 255)];
+        el[i] = t < tot_cur ? ent : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int i = 0; i < NBL; ++i) {
+        const unsigned tex = el[i] >> kSlotBits;
+        xl[i] = buf_load_f32x4(rsrc, tex >= kTexOut ? kOffOut : tex * (unsigned)(C * 4) + vq);
+      }
+#pragma unroll
+      for (int i = 0; i < NBL; ++i) deposit(el[i], ref_of(el[i]), xl[i]);
     }
     lds_order();
     // this lane's sample: sim = fma chain over the taps in grid_sample's order, / C
@@ -923,11 +952,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     acc = acc + (sim * (1.f / (float)C)) * cur.w;
     wsum = wsum + cur.w;
     lds_order();  // the slots are rewritten by the next view
+#if TMVS_DOT_PIPE
     if (v + 1 < V) {
       cur = nxt;
       tot_cur = tot_nxt;
       issue(v + 1, tot_cur, e, val);
     }
+#endif
   }
   if (!active) return;
   sim_out[(size_t)d * HW + pix] = PARTIAL ? acc : acc / wsum;
