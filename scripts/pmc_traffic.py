@@ -16,7 +16,7 @@ import sys
 from collections import defaultdict
 
 ENTRY_KERNELS = {
-    "tmvs_warp_corr": ("warp_corr_kernel", "warp_pair_kernel"),
+    "tmvs_warp_corr": ("warp_corr_kernel", "warp_pair_kernel", "warp_dot_kernel"),
     "tmvs_costregnet": ("conv0_kernel", "conv3d_lds_kernel", "conv3d_direct_kernel", "conv3d_s2c8_tile_kernel",
                         "conv3d_c16_kernel", "deconv3d_lds_kernel", "deconv3d_c8_kernel", "prob_kernel",
                         "prob_wta_kernel", "softmax_wta_kernel"),
