@@ -11,3 +11,6 @@ rm -f gpurun_out/r13i/*.npz
 bash scripts/ab_trace.sh r13i "warp_|fmt_|total" base elubr w4 pipe nbl8 nodot || exit $?
 timeout -k 10 600 python -u -m pytest -x -v -s --timeout 500 --timeout-method thread tests/test_gpu_distributed.py tests/test_gpu_train_c5.py -m gpu > gpurun_out/r13i/pytest_new.log 2>&1
 timeout -k 10 900 python -u scripts/diag/stage1_flip.py gpurun_out/r13i/c4_stage1_flip.json > gpurun_out/r13i/c4_stage1_flip.log 2>&1
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d gpurun_out/r13i/train_full -o run --output-format csv -- python3 scripts/diag/train_prof.py full 5 graph > gpurun_out/r13i/train_full.log 2>&1
+python3 scripts/diag/stats_table.py gpurun_out/r13i/train_full/run_kernel_stats.csv > gpurun_out/r13i/train_full_kernels.txt 2>&1

@@ -44,6 +44,14 @@ MARGIN = 1e-4          # near-tie margin, reported and asserted
 # float64 through FMT, pathway, cost volume and CostRegNet: d6 208.8781 vs d4 208.8774 (margin 7.4e-4,
 # picks 6 = the GPU's pick); the reference's 1 / 4 / 16 torch threads all give 4 (profiles/r09a/c3_flip.txt).
 EXACT_ARITHMETIC_PICKS = {(11, 864, 1152, "stage3"): {(431, 451)}}
+# (n_views, H, W, stage) -> {(y, x)}: fp32 ties -- pixels where the two top logits agree to within fp32
+# resolution, so which one wins depends on rounding alone, on the reference's side as much as on the GPU's.
+# C4 stage 1, pixel (104, 190): reference logits d6 12.228886 vs d40 12.228884 (margin 1.9e-6, 2 ulps of
+# the logit); the reference at 1 thread has them EQUAL (margin 0, argmax = the first index, 6); float64
+# through FMT, cost volume and CostRegNet also picks 6, by 3.3e-5; the GPU picks 40 by 9.8e-7. The fp32
+# reference itself differs from float64 at 3 other stage-1 pixels of this frame (margins up to 3.5e-5;
+# profiles/r13/c4_stage1_flip.json, profiles/r13/c4_stage1_exact.json).
+FP32_TIES = {(11, 1056, 1920, "stage1"): {(104, 190)}}
 # CostRegNet's receptive field in pixels of its own stage: 3 stride-2 levels of 3x3x3 convs (conv1-6),
 # the 3 transposed convs back up, conv0 and prob: 1 + 2(1+1) + 4(1+1) + 8(1+1) + 4 + 2 + 1 = 36 < 40.
 RF_RADIUS = 40
@@ -197,9 +205,25 @@ def test_c3_dtu_11_views_full_forward_parity(model, sd):
 
 def test_c4_tnt_full_forward_parity(model, sd):
     """C4's shape on one GPU: Tanks&Temples 1056x1920, N=11, 48/32/8 against the oracle
-    (models/TransMVSNet.py:141-226 at datasets/tnt_eval.py:24-40 sizes)."""
-    rep = _full_size_parity(model, sd, 11, 1056, 1920)
+    (models/TransMVSNet.py:141-226 at datasets/tnt_eval.py:24-40 sizes). Each stage's own arithmetic
+    meets the bar (fed stages). The cascade meets it too, unless an upstream flip sits on an attributed
+    fp32 tie (FP32_TIES): a flip there moves the next stage's hypotheses around that pixel, so the
+    cascaded depth there is a different -- equally valid -- reconstruction. Then the bar holds outside
+    the footprint of the moved hypotheses, and the flips inside it are bounded (1 % of the footprint)."""
+    cfg = (11, 1056, 1920)
+    rep = _full_size_parity(model, sd, *cfg)
     assert rep["fed_stage3"]["mean_abs_mm"] <= 1e-4, rep
+    c1, c3 = rep["cascade_stage1"], rep["cascade_stage3"]
+    if c3["mean_abs_mm"] > 1e-4:
+        ties = FP32_TIES.get(cfg + ("stage1",), frozenset())
+        assert c1["differing"] == len(c1["differing_pixels"]), c1
+        assert all(tuple(px) in ties for px in c1["differing_pixels"]), ("unattributed stage-1 flip", c1)
+        assert c1["max_flip_margin"] < 1e-5, c1  # a tie at fp32 resolution
+        assert rep["cascade_stage2"]["unexplained"] == [] and c3["unexplained"] == [], rep
+        assert c3["mean_abs_mm_outside_footprint"] <= 1e-4, c3
+        for s in (2, 3):
+            r = rep[f"cascade_stage{s}"]
+            assert r["cascade_explained"] <= 0.01 * max(r["footprint_pixels"], 1), (s, r)
 
 
 def test_c4_tnt_full_forward_properties(model):

@@ -61,7 +61,7 @@ def test_c5_train_sample_full_size_vs_oracle():
     fnet = fnet.to(DEV)
     fnet.train()
     with torch.no_grad():
-        f1, f2, f3 = featurenet_train(fnet.feature, imgs)
+        f1, f2, f3 = featurenet_train(fnet.feature, imgs[0])
     feats = [{"stage1": f1[i:i + 1].cpu(), "stage2": f2[i:i + 1].cpu(), "stage3": f3[i:i + 1].cpu()} for i in range(N5)]
     del fnet
     # the GPU step

@@ -21,20 +21,7 @@ constexpr int kD = 32;
 constexpr int kKV = TMVS_KV_NFLOATS;
 constexpr int kKvBlock = 256;
 
-// elu(x) + 1 with expm1f evaluated for every lane and selected (expm1f(min(x, 0)) is expm1f(x) where
-// it is used): as a branch around expm1f each call was its own basic block with an exec-mask branch,
-// which kept the compiler from interleaving the tile's MFMAs with this VALU (8 calls per tile)
-#ifndef TMVS_ELU_SELECT
-#define TMVS_ELU_SELECT 1
-#endif
-__device__ __forceinline__ float elu1(float x) {
-#if TMVS_ELU_SELECT
-  const float e = expm1f(fminf(x, 0.f));
-  return (x > 0.f ? x : (x <= 0.f ? e : x)) + 1.f;  // NaN stays NaN
-#else
-  return (x > 0.f ? x : expm1f(x)) + 1.f;
-#endif
-}
+__device__ __forceinline__ float elu1(float x) { return (x > 0.f ? x : expm1f(x)) + 1.f; }
 
 __device__ __forceinline__ void load_token(const float* __restrict__ p, float (&x)[kD]) {
 #pragma unroll

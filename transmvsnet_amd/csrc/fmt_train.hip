@@ -19,11 +19,7 @@ constexpr int kTB = 256;
 constexpr float kLnEps = 1e-5f;
 constexpr float kAttnEps = 1e-6f;
 
-// expm1f evaluated unconditionally and selected (no exec-mask branch per call; same values, NaN kept)
-__device__ __forceinline__ float elu1f(float x) {
-  const float e = expm1f(fminf(x, 0.f));
-  return (x > 0.f ? x : (x <= 0.f ? e : x)) + 1.f;
-}
+__device__ __forceinline__ float elu1f(float x) { return (x > 0.f ? x : expm1f(x)) + 1.f; }
 __device__ __forceinline__ float elu1_grad(float x) { return x > 0.f ? 1.f : expf(x); }
 
 // y[t][o] = sum_i W[o][i] x[t][i] + b[o] for a torch Linear weight W [OUT][IN]; TRANS: y[t][o] = sum_i W[i][o] x[t][i]

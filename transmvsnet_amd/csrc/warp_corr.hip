@@ -104,33 +104,6 @@ __device__ __forceinline__ void project(const float rx, const float ry, const fl
   y0i = (int)fminf(fmaxf(y0, -2.f), 32766.f);
 }
 
-// project() that also returns the unnormalised sample position (ix, iy) before the floor, NaN when
-// the point is behind the camera (z < 1e-6); (x0, y0, fx, fy) are project()'s bits
-__device__ __forceinline__ void project_pos(const float rx, const float ry, const float rz, const float tx,
-                                            const float ty, const float tz, const float dep, const float halfw,
-                                            const float halfh, int& x0i, int& y0i, float& fx, float& fy, float& ixo,
-                                            float& iyo) {
-  const float X = rx * dep + tx;
-  const float Y = ry * dep + ty;
-  const float Z = rz * dep + tz;
-  float xn = (X / Z) / halfw - 1.f;
-  float yn = (Y / Z) / halfh - 1.f;
-  const bool behind = Z < 1e-6f;
-  if (behind) {
-    xn = -99.f;
-    yn = -99.f;
-  }
-  const float ix = (xn + 1.f) * halfw;
-  const float iy = (yn + 1.f) * halfh;
-  const float x0 = floorf(ix), y0 = floorf(iy);
-  fx = ix - x0;
-  fy = iy - y0;
-  x0i = (int)fminf(fmaxf(x0, -2.f), 32766.f);
-  y0i = (int)fminf(fmaxf(y0, -2.f), 32766.f);
-  ixo = behind ? __builtin_nanf("") : ix;
-  iyo = behind ? __builtin_nanf("") : iy;
-}
-
 // x from lane (lane ^ R) inside an aligned group of 8 (R compile-time)
 template <int R>
 __device__ __forceinline__ int lane_xor(int x) {
@@ -568,16 +541,17 @@ __device__ __forceinline__ float reduce_scatter(const float* p, int k) {
   return q[0];
 }
 
-// Which samples share a load instruction (TMVS_WARP_PMAJOR, default 1). The address path pays per
-// distinct cache line an instruction touches (≈2 cycles each past the 16-cycle floor of a 64-lane
-// 16-byte load), not per byte. A pixel's consecutive depth planes project ≈0.7 px apart on its
-// epipolar line, so their taps share lines, while different pixels' taps (per-pixel hypotheses)
-// do not. Pixel-major rounds: in round t the wave's SPW groups sample PPR = SPW/LPS pixels ×
-// LPS consecutive planes each (stage 3: 4 pixels × 4 planes, stage 2: 1 pixel × 8 planes)
-// instead of SPW pixels × one plane. Group g's round-t sample is owned by its lane t (geometry
-// broadcast as before), so lane (g, k) owns pixel k·PPR + g/LPS at planes j·LPS + g%LPS, and
-// holds the reference quads of the LPS pixels its rounds visit. Each sample's arithmetic (lane
-// roles, channel order, reduce-scatter) is unchanged: the outputs are bit-identical.
+// Which samples share a load instruction. Plane-major rounds (the original layout): in round t the
+// wave's SPW groups sample SPW pixels at one plane each. Pixel-major rounds (TMVS_WARP_PMAJOR, used
+// for C = 16): the SPW groups sample PPR = SPW/LPS pixels × LPS consecutive planes each (stage 2:
+// 1 pixel × 8 planes), whose taps lie ≈0.7 px apart on one epipolar segment and so share cache lines.
+// Group g's round-t sample is owned by its lane t (geometry broadcast as before), so lane (g, k) owns
+// pixel k·PPR + g/LPS at planes j·LPS + g%LPS and holds the reference quads of the LPS pixels its
+// rounds visit. Each sample's arithmetic (lane roles, channel order, reduce-scatter) is unchanged:
+// the outputs are bit-identical either way. Measured (profiles/r13/warp_pmajor_ab.txt, two
+// alternating reps in one box): stage 2 345.1 -> 323.3 us, stage 3 247.2 -> 252.1 us (the address
+// unit is charged per 4-lane quad, so sharing lines between quads buys little); C = 8 keeps the
+// plane-major rounds.
 #ifndef TMVS_WARP_PMAJOR
 #define TMVS_WARP_PMAJOR 1
 #endif
@@ -590,10 +564,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   constexpr int NQ = C / 4;             // channel quads
   constexpr int LPS = 2 * NQ;           // lanes per pixel: (tap column, quad)
   constexpr int SPW = 64 / LPS, PIX = 4 * SPW, DPT = D / LPS;
-  constexpr int PPR = TMVS_WARP_PMAJOR ? SPW / LPS : SPW;  // pixels per round
+  constexpr bool PM = TMVS_WARP_PMAJOR && C == 16;  // pixel-major rounds
+  constexpr int PPR = PM ? SPW / LPS : SPW;          // pixels per round
   static_assert(C == 8 || C == 16, "row-pair layout for 8 or 16 channels");
   static_assert(D % LPS == 0, "D must be a multiple of the lanes per pixel");
-  static_assert(!TMVS_WARP_PMAJOR || PPR * LPS == SPW, "pixel-major rounds: LPS^2 must divide 64");
+  static_assert(!PM || PPR * LPS == SPW, "pixel-major rounds: LPS^2 must divide 64");
   __shared__ float dep_lds[DPT][256];
   __shared__ float acc_lds[DPT][256];
   const int tid = threadIdx.x;
@@ -604,8 +579,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const int k = lane % LPS, tx = k / NQ, q = k % NQ, g = lane / LPS;
   const int wbase = tile * PIX + (tid >> 6) * SPW;
   // owned samples: pixel `p`, planes j·LPS + dsub (pixel-major) or j·LPS + k (plane-major)
-  const int pix_own = TMVS_WARP_PMAJOR ? k * PPR + g / LPS : g;
-  const int dsub = TMVS_WARP_PMAJOR ? g % LPS : k;
+  const int pix_own = PM ? k * PPR + g / LPS : g;
+  const int dsub = PM ? g % LPS : k;
   int p = wbase + pix_own;
   const bool active = p < HW;
   if (!active) p = HW - 1;
@@ -614,7 +589,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   float4 r4[LPS];  // reference quad q of the pixel round t samples
 #pragma unroll
   for (int t = 0; t < LPS; ++t) {
-    const int pt = TMVS_WARP_PMAJOR ? min(wbase + t * PPR + g / LPS, HW - 1) : p;
+    const int pt = PM ? min(wbase + t * PPR + g / LPS, HW - 1) : p;
     r4[t] = *reinterpret_cast<const float4*>(ref + (size_t)pt * C + 4 * q);
   }
 #pragma unroll
@@ -661,326 +636,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   if (PARTIAL && dsub == 0) wsum_out[p] = wsum;
 }
 
-// ---------------------------------------------------------------- stages 2/3: "dot first" over unique taps
-// The row-pair kernel above gathers every (pixel, plane, view) tap through the vector-memory address
-// unit, 16 B per lane, and runs at 0.6-0.8 of that unit's rate. A pixel's D hypotheses
-// project onto a short segment of its epipolar line (≈0.7 px apart on the synthetic DTU rig), so its
-// D·4 taps hold only ≈1.5·D distinct texels (48 of 128 at stage 2, 14 of 32 at stage 3), and the
-// similarity factors over them:
-//   sim(p, d) = (1/C) Σ_c ref_c · Σ_tap w_tap(d) src_tap,c = (1/C) Σ_tap w_tap(d) · dot(p, tap),
-// dot(p, T) = Σ_c ref_c src_T,c. warp_dot_kernel loads each distinct texel of a pixel-view once,
-// reduces it to its dot with the reference features, parks the dot in a per-pixel LDS window, and
-// forms each plane's bilinear sample from 4 window reads.
-//
-// Lanes: a wave holds NPW = 64/D pixels × D planes; lane (p, d) owns plane d of pixel p (one sample per
-// view; its accumulator is a register). Per view:
-//  1. each lane projects its plane (project(): the forward's rounding) -> block (x0, y0) of 2×2 taps; a
-//     block with no tap inside the image is dead (sim 0: the reference's zero padding);
-//  2. the taps of its block not in plane d-1's block are new (hypotheses increase with d, so a pixel's
-//     blocks walk monotonically along the segment and each texel is new once); the wave's new texels
-//     are listed in LDS (byte offset, window slot) at a ballot prefix sum;
-//  3. load rounds: C/4 lanes per listed texel (a channel quad each; buffer loads, out-of-image texels
-//     read 0), dot with the pixel's reference quad, quad sum by DPP, store into the window;
-//  4. each lane reads its 4 taps' dots and forms sim = fma chain in grid_sample's order (nw, ne, sw, se)
-//     × 1/C; acc += sim · w_view as in the other kernels.
-// Window: MX × kWinRows floats per pixel, addressed along the segment: u = major − lo (major = the axis
-// the segment advances most along; lo from the end samples, planes 0 and D-1), v = minor −
-// floor(line(major)) + 3 with line() through the end samples: every tap lies within 2 texels of it, so
-// v ∈ [1, 6]. Each lane checks its own taps' slots; a pixel with any tap outside the window (a segment
-// longer than ≈MX − 4, hypotheses not increasing, a camera behind a plane) is gathered per lane (its 4
-// taps, same dot and quad-sum order: the same bits, without the reuse).
-// Numerics: the channel sum runs before the bilinear sum (the reference samples every channel, then
-// takes the channel mean), so similarities differ from the product form by a few ulps (5e-7 bar,
-// tests/test_gpu_parity.py).
-constexpr int kWinRows = 8;
-// LDS list entry: texel index y*W + x (kTexOut: outside the image) << kSlotBits | window slot
-constexpr int kSlotBits = 11;
-constexpr unsigned kTexOut = (1u << (32 - kSlotBits)) - 1u;
-
-template <int D>
-struct DotCfg {
-  static constexpr int MX = D <= 8 ? 16 : D <= 16 ? 32 : D <= 32 ? 48 : 96;
-};
-
-// Cross-lane hand-offs through the wave's private LDS (list, window): the LDS executes one wave's
-// DS instructions in issue order, so a read issued after a write (by any lane of the wave) sees it;
-// only the compiler must not reorder them.
-__device__ __forceinline__ void lds_order() {
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");
-}
-
-// window slot of texel (X, Y) for the pixel's line (xmaj, lo, m0, M0, b); -1 when outside the window
-__device__ __forceinline__ int win_slot(int X, int Y, bool xmaj, int lo, float m0, float M0, float b, int MX) {
-  const int M = xmaj ? X : Y, m = xmaj ? Y : X;
-  const int u = M - lo;
-  const int v = m - (int)floorf(m0 + b * ((float)M - M0)) + 3;
-  return ((unsigned)u < (unsigned)MX && (unsigned)v < (unsigned)kWinRows) ? u * kWinRows + v : -1;
-}
-
-// dot of a texel's channel quad with the reference quad: serial FMA chain (the gather path and the load
-// rounds must agree bit for bit)
-__device__ __forceinline__ float quad_dot(const float4& r, const floatx4& s) {
-  float a = r.x * s[0];
-  a = fmaf(r.y, s[1], a);
-  a = fmaf(r.z, s[2], a);
-  return fmaf(r.w, s[3], a);
-}
-
-// One lane's view of one plane (phase 1's output, consumed one pipeline step later)
-struct DotLane {
-  int x0, y0;
-  float fx, fy, w;
-  int s[4];  // slots of the taps nw, ne, sw, se
-  bool live;
-};
-
-#ifndef TMVS_DOT_NB
-#define TMVS_DOT_NB 6
-#endif
-#ifndef TMVS_DOT_PIPE
-#define TMVS_DOT_PIPE 0
-#endif
-#ifndef TMVS_DOT_NBL
-#define TMVS_DOT_NBL 4
-#endif
-#ifndef TMVS_DOT_WAVES
-#define TMVS_DOT_WAVES 6
-#endif
-template <int C, int D, bool PARTIAL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_DOT_WAVES, TMVS_DOT_WAVES))) void warp_dot_kernel(
-    const float* __restrict__ ref, const float* __restrict__ src, const float* __restrict__ hyp,
-    const float* __restrict__ vw_in, float* __restrict__ sim_out, float* __restrict__ wsum_out, int V, int H, int W,
-    int vw_shift, int vw_offset, WarpArgs args) {
-  constexpr int NPW = 64 / D;             // pixels per wave
-  constexpr int LPT = C / 4;              // lanes per texel (channel quads)
-  constexpr int TPR = 64 / LPT;           // texels per load round
-  constexpr int MX = DotCfg<D>::MX;
-  constexpr int WIN = MX * kWinRows;      // window floats per pixel
-  constexpr int NWIN = NPW * WIN;         // window slots of the wave; then 256 direct slots (lane*4 + tap)
-  constexpr int NB = TMVS_DOT_NB;         // load rounds issued one view ahead (TMVS_DOT_PIPE)
-  constexpr int NBL = TMVS_DOT_NBL;       // load rounds in flight otherwise
-  static_assert(64 % D == 0 && (C == 8 || C == 16), "warp_dot_kernel: D divides 64, C in {8, 16}");
-  static_assert(NWIN + 256 <= (1 << kSlotBits), "slots must fit the list entry");
-  __shared__ float slot_lds[4][NWIN + 256];
-  __shared__ unsigned list_lds[4][TMVS_DOT_PIPE ? 2 : 1][256];
-  __shared__ float4 ref_lds[4][NPW * LPT];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int p = lane / D, d = lane % D;
-  const int q = lane % LPT;
-  const int HW = H * W;
-  const int nblk = (HW + 4 * NPW - 1) / (4 * NPW);
-  const int tile = xcd_remap(blockIdx.x, nblk);
-  const int wbase = tile * 4 * NPW + wave * NPW;
-  int pix = wbase + p;
-  const bool active = pix < HW;
-  if (!active) pix = HW - 1;
-  float* slot = slot_lds[wave];
-  const float4* refq = ref_lds[wave];
-  if (lane < NPW * LPT) {
-    const int pp = min(wbase + lane / LPT, HW - 1);
-    ref_lds[wave][lane] = *reinterpret_cast<const float4*>(ref + (size_t)pp * C + 4 * (lane % LPT));
-  }
-  const int py = pix / W, px = pix - py * W;
-  const float fxp = (float)px, fyp = (float)py;
-  const float dep = hyp[(size_t)d * HW + pix];
-  const float halfw = (float)(W - 1) / 2.f;
-  const float halfh = (float)(H - 1) / 2.f;
-  const int Ws = W >> vw_shift, Hs = H >> vw_shift;
-  const float* wv = vw_in + (size_t)vw_offset * Hs * Ws + (py >> vw_shift) * Ws + (px >> vw_shift);
-  const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, V * HW * C * 4, kRsrcWord3);
-  const unsigned long long lanes_below = (1ull << lane) - 1ull;
-  const unsigned long long pix_mask = D == 64 ? ~0ull : ((1ull << D) - 1ull);
-  const int rot_plain = args.rot_plain;
-
-  // phase 1 (view v): project, window slots, list the new texels -> number listed (wave-uniform)
-  auto geometry = [&](int v, DotLane& L) -> int {
-    float R[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) R[k] = args.proj[v][k];
-    const float rx = rot_row(R, fxp, fyp, rot_plain);
-    const float ry = rot_row(R + 4, fxp, fyp, rot_plain);
-    const float rz = rot_row(R + 8, fxp, fyp, rot_plain);
-    L.w = wv[(size_t)v * Hs * Ws];
-    float ix, iy;
-    project_pos(rx, ry, rz, R[3], R[7], R[11], dep, halfw, halfh, L.x0, L.y0, L.fx, L.fy, ix, iy);
-    const int x0 = L.x0, y0 = L.y0;
-    const bool inx0 = (unsigned)x0 < (unsigned)W, inx1 = (unsigned)(x0 + 1) < (unsigned)W;
-    const bool iny0 = (unsigned)y0 < (unsigned)H, iny1 = (unsigned)(y0 + 1) < (unsigned)H;
-    L.live = (inx0 || inx1) && (iny0 || iny1);
-    const float e0x = __shfl(ix, p * D), e0y = __shfl(iy, p * D);
-    const float e1x = __shfl(ix, p * D + D - 1), e1y = __shfl(iy, p * D + D - 1);
-    const bool xmaj = fabsf(e1x - e0x) >= fabsf(e1y - e0y);
-    const float M0 = xmaj ? e0x : e0y, m0 = xmaj ? e0y : e0x;
-    const float dM = xmaj ? e1x - e0x : e1y - e0y, dm = xmaj ? e1y - e0y : e1x - e0x;
-    const float b = dM != 0.f ? dm * __builtin_amdgcn_rcpf(dM) : 0.f;  // |b| <= 1 (up to the rcp's ulp)
-    const float Mlo = fminf(M0, M0 + dM);
-    const bool line_ok = Mlo == Mlo && b == b && m0 == m0 && fabsf(Mlo) < 1e6f && fabsf(m0) < 1e6f;
-    const int lo = line_ok ? (int)floorf(Mlo) - 1 : 0;
-    // the block's 2 major-axis lines (x-major: columns x0, x0+1; else rows y0, y0+1), each holding 2
-    // consecutive window rows: slot(major i, minor j) = (u + i)·kWinRows + v_i + j
-    const int Mb = xmaj ? x0 : y0, mb = xmaj ? y0 : x0;
-    const int u = Mb - lo;
-    const int v0 = mb - (int)floorf(m0 + b * ((float)Mb - M0)) + 3;
-    const int v1 = mb - (int)floorf(m0 + b * ((float)(Mb + 1) - M0)) + 3;
-    const bool fits = line_ok && (unsigned)u < (unsigned)(MX - 1) && (unsigned)v0 < (unsigned)(kWinRows - 1) &&
-                      (unsigned)v1 < (unsigned)(kWinRows - 1);
-    const bool direct = ((__ballot(L.live && !fits) >> (p * D)) & pix_mask) != 0ull;
-    {
-      const int w0 = p * WIN + u * kWinRows + v0, w1 = p * WIN + (u + 1) * kWinRows + v1;
-      const int dbase = NWIN + 4 * lane;
-      // taps nw (x0,y0), ne (x0+1,y0), sw (x0,y0+1), se (x0+1,y0+1)
-      L.s[0] = direct ? dbase : w0;
-      L.s[1] = direct ? dbase + 1 : (xmaj ? w1 : w0 + 1);
-      L.s[2] = direct ? dbase + 2 : (xmaj ? w0 + 1 : w1);
-      L.s[3] = direct ? dbase + 3 : w1 + 1;
-    }
-    // the taps not in plane d-1's block (window pixels); every tap of a direct pixel's plane
-    const bool chainable = L.live && !direct;
-    const unsigned me = chainable ? (unsigned)(x0 + 2) | ((unsigned)(y0 + 2) << 16) : 0xFFFFFFFFu;
-    const unsigned prev = __shfl(me, lane - 1);
-    const bool chain = chainable && d > 0 && prev != 0xFFFFFFFFu;
-    const int ddx = x0 - ((int)(prev & 0xFFFFu) - 2), ddy = y0 - ((int)(prev >> 16) - 2);
-    const bool c0s = chain && (unsigned)ddx <= 1u, c1s = chain && (unsigned)(ddx + 1) <= 1u;  // column x0 / x0+1 seen
-    const bool r0s = (unsigned)ddy <= 1u, r1s = (unsigned)(ddy + 1) <= 1u;                   // row y0 / y0+1 seen
-    unsigned nb = 0;
-    nb |= (L.live && !(c0s && r0s)) ? 1u : 0u;
-    nb |= (L.live && !(c1s && r0s)) ? 2u : 0u;
-    nb |= (L.live && !(c0s && r1s)) ? 4u : 0u;
-    nb |= (L.live && !(c1s && r1s)) ? 8u : 0u;
-    const int cnt = __builtin_popcount(nb);
-    const unsigned long long c0 = __ballot(cnt & 1), c1 = __ballot(cnt & 2), c2 = __ballot(cnt & 4);
-    unsigned* list = list_lds[wave][TMVS_DOT_PIPE ? v & 1 : 0];
-    int o = __popcll(c0 & lanes_below) + 2 * __popcll(c1 & lanes_below) + 4 * __popcll(c2 & lanes_below);
-    const unsigned tb = (unsigned)(y0 * W + x0);
-    const bool in4[4] = {inx0 && iny0, inx1 && iny0, inx0 && iny1, inx1 && iny1};
-    const unsigned to4[4] = {0u, 1u, (unsigned)W, (unsigned)W + 1u};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (nb & (1u << k)) {
-        list[o] = ((in4[k] ? tb + to4[k] : kTexOut) << kSlotBits) | (unsigned)L.s[k];
-        ++o;
-      }
-    }
-    return __popcll(c0) + 2 * __popcll(c1) + 4 * __popcll(c2);
-  };
-  // phase 2 (view v): the first NB load rounds (texel t = round·TPR + lane/LPT, channel quad q)
-  [[maybe_unused]] auto issue = [&](int v, int total, unsigned (&e)[NB], floatx4 (&val)[NB]) {
-    const unsigned* list = list_lds[wave][TMVS_DOT_PIPE ? v & 1 : 0];
-    const unsigned vq = (unsigned)(v * HW * C * 4) + 16u * (unsigned)q;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int t = i * TPR + lane / LPT;
-      const unsigned ent = list[t];
-      e[i] = t < total ? ent : 0xFFFFFFFFu;
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const unsigned tex = e[i] >> kSlotBits;
-      val[i] = buf_load_f32x4(rsrc, tex >= kTexOut ? kOffOut : tex * (unsigned)(C * 4) + vq);  // kOffOut: reads 0
-    }
-  };
-  // dot of a loaded texel quad with its pixel's reference quad, quad sum, into its slot
-  auto deposit = [&](unsigned ent, const float4& r, const floatx4& val) {
-    float part = quad_dot(r, val);
-    if constexpr (LPT >= 2) part = part + lane_xor_f<1>(part);
-    if constexpr (LPT >= 4) part = part + lane_xor_f<2>(part);
-    if (q == 0 && ent != 0xFFFFFFFFu) slot[ent & ((1u << kSlotBits) - 1u)] = part;
-  };
-  auto ref_of = [&](unsigned ent) -> float4 {
-    const unsigned sl = ent & ((1u << kSlotBits) - 1u);
-    const unsigned pp = sl < (unsigned)NWIN ? sl / WIN : ((sl - NWIN) >> 2) / D;
-    return refq[(pp % NPW) * LPT + q];
-  };
-
-  float acc = 0.f;
-  float wsum = PARTIAL ? 0.f : 1e-5f;
-#if TMVS_DOT_PIPE
-  DotLane cur, nxt;
-  int tot_cur = geometry(0, cur), tot_nxt = 0;
-  lds_order();
-  unsigned e[NB];
-  floatx4 val[NB];
-  issue(0, tot_cur, e, val);
-#endif
-  for (int v = 0; v < V; ++v) {
-#if TMVS_DOT_PIPE
-    if (v + 1 < V) tot_nxt = geometry(v + 1, nxt);  // while view v's loads are in flight
-    float4 rr[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) rr[i] = ref_of(e[i]);
-#pragma unroll
-    for (int i = 0; i < NB; ++i) deposit(e[i], rr[i], val[i]);
-    const int t_rest = NB * TPR;
-#else
-    DotLane cur;
-    const int tot_cur = geometry(v, cur);
-    lds_order();
-    const int t_rest = 0;
-#endif
-    // load rounds not issued ahead (all of them without the pipeline)
-    const unsigned* list = list_lds[wave][TMVS_DOT_PIPE ? v & 1 : 0];
-    const unsigned vq = (unsigned)(v * HW * C * 4) + 16u * (unsigned)q;
-    for (int t0 = t_rest; t0 < tot_cur; t0 += NBL * TPR) {
-      unsigned el[NBL];
-      floatx4 xl[NBL];
-#pragma unroll
-      for (int i = 0; i < NBL; ++i) {
-        const int t = t0 + i * TPR + lane / LPT;
-        const unsigned ent = list[min(t, 255)];
-        el[i] = t < tot_cur ? ent : 0xFFFFFFFFu;
-      }
-#pragma unroll
-      for (int i = 0; i < NBL; ++i) {
-        const unsigned tex = el[i] >> kSlotBits;
-        xl[i] = buf_load_f32x4(rsrc, tex >= kTexOut ? kOffOut : tex * (unsigned)(C * 4) + vq);
-      }
-#pragma unroll
-      for (int i = 0; i < NBL; ++i) deposit(el[i], ref_of(el[i]), xl[i]);
-    }
-    lds_order();
-    // this lane's sample: sim = fma chain over the taps in grid_sample's order, / C
-    float dt[4] = {0.f, 0.f, 0.f, 0.f};
-    if (cur.live) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) dt[k] = slot[cur.s[k]];
-    }
-    const float ea = 1.f - cur.fx, sy = 1.f - cur.fy;
-    const float sim =
-        fmaf(dt[3], cur.fy * cur.fx, fmaf(dt[2], cur.fy * ea, fmaf(dt[1], sy * cur.fx, dt[0] * (sy * ea))));
-    acc = acc + (sim * (1.f / (float)C)) * cur.w;
-    wsum = wsum + cur.w;
-    lds_order();  // the slots are rewritten by the next view
-#if TMVS_DOT_PIPE
-    if (v + 1 < V) {
-      cur = nxt;
-      tot_cur = tot_nxt;
-      issue(v + 1, tot_cur, e, val);
-    }
-#endif
-  }
-  if (!active) return;
-  sim_out[(size_t)d * HW + pix] = PARTIAL ? acc : acc / wsum;
-  if (PARTIAL && d == 0) wsum_out[pix] = wsum;
-}
-
 template <int C, int D, bool PW, bool PARTIAL>
 static int launch_warp(const float* ref, const float* src, const float* hyp, const float* vw_in, float* sim,
                        float* wsum, float* vw_out, int V, int H, int W, int vw_shift, int vw_offset, int vw_total,
                        const WarpArgs& args, hipStream_t st) {
-#ifndef TMVS_WARP_DOT
-#define TMVS_WARP_DOT 1
-#endif
-  // warp_dot_kernel's list entries hold a texel index below kTexOut (= 2^21 - 1)
-  if constexpr (TMVS_WARP_DOT && (C == 8 || C == 16) && !PW && 64 % D == 0) if ((long long)H * W < (long long)kTexOut) {
-    constexpr int PIXD = 4 * (64 / D);
-    const int nblk = (H * W + PIXD - 1) / PIXD;
-    hipLaunchKernelGGL((warp_dot_kernel<C, D, PARTIAL>), dim3(nblk), dim3(256), 0, st, ref, src, hyp, vw_in, sim,
-                       wsum, V, H, W, vw_shift, vw_offset, args);
-    TMVS_CHECK_LAUNCH();
-    return TMVS_OK;
-  }
   if constexpr ((C == 8 || C == 16) && !PW) {
     constexpr int PIXP = 4 * (64 / (C / 2));
     const int nblk = (H * W + PIXP - 1) / PIXP;
