@@ -1,7 +1,8 @@
 #!/bin/bash
-# r14a: (1) DCN backward data A/B (LDS-staged offset/mask planes + pipelined taps vs the committed
-# kernel): bitwise compare and timing; (2) prob walk with one plane of lookahead vs the committed
-# prob kernels: bitwise hot-path outputs and kernel trace; (3) the whole -m gpu suite + smoke, bench
+# r14a: A/Bs on one box. (1) DCN backward data (LDS-staged offset/mask planes + pipelined taps vs the
+# committed kernel): bitwise + timing. (2) CostRegNet: prob walk one plane ahead, conv0 fused into
+# conv1 and conv11's skip, deconv chunk prefetch, conv weight lookahead -- bitwise hot-path outputs
+# vs the committed costreg (probold) and per-kernel trace times for the variants.
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r14a
 mkdir -p $O
@@ -17,8 +18,7 @@ timeout -k 10 120 python scripts/diag/out_bits.py $O/pnew.npz > $O/prob_bits.log
 TMVS_LIB_PATH=variants/probold/libtransmvs_hip.so timeout -k 10 120 python scripts/diag/out_bits.py $O/pold.npz >> $O/prob_bits.log 2>&1 &&
 python scripts/diag/out_bits.py --compare $O/pold.npz $O/pnew.npz >> $O/prob_bits.log 2>&1 &&
 rm -f $O/pold.npz $O/pnew.npz &&
-bash scripts/diag/ab_kernels.sh r14a/ab "prob conv0" probold > $O/prob_ab.txt 2>&1 || exit $?
-rm -rf $O/ab/default $O/ab/probold
-export TMVS_REPORT_DIR=$PWD/$O/fullsize
-bash scripts/gpu/full_check.sh r14a || exit $?
-timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
+bash scripts/diag/ab_kernels.sh r14a/ab "prob conv0 deconv3d conv3d_lds s2c8" probold wla4 wla6 pfmin3 nopf > $O/cr_ab.txt 2>&1
+rc=$?
+rm -rf $O/ab/*/
+exit $rc
