@@ -59,15 +59,6 @@ struct Geo {
 
 __device__ __forceinline__ float act(float v, float lo) { return v > lo ? v : lo; }
 
-// conv0 (1 -> 8, models/module.py:428) recomputed inside its consumers (conv1, and conv11's skip)
-// from the 1-channel cost volume instead of being stored and read back at 32 B per voxel
-struct Conv0Fuse {
-  const float* x0;  // cost volume [B][D][H][W] (1 channel)
-  const float* w0;  // conv0 weights [27][8] (tap-major, as conv0_kernel)
-  const float* al0;
-  const float* sh0;
-};
-
 // ---------------------------------------------------------------- conv3d k3 p1, stride S
 // Workgroup tile: 16 output voxels along w x TH rows x TD depth slices, MBB blocks of 16
 // output channels. Per CK-channel chunk the input tile (+halo) is staged once into LDS
@@ -78,9 +69,6 @@ struct Conv0Fuse {
 template <int CIN, int COUT, int S, int TD, int TH, int MBB, bool KDSKIP = false>
 #ifndef TMVS_LDS_WPE
 #define TMVS_LDS_WPE 3
-#endif
-#ifndef TMVS_WLA1
-#define TMVS_WLA1 2  // A-fragment lookahead (taps) of the full-depth schedule, one row per wave
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WPE, TMVS_LDS_WPE))) void conv3d_lds_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                          const float* __restrict__ alpha,
@@ -176,10 +164,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
           a[m].zero();
       }
     };
-    // A fragments requested WLA taps ahead (a ring of WLA + 1 tap slots; KDSKIP, and two rows per
-    // wave within the VGPR budget: two taps ahead)
-    constexpr int WLA = (KDSKIP || NBW > 1) ? 2 : TMVS_WLA1;
-    VecN<PL> aw[WLA + 1][MBB];
+    VecN<PL> aw[3][MBB];
     // one tap: B fragments from the LDS tile, NBW x MBB x PL MFMAs
     auto tap_mfma = [&](int kd, int kh, int kw, const VecN<PL>* a) {
       VecN<PL> b[NBW];
@@ -216,12 +201,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
     wload(0, aw[0]);
     wload(1, aw[1]);
 #pragma unroll
-    for (int p = 2; p < WLA; ++p) wload(p, aw[p]);
-#pragma unroll
     for (int tap = 0; tap < 27; ++tap) {
       const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
-      if (tap + WLA < 27) wload(tap + WLA, aw[(tap + WLA) % (WLA + 1)]);
-      const VecN<PL>* a = aw[tap % (WLA + 1)];
+      if (tap + 2 < 27) wload(tap + 2, aw[(tap + 2) % 3]);
+      const VecN<PL>* a = aw[tap % 3];
       VecN<PL> b[NBW];
 #pragma unroll
       for (int r = 0; r < NBW; ++r) {
@@ -380,12 +363,6 @@ __global__ __launch_bounds__(256) void conv3d_direct_kernel(const float* __restr
 // 32 x 2THI x 2TDI). Each wave owns TDI*THI/4 input-grid rows and all 8 output parity
 // classes of them (a class = 16 outputs with one parity per dimension = one tap set of
 // 1, 2, 4 or 8 taps), so the waves carry equal work. Input tile (+1 halo) staged in LDS.
-#ifndef TMVS_DECONV_PF
-#define TMVS_DECONV_PF 1
-#endif
-#ifndef TMVS_DECONV_PF_MIN
-#define TMVS_DECONV_PF_MIN 2  // chunks (CIN / 16) from which the next chunk is prefetched
-#endif
 template <int CIN, int COUT, int TDI, int THI, int MBB>
 __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restrict__ x,
                                                            const float* __restrict__ wpk,
@@ -434,57 +411,8 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
 #pragma unroll
       for (int m = 0; m < MBB; ++m) acc[r][c][m] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // channel chunk ch: input tile + weights, global -> LDS. PF: the next chunk's are fetched into
-  // registers during this chunk's MFMAs (at 1-2 waves/SIMD the synchronous staging left the
-  // matrix cores idle for a full memory latency per chunk)
-  constexpr int NCH = CIN / CK;
-  constexpr bool PF = TMVS_DECONV_PF && NCH >= TMVS_DECONV_PF_MIN;
-  constexpr int NLT = PF ? (NVOX * PL + 255) / 256 : 1, NLW = PF ? (27 * RM * 4 + 255) / 256 : 1;
-  float4 pt[NLT], pwt[NLW];
-  auto fetch = [&](int ch) {
-#pragma unroll
-    for (int k = 0; k < NLT; ++k) {
-      const int idx = threadIdx.x + 256 * k;
-      const int vox = idx / PL, q = idx - vox * PL;
-      const int lw = vox % LW, rest = vox / LW, lh = rest % LH, ld = rest / LH;
-      const int iw = mw0 + lw, ih = mh0 + lh, id = md0 + ld;
-      pt[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (idx < NVOX * PL && iw < g.Wi && ih < g.Hi && id < g.Di)
-        pt[k] = *reinterpret_cast<const float4*>(x + (in_n + ((size_t)id * g.Hi + ih) * g.Wi + iw) * CIN + ch * CK + 4 * q);
-    }
-#pragma unroll
-    for (int k = 0; k < NLW; ++k) {
-      const int idx = threadIdx.x + 256 * k;
-      const int q = idx & 3, row = (idx >> 2) % RM, tap = (idx >> 2) / RM;
-      if (idx < 27 * RM * 4)
-        pwt[k] = *reinterpret_cast<const float4*>(wpk + ((size_t)tap * COUT + mg * 16 + row) * CIN + ch * CK + 4 * q);
-    }
-  };
-  auto commit = [&]() {
-#pragma unroll
-    for (int k = 0; k < NLT; ++k) {
-      const int idx = threadIdx.x + 256 * k;
-      const int vox = idx / PL, q = idx - vox * PL;
-      const int qs = SWZ ? (q ^ ((vox >> 1) & 3)) : q;
-      if (idx < NVOX * PL) *reinterpret_cast<float4*>(tile + vox * VST + 4 * qs) = pt[k];
-    }
-#pragma unroll
-    for (int k = 0; k < NLW; ++k) {
-      const int idx = threadIdx.x + 256 * k;
-      const int q = idx & 3, row = (idx >> 2) % RM, tap = (idx >> 2) / RM;
-      if (idx < 27 * RM * 4) *reinterpret_cast<float4*>(wts + (tap * RM + row) * 16 + 4 * (q ^ ((row >> 1) & 3))) = pwt[k];
-    }
-  };
-  if constexpr (PF) {
-    fetch(0);
-    commit();
-    __syncthreads();
-  }
 #pragma unroll 1
-  for (int ch = 0; ch < NCH; ++ch) {
-    if constexpr (PF) {
-      if (ch + 1 < NCH) fetch(ch + 1);
-    } else {
+  for (int ch = 0; ch < CIN / CK; ++ch) {
     if (ch) __syncthreads();
     for (int idx = threadIdx.x; idx < NVOX * PL; idx += 256) {
       const int vox = idx / PL, q = idx - vox * PL;
@@ -502,7 +430,6 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
       *reinterpret_cast<float4*>(wts + (tap * RM + row) * 16 + 4 * (q ^ ((row >> 1) & 3))) = v;
     }
     __syncthreads();
-    }
 #pragma unroll
     for (int cls = 0; cls < 8; ++cls) {
       const int pd = cls >> 2, ph = (cls >> 1) & 1, pw = cls & 1;
@@ -536,13 +463,6 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
                   acc[r][cls][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b.v[j], acc[r][cls][m], 0, 0, 0);
             }
           }
-    }
-    if constexpr (PF) {
-      if (ch + 1 < NCH) {
-        __syncthreads();
-        commit();
-        __syncthreads();
-      }
     }
   }
   const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
@@ -1031,33 +951,18 @@ static int launch_conv_c16(const float* x, const float* w, const float* al, cons
 // taps are taken in pairs (a, b): lanes kgrp 0/1 read channel quads 0/1 of tap a, lanes 2/3
 // of tap b, one 16-byte read each; MFMA j contracts k = (tap, quad) over channel j of each
 // quad, and the A fragments are laid out to match (the 14th pair is half empty).
-// F0 (inference trunk): the conv0 input tile is computed in place from the cost volume -- the
-// tile's box of it (conv0 footprint + 1 halo, 4 B per voxel instead of 32) is staged in LDS, each
-// thread runs conv0_kernel's FMA chains and epilogue for whole voxels (all 8 channels: wave-uniform
-// weights) and writes them into the same parity-split LDS layout, zero outside the volume (conv1's
-// padding) -- so the MFMA phase sees exactly the values conv0_kernel stores.
-template <int TD, int TH, bool F0 = false>
+template <int TD, int TH>
 __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ wpk,
                                                                const float* __restrict__ alpha,
                                                                const float* __restrict__ shift, float* __restrict__ y,
-                                                               Geo g, int ntiles, const float* __restrict__ f0x,
-                                                               const float* __restrict__ f0w,
-                                                               const float* __restrict__ f0al,
-                                                               const float* __restrict__ f0sh) {
-  // (restrict-qualified parameters, not a struct: the weights then load through the scalar cache)
-  const struct {
-    const float *x0, *w0, *al0, *sh0;
-  } f0{f0x, f0w, f0al, f0sh};
+                                                               Geo g, int ntiles) {
   constexpr int CIN = 8, COUT = 16, NBW = TD * TH / 4;
   constexpr int LW = 33, LH = 2 * TH + 1, LD = 2 * TD + 1, SW = 17;
   constexpr int NROW = LD * LH, NQ = NROW * LW * 2;  // float4 quads per tile
-  constexpr int NLD = F0 ? 0 : (NQ + 255) / 256;
-  constexpr int XD = LD + 2, XH = LH + 2, XW = LW + 2, NX = XD * XH * XW;  // F0: cost-volume box
-  constexpr int NLX = F0 ? (NX + 255) / 256 : 0;
+  constexpr int NLD = (NQ + 255) / 256;
   __shared__ __attribute__((aligned(16))) float tile[NROW * 2 * SW * 8];
   __shared__ __attribute__((aligned(16))) float wts[28 * 16 * 8];
-  __shared__ float xs[F0 ? NX : 1];
   const int nws = (g.Wo + 15) / 16, nhs = (g.Ho + TH - 1) / TH, nds = (g.Do + TD - 1) / TD;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int col = lane & 15, kgrp = lane >> 4;
@@ -1079,7 +984,7 @@ __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __re
     c.n = t / nds;
     return c;
   };
-  float4 pf[NLD > 0 ? NLD : 1];
+  float4 pf[NLD];
   auto fetch = [&](int t) {
     const TileCoord c = coord(t);
     const size_t in_n = (size_t)c.n * g.Di * g.Hi * g.Wi;
@@ -1103,64 +1008,6 @@ __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __re
       if (idx < NQ) *reinterpret_cast<float4*>(tile + ((row * 2 + (lw & 1)) * SW + (lw >> 1)) * 8 + 4 * q) = pf[k];
     }
   };
-  float px[NLX > 0 ? NLX : 1];
-  auto fetch_x = [&](int t) {  // F0: the tile's cost-volume box (zero outside the volume)
-    const TileCoord c = coord(t);
-    const float* x0n = f0.x0 + (size_t)c.n * g.Di * g.Hi * g.Wi;
-#pragma unroll
-    for (int k = 0; k < NLX; ++k) {
-      const int idx = threadIdx.x + 256 * k;
-      const int xw = idx % XW, rest = idx / XW, xh = rest % XH, xd = rest / XH;
-      const int iw = 2 * c.ow0 - 2 + xw, ih = 2 * c.oh0 - 2 + xh, id = 2 * c.od0 - 2 + xd;
-      px[k] = 0.f;
-      if (idx < NX && (unsigned)iw < (unsigned)g.Wi && (unsigned)ih < (unsigned)g.Hi && (unsigned)id < (unsigned)g.Di)
-        px[k] = x0n[((size_t)id * g.Hi + ih) * g.Wi + iw];
-    }
-  };
-  auto commit_x = [&]() {
-#pragma unroll
-    for (int k = 0; k < NLX; ++k) {
-      const int idx = threadIdx.x + 256 * k;
-      if (idx < NX) xs[idx] = px[k];
-    }
-  };
-  // F0: conv0 for the tile's 5x5x33-voxel (TD = TH = 2) input footprint from the box in LDS
-  auto conv0_tile = [&](const TileCoord& c) {
-#pragma unroll 1
-    for (int v = threadIdx.x; v < NROW * LW; v += 256) {
-      const int lw = v % LW, row = v / LW, lh = row % LH, ld = row / LH;
-      const int iw = 2 * c.ow0 - 1 + lw, ih = 2 * c.oh0 - 1 + lh, id = 2 * c.od0 - 1 + ld;
-      float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if ((unsigned)iw < (unsigned)g.Wi && (unsigned)ih < (unsigned)g.Hi && (unsigned)id < (unsigned)g.Di) {
-        float2_v a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
-        const float* xb = xs + (ld * XH + lh) * XW + lw;
-#pragma unroll
-        for (int kd = 0; kd < 3; ++kd) {
-          // this kd's 72 weights through an opaque (uniform) offset: loaded here, not all 216
-          // hoisted out of the voxel loop into SGPRs
-          int wo = kd * 72;
-          asm volatile("" : "+s"(wo));
-          const float* wk = f0.w0 + __builtin_amdgcn_readfirstlane(wo);
-#pragma unroll
-          for (int t9 = 0; t9 < 9; ++t9) {
-            const float xv = xb[(kd * XH + t9 / 3) * XW + t9 % 3];
-#pragma unroll
-            for (int cp = 0; cp < 4; ++cp)
-              a[cp] = __builtin_elementwise_fma(*reinterpret_cast<const float2_v*>(wk + t9 * 8 + 2 * cp),
-                                                float2_v{xv, xv}, a[cp]);
-          }
-        }
-#pragma unroll
-        for (int cp = 0; cp < 4; ++cp) {
-          o[2 * cp] = act(fmaf(a[cp].x, f0.al0[2 * cp], f0.sh0[2 * cp]), 0.f);
-          o[2 * cp + 1] = act(fmaf(a[cp].y, f0.al0[2 * cp + 1], f0.sh0[2 * cp + 1]), 0.f);
-        }
-      }
-      float* dst = tile + ((row * 2 + (lw & 1)) * SW + (lw >> 1)) * 8;
-      *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
-      *reinterpret_cast<float4*>(dst + 4) = make_float4(o[4], o[5], o[6], o[7]);
-    }
-  };
   for (int idx = threadIdx.x; idx < 28 * 16 * 2; idx += 256) {  // tap 27: zero (the empty half of pair 13)
     const int q = idx & 1, row = (idx >> 1) & 15, tap = idx >> 5;
     const float4 v = tap < 27 ? *reinterpret_cast<const float4*>(wpk + ((size_t)tap * COUT + row) * CIN + 4 * q)
@@ -1172,25 +1019,14 @@ __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __re
   const float4 sh = *reinterpret_cast<const float4*>(shift + co);
   int t = t_lo + kx;
   if (t < t_hi) {
-    if constexpr (F0) {
-      fetch_x(t);
-      commit_x();
-    } else {
-      fetch(t);
-      commit();
-    }
+    fetch(t);
+    commit();
   }
   __syncthreads();
   for (; t < t_hi; t += per_xcd) {
     const TileCoord c = coord(t);
     const int tn = t + per_xcd;
-    if constexpr (F0) {
-      conv0_tile(c);
-      __syncthreads();  // the conv0 tile is complete; the cost-volume box is free
-      if (tn < t_hi) fetch_x(tn);
-    } else {
-      if (tn < t_hi) fetch(tn);
-    }
+    if (tn < t_hi) fetch(tn);
     floatx4 acc[NBW];
 #pragma unroll
     for (int r = 0; r < NBW; ++r) acc[r] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -1232,24 +1068,19 @@ __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __re
       o.w = act(fmaf(acc[r][3], al.w, sh.w), g.lo);
       *reinterpret_cast<float4*>(y + (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co) = o;
     }
-    if constexpr (F0) {
-      if (tn < t_hi) commit_x();  // the box was released at the mid-tile barrier
-      __syncthreads();            // every wave is done with the conv0 tile
-    } else {
-      __syncthreads();
-      if (tn < t_hi) commit();
-      __syncthreads();
-    }
+    __syncthreads();
+    if (tn < t_hi) commit();
+    __syncthreads();
   }
 }
 
-template <int TD, int TH, bool F0 = false>
+template <int TD, int TH>
 static int launch_conv_s2c8_tile(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
-                                 const Geo& g, hipStream_t st, Conv0Fuse f0 = Conv0Fuse{}) {
+                                 const Geo& g, hipStream_t st) {
   const long ntiles = (long)B * ((g.Do + TD - 1) / TD) * ((g.Ho + TH - 1) / TH) * ((g.Wo + 15) / 16);
-  const int grid = persistent_grid(conv3d_s2c8_tile_kernel<TD, TH, F0>, ntiles);
-  hipLaunchKernelGGL((conv3d_s2c8_tile_kernel<TD, TH, F0>), dim3(grid), dim3(256), 0, st, x, w, al, sh, y, g,
-                     (int)ntiles, f0.x0, f0.w0, f0.al0, f0.sh0);
+  const int grid = persistent_grid(conv3d_s2c8_tile_kernel<TD, TH>, ntiles);
+  hipLaunchKernelGGL((conv3d_s2c8_tile_kernel<TD, TH>), dim3(grid), dim3(256), 0, st, x, w, al, sh, y, g,
+                     (int)ntiles);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -1299,43 +1130,21 @@ static int launch_conv_direct(const float* x, const float* w, const float* al, c
 // are requested before the MFMAs too, so neither latency sits between MFMA phases.
 // Tiles are dealt out XCD-contiguously (an XCD's workgroups share one L2: neighbouring tiles
 // share their halo voxels).
-// F0 (inference trunk): the skip -- conv0's output, models/module.py:455 "x = conv0 + self.conv11(x)"
-// -- is recomputed from the 1-channel cost volume instead of read back (32 B per output voxel of
-// HBM traffic, and conv0 no longer has to be kept for it). A tile's cost-volume box (outputs +1
-// halo, 4 B per voxel) is staged in LDS with the input tile; the lanes then run conv0_kernel's FMA
-// chains for the tile's outputs: per pair of output rows (one depth parity, both height parities)
-// two passes of 4 channels each -- pass p takes channels 4p..4p+3 with wave-uniform weight pairs,
-// the even lane of a column pair the (ph = p) row, the odd lane the other -- so a lane ends with
-// its store-layout quad of one row and the neighbour's quad of the other (one DPP swap). Same
-// chains, same epilogue as conv0_kernel, so the sum equals the unfused conv0 + conv11 bit for bit.
-// The accumulator exchange to the store layout is a lane permutation (ds_bpermute; no LDS
-// buffer), which keeps the kernel at 4 workgroups per CU with the cost-volume box.
-template <int TDI, int THI, bool F0 = false>
+template <int TDI, int THI>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void deconv3d_c8_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                           const float* __restrict__ alpha,
                                                           const float* __restrict__ shift,
                                                           const float* __restrict__ skip, float* __restrict__ y,
-                                                          Geo g, int ntiles, const float* __restrict__ f0x,
-                                                          const float* __restrict__ f0w,
-                                                          const float* __restrict__ f0al,
-                                                          const float* __restrict__ f0sh) {
-  const struct {
-    const float *x0, *w0, *al0, *sh0;
-  } f0{f0x, f0w, f0al, f0sh};
+                                                          Geo g, int ntiles) {
   constexpr int CIN = 16, COUT = 8, PL = 4;
   constexpr int NBW = TDI * THI / 4;
   constexpr int LW = 17, LH = THI + 1, LD = TDI + 1, VST = 16;
   constexpr int NVOX = LD * LH * LW;
   constexpr int NLD = (NVOX * 4 + 255) / 256;  // float4 staging loads per thread and tile
-  // F0: the cost-volume box of the tile's outputs (2TDI x 2THI x 32) plus the 3x3x3 halo
-  constexpr int XD = 2 * TDI + 2, XH = 2 * THI + 2, XW = 34, NX = XD * XH * XW;
-  constexpr int NLX = F0 ? (NX + 255) / 256 : 0;
   static_assert((TDI * THI) % 4 == 0, "tile");
   __shared__ __attribute__((aligned(16))) float tile[2][NVOX * VST];
   __shared__ __attribute__((aligned(16))) float wts[27 * 8 * 16];
-  __shared__ __attribute__((aligned(16))) float ep[F0 ? 1 : 4][32 * 8];
-  __shared__ float xs[F0 ? NX : 1];
-  __shared__ __attribute__((aligned(16))) float w0s[F0 ? 27 * 8 : 4];
+  __shared__ __attribute__((aligned(16))) float ep[4][32 * 8];
 
   const int nws = (g.Wi + 15) / 16, nhs = (g.Hi + THI - 1) / THI, nds = (g.Di + TDI - 1) / TDI;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1382,55 +1191,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       if (vox < NVOX) *reinterpret_cast<float4*>(buf + vox * VST + 4 * (q ^ ((vox >> 1) & 3))) = pf[k];
     }
   };
-  float px[NLX > 0 ? NLX : 1];
-  auto fetch_x = [&](int t) {  // F0: the tile's cost-volume box (zero outside the volume)
-    const TileCoord c = coord(t);
-    const float* x0n = f0.x0 + (size_t)c.n * g.Do * g.Ho * g.Wo;
-#pragma unroll
-    for (int k = 0; k < NLX; ++k) {
-      const int idx = threadIdx.x + 256 * k;
-      const int xw = idx % XW, rest = idx / XW, xh = rest % XH, xd = rest / XH;
-      const int ow = 2 * c.mw0 - 1 + xw, oh = 2 * c.mh0 - 1 + xh, od = 2 * c.md0 - 1 + xd;
-      px[k] = 0.f;
-      if (idx < NX && (unsigned)ow < (unsigned)g.Wo && (unsigned)oh < (unsigned)g.Ho && (unsigned)od < (unsigned)g.Do)
-        px[k] = x0n[((size_t)od * g.Ho + oh) * g.Wo + ow];
-    }
-  };
-  auto commit_x = [&]() {
-#pragma unroll
-    for (int k = 0; k < NLX; ++k) {
-      const int idx = threadIdx.x + 256 * k;
-      if (idx < NX) xs[idx] = px[k];
-    }
-  };
 
   for (int idx = threadIdx.x; idx < 27 * 8 * 4; idx += 256) {
     const int q = idx & 3, row = (idx >> 2) & 7, tap = idx >> 5;
     const float4 v = *reinterpret_cast<const float4*>(wpk + ((size_t)tap * COUT + row) * CIN + 4 * q);
     *reinterpret_cast<float4*>(wts + (tap * 8 + row) * 16 + 4 * (q ^ ((row >> 1) & 3))) = v;
   }
-  if constexpr (F0)
-    for (int idx = threadIdx.x; idx < 27 * 8; idx += 256) w0s[idx] = f0.w0[idx];
   const int co = col & 7;    // A row -> output channel
   const bool hi = col >= 8;  // rows 8-15: the odd-w output
-  float* eb = ep[F0 ? 0 : wv];
+  float* eb = ep[wv];
   const int cq = 4 * (kgrp & 1);
   const float4 al = *reinterpret_cast<const float4*>(alpha + cq);
   const float4 sh = *reinterpret_cast<const float4*>(shift + cq);
   auto wfrag = [&](int tap, VecN<PL>& a) { a.load(wts + (tap * 8 + co) * 16 + 4 * (kgrp ^ ((co >> 1) & 3))); };
-  // store layout: lane M holds channels 4*(M&1).. of output column 2*mw0 + (M>>1); the MFMA lane
-  // holding them is 16*(M&3) + (M>>2) (F0's permute source, in bytes)
-  const int perm_src = (16 * (lane & 3) + (lane >> 2)) * 4;
-  const int half = lane & 1, wl = lane >> 1;
 
   int t = t_lo + kx;
   if (t < t_hi) {
     fetch(t);
     commit(tile[0]);
-    if constexpr (F0) {
-      fetch_x(t);
-      commit_x();
-    }
   }
   __syncthreads();
   for (int it = 0; t < t_hi; t += per_xcd, ++it) {
@@ -1451,15 +1229,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const int md = c.md0 + rr / THI, mh = c.mh0 + rr % THI;
       ok[r] = md < g.Di && mh < g.Hi && ow < 2 * g.Wi;
       oo[r] = (out_n + ((size_t)(2 * md) * g.Ho + 2 * mh) * g.Wo + ow) * 8 + (lane & 1) * 4;
-      if constexpr (!F0) {
 #pragma unroll
-        for (int pdh = 0; pdh < 4; ++pdh)
-          sk[r][pdh] = (ok[r] && skip) ? *reinterpret_cast<const float4*>(skip + oo[r] + (pdh >> 1) * plane + (pdh & 1) * row)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+      for (int pdh = 0; pdh < 4; ++pdh)
+        sk[r][pdh] = (ok[r] && skip) ? *reinterpret_cast<const float4*>(skip + oo[r] + (pdh >> 1) * plane + (pdh & 1) * row)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if constexpr (F0)
-      if (tn < t_hi) fetch_x(tn);
     floatx4 acc[NBW][4];
 #pragma unroll
     for (int r = 0; r < NBW; ++r)
@@ -1500,83 +1274,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         }
     }
     // epilogue: lane (col, kgrp) holds channels 4*(kgrp&1).. of output w 2*(mw0+col) + (kgrp>>1);
-    // exchanged (LDS round trip, or F0's lane permute) so the skip read and the store are
-    // contiguous 1 KiB rows
+    // exchanged through LDS so the skip read and the store are contiguous 1 KiB rows
 #pragma unroll
     for (int r = 0; r < NBW; ++r)
 #pragma unroll
       for (int pdh = 0; pdh < 4; ++pdh) {
-        if constexpr (F0) {
-          if ((pdh & 1) == 0) {
-            // conv0 at this depth parity's two output rows from the cost-volume box
-            // (conv0_kernel's chains and epilogue)
-            const int rr = wv * NBW + r;
-            const int mdl = rr / THI, mhl = rr % THI, pd = pdh >> 1;
-            float4 res[2];
-#pragma unroll
-            for (int pass = 0; pass < 2; ++pass) {
-              const int ph = (pass == half) ? 0 : 1;
-              const float* xb = xs + ((2 * mdl + pd) * XH + 2 * mhl + ph) * XW + wl;
-              float2_v a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
-#pragma unroll
-              for (int tp = 0; tp < 27; ++tp) {
-                const float xv = xb[((tp / 9) * XH + (tp / 3) % 3) * XW + tp % 3];
-                const float4 wq = *reinterpret_cast<const float4*>(w0s + tp * 8 + 4 * pass);
-                a0 = __builtin_elementwise_fma(float2_v{wq.x, wq.y}, float2_v{xv, xv}, a0);
-                a1 = __builtin_elementwise_fma(float2_v{wq.z, wq.w}, float2_v{xv, xv}, a1);
-              }
-              const float* ab = f0.al0 + 4 * pass;
-              const float* sb = f0.sh0 + 4 * pass;
-              res[pass] = make_float4(act(fmaf(a0.x, ab[0], sb[0]), 0.f), act(fmaf(a0.y, ab[1], sb[1]), 0.f),
-                                      act(fmaf(a1.x, ab[2], sb[2]), 0.f), act(fmaf(a1.y, ab[3], sb[3]), 0.f));
-              __builtin_amdgcn_sched_barrier(0);  // one pass's taps and weights in registers at a time
-            }
-            // row ph = 0: this lane's own quad; row ph = 1: the neighbour's (quad_perm [1,0,3,2])
-            const float4 mine = half ? res[0] : res[1];
-            sk[r][pdh] = half ? res[1] : res[0];
-            sk[r][pdh + 1] = make_float4(
-                __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mine.x), 0xB1, 0xF, 0xF, false)),
-                __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mine.y), 0xB1, 0xF, 0xF, false)),
-                __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mine.z), 0xB1, 0xF, 0xF, false)),
-                __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mine.w), 0xB1, 0xF, 0xF, false)));
-          }
-        }
         const floatx4 a = acc[r][pdh];
-        const float4 o = make_float4(act(fmaf(a[0], al.x, sh.x), g.lo), act(fmaf(a[1], al.y, sh.y), g.lo),
-                                     act(fmaf(a[2], al.z, sh.z), g.lo), act(fmaf(a[3], al.w, sh.w), g.lo));
-        float4 v;
-        if constexpr (F0) {
-          v = make_float4(__int_as_float(__builtin_amdgcn_ds_bpermute(perm_src, __float_as_int(o.x))),
-                          __int_as_float(__builtin_amdgcn_ds_bpermute(perm_src, __float_as_int(o.y))),
-                          __int_as_float(__builtin_amdgcn_ds_bpermute(perm_src, __float_as_int(o.z))),
-                          __int_as_float(__builtin_amdgcn_ds_bpermute(perm_src, __float_as_int(o.w))));
-        } else {
-          *reinterpret_cast<float4*>(eb + (2 * col + (kgrp >> 1)) * 8 + cq) = o;
-          __builtin_amdgcn_wave_barrier();
-          v = *reinterpret_cast<const float4*>(eb + lane * 4);
-          __builtin_amdgcn_wave_barrier();
-        }
+        *reinterpret_cast<float4*>(eb + (2 * col + (kgrp >> 1)) * 8 + cq) =
+            make_float4(act(fmaf(a[0], al.x, sh.x), g.lo), act(fmaf(a[1], al.y, sh.y), g.lo), act(fmaf(a[2], al.z, sh.z), g.lo),
+                        act(fmaf(a[3], al.w, sh.w), g.lo));
+        __builtin_amdgcn_wave_barrier();
+        const float4 v = *reinterpret_cast<const float4*>(eb + lane * 4);
+        __builtin_amdgcn_wave_barrier();
         const float4 sv = sk[r][pdh];
         if (ok[r])
           *reinterpret_cast<float4*>(y + oo[r] + (pdh >> 1) * plane + (pdh & 1) * row) =
               make_float4(sv.x + v.x, sv.y + v.y, sv.z + v.z, sv.w + v.w);
       }
     if (tn < t_hi) commit(tile[(it + 1) & 1]);
-    if constexpr (F0) {
-      __syncthreads();  // every wave is done with the cost-volume box: the next one may be committed
-      if (tn < t_hi) commit_x();
-    }
     __syncthreads();
   }
 }
 
-template <int TDI, int THI, bool F0 = false>
+template <int TDI, int THI>
 static int launch_deconv_c8(const float* x, const float* w, const float* al, const float* sh, const float* skip,
-                            float* y, int B, const Geo& g, hipStream_t st, Conv0Fuse f0 = Conv0Fuse{}) {
+                            float* y, int B, const Geo& g, hipStream_t st) {
   const long ntiles = (long)B * ((g.Di + TDI - 1) / TDI) * ((g.Hi + THI - 1) / THI) * ((g.Wi + 15) / 16);
-  const long grid = persistent_grid(deconv3d_c8_kernel<TDI, THI, F0>, ntiles);
-  hipLaunchKernelGGL((deconv3d_c8_kernel<TDI, THI, F0>), dim3((unsigned)grid), dim3(256), 0, st, x, w, al, sh, skip, y,
-                     g, (int)ntiles, f0.x0, f0.w0, f0.al0, f0.sh0);
+  const long grid = persistent_grid(deconv3d_c8_kernel<TDI, THI>, ntiles);
+  hipLaunchKernelGGL((deconv3d_c8_kernel<TDI, THI>), dim3((unsigned)grid), dim3(256), 0, st, x, w, al, sh, skip, y, g,
+                     (int)ntiles);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -1681,21 +1407,6 @@ static int deconv_dispatch(const float* x, int B, int cin, int d, int h, int w, 
   return TMVS_ERR_SHAPE;
 }
 
-// conv11 (16 -> 8) + conv0 recomputed from the cost volume x0 as its skip (deconv3d_c8_kernel F0)
-static int deconv11_conv0_skip(const float* x, int B, int d, int h, int w, const float* wpk, const float* al,
-                               const float* sh, const Conv0Fuse& f0, float* y, hipStream_t st) {
-  Geo g;
-  g.lo = 0.f;
-  g.Di = d;
-  g.Hi = h;
-  g.Wi = w;
-  g.Do = 2 * d;
-  g.Ho = 2 * h;
-  g.Wo = 2 * w;
-  if (g.Di % 2 == 0) return launch_deconv_c8<2, 2, true>(x, wpk, al, sh, nullptr, y, B, g, st, f0);
-  return launch_deconv_c8<1, 4, true>(x, wpk, al, sh, nullptr, y, B, g, st, f0);
-}
-
 }  // namespace tmvs
 
 using namespace tmvs;
@@ -1781,9 +1492,6 @@ extern "C" size_t tmvs_costregnet_workspace(int batch, int depth, int height, in
   return bytes;
 }
 
-#ifndef TMVS_DECONV11_F0
-#define TMVS_DECONV11_F0 1
-#endif
 // CostRegNet up to conv11 + skip (models/module.py:447-455); *x11_out = the 8-channel
 // full-resolution NDHWC volume the prob conv reads, *c0_out = conv0's (dead once x11 exists).
 static int costregnet_trunk(const float* x, int batch, int depth, int height, int width, const TmvsCostRegWeights* w,
@@ -1823,29 +1531,11 @@ static int costregnet_trunk(const float* x, int batch, int depth, int height, in
   const int D2 = D1 / 2, H2 = H1 / 2, W2 = W1 / 2;
   const int D3 = D2 / 2, H3 = H2 / 2, W3 = W2 / 2;
   int rc;
-#ifndef TMVS_CONV1_F0
-#define TMVS_CONV1_F0 1
-#endif
-  const Conv0Fuse f0{x, w->w[0], w->alpha[0], w->shift[0]};
-  if (TMVS_CONV1_F0 && TMVS_DECONV11_F0) {  // conv0 lives only inside conv1 and conv11's skip
-    Geo g;
-    g.lo = 0.f;
-    g.Di = D0;
-    g.Hi = H0;
-    g.Wi = W0;
-    g.Do = D0 / 2;
-    g.Ho = H0 / 2;
-    g.Wo = W0 / 2;
-    if ((rc = launch_conv_s2c8_tile<TMVS_S2C8_TD, TMVS_S2C8_TH, true>(nullptr, w->w[1], w->alpha[1], w->shift[1], c1,
-                                                                       batch, g, st, f0)))
-      return rc;
-  } else {
-    const dim3 g0x((unsigned)(((W0 + kProbCols - 1) / kProbCols) * ((H0 + 3) / 4) * batch * ((D0 + kDChunk - 1) / kDChunk)));
-    hipLaunchKernelGGL(conv0_kernel, g0x, dim3(256), 0, st, x, c0, D0, H0, W0, w->w[0], w->alpha[0], w->shift[0],
-                       0.f);
-    TMVS_CHECK_LAUNCH();
-    if ((rc = conv_dispatch(c0, batch, c, D0, H0, W0, w->w[1], w->alpha[1], w->shift[1], 2 * c, 2, c1, st))) return rc;
-  }
+  const dim3 g0x((unsigned)(((W0 + kProbCols - 1) / kProbCols) * ((H0 + 3) / 4) * batch * ((D0 + kDChunk - 1) / kDChunk)));
+  hipLaunchKernelGGL(conv0_kernel, g0x, dim3(256), 0, st, x, c0, D0, H0, W0, w->w[0], w->alpha[0], w->shift[0],
+                     0.f);
+  TMVS_CHECK_LAUNCH();
+  if ((rc = conv_dispatch(c0, batch, c, D0, H0, W0, w->w[1], w->alpha[1], w->shift[1], 2 * c, 2, c1, st))) return rc;
   if ((rc = conv_dispatch(c1, batch, 2 * c, D1, H1, W1, w->w[2], w->alpha[2], w->shift[2], 2 * c, 1, c2, st)))
     return rc;
   if ((rc = conv_dispatch(c2, batch, 2 * c, D1, H1, W1, w->w[3], w->alpha[3], w->shift[3], 4 * c, 2, c3, st)))
@@ -1860,12 +1550,8 @@ static int costregnet_trunk(const float* x, int batch, int depth, int height, in
     return rc;
   if ((rc = deconv_dispatch(x7, batch, 4 * c, D2, H2, W2, w->w[8], w->alpha[8], w->shift[8], 2 * c, c2, x9, st)))
     return rc;
-#if TMVS_DECONV11_F0
-  if ((rc = deconv11_conv0_skip(x9, batch, D1, H1, W1, w->w[9], w->alpha[9], w->shift[9], f0, x11, st))) return rc;
-#else
   if ((rc = deconv_dispatch(x9, batch, 2 * c, D1, H1, W1, w->w[9], w->alpha[9], w->shift[9], c, c0, x11, st)))
     return rc;
-#endif
   *x11_out = x11;
   *c0_out = c0;
   return TMVS_OK;
