@@ -189,10 +189,10 @@ __device__ __forceinline__ void tile_reduce(long v0, long v1, LoadA load_a, Load
 }
 
 // the matrix-core form (reduce_mfma.h) wherever both sides have >= 8 channels
-template <int A, int BC, typename LoadA, typename LoadB>
+template <int A, int BC, bool BROW = false, typename LoadA, typename LoadB>
 __device__ __forceinline__ void tile_reduce_any(long v0, long v1, LoadA load_a, LoadB load_b, double* __restrict__ out) {
   if constexpr (A % 8 == 0 && BC % 8 == 0)
-    tile_reduce_mfma<A, BC>(v0, v1, load_a, load_b, out);
+    tile_reduce_mfma<A, BC, BROW>(v0, v1, load_a, load_b, out);
   else
     tile_reduce<A, BC>(v0, v1, load_a, load_b, out);
 }
@@ -574,7 +574,12 @@ __global__ __launch_bounds__(kBlk) void dcn_gather_windows_kernel(const float* _
   dx[i] = dx[i] + s;
 }
 
-// dW[k][o][c] = sum_p dy[p][o] col_k[p][c]: grid (nblk, 9), block partials [nblk][9][CO][32]
+// dW[k][o][c] = sum_p dy[p][o] col_k[p][c]: grid (nblk, 9), block partials [nblk][9][CO][32]. A thread
+// stages two channel quads of one pixel (BROW), so the pixel's sample geometry (offsets, sigmoid mask,
+// bilinear weights) is derived once for both instead of once per quad.
+#ifndef TMVS_DCNW_BROW
+#define TMVS_DCNW_BROW 1
+#endif
 template <int CO>
 __global__ __launch_bounds__(kBlk) void dcn_bwd_weight_kernel(const float* __restrict__ x, const float* __restrict__ om,
                                                              const float* __restrict__ dy, int B, int H, int W, long ppb,
@@ -583,12 +588,8 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_weight_kernel(const float* __res
   const long HW = (long)H * W, np = (long)B * HW;
   const long v0 = (long)blockIdx.x * ppb, v1 = v0 + ppb < np ? v0 + ppb : np;
   auto la = [&](long v, int q) { return *reinterpret_cast<const float4*>(dy + (size_t)v * CO + 4 * q); };
-  auto lb = [&](long v, int q) {
-    const int b = (int)(v / HW);
-    const long p = v - (long)b * HW;
-    const int yy = (int)(p / W), xx = (int)(p % W);
-    const DcnSample s = dcn_sample(om + (size_t)b * 27 * HW + p, (size_t)HW, yy, xx, k, H, W);
-    if (!s.inside) return make_float4(0.f, 0.f, 0.f, 0.f);
+  // the column value of one channel quad at (pixel v, tap k), given the pixel's sample
+  auto col_quad = [&](const DcnSample& s, int b, int q) {
     const float wq[4] = {s.hy * s.hx, s.hy * s.lx, s.ly * s.hx, s.ly * s.lx};
     const float* xb = x + (size_t)b * HW * 32 + 4 * q;
     float4 v4[4];
@@ -608,7 +609,29 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_weight_kernel(const float* __res
     return make_float4(blend(v4[0].x, v4[1].x, v4[2].x, v4[3].x), blend(v4[0].y, v4[1].y, v4[2].y, v4[3].y),
                        blend(v4[0].z, v4[1].z, v4[2].z, v4[3].z), blend(v4[0].w, v4[1].w, v4[2].w, v4[3].w));
   };
-  tile_reduce_any<CO, 32>(v0, v1, la, lb, partial + ((size_t)blockIdx.x * 9 + k) * CO * 32);
+  auto sample_at = [&](long v, int& b) {
+    b = (int)(v / HW);
+    const long p = v - (long)b * HW;
+    const int yy = (int)(p / W), xx = (int)(p % W);
+    return dcn_sample(om + (size_t)b * 27 * HW + p, (size_t)HW, yy, xx, k, H, W);
+  };
+#if TMVS_DCNW_BROW
+  auto lb = [&](long v, int q0, float4 (&o)[2]) {
+    int b;
+    const DcnSample s = sample_at(v, b);
+    if (!s.inside) return;  // (o is zero)
+    o[0] = col_quad(s, b, q0);
+    o[1] = col_quad(s, b, q0 + 1);
+  };
+#else
+  auto lb = [&](long v, int q) {
+    int b;
+    const DcnSample s = sample_at(v, b);
+    if (!s.inside) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return col_quad(s, b, q);
+  };
+#endif
+  tile_reduce_any<CO, 32, TMVS_DCNW_BROW>(v0, v1, la, lb, partial + ((size_t)blockIdx.x * 9 + k) * CO * 32);
 }
 
 // ---------------------------------------------------------------- small backward pieces

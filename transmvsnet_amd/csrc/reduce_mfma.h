@@ -14,7 +14,11 @@ namespace tmvs {
 // load_a(v, q) / load_b(v, q): float4 q of row v (zeros where a gathered tap is outside); out: the
 // block's A x BC partial, fp64. The next chunk's rows are loaded into registers while this chunk's MFMAs run.
 typedef float floatx4_t __attribute__((ext_vector_type(4)));
-template <int A, int BC, typename LoadA, typename LoadB>
+// BROW: thread t stages B quads 2(t&3), 2(t&3)+1 of row t>>2 (BC = 32) with one loader call
+// load_b(v, q0, float4 (&)[2]) instead of quad t&7 of rows t>>3 and t>>3 + 32: a gathered B row whose
+// loader derives per-row state (the DCN sample geometry) derives it once for both quads. Same LDS
+// contents, same sums.
+template <int A, int BC, bool BROW = false, typename LoadA, typename LoadB>
 __device__ __forceinline__ void tile_reduce_mfma(long v0, long v1, LoadA load_a, LoadB load_b,
                                                  double* __restrict__ out) {
   // A or BC of 8 are zero-padded to 16 (half the matrix-core rows idle, still far above the VALU form)
@@ -26,6 +30,7 @@ __device__ __forceinline__ void tile_reduce_mfma(long v0, long v1, LoadA load_a,
   static_assert(A % 4 == 0 && BC % 4 == 0 && (NT % 4 == 0 || 4 % NT == 0), "tile");
   constexpr int LA = CH * AP / 4 / 256, LB = CH * BP / 4 / 256;  // float4 loads per thread and chunk
   static_assert(CH * AP / 4 % 256 == 0 && CH * BP / 4 % 256 == 0, "staging");
+  static_assert(!BROW || (BP == 32 && LB == 2), "BROW: 64 rows x 8 quads, 2 per thread");
   __shared__ __attribute__((aligned(16))) float lds[CH * (SA + SB)];
   __shared__ double cmb[KS > 1 ? (KS - 1) * NT * 256 : 1];
   float* sa = lds;
@@ -45,10 +50,16 @@ __device__ __forceinline__ void tile_reduce_mfma(long v0, long v1, LoadA load_a,
       const int i = threadIdx.x + 256 * k, r = i / (AP / 4), q = i % (AP / 4);
       pa[k] = (vb + r < v1 && q < A / 4) ? load_a(vb + r, q) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    if constexpr (BROW) {  // load_b(v, q0, float4 (&)[2]): quads q0, q0 + 1 of row v
+      const int r = (int)threadIdx.x >> 2;
+      pb[0] = pb[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (vb + r < v1) load_b(vb + r, 2 * (int)(threadIdx.x & 3), pb);
+    } else {
 #pragma unroll
-    for (int k = 0; k < LB; ++k) {
-      const int i = threadIdx.x + 256 * k, r = i / (BP / 4), q = i % (BP / 4);
-      pb[k] = (vb + r < v1 && q < BC / 4) ? load_b(vb + r, q) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k = 0; k < LB; ++k) {
+        const int i = threadIdx.x + 256 * k, r = i / (BP / 4), q = i % (BP / 4);
+        pb[k] = (vb + r < v1 && q < BC / 4) ? load_b(vb + r, q) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
   };
   auto commit = [&]() {
@@ -59,7 +70,8 @@ __device__ __forceinline__ void tile_reduce_mfma(long v0, long v1, LoadA load_a,
     }
 #pragma unroll
     for (int k = 0; k < LB; ++k) {
-      const int i = threadIdx.x + 256 * k, r = i / (BP / 4), q = i % (BP / 4);
+      const int i = threadIdx.x + 256 * k;
+      const int r = BROW ? (int)threadIdx.x >> 2 : i / (BP / 4), q = BROW ? 2 * (threadIdx.x & 3) + k : i % (BP / 4);
       *reinterpret_cast<float4*>(sb + r * SB + 4 * q) = pb[k];
     }
   };
