@@ -580,13 +580,24 @@ __global__ __launch_bounds__(kBlk) void dcn_gather_windows_kernel(const float* _
 #ifndef TMVS_DCNW_BROW
 #define TMVS_DCNW_BROW 1
 #endif
+#ifndef TMVS_DCNW_XCD
+#define TMVS_DCNW_XCD 1
+#endif
 template <int CO>
 __global__ __launch_bounds__(kBlk) void dcn_bwd_weight_kernel(const float* __restrict__ x, const float* __restrict__ om,
                                                              const float* __restrict__ dy, int B, int H, int W, long ppb,
-                                                             double* __restrict__ partial) {
-  const int k = blockIdx.y;
+                                                             int nblk, double* __restrict__ partial) {
+#if TMVS_DCNW_XCD
+  // 1-D grid of (pixel range, tap) pairs dealt out so that the 9 taps of a pixel range share blockIdx % 8,
+  // i.e. one XCD and its L2: the taps gather the same input neighbourhood and the same dy rows
+  const int grp = blockIdx.x / 72, within = blockIdx.x % 72;
+  const int k = within / 8, rb = grp * 8 + within % 8;
+  if (rb >= nblk) return;
+#else
+  const int k = blockIdx.y, rb = blockIdx.x;
+#endif
   const long HW = (long)H * W, np = (long)B * HW;
-  const long v0 = (long)blockIdx.x * ppb, v1 = v0 + ppb < np ? v0 + ppb : np;
+  const long v0 = (long)rb * ppb, v1 = v0 + ppb < np ? v0 + ppb : np;
   auto la = [&](long v, int q) { return *reinterpret_cast<const float4*>(dy + (size_t)v * CO + 4 * q); };
   // the column value of one channel quad at (pixel v, tap k), given the pixel's sample
   auto col_quad = [&](const DcnSample& s, int b, int q) {
@@ -631,7 +642,7 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_weight_kernel(const float* __res
     return col_quad(s, b, q);
   };
 #endif
-  tile_reduce_any<CO, 32, TMVS_DCNW_BROW>(v0, v1, la, lb, partial + ((size_t)blockIdx.x * 9 + k) * CO * 32);
+  tile_reduce_any<CO, 32, TMVS_DCNW_BROW>(v0, v1, la, lb, partial + ((size_t)rb * 9 + k) * CO * 32);
 }
 
 // ---------------------------------------------------------------- small backward pieces
@@ -820,8 +831,8 @@ extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, 
     hipLaunchKernelGGL(dcn_gather_windows_kernel, dim3((unsigned)((np * 32 + kBlk - 1) / kBlk)), dim3(kBlk), 0, st,  \
                        (const float*)scratch, batch, height, width, dx_nhwc);                                     \
     TMVS_CHECK_LAUNCH();                                                                                          \
-    hipLaunchKernelGGL(dcn_bwd_weight_kernel<CO>, dim3(nblk, 9), dim3(kBlk), 0, st, x_nhwc, offset_mask, dy_nhwc,   \
-                       batch, height, width, ppb, part);                                                          \
+    hipLaunchKernelGGL(dcn_bwd_weight_kernel<CO>, TMVS_DCNW_XCD ? dim3((nblk + 7) / 8 * 72) : dim3(nblk, 9), dim3(kBlk), \
+                       0, st, x_nhwc, offset_mask, dy_nhwc, batch, height, width, ppb, nblk, part);             \
     break;
   switch (cout) {
     TMVS_DCNB(8)
