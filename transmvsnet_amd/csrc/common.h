@@ -26,6 +26,31 @@ __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 
 // Bijective XCD-aware block remap (cdna_hip_programming.md T1): blocks b and b+8 share
 // an XCD, so give each XCD a contiguous chunk of the tile space.
+// Weight-gradient grids of (pixel-range block, tap) pairs as a 1-D grid of xcd_range_tap_grid(ntaps, nblk)
+// blocks, dealt out so the ntaps blocks of one range share blockIdx % 8 -- one XCD, one L2: the taps
+// gather overlapping input neighbourhoods and the same output-gradient rows. false for padding blocks.
+#ifndef TMVS_WGRAD_XCD
+#define TMVS_WGRAD_XCD 1
+#endif
+__device__ __forceinline__ bool xcd_range_tap(int ntaps, int nblk, int& rb, int& k) {
+#if TMVS_WGRAD_XCD
+  const int per = 8 * ntaps;
+  const int grp = blockIdx.x / per, within = blockIdx.x % per;
+  k = within / 8;
+  rb = grp * 8 + within % 8;
+  return rb < nblk;
+#else
+  (void)ntaps;
+  (void)nblk;
+  k = blockIdx.y;
+  rb = blockIdx.x;
+  return true;
+#endif
+}
+static inline dim3 xcd_range_tap_grid(int ntaps, int nblk) {
+  return TMVS_WGRAD_XCD ? dim3((unsigned)((nblk + 7) / 8 * 8 * ntaps)) : dim3((unsigned)nblk, (unsigned)ntaps);
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   const int xcd = bid & 7;
   const int q = nblk >> 3, r = nblk & 7;

@@ -184,12 +184,13 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_kernel(
 template <int A, int BC>
 __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_tile_kernel(
     const float* __restrict__ direct, const float* __restrict__ gath, int B, int Pd, int Ph, int Pw, int Gd, int Gh,
-    int Gw, int stride, long vpb, double* __restrict__ partial) {
-  const int k = blockIdx.y;
+    int Gw, int stride, long vpb, int nblk, double* __restrict__ partial) {
+  int rb, k;  // the 27 taps of a voxel range on one XCD (common.h)
+  if (!xcd_range_tap(27, nblk, rb, k)) return;
   const int kd = k / 9, kh = (k / 3) % 3, kw = k % 3;
   if constexpr (A % 8 == 0 && BC % 8 == 0) {  // on the matrix cores (reduce_mfma.h)
     const long nv = (long)B * Pd * Ph * Pw;
-    const long u0 = (long)blockIdx.x * vpb, u1 = u0 + vpb < nv ? u0 + vpb : nv;
+    const long u0 = (long)rb * vpb, u1 = u0 + vpb < nv ? u0 + vpb : nv;
     auto la = [&](long v, int q) { return *reinterpret_cast<const float4*>(direct + v * A + 4 * q); };
     auto lb = [&](long v, int q) {
       const int pw = (int)(v % Pw);
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_tile_kernel(
       if (gd < 0 || gh < 0 || gw < 0 || gd >= Gd || gh >= Gh || gw >= Gw) return make_float4(0.f, 0.f, 0.f, 0.f);
       return *reinterpret_cast<const float4*>(gath + ((((size_t)b * Gd + gd) * Gh + gh) * Gw + gw) * BC + 4 * q);
     };
-    tile_reduce_mfma<A, BC>(u0, u1, la, lb, partial + ((size_t)blockIdx.x * 27 + k) * A * BC);
+    tile_reduce_mfma<A, BC>(u0, u1, la, lb, partial + ((size_t)rb * 27 + k) * A * BC);
     return;
   }
   constexpr int CH = 64, TA = A / 8, TB = BC / 8, SA = A + 4, SB = BC + 4;
@@ -213,7 +214,7 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_tile_kernel(
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ci = lane & 7, ai = lane >> 3;
   const long nvox = (long)B * Pd * Ph * Pw;
-  const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
+  const long v0 = (long)rb * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
   double acc[TA][TB];
 #pragma unroll
   for (int i = 0; i < TA; ++i)
@@ -294,7 +295,7 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_tile_kernel(
         for (int j = 0; j < TB; ++j) acc[i][j] += cmb[(ai * TA + i) * BC + ci * TB + j];
   }
   if (wv == 0) {
-    double* out = partial + ((size_t)blockIdx.x * 27 + k) * A * BC;
+    double* out = partial + ((size_t)rb * 27 + k) * A * BC;
 #pragma unroll
     for (int i = 0; i < TA; ++i)
 #pragma unroll
@@ -703,8 +704,8 @@ static int launch_wgrad(const float* direct, const float* gath, int B, int Pd, i
     hipLaunchKernelGGL((conv3d_wgrad_small_kernel<A, BC>), dim3(nblk, 27), dim3(kTrainBlock), 0, st, direct, gath, B,
                        Pd, Ph, Pw, Gd, Gh, Gw, stride, vpb, ws);
   else if constexpr (A >= 8 && BC >= 8)
-    hipLaunchKernelGGL((conv3d_wgrad_tile_kernel<A, BC>), dim3(nblk, 27), dim3(kTrainBlock), 0, st, direct, gath, B,
-                       Pd, Ph, Pw, Gd, Gh, Gw, stride, vpb, ws);
+    hipLaunchKernelGGL((conv3d_wgrad_tile_kernel<A, BC>), xcd_range_tap_grid(27, nblk), dim3(kTrainBlock), 0, st, direct,
+                       gath, B, Pd, Ph, Pw, Gd, Gh, Gw, stride, vpb, nblk, ws);
   else
     hipLaunchKernelGGL((conv3d_wgrad_kernel<A, BC>), dim3(nblk, 27), dim3(kTrainBlock), 0, st, direct, gath, B, Pd,
                        Ph, Pw, Gd, Gh, Gw, stride, vpb, ws);

@@ -211,10 +211,12 @@ template <int AP, int BC>
 __global__ __launch_bounds__(kBlk) void conv2d_wgrad_kernel(const float* __restrict__ direct, int a_ch,
                                                            const float* __restrict__ gath, int B, int Ph, int Pw,
                                                            int Gh, int Gw, int K, int stride, int pad, long ppb,
-                                                           double* __restrict__ partial) {
-  const int k = blockIdx.y, kh = k / K, kw = k % K;
+                                                           int nblk, double* __restrict__ partial) {
+  int rb, k;
+  if (!xcd_range_tap(K * K, nblk, rb, k)) return;
+  const int kh = k / K, kw = k % K;
   const long np = (long)B * Ph * Pw;
-  const long v0 = (long)blockIdx.x * ppb, v1 = v0 + ppb < np ? v0 + ppb : np;
+  const long v0 = (long)rb * ppb, v1 = v0 + ppb < np ? v0 + ppb : np;
   auto la = [&](long v, int q) { return load_row4(direct, v, a_ch, q); };
   auto lb = [&](long v, int q) {
     const int pw = (int)(v % Pw);
@@ -224,7 +226,7 @@ __global__ __launch_bounds__(kBlk) void conv2d_wgrad_kernel(const float* __restr
     if (gh < 0 || gw < 0 || gh >= Gh || gw >= Gw) return make_float4(0.f, 0.f, 0.f, 0.f);
     return *reinterpret_cast<const float4*>(gath + (((size_t)b * Gh + gh) * Gw + gw) * BC + 4 * q);
   };
-  tile_reduce_any<AP, BC>(v0, v1, la, lb, partial + ((size_t)blockIdx.x * K * K + k) * AP * BC);
+  tile_reduce_any<AP, BC>(v0, v1, la, lb, partial + ((size_t)rb * K * K + k) * AP * BC);
 }
 
 // few channels on the gathered side (the image: 3): thread t owns pairs t, t+256, .. of a x b,
@@ -233,12 +235,14 @@ template <int A, int BC>
 __global__ __launch_bounds__(kBlk) void conv2d_wgrad_small_kernel(const float* __restrict__ direct,
                                                                  const float* __restrict__ gath, int B, int Ph, int Pw,
                                                                  int Gh, int Gw, int K, int stride, int pad, long ppb,
-                                                                 double* __restrict__ partial) {
+                                                                 int nblk, double* __restrict__ partial) {
   constexpr int NPR = A * BC;
   __shared__ double red[NPR][kBlk / 64];
-  const int k = blockIdx.y, kh = k / K, kw = k % K;
+  int rb, k;
+  if (!xcd_range_tap(K * K, nblk, rb, k)) return;
+  const int kh = k / K, kw = k % K;
   const long np = (long)B * Ph * Pw;
-  const long v0 = (long)blockIdx.x * ppb, v1 = v0 + ppb < np ? v0 + ppb : np;
+  const long v0 = (long)rb * ppb, v1 = v0 + ppb < np ? v0 + ppb : np;
   float acc[NPR];
 #pragma unroll
   for (int q = 0; q < NPR; ++q) acc[q] = 0.f;
@@ -269,7 +273,7 @@ __global__ __launch_bounds__(kBlk) void conv2d_wgrad_small_kernel(const float* _
   }
   __syncthreads();
   for (int i = threadIdx.x; i < NPR; i += kBlk)
-    partial[((size_t)blockIdx.x * K * K + k) * NPR + i] = (red[i][0] + red[i][1]) + (red[i][2] + red[i][3]);
+    partial[((size_t)rb * K * K + k) * NPR + i] = (red[i][0] + red[i][1]) + (red[i][2] + red[i][3]);
 }
 
 // out[i] = sum_j partial[j][i] in a fixed order (8 interleaved chains, then the chains in order)
@@ -580,22 +584,13 @@ __global__ __launch_bounds__(kBlk) void dcn_gather_windows_kernel(const float* _
 #ifndef TMVS_DCNW_BROW
 #define TMVS_DCNW_BROW 1
 #endif
-#ifndef TMVS_DCNW_XCD
-#define TMVS_DCNW_XCD 1
-#endif
 template <int CO>
 __global__ __launch_bounds__(kBlk) void dcn_bwd_weight_kernel(const float* __restrict__ x, const float* __restrict__ om,
                                                              const float* __restrict__ dy, int B, int H, int W, long ppb,
                                                              int nblk, double* __restrict__ partial) {
-#if TMVS_DCNW_XCD
-  // 1-D grid of (pixel range, tap) pairs dealt out so that the 9 taps of a pixel range share blockIdx % 8,
-  // i.e. one XCD and its L2: the taps gather the same input neighbourhood and the same dy rows
-  const int grp = blockIdx.x / 72, within = blockIdx.x % 72;
-  const int k = within / 8, rb = grp * 8 + within % 8;
-  if (rb >= nblk) return;
-#else
-  const int k = blockIdx.y, rb = blockIdx.x;
-#endif
+  // the 9 taps of a pixel range on one XCD (common.h: they gather the same input neighbourhood, r14l)
+  int rb, k;
+  if (!xcd_range_tap(9, nblk, rb, k)) return;
   const long HW = (long)H * W, np = (long)B * HW;
   const long v0 = (long)rb * ppb, v1 = v0 + ppb < np ? v0 + ppb : np;
   auto la = [&](long v, int q) { return *reinterpret_cast<const float4*>(dy + (size_t)v * CO + 4 * q); };
@@ -740,16 +735,16 @@ extern "C" int tmvs_conv2d_wgrad(const float* direct, int a_ch, int batch, int p
   bool done = false;
 #define TMVS_WG2(AP, BC)                                                                                         \
   if (!done && ap == AP && b_ch == BC) {                                                                         \
-    hipLaunchKernelGGL((conv2d_wgrad_kernel<AP, BC>), dim3(nblk, k * k), dim3(kBlk), 0, st, direct, a_ch, gathered, \
-                       batch, ph, pw, gh, gw, k, stride, pad, ppb, part);                                        \
+    hipLaunchKernelGGL((conv2d_wgrad_kernel<AP, BC>), xcd_range_tap_grid(k * k, nblk), dim3(kBlk), 0, st, direct,   \
+                       a_ch, gathered, batch, ph, pw, gh, gw, k, stride, pad, ppb, nblk, part);                 \
     done = true;                                                                                                 \
   }
   TMVS_WG2(8, 8) TMVS_WG2(8, 16) TMVS_WG2(8, 32) TMVS_WG2(16, 8) TMVS_WG2(16, 16) TMVS_WG2(16, 32) TMVS_WG2(32, 8)
   TMVS_WG2(32, 16) TMVS_WG2(32, 32)
 #undef TMVS_WG2
   if (!done && a_ch == 8 && b_ch == 3) {
-    hipLaunchKernelGGL((conv2d_wgrad_small_kernel<8, 3>), dim3(nblk, k * k), dim3(kBlk), 0, st, direct, gathered,
-                       batch, ph, pw, gh, gw, k, stride, pad, ppb, part);
+    hipLaunchKernelGGL((conv2d_wgrad_small_kernel<8, 3>), xcd_range_tap_grid(k * k, nblk), dim3(kBlk), 0, st, direct,
+                       gathered, batch, ph, pw, gh, gw, k, stride, pad, ppb, nblk, part);
     ap = 8;
     done = true;
   }
@@ -831,8 +826,8 @@ extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, 
     hipLaunchKernelGGL(dcn_gather_windows_kernel, dim3((unsigned)((np * 32 + kBlk - 1) / kBlk)), dim3(kBlk), 0, st,  \
                        (const float*)scratch, batch, height, width, dx_nhwc);                                     \
     TMVS_CHECK_LAUNCH();                                                                                          \
-    hipLaunchKernelGGL(dcn_bwd_weight_kernel<CO>, TMVS_DCNW_XCD ? dim3((nblk + 7) / 8 * 72) : dim3(nblk, 9), dim3(kBlk), \
-                       0, st, x_nhwc, offset_mask, dy_nhwc, batch, height, width, ppb, nblk, part);             \
+    hipLaunchKernelGGL(dcn_bwd_weight_kernel<CO>, xcd_range_tap_grid(9, nblk), dim3(kBlk), 0, st, x_nhwc,          \
+                       offset_mask, dy_nhwc, batch, height, width, ppb, nblk, part);                            \
     break;
   switch (cout) {
     TMVS_DCNB(8)
