@@ -498,15 +498,36 @@ __global__ __launch_bounds__(kTrainBlock) void bn_stats_partial_kernel(const flo
   const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
   double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};  // 4 independent chains
   long v = v0 + r0;
-  for (; v + 3L * rs < v1; v += 4L * rs) {
-    float x[4];
+  // groups of 4 rows, two in flight: group g+1's loads are issued before group g is accumulated
+  // (a block walks up to thousands of rows; one group at a time left each load's latency exposed);
+  // the groups are accumulated in order. (A generic ring of 2-4 groups under a rolled loop measured
+  // slower than this hand-unrolled pair, r14t.)
+  auto load4 = [&](long vv, float (&x)[4]) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) x[j] = z[(v + (long)j * rs) * C + c];
+    for (int j = 0; j < 4; ++j) x[j] = z[(vv + (long)j * rs) * C + c];
+  };
+  auto add4 = [&](const float (&x)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       s[j] += (double)x[j];
       q[j] += (double)x[j] * (double)x[j];
     }
+  };
+  float xa[4], xb[4];
+  if (v + 3L * rs < v1) load4(v, xa);
+  while (v + 3L * rs < v1) {
+    const long vb = v + 4L * rs;
+    const bool hb = vb + 3L * rs < v1;
+    if (hb) load4(vb, xb);
+    add4(xa);
+    v = vb;
+    if (!hb) break;
+    const long va = v + 4L * rs;
+    const bool ha = va + 3L * rs < v1;
+    if (ha) load4(va, xa);
+    add4(xb);
+    v = va;
+    if (!ha) break;
   }
   for (; v < v1; v += rs) {
     const double x = (double)z[v * C + c];
@@ -636,19 +657,37 @@ __global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_partial_kernel(
   const long v0 = (long)blockIdx.x * vpb, v1 = v0 + vpb < nvox ? v0 + vpb : nvox;
   double sg[4] = {0.0, 0.0, 0.0, 0.0}, sgx[4] = {0.0, 0.0, 0.0, 0.0};
   long v = v0 + r0;
-  for (; v + 3L * rs < v1; v += 4L * rs) {
-    float zz[4], gg[4];
+  // groups of 4 rows, two in flight (as bn_stats_partial_kernel), accumulated in the same order
+  auto load4 = [&](long vv, float (&zz)[4], float (&gg)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      zz[j] = z[(v + (long)j * rs) * C + c];
-      gg[j] = dy[(v + (long)j * rs) * C + c];
+      zz[j] = z[(vv + (long)j * rs) * C + c];
+      gg[j] = dy[(vv + (long)j * rs) * C + c];
     }
+  };
+  auto add4 = [&](const float (&zz)[4], const float (&gg)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float g = fmaf(zz[j], al, sh) > 0.f ? gg[j] : 0.f;
       sg[j] += (double)g;
       sgx[j] += (double)g * (double)((zz[j] - m) * rstd);
     }
+  };
+  float za[4], ga[4], zb[4], gb[4];
+  if (v + 3L * rs < v1) load4(v, za, ga);
+  while (v + 3L * rs < v1) {
+    const long vb = v + 4L * rs;
+    const bool hb = vb + 3L * rs < v1;
+    if (hb) load4(vb, zb, gb);
+    add4(za, ga);
+    v = vb;
+    if (!hb) break;
+    const long va = v + 4L * rs;
+    const bool ha = va + 3L * rs < v1;
+    if (ha) load4(va, za, ga);
+    add4(zb, gb);
+    v = va;
+    if (!ha) break;
   }
   for (; v < v1; v += rs) {
     const float zz = z[v * C + c];
