@@ -427,6 +427,12 @@ int tmvs_conv3x3_nhwc(const float* x_nhwc, const float* w_packed, const float* b
                       const float* bn_shift, int relu, int batch, int cin, int cout, int height, int width,
                       float* out, float* out_nhwc, void* stream);
 
+/* out_nhwc [B][H][W][32] += conv3x3(x_nhwc) with tmvs_conv3x3_nhwc's kernel and no bias / BN / ReLU
+ * (each element out + conv, the operand order of torch's out += conv): the FeatureNet backward's data
+ * gradient of the DCN offset/mask conv added into the DCN's input gradient in the conv's epilogue. */
+int tmvs_conv3x3_nhwc_acc(const float* x_nhwc, const float* w_packed, int batch, int cin, int cout, int height,
+                          int width, float* out_nhwc, void* stream);
+
 /* FeatureNet FPN merge (models/module.py:409-417): intra = interpolate(prev, 2, nearest) + inner(lat),
  * inner = Conv2d(lat_channels, 32, 1, bias=True) with w_inner [32][lat_channels], b_inner [32].
  * prev_nhwc [B][height][width][32], lat_nhwc [B][2 height][2 width][lat_channels] (8 or 16),

@@ -46,6 +46,7 @@ SIGNATURES = {
     "tmvs_deform_conv2d": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P, P, P]),
     "tmvs_dcn_fused": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P]),
     "tmvs_conv3x3_nhwc": (I, [P, P, P, P, P, I, I, I, I, I, I, P, P, P]),
+    "tmvs_conv3x3_nhwc_acc": (I, [P, P, I, I, I, I, I, P, P]),
     "tmvs_fpn_merge": (I, [P, P, I, P, P, I, I, I, P, P]),
     "tmvs_conv2d_packed_floats": (S, [I, I, I]),
     "tmvs_conv2d_pack": (I, [P, I, I, I, P]),

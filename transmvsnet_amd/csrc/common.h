@@ -51,6 +51,27 @@ static inline dim3 xcd_range_tap_grid(int ntaps, int nblk) {
   return TMVS_WGRAD_XCD ? dim3((unsigned)((nblk + 7) / 8 * 8 * ntaps)) : dim3((unsigned)nblk, (unsigned)ntaps);
 }
 
+// s + p[j0 * stride] + p[(j0 + step) * stride] + ... (j < n), added in that order in fp64 -- the partial
+// combines' fixed-order sums -- with 8 loads in flight ahead of their adds (a plain loop waits on each
+// load before its dependent add)
+#ifndef TMVS_SUM_BATCH
+#define TMVS_SUM_BATCH 8
+#endif
+template <typename T>
+__device__ __forceinline__ double strided_sum(const T* __restrict__ p, long j0, long n, long step, size_t stride,
+                                              double s) {
+  long j = j0;
+  for (; j + (TMVS_SUM_BATCH - 1) * step < n; j += TMVS_SUM_BATCH * step) {
+    T t[TMVS_SUM_BATCH];
+#pragma unroll
+    for (int u = 0; u < TMVS_SUM_BATCH; ++u) t[u] = p[(size_t)(j + u * step) * stride];
+#pragma unroll
+    for (int u = 0; u < TMVS_SUM_BATCH; ++u) s += (double)t[u];
+  }
+  for (; j < n; j += step) s += (double)p[(size_t)j * stride];
+  return s;
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   const int xcd = bid & 7;
   const int q = nblk >> 3, r = nblk & 7;

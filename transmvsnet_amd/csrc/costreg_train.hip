@@ -474,7 +474,7 @@ __global__ __launch_bounds__(kTrainBlock) void sum_partials_kernel(const double*
   const long i = (long)blockIdx.x * 32 + q;
   double s = 0.0;
   if (i < n)
-    for (int j = g; j < nblk; j += 8) s += partial[(size_t)j * n + i];
+    s = strided_sum(partial + i, g, nblk, 8, (size_t)n, s);
   red[g][q] = s;
   __syncthreads();
   if (g == 0 && i < n) {
@@ -557,7 +557,7 @@ __global__ __launch_bounds__(kTrainBlock) void sum_double_partials_kernel(const 
   partial += (size_t)blockIdx.y * nblk * K;  // grid.y = group
   out += (size_t)blockIdx.y * K;
   double a = 0.0;
-  for (int j = threadIdx.x; j < nblk; j += kTrainBlock) a += partial[(size_t)j * K + k];
+  a = strided_sum(partial + k, threadIdx.x, nblk, kTrainBlock, (size_t)K, a);
   red[threadIdx.x] = a;
   __syncthreads();
   for (int st = kTrainBlock / 2; st > 0; st >>= 1) {

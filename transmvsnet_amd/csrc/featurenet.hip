@@ -393,12 +393,21 @@ __global__ __launch_bounds__(512) void conv3x3_window_kernel(const float* __rest
           float y = acc[m][i];
           if (bias) y = y + bias[co0 + i];
           if (alpha) y = fmaf(y, alpha[co0 + i], shift[co0 + i]);
-          if (relu) y = fmaxf(y, 0.f);
+          if (relu & 1) y = fmaxf(y, 0.f);
           r[i] = y;
           if (out) out[((size_t)b * 32 + co0 + i) * HW + pq] = y;
         }
-        if (out_nhwc)
-          *reinterpret_cast<float4*>(out_nhwc + ((size_t)b * HW + pq) * 32 + co0) = make_float4(r[0], r[1], r[2], r[3]);
+        if (out_nhwc) {
+          float4* op = reinterpret_cast<float4*>(out_nhwc + ((size_t)b * HW + pq) * 32 + co0);
+          if (relu & 2) {  // accumulate (tmvs_conv3x3_nhwc_acc): out + conv, the operand order of out += conv
+            const float4 o = *op;
+            r[0] = o.x + r[0];
+            r[1] = o.y + r[1];
+            r[2] = o.z + r[2];
+            r[3] = o.w + r[3];
+          }
+          *op = make_float4(r[0], r[1], r[2], r[3]);
+        }
       }
     }
   }
@@ -560,13 +569,10 @@ extern "C" int tmvs_dcn_fused(const float* x_nhwc, const float* wom_packed, cons
                              height, width, out, out_nhwc, st);
 }
 
-extern "C" int tmvs_conv3x3_nhwc(const float* x_nhwc, const float* w_packed, const float* bias, const float* bn_alpha,
-                                 const float* bn_shift, int relu, int batch, int cin, int cout, int height, int width,
-                                 float* out, float* out_nhwc, void* stream) {
-  if (!x_nhwc || !w_packed || (!out && !out_nhwc) || batch <= 0 || height <= 0 || width <= 0) return TMVS_ERR_ARG;
-  if ((bn_alpha == nullptr) != (bn_shift == nullptr)) return TMVS_ERR_ARG;
-  if (cin != 32 || cout != 32) return TMVS_ERR_SHAPE;
-  if ((long long)height * width * cin * 4 >= (1LL << 31)) return TMVS_ERR_SHAPE;
+static int conv3x3_launch(const float* x_nhwc, const float* w_packed, const float* bias, const float* bn_alpha,
+                          const float* bn_shift, int flags, int batch, int height, int width, float* out,
+                          float* out_nhwc, void* stream) {
+  if ((long long)height * width * 32 * 4 >= (1LL << 31)) return TMVS_ERR_SHAPE;
   static int grid = 0;
   if (!grid) {
     int dev = 0, ncu = 0, occ = 0;
@@ -579,9 +585,29 @@ extern "C" int tmvs_conv3x3_nhwc(const float* x_nhwc, const float* w_packed, con
       (long long)batch * ((height + dcn::WAVES - 1) / dcn::WAVES) * ((width + dcn::TW - 1) / dcn::TW);
   const int nblk = (int)std::min<long long>(grid, nunits);
   hipLaunchKernelGGL(conv3x3_window_kernel, dim3(nblk), dim3(512), 0, (hipStream_t)stream, x_nhwc, w_packed, bias,
-                     bn_alpha, bn_shift, relu, batch, height, width, out, out_nhwc);
+                     bn_alpha, bn_shift, flags, batch, height, width, out, out_nhwc);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
+}
+
+extern "C" int tmvs_conv3x3_nhwc(const float* x_nhwc, const float* w_packed, const float* bias, const float* bn_alpha,
+                                 const float* bn_shift, int relu, int batch, int cin, int cout, int height, int width,
+                                 float* out, float* out_nhwc, void* stream) {
+  if (!x_nhwc || !w_packed || (!out && !out_nhwc) || batch <= 0 || height <= 0 || width <= 0) return TMVS_ERR_ARG;
+  if ((bn_alpha == nullptr) != (bn_shift == nullptr)) return TMVS_ERR_ARG;
+  if (cin != 32 || cout != 32) return TMVS_ERR_SHAPE;
+  return conv3x3_launch(x_nhwc, w_packed, bias, bn_alpha, bn_shift, relu ? 1 : 0, batch, height, width, out, out_nhwc,
+                        stream);
+}
+
+// out_nhwc += conv3x3(x_nhwc) (no bias / BN / ReLU): the FeatureNet backward's data gradient of a 3x3 conv
+// added into an existing gradient in the conv's epilogue instead of a separate add pass
+extern "C" int tmvs_conv3x3_nhwc_acc(const float* x_nhwc, const float* w_packed, int batch, int cin, int cout,
+                                     int height, int width, float* out_nhwc, void* stream) {
+  if (!x_nhwc || !w_packed || !out_nhwc || batch <= 0 || height <= 0 || width <= 0) return TMVS_ERR_ARG;
+  if (cin != 32 || cout != 32) return TMVS_ERR_SHAPE;
+  return conv3x3_launch(x_nhwc, w_packed, nullptr, nullptr, nullptr, 2, batch, height, width, nullptr, out_nhwc,
+                        stream);
 }
 
 extern "C" int tmvs_fpn_merge(const float* prev_nhwc, const float* lat_nhwc, int lat_channels, const float* w_inner,

@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kBlk) void sum_partials_f32_kernel(const double* __
   const long i = (long)blockIdx.x * 32 + q;
   double s = 0.0;
   if (i < n)
-    for (int j = g; j < nblk; j += 8) s += partial[(size_t)j * n + i];
+    s = strided_sum(partial + i, g, nblk, 8, (size_t)n, s);
   red[g][q] = s;
   __syncthreads();
   if (g == 0 && i < n) {
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(kBlk) void sum_partials_rows_kernel(const double* _
   const long np = n / per * ap * bc;
   double s = 0.0;
   if (i < n)
-    for (int j = g; j < nblk; j += 8) s += partial[(size_t)j * np + src];
+    s = strided_sum(partial + src, g, nblk, 8, (size_t)np, s);
   red[g][q] = s;
   __syncthreads();
   if (g == 0 && i < n) {
@@ -324,8 +324,7 @@ __global__ __launch_bounds__(kBlk) void colsum_partial_kernel(const float* __res
   const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;
   const long v0 = (long)blockIdx.x * ppb, v1 = v0 + ppb < n ? v0 + ppb : n;
   double s = 0.0;
-  if (c < C)
-    for (long v = v0 + r0; v < v1; v += 8) s += (double)x[v * C + c];
+  if (c < C) s = strided_sum(x + c, v0 + r0, v1, 8, (size_t)C, s);
   red[r0][c] = s;
   __syncthreads();
   if (r0 == 0 && c < C) {
@@ -424,13 +423,27 @@ __device__ __forceinline__ int dcn_fix_shift(const unsigned* __restrict__ mx, in
 // written whole to scratch [block][cell][32] (plain, coalesced stores); dcn_gather_windows_kernel then
 // sums, for every texel, the <= 4 windows covering it in a fixed block order (no global atomics).
 // Corners beyond the window (offsets over R px) are added to dx with fp32 atomics before that pass.
+// dcol on the matrix cores (TMVS_DCNB_MFMA, the 32-output-channel instance): per pass and tap pair,
+// each wave computes the 16 x 64 tile D[(tap, channel)][pixel] = sum_o W[o][channel][tap] dy[pixel][o]
+// as v_mfma_f32_16x16x4f32 chains over o (the same fmaf chain, bitwise, as the VALU form's
+// dc[c] = fmaf(g[o], w[o][c], dc[c]), o ascending), parks it in a wave-private LDS tile, and every lane
+// reads its pixel's 8 channels back, so the 9216 dcol MACs per pixel run beside the VALU's sampling,
+// offset gradients and scatter (r14w: 2163 -> 2066 / 622 -> 559 / 200 -> 158 us at 4 x 576x768 /
+// 288x384 / 144x192; the 8- and 16-channel instances measured slower that way and keep the VALU form).
+#ifndef TMVS_DCNB_MFMA
+#define TMVS_DCNB_MFMA 1
+#endif
+#ifndef TMVS_DCNB_FIX32
+#define TMVS_DCNB_FIX32 0
+#endif
 template <int CO>
-__global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ om,
-                                                           const float* __restrict__ wt, const float* __restrict__ dy,
-                                                           int B, int H, int W, const unsigned* __restrict__ absmax,
-                                                           float* __restrict__ dx, float* __restrict__ dom,
-                                                           float* __restrict__ scratch) {
+__global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(CO == 8 ? 4 : 3,
+                                                                     CO == 8 ? 4 : 3)))
+void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ om, const float* __restrict__ wt,
+                         const float* __restrict__ dy, int B, int H, int W, const unsigned* __restrict__ absmax,
+                         float* __restrict__ dx, float* __restrict__ dom, float* __restrict__ scratch) {
   using namespace dbw;
+  constexpr bool kMf = TMVS_DCNB_MFMA && CO == 32;
   __shared__ unsigned long long win[WR * WC * CC];
   const int kfix = dcn_fix_shift(absmax, CO);
   const int tid = threadIdx.x;
@@ -444,15 +457,58 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
   const size_t HW = (size_t)H * W;
   const int wy0 = by * TY - R - 1, wx0 = bx * TX - R - 1;
   const size_t pix = (size_t)b * HW + (size_t)(live ? y : 0) * W + (live ? xq : 0);
-  float g[CO];
+  static_assert(CC == 8 && kBlk == 256 && CO % 4 == 0, "dcol tile: 2 taps x 8 channels, 4 waves");
+  // wave-private [64 pixels][16] dcol tiles; quad q of pixel p at quad q ^ ((p >> 1) & 3) (conflict-free
+  // b128 writes of a lane group's 16 pixels and b128 reads of 8 consecutive pixels)
+  __shared__ __attribute__((aligned(16))) float dcl[kMf ? kBlk * 16 : 4];
+  const int lane = tid & 63, l15 = lane & 15, lg = lane >> 4;
+  float* dw = dcl + (kMf ? (tid & ~63) * 16 : 0);
+  float g[CO];        // VALU form: this pixel's dy row
+  float dyt[4][CO / 4];  // MFMA form, B operand dy^T: lane (g, n) of pixel block i holds dy[pixel 16 i + n][4 s + g]
+  if constexpr (kMf) {
 #pragma unroll
-  for (int o4 = 0; o4 < CO / 4; ++o4) {
-    const float4 t = live ? *reinterpret_cast<const float4*>(dy + pix * CO + 4 * o4) : make_float4(0.f, 0.f, 0.f, 0.f);
-    g[4 * o4] = t.x;
-    g[4 * o4 + 1] = t.y;
-    g[4 * o4 + 2] = t.z;
-    g[4 * o4 + 3] = t.w;
+    for (int i = 0; i < 4; ++i) {
+      const int t2 = (tid & ~63) + 16 * i + l15;
+      const int y2 = by * TY + t2 / TX, x2 = bx * TX + t2 % TX;
+      const bool ok2 = y2 < H && x2 < W;
+      const float* dp = dy + ((size_t)b * HW + (size_t)(ok2 ? y2 : 0) * W + (ok2 ? x2 : 0)) * CO + lg;
+#pragma unroll
+      for (int s = 0; s < CO / 4; ++s) dyt[i][s] = ok2 ? dp[4 * s] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int o4 = 0; o4 < CO / 4; ++o4) {
+      const float4 t = live ? *reinterpret_cast<const float4*>(dy + pix * CO + 4 * o4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      g[4 * o4] = t.x;
+      g[4 * o4 + 1] = t.y;
+      g[4 * o4 + 2] = t.z;
+      g[4 * o4 + 3] = t.w;
+    }
   }
+  // A operand: W^T, lane (g, n) holds W[4 s + g][channel n & 7][tap 2 j + (n >> 3)] (0 past tap 8)
+  auto load_wa = [&](int j, int cc, float (&wa)[CO / 4]) {
+    const int kk = 2 * j + (l15 >> 3);
+    const float* wp = wt + ((size_t)(kk < 9 ? kk : 0) * CO + lg) * 32 + cc * CC + (l15 & 7);
+#pragma unroll
+    for (int s = 0; s < CO / 4; ++s) wa[s] = kk < 9 ? wp[(size_t)(4 * s) * 32] : 0.f;
+  };
+  // taps 2j, 2j+1 of the pass: D rows 4g + r = (tap 2j + (g >> 1), channel 4 (g & 1) + r), column n
+  auto dcol_pair = [&](const float (&wa)[CO / 4]) {
+    floatx4_t d[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[i] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < CO / 4; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) d[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[s], dyt[i][s], d[i], 0, 0, 0);
+    asm volatile("" ::: "memory");  // the previous pair's reads of the tile precede these writes
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = 16 * i + l15;
+      *reinterpret_cast<floatx4_t*>(dw + p * 16 + 4 * (lg ^ ((p >> 1) & 3))) = d[i];
+    }
+    asm volatile("" ::: "memory");  // one wave's LDS operations complete in order
+  };
   const float* xb = x + (size_t)b * HW * 32;
   float* dxb = dx + (size_t)b * HW * 32;
   const float* omp = om + (size_t)b * 27 * HW + (size_t)(live ? y : 0) * W + (live ? xq : 0);
@@ -463,20 +519,38 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
   for (int cc = 0; cc < 32 / CC; ++cc) {
     for (int i = tid; i < WR * WC * CC; i += kBlk) win[i] = 0ull;
     __syncthreads();
-    if (live) {
+    float wa[CO / 4];
+    if constexpr (kMf) load_wa(0, cc, wa);
 #pragma unroll 1
-      for (int k = 0; k < 9; ++k) {
+    for (int k = 0; k < 9; ++k) {
+      if constexpr (kMf)
+        if ((k & 1) == 0) {  // wave-uniform: the pair's tile, then the next pair's weights in flight
+          dcol_pair(wa);
+          if (k < 8) load_wa((k >> 1) + 1, cc, wa);
+        }
+      if (live) {
         const DcnSample s = dcn_sample(omp, HW, y, xq, k, H, W);
         if (!s.inside) continue;  // the column is 0 and carries no gradient (torchvision)
-        // dcol: the tap's weights are block-uniform -- scalar loads, SGPR operands of the FMAs
-        const float* wk = wt + (size_t)k * CO * 32 + cc * CC;
         float dc[CC];
+        if constexpr (kMf) {
+          const int q0 = 2 * (k & 1);
+          const floatx4_t d0 = *reinterpret_cast<const floatx4_t*>(dw + lane * 16 + 4 * (q0 ^ ((lane >> 1) & 3)));
+          const floatx4_t d1 = *reinterpret_cast<const floatx4_t*>(dw + lane * 16 + 4 * ((q0 + 1) ^ ((lane >> 1) & 3)));
 #pragma unroll
-        for (int c = 0; c < CC; ++c) dc[c] = 0.f;
+          for (int c = 0; c < 4; ++c) {
+            dc[c] = d0[c];
+            dc[4 + c] = d1[c];
+          }
+        } else {
+          // dcol: the tap's weights are block-uniform -- scalar loads, SGPR operands of the FMAs
+          const float* wk = wt + (size_t)k * CO * 32 + cc * CC;
 #pragma unroll
-        for (int o = 0; o < CO; ++o)
+          for (int c = 0; c < CC; ++c) dc[c] = 0.f;
 #pragma unroll
-          for (int c = 0; c < CC; ++c) dc[c] = fmaf(g[o], wk[o * 32 + c], dc[c]);
+          for (int o = 0; o < CO; ++o)
+#pragma unroll
+            for (int c = 0; c < CC; ++c) dc[c] = fmaf(g[o], wk[o * 32 + c], dc[c]);
+        }
         const float wq[4] = {s.hy * s.hx, s.hy * s.lx, s.ly * s.hx, s.ly * s.lx};
         float v[4][CC];
         bool ok[4];
@@ -517,7 +591,9 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_data_kernel(const float* __restr
 #pragma unroll
             for (int c = 0; c < CC; ++c)
               atomicAdd(wp + c * (WR * WC),
-                        (unsigned long long)(kfix == kFixBad ? 0ll : __double2ll_rn(ldexp((double)(f * dc[c]), kfix))));
+                        (unsigned long long)(kfix == kFixBad ? 0ll
+                                             : TMVS_DCNB_FIX32 ? (long long)llrintf(ldexpf(f * dc[c], kfix))
+                                                               : __double2ll_rn(ldexp((double)(f * dc[c]), kfix))));
           } else {  // an offset beyond the window: straight to global memory
             float* gp = dxb + ((size_t)cy * W + cx) * 32 + cc * CC;
 #pragma unroll

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kTB) void fmt_sum_partials_kernel(const double* __r
   const long i = (long)blockIdx.x * 16 + k;
   double s = 0.0;
   if (i < n)
-    for (int j = g; j < nblk; j += 16) s += partial[(size_t)j * n + i];
+    s = strided_sum(partial + i, g, nblk, 16, (size_t)n, s);
   red[g][k] = s;
   __syncthreads();
   if (g == 0 && i < n) {

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(kPwBlock) void pw_sum_partials_kernel(const double*
                                                                    double* __restrict__ out) {
   __shared__ double red[kPwBlock];
   double a = 0.0;
-  for (int j = threadIdx.x; j < nblk; j += kPwBlock) a += partial[(size_t)j * K + blockIdx.x];
+  a = strided_sum(partial + blockIdx.x, threadIdx.x, nblk, kPwBlock, (size_t)K, a);
   red[threadIdx.x] = a;
   __syncthreads();
   for (int st = kPwBlock / 2; st > 0; st >>= 1) {

@@ -771,6 +771,24 @@ __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restr
   unsigned skey[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
   float scoef[4] = {0.f, 0.f, 0.f, 0.f};
   unsigned long long* dv = dsrc_fix + (size_t)v * HW * C;
+  // the block's reference rows in LDS (TMVS_WARP_BWD_SREF): a flush round reads its items' rows from
+  // there, not from global memory -- one round is a chain of lane exchanges, the row read, the
+  // fixed-point conversion and the atomic, and a global read had put a memory latency into every round
+#ifndef TMVS_WARP_BWD_SREF
+#define TMVS_WARP_BWD_SREF 1
+#endif
+  constexpr bool kSref = SCATTER && TMVS_WARP_BWD_SREF;
+  __shared__ __attribute__((aligned(16))) float sref[kSref ? 256 * C : 4];
+  if constexpr (kSref) {
+    static_assert(C % 4 == 0, "float4 rows");
+    const int p0 = blockIdx.x * blockDim.x;
+    for (int i = threadIdx.x; i < 256 * C / 4; i += 256) {
+      const int pp = p0 + i / (C / 4);
+      reinterpret_cast<float4*>(sref)[i] =
+          pp < HW ? reinterpret_cast<const float4*>(ref)[(size_t)pp * (C / 4) + i % (C / 4)] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+  }
   // Wave-cooperative flush: the pending (lane, slot) items are served 64/C at a time, lane c % C adding
   // channel c of item lane / C, so each atomic instruction covers whole C-channel rows (coalesced per
   // cache line) instead of 64 scattered rows. The added value per (texel, channel) is unchanged.
@@ -789,9 +807,10 @@ __global__ __launch_bounds__(256) void warp_corr_bwd_kernel(const float* __restr
       const int srcl = mine < 0 ? 0 : mine;
       const unsigned key = (unsigned)__shfl((int)skey[sl], srcl);
       const float coef = __shfl(scoef[sl], srcl);
-      const int pp = __shfl(pc, srcl);
+      const int pp = kSref ? 0 : __shfl(pc, srcl);
       if (mine >= 0) {
-        const float sc = ldexpf(coef * ref[(size_t)pp * C + ch], kfix);
+        const float rv = kSref ? sref[((threadIdx.x & ~63) + srcl) * C + ch] : ref[(size_t)pp * C + ch];
+        const float sc = ldexpf(coef * rv, kfix);
         if (sc != 0.f)
           atomicAdd(dv + ((size_t)(key >> 16) * W + (key & 0xFFFFu)) * C + ch,
                     (unsigned long long)(long long)llrintf(sc));

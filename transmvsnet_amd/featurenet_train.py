@@ -203,7 +203,8 @@ def _dcn_bwd(dcn, x, om, dy, grads):
     _acc(grads, com.bias, ops.colsum(dom)[:27].contiguous())
     wp = torch.zeros(32, 32, 3, 3, device=x.device)  # [co 27 + 5 zero rows][ci][3][3]
     wp[:27] = com.weight.detach().float()
-    dx.add_(dgrad_same(dom, wp, (x.shape[1], x.shape[2])))
+    # dx += its data gradient (dgrad_same's 32 -> 32 3x3 form), added in the conv's epilogue
+    ops.conv3x3_nhwc_acc(dom, device_pack("dcn", _flip_t(wp)), dx)
     return dx
 
 

@@ -459,6 +459,20 @@ def conv3x3_nhwc(x_nhwc, w_packed, bn=None, relu=False, bias=None, want_nchw=Fal
     return out, out_nhwc
 
 
+def conv3x3_nhwc_acc(x_nhwc, w_packed, out_nhwc):
+    """out_nhwc [B,H,W,32] += Conv2d(32, 32, 3, 1, 1, bias=False)(x_nhwc) in the conv's epilogue
+    (tmvs_conv3x3_nhwc_acc; each element out + conv, as out.add_(conv))."""
+    for t, n in ((x_nhwc, "x_nhwc"), (w_packed, "w_packed"), (out_nhwc, "out_nhwc")):
+        _dev(t, n)
+    if not x_nhwc.is_contiguous() or not out_nhwc.is_contiguous() or out_nhwc.shape != x_nhwc.shape:
+        raise ValueError("conv3x3_nhwc_acc: expects contiguous x_nhwc and out_nhwc [B,H,W,32] of one shape")
+    b, h, w, cin = x_nhwc.shape
+    with _Span("tmvs_conv3x3_nhwc_acc"):
+        _lib.check(_lib_h().tmvs_conv3x3_nhwc_acc(_ptr(x_nhwc), _ptr(w_packed), b, cin, 32, h, w, _ptr(out_nhwc),
+                                                  _stream()), "tmvs_conv3x3_nhwc_acc")
+    return out_nhwc
+
+
 def fpn_merge(prev_nhwc, lat_nhwc, w_inner, b_inner):
     """interpolate(prev, 2, nearest) + Conv2d_1x1(lat) (models/module.py:409-417), all NHWC:
     prev [B,h,w,32], lat [B,2h,2w,cl] (cl 8/16), w_inner [32,cl] -> [B,2h,2w,32]."""
@@ -1105,7 +1119,7 @@ def softmax_backward(prob, dprob):
     return out
 
 
-for _name in ("conv2d_generic", "conv2d_wgrad", "colsum", "dcn_forward_train", "dcn_backward",
+for _name in ("conv2d_generic", "conv2d_wgrad", "colsum", "dcn_forward_train", "dcn_backward", "conv3x3_nhwc_acc",
               "nearest_up2_backward_nhwc", "softmax_backward"):
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name
