@@ -433,8 +433,13 @@ __device__ __forceinline__ int dcn_fix_shift(const unsigned* __restrict__ mx, in
 #ifndef TMVS_DCNB_MFMA
 #define TMVS_DCNB_MFMA 1
 #endif
+// The scatter's fixed-point conversion in fp32 (TMVS_DCNB_FIX32): ldexpf(f * dcol, k) is exact (a power-of-two
+// scale of an fp32 value, no overflow below 2^62, and a result in the denormal range rounds to 0 either
+// way) and llrintf rounds it to nearest-even as __double2ll_rn does the fp64 value: the same integers
+// (bitwise, r14x). Faster for the VALU-dcol instances (32 -> 8: 1725 -> 1599 us), slower for the MFMA one
+// (2109 -> 2228 us, 2 VGPRs spilled), so only there.
 #ifndef TMVS_DCNB_FIX32
-#define TMVS_DCNB_FIX32 0
+#define TMVS_DCNB_FIX32 1
 #endif
 template <int CO>
 __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(CO == 8 ? 4 : 3,
@@ -592,7 +597,7 @@ void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ 
             for (int c = 0; c < CC; ++c)
               atomicAdd(wp + c * (WR * WC),
                         (unsigned long long)(kfix == kFixBad ? 0ll
-                                             : TMVS_DCNB_FIX32 ? (long long)llrintf(ldexpf(f * dc[c], kfix))
+                                             : TMVS_DCNB_FIX32 && !kMf ? (long long)llrintf(ldexpf(f * dc[c], kfix))
                                                                : __double2ll_rn(ldexp((double)(f * dc[c]), kfix))));
           } else {  // an offset beyond the window: straight to global memory
             float* gp = dxb + ((size_t)cy * W + cx) * 32 + cc * CC;
