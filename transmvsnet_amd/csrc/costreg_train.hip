@@ -568,17 +568,35 @@ __global__ __launch_bounds__(kTrainBlock) void sum_double_partials_kernel(const 
 }
 
 // mean, biased var (fp32) from the summed (sum z, sum z^2)
-__global__ void bn_stats_finalize_kernel(const double* __restrict__ sums, int C, long nvox, float* __restrict__ mean,
-                                         float* __restrict__ var) {
-  const int c = threadIdx.x;
-  if (c >= C) return;
-  sums += (size_t)blockIdx.x * 2 * C;  // grid = groups
-  mean += (size_t)blockIdx.x * C;
-  var += (size_t)blockIdx.x * C;
-  const double m = sums[c] / (double)nvox;
-  const double v = sums[C + c] / (double)nvox - m * m;
-  mean[c] = (float)m;
-  var[c] = (float)(v > 0.0 ? v : 0.0);
+__device__ __forceinline__ void bn_stats_from_sums(double s, double s2, long nvox, float& mean, float& var) {
+  const double m = s / (double)nvox;
+  const double v = s2 / (double)nvox - m * m;
+  mean = (float)m;
+  var = (float)(v > 0.0 ? v : 0.0);
+}
+
+// sum_double_partials_kernel's two sums of channel c (sum z, sum z^2; the same thread strides and LDS
+// tree) and bn_stats_from_sums in one launch: grid (C, groups)
+__global__ __launch_bounds__(kTrainBlock) void bn_sums_stats_kernel(const double* __restrict__ partial, int nblk, int C,
+                                                                    long nvox, float* __restrict__ mean,
+                                                                    float* __restrict__ var) {
+  __shared__ double red[kTrainBlock];
+  __shared__ double tot[2];
+  const int c = blockIdx.x, K = 2 * C;
+  partial += (size_t)blockIdx.y * nblk * K;
+#pragma unroll 1
+  for (int h = 0; h < 2; ++h) {
+    red[threadIdx.x] = strided_sum(partial + h * C + c, threadIdx.x, nblk, kTrainBlock, (size_t)K, 0.0);
+    __syncthreads();
+    for (int st = kTrainBlock / 2; st > 0; st >>= 1) {
+      if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) tot[h] = red[0];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    bn_stats_from_sums(tot[0], tot[1], nvox, mean[(size_t)blockIdx.y * C + c], var[(size_t)blockIdx.y * C + c]);
 }
 
 __device__ __forceinline__ void bn_affine(float mean, float var, float g, float bt, float eps, float& al, float& sh) {
@@ -711,10 +729,11 @@ __global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_partial_kernel(
 
 // dbeta = sum g, dgamma = sum g*xhat from the summed partials: per group in fp32, then added over the
 // groups in order (as autograd accumulates the per-view gradients of a module called per view)
-__global__ void bn_relu_bwd_finalize_kernel(const double* __restrict__ sums, int C, int groups,
-                                            float* __restrict__ dgamma, float* __restrict__ dbeta) {
+// (run by the first block of the backward apply kernels, thread c < C: one launch less per BatchNorm)
+__device__ __forceinline__ void bn_relu_bwd_finalize(const double* __restrict__ sums, int C, int groups,
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta) {
   const int c = threadIdx.x;
-  if (c >= C) return;
+  if (blockIdx.x != 0 || c >= C) return;
   float b = (float)sums[c], g = (float)sums[C + c];
   for (int k = 1; k < groups; ++k) {
     b = b + (float)sums[(size_t)k * 2 * C + c];
@@ -728,7 +747,9 @@ __global__ void bn_relu_bwd_finalize_kernel(const double* __restrict__ sums, int
 __global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_apply_kernel(
     const float* __restrict__ dy, const float* __restrict__ z, long n, int C, long nvox, const float* __restrict__ mean,
     const float* __restrict__ var, const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-    const double* __restrict__ sums, float* __restrict__ dz) {
+    const double* __restrict__ sums, int groups, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    float* __restrict__ dz) {
+  bn_relu_bwd_finalize(sums, C, groups, dgamma, dbeta);
   const long i = (long)blockIdx.x * kTrainBlock + threadIdx.x;
   if (i >= n) return;
   const int c = (int)(i % C);
@@ -750,7 +771,9 @@ __global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_apply_kernel(
 __global__ __launch_bounds__(kTrainBlock) void bn_relu_bwd_apply4_kernel(
     const float4* __restrict__ dy, const float4* __restrict__ z, long n4, int C, long nvox,
     const float* __restrict__ mean, const float* __restrict__ var, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float eps, const double* __restrict__ sums, float4* __restrict__ dz) {
+    const float* __restrict__ beta, float eps, const double* __restrict__ sums, int groups, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, float4* __restrict__ dz) {
+  bn_relu_bwd_finalize(sums, C, groups, dgamma, dbeta);
   const long i4 = (long)blockIdx.x * kTrainBlock + threadIdx.x;
   if (i4 >= n4) return;
   const long i = 4 * i4;
@@ -920,12 +943,8 @@ extern "C" int tmvs_bn_stats_grouped(const float* z, int groups, long nvox, int 
   hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(nblk, groups), dim3(kTrainBlock), 0, st, z, nvox, channels, vpb,
                      part);
   TMVS_CHECK_LAUNCH();
-  double* sums = part + (size_t)groups * nblk * 2 * channels;
-  hipLaunchKernelGGL(sum_double_partials_kernel, dim3(2 * channels, groups), dim3(kTrainBlock), 0, st,
-                     (const double*)part, nblk, 2 * channels, sums);
-  TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(groups), dim3(64), 0, st, (const double*)sums, channels, nvox,
-                     mean, var);
+  hipLaunchKernelGGL(bn_sums_stats_kernel, dim3(channels, groups), dim3(kTrainBlock), 0, st, (const double*)part,
+                     nblk, channels, nvox, mean, var);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -980,19 +999,16 @@ extern "C" int tmvs_bn_relu_backward_grouped(const float* dy, const float* z, in
   hipLaunchKernelGGL(sum_double_partials_kernel, dim3(2 * channels, groups), dim3(kTrainBlock), 0, st,
                      (const double*)part, nblk, 2 * channels, sums);
   TMVS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_relu_bwd_finalize_kernel, dim3(1), dim3(64), 0, st, (const double*)sums, channels, groups,
-                     dgamma, dbeta);
-  TMVS_CHECK_LAUNCH();
   const long n = nvox * channels * groups;
   if (TMVS_BN_VEC4 && channels % 4 == 0 && aligned16(dy) && aligned16(z) && aligned16(dz)) {
     const long n4 = n / 4;
     hipLaunchKernelGGL(bn_relu_bwd_apply4_kernel, dim3((unsigned)((n4 + kTrainBlock - 1) / kTrainBlock)),
                        dim3(kTrainBlock), 0, st, (const float4*)dy, (const float4*)z, n4, channels, nvox, mean, var,
-                       gamma, beta, eps, (const double*)sums, (float4*)dz);
+                       gamma, beta, eps, (const double*)sums, groups, dgamma, dbeta, (float4*)dz);
   } else {
     hipLaunchKernelGGL(bn_relu_bwd_apply_kernel, dim3((unsigned)((n + kTrainBlock - 1) / kTrainBlock)),
                        dim3(kTrainBlock), 0, st, dy, z, n, channels, nvox, mean, var, gamma, beta, eps,
-                       (const double*)sums, dz);
+                       (const double*)sums, groups, dgamma, dbeta, dz);
   }
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;

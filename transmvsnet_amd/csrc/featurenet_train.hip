@@ -433,6 +433,9 @@ __device__ __forceinline__ int dcn_fix_shift(const unsigned* __restrict__ mx, in
 #ifndef TMVS_DCNB_MFMA
 #define TMVS_DCNB_MFMA 1
 #endif
+#ifndef TMVS_DCNB_RELOAD
+#define TMVS_DCNB_RELOAD 0
+#endif
 // The scatter's fixed-point conversion in fp32 (TMVS_DCNB_FIX32): ldexpf(f * dcol, k) is exact (a power-of-two
 // scale of an fp32 value, no overflow below 2^62, and a result in the denormal range rounds to 0 either
 // way) and llrintf rounds it to nearest-even as __double2ll_rn does the fp64 value: the same integers
@@ -470,6 +473,8 @@ void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ 
   float* dw = dcl + (kMf ? (tid & ~63) * 16 : 0);
   float g[CO];        // VALU form: this pixel's dy row
   float dyt[4][CO / 4];  // MFMA form, B operand dy^T: lane (g, n) of pixel block i holds dy[pixel 16 i + n][4 s + g]
+  unsigned dyo[4];        // (TMVS_DCNB_RELOAD: re-read per tap pair from L1/L2 at these byte offsets instead)
+  const __amdgpu_buffer_rsrc_t rdy = raw_rsrc(dy, (unsigned)((size_t)B * HW * CO * 4));
   if constexpr (kMf) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -477,8 +482,10 @@ void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ 
       const int y2 = by * TY + t2 / TX, x2 = bx * TX + t2 % TX;
       const bool ok2 = y2 < H && x2 < W;
       const float* dp = dy + ((size_t)b * HW + (size_t)(ok2 ? y2 : 0) * W + (ok2 ? x2 : 0)) * CO + lg;
+      dyo[i] = ok2 ? (unsigned)((((size_t)b * HW + (size_t)y2 * W + x2) * CO + lg) * 4) : kOffOut;
+      if (!TMVS_DCNB_RELOAD)
 #pragma unroll
-      for (int s = 0; s < CO / 4; ++s) dyt[i][s] = ok2 ? dp[4 * s] : 0.f;
+        for (int s = 0; s < CO / 4; ++s) dyt[i][s] = ok2 ? dp[4 * s] : 0.f;
     }
   } else {
 #pragma unroll
@@ -505,7 +512,9 @@ void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ 
 #pragma unroll
     for (int s = 0; s < CO / 4; ++s)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) d[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[s], dyt[i][s], d[i], 0, 0, 0);
+      for (int i = 0; i < 4; ++i)
+        d[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+            wa[s], TMVS_DCNB_RELOAD ? buf_load_f32(rdy, dyo[i] + 16u * s) : dyt[i][s], d[i], 0, 0, 0);
     asm volatile("" ::: "memory");  // the previous pair's reads of the tile precede these writes
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -597,7 +606,8 @@ void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ 
             for (int c = 0; c < CC; ++c)
               atomicAdd(wp + c * (WR * WC),
                         (unsigned long long)(kfix == kFixBad ? 0ll
-                                             : TMVS_DCNB_FIX32 && !kMf ? (long long)llrintf(ldexpf(f * dc[c], kfix))
+                                             : TMVS_DCNB_FIX32 && (!kMf || TMVS_DCNB_FIX32 == 2)
+                                                   ? (long long)llrintf(ldexpf(f * dc[c], kfix))
                                                                : __double2ll_rn(ldexp((double)(f * dc[c]), kfix))));
           } else {  // an offset beyond the window: straight to global memory
             float* gp = dxb + ((size_t)cy * W + cx) * 32 + cc * CC;
