@@ -433,14 +433,12 @@ __device__ __forceinline__ int dcn_fix_shift(const unsigned* __restrict__ mx, in
 #ifndef TMVS_DCNB_MFMA
 #define TMVS_DCNB_MFMA 1
 #endif
-#ifndef TMVS_DCNB_RELOAD
-#define TMVS_DCNB_RELOAD 0
-#endif
 // The scatter's fixed-point conversion in fp32 (TMVS_DCNB_FIX32): ldexpf(f * dcol, k) is exact (a power-of-two
 // scale of an fp32 value, no overflow below 2^62, and a result in the denormal range rounds to 0 either
 // way) and llrintf rounds it to nearest-even as __double2ll_rn does the fp64 value: the same integers
 // (bitwise, r14x). Faster for the VALU-dcol instances (32 -> 8: 1725 -> 1599 us), slower for the MFMA one
-// (2109 -> 2228 us, 2 VGPRs spilled), so only there.
+// (2109 -> 2228 us, 2 VGPRs spilled; with the dy^T operands re-read per tap pair to make room, 3480 us,
+// r14z), so only there.
 #ifndef TMVS_DCNB_FIX32
 #define TMVS_DCNB_FIX32 1
 #endif
@@ -473,8 +471,6 @@ void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ 
   float* dw = dcl + (kMf ? (tid & ~63) * 16 : 0);
   float g[CO];        // VALU form: this pixel's dy row
   float dyt[4][CO / 4];  // MFMA form, B operand dy^T: lane (g, n) of pixel block i holds dy[pixel 16 i + n][4 s + g]
-  unsigned dyo[4];        // (TMVS_DCNB_RELOAD: re-read per tap pair from L1/L2 at these byte offsets instead)
-  const __amdgpu_buffer_rsrc_t rdy = raw_rsrc(dy, (unsigned)((size_t)B * HW * CO * 4));
   if constexpr (kMf) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -482,10 +478,8 @@ void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ 
       const int y2 = by * TY + t2 / TX, x2 = bx * TX + t2 % TX;
       const bool ok2 = y2 < H && x2 < W;
       const float* dp = dy + ((size_t)b * HW + (size_t)(ok2 ? y2 : 0) * W + (ok2 ? x2 : 0)) * CO + lg;
-      dyo[i] = ok2 ? (unsigned)((((size_t)b * HW + (size_t)y2 * W + x2) * CO + lg) * 4) : kOffOut;
-      if (!TMVS_DCNB_RELOAD)
 #pragma unroll
-        for (int s = 0; s < CO / 4; ++s) dyt[i][s] = ok2 ? dp[4 * s] : 0.f;
+      for (int s = 0; s < CO / 4; ++s) dyt[i][s] = ok2 ? dp[4 * s] : 0.f;
     }
   } else {
 #pragma unroll
@@ -512,9 +506,7 @@ void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ 
 #pragma unroll
     for (int s = 0; s < CO / 4; ++s)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        d[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-            wa[s], TMVS_DCNB_RELOAD ? buf_load_f32(rdy, dyo[i] + 16u * s) : dyt[i][s], d[i], 0, 0, 0);
+      for (int i = 0; i < 4; ++i) d[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[s], dyt[i][s], d[i], 0, 0, 0);
     asm volatile("" ::: "memory");  // the previous pair's reads of the tile precede these writes
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -606,8 +598,7 @@ void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ 
             for (int c = 0; c < CC; ++c)
               atomicAdd(wp + c * (WR * WC),
                         (unsigned long long)(kfix == kFixBad ? 0ll
-                                             : TMVS_DCNB_FIX32 && (!kMf || TMVS_DCNB_FIX32 == 2)
-                                                   ? (long long)llrintf(ldexpf(f * dc[c], kfix))
+                                             : TMVS_DCNB_FIX32 && !kMf ? (long long)llrintf(ldexpf(f * dc[c], kfix))
                                                                : __double2ll_rn(ldexp((double)(f * dc[c]), kfix))));
           } else {  // an offset beyond the window: straight to global memory
             float* gp = dxb + ((size_t)cy * W + cx) * 32 + cc * CC;
@@ -644,17 +635,15 @@ void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ 
 }
 
 // dx[q][c] += sum over the blocks whose windows cover texel q (block rows / columns ascending) of their
-// window value: one thread per (texel, channel)
+// window value: one thread per (texel, channel); grid (ceil(32 W / 256), H, B), so a thread's texel comes
+// from its block coordinates (a flat index had cost two 64-bit divisions per element)
 __global__ __launch_bounds__(kBlk) void dcn_gather_windows_kernel(const float* __restrict__ scratch, int B, int H,
                                                                  int W, float* __restrict__ dx) {
   using namespace dbw;
-  const long i = (long)blockIdx.x * kBlk + threadIdx.x;
-  if (i >= (long)B * H * W * 32) return;
-  const int c = (int)(i & 31);
-  long t = i >> 5;
-  const int xq = (int)(t % W);
-  t /= W;
-  const int y = (int)(t % H), b = (int)(t / H);
+  const int j = blockIdx.x * kBlk + threadIdx.x;
+  if (j >= W * 32) return;
+  const int c = j & 31, xq = j >> 5, y = blockIdx.y, b = blockIdx.z;
+  const size_t i = ((size_t)b * H + y) * W * 32 + j;
   const int ntx = (W + TX - 1) / TX, nty = (H + TY - 1) / TY;
   // block row by covers window rows [by*TY - R - 1, by*TY - R - 1 + WR)
   const int by0 = max(0, (y + R + 1 - WR + 1 + TY - 1) / TY), by1 = min(nty - 1, (y + R + 1) / TY);
@@ -914,7 +903,8 @@ extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, 
     hipLaunchKernelGGL(dcn_bwd_data_kernel<CO>, dim3(nbd), dim3(kBlk), 0, st, x_nhwc, offset_mask, w_taps, dy_nhwc, \
                        batch, height, width, (const unsigned*)absmax, dx_nhwc, dom_nhwc, scratch);                \
     TMVS_CHECK_LAUNCH();                                                                                          \
-    hipLaunchKernelGGL(dcn_gather_windows_kernel, dim3((unsigned)((np * 32 + kBlk - 1) / kBlk)), dim3(kBlk), 0, st,  \
+    hipLaunchKernelGGL(dcn_gather_windows_kernel, dim3((unsigned)((width * 32 + kBlk - 1) / kBlk), height, batch),  \
+                       dim3(kBlk), 0, st,                                                                         \
                        (const float*)scratch, batch, height, width, dx_nhwc);                                     \
     TMVS_CHECK_LAUNCH();                                                                                          \
     hipLaunchKernelGGL(dcn_bwd_weight_kernel<CO>, xcd_range_tap_grid(9, nblk), dim3(kBlk), 0, st, x_nhwc,          \
