@@ -51,6 +51,38 @@ static inline dim3 xcd_range_tap_grid(int ntaps, int nblk) {
   return TMVS_WGRAD_XCD ? dim3((unsigned)((nblk + 7) / 8 * 8 * ntaps)) : dim3((unsigned)nblk, (unsigned)ntaps);
 }
 
+// (b, y, x) of row v of a [B][H][W] pixel grid, for a loader whose wave's rows all lie in the 64-row chunk
+// starting at v & ~63 (the weight-gradient reductions stage 64-row chunks from 64-aligned block starts):
+// the chunk start's coordinates by one scalar (wave-uniform) division, the row's by carrying from it --
+// instead of two divisions per lane and row
+#ifndef TMVS_CHUNK_COORDS
+#define TMVS_CHUNK_COORDS 1
+#endif
+__device__ __forceinline__ void chunk_row_coords(long v, int H, int W, int& b, int& y, int& x) {
+  if (!TMVS_CHUNK_COORDS) {
+    const long t = v / W;
+    x = (int)(v - t * W);
+    y = (int)(t % H);
+    b = (int)(t / H);
+    return;
+  }
+  const long vl = v & ~63L;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)vl);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long)vl >> 32));
+  const long vb = (long)(((unsigned long)hi << 32) | lo);
+  const long t = vb / W;
+  x = (int)(vb - t * W) + (int)(v - vb);
+  y = (int)(t % H);
+  b = (int)(t / H);
+  while (x >= W) {
+    x -= W;
+    if (++y == H) {
+      y = 0;
+      ++b;
+    }
+  }
+}
+
 // s + p[j0 * stride] + p[(j0 + step) * stride] + ... (j < n), added in that order in fp64 -- the partial
 // combines' fixed-order sums -- with 8 loads in flight ahead of their adds (a plain loop waits on each
 // load before its dependent add)

@@ -219,9 +219,8 @@ __global__ __launch_bounds__(kBlk) void conv2d_wgrad_kernel(const float* __restr
   const long v0 = (long)rb * ppb, v1 = v0 + ppb < np ? v0 + ppb : np;
   auto la = [&](long v, int q) { return load_row4(direct, v, a_ch, q); };
   auto lb = [&](long v, int q) {
-    const int pw = (int)(v % Pw);
-    const long t = v / Pw;
-    const int ph = (int)(t % Ph), b = (int)(t / Ph);
+    int b, ph, pw;
+    chunk_row_coords(v, Ph, Pw, b, ph, pw);  // rows of 64-aligned chunks (ppb_for: multiples of 1024)
     const int gh = ph * stride - pad + kh, gw = pw * stride - pad + kw;
     if (gh < 0 || gw < 0 || gh >= Gh || gw >= Gw) return make_float4(0.f, 0.f, 0.f, 0.f);
     return *reinterpret_cast<const float4*>(gath + (((size_t)b * Gh + gh) * Gw + gw) * BC + 4 * q);
@@ -648,14 +647,29 @@ __global__ __launch_bounds__(kBlk) void dcn_gather_windows_kernel(const float* _
   // block row by covers window rows [by*TY - R - 1, by*TY - R - 1 + WR)
   const int by0 = max(0, (y + R + 1 - WR + 1 + TY - 1) / TY), by1 = min(nty - 1, (y + R + 1) / TY);
   const int bx0 = max(0, (xq + R + 1 - WC + 1 + TX - 1) / TX), bx1 = min(ntx - 1, (xq + R + 1) / TX);
-  float s = 0.f;
-  for (int by = by0; by <= by1; ++by)
-    for (int bx = bx0; bx <= bx1; ++bx) {
+  // at most 2 x 2 windows (WR < 2 TY, WC < 2 TX): all their loads issued before the adds, which run in
+  // the loop order (block rows, then columns, ascending) from 0
+  static_assert(WR < 2 * TY && WC < 2 * TX, "a texel is covered by at most 2 x 2 windows");
+  float v[2][2];
+  bool ok[2][2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int by = by0 + r, bx = bx0 + q;
+      ok[r][q] = by <= by1 && bx <= bx1;
       const int cell = (y - (by * TY - R - 1)) * WC + (xq - (bx * TX - R - 1));
       const size_t blk = ((size_t)b * nty + by) * ntx + bx;
-      s += scratch[(blk * (WR * WC) + cell) * 32 + c];
+      v[r][q] = ok[r][q] ? scratch[(blk * (WR * WC) + cell) * 32 + c] : 0.f;
     }
-  dx[i] = dx[i] + s;
+  const float d0 = dx[i];
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (ok[r][q]) s += v[r][q];
+  dx[i] = d0 + s;
 }
 
 // dW[k][o][c] = sum_p dy[p][o] col_k[p][c]: grid (nblk, 9), block partials [nblk][9][CO][32]. A thread
@@ -696,9 +710,9 @@ __global__ __launch_bounds__(kBlk) void dcn_bwd_weight_kernel(const float* __res
                        blend(v4[0].z, v4[1].z, v4[2].z, v4[3].z), blend(v4[0].w, v4[1].w, v4[2].w, v4[3].w));
   };
   auto sample_at = [&](long v, int& b) {
-    b = (int)(v / HW);
-    const long p = v - (long)b * HW;
-    const int yy = (int)(p / W), xx = (int)(p % W);
+    int yy, xx;
+    chunk_row_coords(v, H, W, b, yy, xx);  // rows of 64-aligned chunks (ppb_for: multiples of 1024)
+    const long p = (long)yy * W + xx;
     return dcn_sample(om + (size_t)b * 27 * HW + p, (size_t)HW, yy, xx, k, H, W);
   };
 #if TMVS_DCNW_BROW
