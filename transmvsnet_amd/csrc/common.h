@@ -83,6 +83,39 @@ __device__ __forceinline__ void chunk_row_coords(long v, int H, int W, int& b, i
   }
 }
 
+// the same for row v of a [B][D][H][W] voxel grid: (b, z, y, x)
+__device__ __forceinline__ void chunk_row_coords3(long v, int D, int H, int W, int& b, int& z, int& y, int& x) {
+  if (!TMVS_CHUNK_COORDS) {
+    long t = v / W;
+    x = (int)(v - t * W);
+    y = (int)(t % H);
+    t /= H;
+    z = (int)(t % D);
+    b = (int)(t / D);
+    return;
+  }
+  const long vl = v & ~63L;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)vl);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long)vl >> 32));
+  const long vb = (long)(((unsigned long)hi << 32) | lo);
+  long t = vb / W;
+  x = (int)(vb - t * W) + (int)(v - vb);
+  y = (int)(t % H);
+  t /= H;
+  z = (int)(t % D);
+  b = (int)(t / D);
+  while (x >= W) {
+    x -= W;
+    if (++y == H) {
+      y = 0;
+      if (++z == D) {
+        z = 0;
+        ++b;
+      }
+    }
+  }
+}
+
 // s + p[j0 * stride] + p[(j0 + step) * stride] + ... (j < n), added in that order in fp64 -- the partial
 // combines' fixed-order sums -- with 8 loads in flight ahead of their adds (a plain loop waits on each
 // load before its dependent add)

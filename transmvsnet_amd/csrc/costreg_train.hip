@@ -193,11 +193,8 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_tile_kernel(
     const long u0 = (long)rb * vpb, u1 = u0 + vpb < nv ? u0 + vpb : nv;
     auto la = [&](long v, int q) { return *reinterpret_cast<const float4*>(direct + v * A + 4 * q); };
     auto lb = [&](long v, int q) {
-      const int pw = (int)(v % Pw);
-      long t = v / Pw;
-      const int ph = (int)(t % Ph);
-      t /= Ph;
-      const int pd = (int)(t % Pd), b = (int)(t / Pd);
+      int b, pd, ph, pw;
+      chunk_row_coords3(v, Pd, Ph, Pw, b, pd, ph, pw);  // rows of 64-aligned chunks (wgrad_vpb: multiples of 2048)
       const int gd = pd * stride - 1 + kd, gh = ph * stride - 1 + kh, gw = pw * stride - 1 + kw;
       if (gd < 0 || gh < 0 || gw < 0 || gd >= Gd || gh >= Gh || gw >= Gw) return make_float4(0.f, 0.f, 0.f, 0.f);
       return *reinterpret_cast<const float4*>(gath + ((((size_t)b * Gd + gd) * Gh + gh) * Gw + gw) * BC + 4 * q);
