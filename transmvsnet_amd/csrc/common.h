@@ -116,6 +116,35 @@ __device__ __forceinline__ void chunk_row_coords3(long v, int D, int H, int W, i
   }
 }
 
+// The fp64 wave sum of the xor butterfly x += __shfl_xor(x, off), off = 32, 16, ..., 1 (the same pairs and
+// operand order, so the same bits), with the partner moved by DPP row permutes for 1, 2, 4 (half mirror
+// then quad reverse) and 8 (row mirror then half mirror), ds_swizzle (bit mode) for 16 and ds_bpermute for
+// 32: 4 instead of 12 LDS-unit operations per value
+template <int OFF>
+__device__ __forceinline__ int xor_lane_dpp(int v) {
+  if constexpr (OFF == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
+  else if constexpr (OFF == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
+  else if constexpr (OFF == 4)
+    return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false), 0x1B, 0xF, 0xF, false);
+  else if constexpr (OFF == 8)
+    return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false), 0x141, 0xF, 0xF, false);
+  else if constexpr (OFF == 16) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (16 << 10));
+  else return __shfl_xor(v, 32, 64);
+}
+template <int OFF>
+__device__ __forceinline__ double xor_add_dpp(double x) {
+  const int lo = xor_lane_dpp<OFF>(__double2loint(x)), hi = xor_lane_dpp<OFF>(__double2hiint(x));
+  return x + __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_xor_sum_dpp(double x) {
+  x = xor_add_dpp<32>(x);
+  x = xor_add_dpp<16>(x);
+  x = xor_add_dpp<8>(x);
+  x = xor_add_dpp<4>(x);
+  x = xor_add_dpp<2>(x);
+  return xor_add_dpp<1>(x);
+}
+
 // s + p[j0 * stride] + p[(j0 + step) * stride] + ... (j < n), added in that order in fp64 -- the partial
 // combines' fixed-order sums -- with 8 loads in flight ahead of their adds (a plain loop waits on each
 // load before its dependent add)

@@ -368,6 +368,9 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_small_kernel(
 // `direct` row once per kd and the 9 neighbours' `gathered` rows (L1/L2 hits), keeping 9 x A x BC fp32
 // sums over its voxels; then per value a fixed wave butterfly (fp64) and the 4 waves in order.
 // Replaces 27 passes over `direct` with 3.
+#ifndef TMVS_TAPS_DPP
+#define TMVS_TAPS_DPP 1
+#endif
 template <int A, int BC>
 __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_taps_kernel(
     const float* __restrict__ direct, const float* __restrict__ gath, int B, int Pd, int Ph, int Pw, int Gd, int Gh,
@@ -452,8 +455,12 @@ __global__ __launch_bounds__(kTrainBlock) void conv3d_wgrad_taps_kernel(
 #pragma unroll
     for (int q = 0; q < NPR; ++q) {
       double x = (double)acc[k][q];
+      if (TMVS_TAPS_DPP) {
+        x = wave_xor_sum_dpp(x);  // the same butterfly (common.h)
+      } else {
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+      }
       if (lane == 0) red[k * NPR + q][wv] = x;
     }
   __syncthreads();

@@ -67,29 +67,10 @@ __device__ __forceinline__ void pw_chain(float s, const float* __restrict__ p, c
   c.sg = 1.f / (1.f + expf(-c.o));
 }
 
-// x[lane ^ OFF] of a double: DPP row moves for 1, 2, 4 (half mirror then quad reverse) and 8 (row
-// mirror then half mirror), ds_swizzle (bit mode) for 16, ds_bpermute for 32 -- the values __shfl_xor
-// returns, with 4 instead of 12 LDS-unit operations per 6-step butterfly
+// (TMVS_PW_DPP: the pass-2 wave sums by common.h's DPP butterfly, r15a)
 #ifndef TMVS_PW_DPP
 #define TMVS_PW_DPP 1
 #endif
-template <int OFF>
-__device__ __forceinline__ int xor_lane(int v) {
-  if constexpr (OFF == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
-  else if constexpr (OFF == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
-  else if constexpr (OFF == 4)
-    return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false), 0x1B, 0xF, 0xF, false);
-  else if constexpr (OFF == 8)
-    return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false), 0x141, 0xF, 0xF, false);
-  else if constexpr (OFF == 16) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (16 << 10));
-  else return __shfl_xor(v, 32, 64);
-}
-template <int OFF, bool DPP>
-__device__ __forceinline__ double xor_add(double x) {
-  const int lo = xor_lane<OFF>(__double2loint(x)), hi = xor_lane<OFF>(__double2hiint(x));
-  return x + __hiloint2double(hi, lo);
-}
-
 // fp64 block reduction of NV values per thread into partial[blockIdx.x][NV]: a fixed xor butterfly
 // inside each wave, then the 4 wave sums in a fixed order (deterministic). The DPP moves only for the
 // 160-value pass-2 reduction: with 25 values (pass 1) they raised the kernel to 178 VGPRs (2 waves/SIMD)
@@ -102,12 +83,7 @@ __device__ __forceinline__ void block_reduce_store(const T (&v)[NV], double* __r
   for (int i = 0; i < NV; ++i) {
     double x = (double)v[i];
     if constexpr (kDpp) {
-      x = xor_add<32, true>(x);
-      x = xor_add<16, true>(x);
-      x = xor_add<8, true>(x);
-      x = xor_add<4, true>(x);
-      x = xor_add<2, true>(x);
-      x = xor_add<1, true>(x);
+      x = wave_xor_sum_dpp(x);
     } else {
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
