@@ -18,12 +18,6 @@ typedef float floatx4_t __attribute__((ext_vector_type(4)));
 // load_b(v, q0, float4 (&)[2]) instead of quad t&7 of rows t>>3 and t>>3 + 32: a gathered B row whose
 // loader derives per-row state (the DCN sample geometry) derives it once for both quads. Same LDS
 // contents, same sums.
-// PF2 (TMVS_WGRAD_PF2, launches with fewer than 4 tiles): two chunks' rows in flight in registers (the
-// loop unrolled by two over named register sets) instead of one: a 1-tile reduction runs only 4 MFMAs per
-// wave and chunk, too few to cover one chunk's loads. The same chunks and sums, the same LDS.
-#ifndef TMVS_WGRAD_PF2
-#define TMVS_WGRAD_PF2 1
-#endif
 template <int A, int BC, bool BROW = false, typename LoadA, typename LoadB>
 __device__ __forceinline__ void tile_reduce_mfma(long v0, long v1, LoadA load_a, LoadB load_b,
                                                  double* __restrict__ out) {
@@ -50,7 +44,7 @@ __device__ __forceinline__ void tile_reduce_mfma(long v0, long v1, LoadA load_a,
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc[t][r] = 0.0;
   float4 pa[LA], pb[LB];
-  auto fetch = [&](long vb, float4 (&pa)[LA], float4 (&pb)[LB]) {
+  auto fetch = [&](long vb) {
 #pragma unroll
     for (int k = 0; k < LA; ++k) {
       const int i = threadIdx.x + 256 * k, r = i / (AP / 4), q = i % (AP / 4);
@@ -68,7 +62,7 @@ __device__ __forceinline__ void tile_reduce_mfma(long v0, long v1, LoadA load_a,
       }
     }
   };
-  auto commit = [&](const float4 (&pa)[LA], const float4 (&pb)[LB]) {
+  auto commit = [&]() {
 #pragma unroll
     for (int k = 0; k < LA; ++k) {
       const int i = threadIdx.x + 256 * k, r = i / (AP / 4), q = i % (AP / 4);
@@ -81,7 +75,13 @@ __device__ __forceinline__ void tile_reduce_mfma(long v0, long v1, LoadA load_a,
       *reinterpret_cast<float4*>(sb + r * SB + 4 * q) = pb[k];
     }
   };
-  auto chunk = [&]() {  // this chunk's MFMA chains, then their fp64 adds
+  if (v0 < v1) fetch(v0);
+#pragma unroll 1
+  for (long vb = v0; vb < v1; vb += CH) {
+    __syncthreads();
+    commit();
+    __syncthreads();
+    if (vb + CH < v1) fetch(vb + CH);  // lands during this chunk's MFMAs
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
       const int tile = KS > 1 ? wv / KS : wv * TPW + t;
@@ -94,35 +94,6 @@ __device__ __forceinline__ void tile_reduce_mfma(long v0, long v1, LoadA load_a,
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[t][r] += (double)d[r];
-    }
-  };
-  if constexpr (TMVS_WGRAD_PF2 && NT < 4 && !BROW) {
-    float4 qa[LA], qb[LB];
-    if (v0 < v1) fetch(v0, pa, pb);
-    if (v0 + CH < v1) fetch(v0 + CH, qa, qb);
-#pragma unroll 1
-    for (long vb = v0; vb < v1; vb += 2 * CH) {
-      __syncthreads();
-      commit(pa, pb);
-      __syncthreads();
-      if (vb + 2 * CH < v1) fetch(vb + 2 * CH, pa, pb);
-      chunk();
-      if (vb + CH >= v1) break;  // (block-uniform)
-      __syncthreads();
-      commit(qa, qb);
-      __syncthreads();
-      if (vb + 3 * CH < v1) fetch(vb + 3 * CH, qa, qb);
-      chunk();
-    }
-  } else {
-    if (v0 < v1) fetch(v0, pa, pb);
-#pragma unroll 1
-    for (long vb = v0; vb < v1; vb += CH) {
-      __syncthreads();
-      commit(pa, pb);
-      __syncthreads();
-      if (vb + CH < v1) fetch(vb + CH, pa, pb);  // lands during this chunk's MFMAs
-      chunk();
     }
   }
   // lane (col, kg) of tile (ma, nb) holds D[16 ma + 4 kg + r][16 nb + col]
