@@ -257,6 +257,9 @@ __global__ __launch_bounds__(kTB) void layer_norm_fwd_kernel(const float* __rest
 }
 
 // dx = rstd/32 * (32*gy - sum gy - xhat * sum gy*xhat), gy = dy * g; partial[blk] = {sum dy*xhat (32), sum dy (32)}
+#ifndef TMVS_LN_DPP
+#define TMVS_LN_DPP 1
+#endif
 __global__ __launch_bounds__(kTB) void layer_norm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                              long T, const float* __restrict__ g, long tpb,
                                                              float* __restrict__ dx, double* __restrict__ partial) {
@@ -268,9 +271,17 @@ __global__ __launch_bounds__(kTB) void layer_norm_bwd_kernel(const float* __rest
   for (long t = t0 + threadIdx.x; t < t1; t += kTB) {
     float v[32], d[32];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      v[i] = x[t * 32 + i];
-      d[i] = dy[t * 32 + i];
+    for (int i = 0; i < 32; i += 4) {  // 16-byte loads of the token's rows (the same values)
+      const float4 a = *reinterpret_cast<const float4*>(x + t * 32 + i);
+      const float4 b = *reinterpret_cast<const float4*>(dy + t * 32 + i);
+      v[i] = a.x;
+      v[i + 1] = a.y;
+      v[i + 2] = a.z;
+      v[i + 3] = a.w;
+      d[i] = b.x;
+      d[i + 1] = b.y;
+      d[i + 2] = b.z;
+      d[i + 3] = b.w;
     }
     float mean, rstd;
     ln_stats(v, mean, rstd);
@@ -284,19 +295,27 @@ __global__ __launch_bounds__(kTB) void layer_norm_bwd_kernel(const float* __rest
       pg[i] = fmaf(d[i], xh, pg[i]);
       pb[i] += d[i];
     }
+    float o[32];
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
       const float xh = (v[i] - mean) * rstd;
-      dx[t * 32 + i] = (rstd / 32.f) * ((32.f * (d[i] * g[i]) - s1) - xh * s2);
+      o[i] = (rstd / 32.f) * ((32.f * (d[i] * g[i]) - s1) - xh * s2);
     }
+#pragma unroll
+    for (int i = 0; i < 32; i += 4)
+      *reinterpret_cast<float4*>(dx + t * 32 + i) = make_float4(o[i], o[i + 1], o[i + 2], o[i + 3]);
   }
   // fp64 block reduction of the 64 per-thread sums (fixed butterfly per wave, then the 4 waves in order)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < 64; ++i) {
     double val = (double)(i < 32 ? pg[i] : pb[i - 32]);
+    if (TMVS_LN_DPP) {
+      val = wave_xor_sum_dpp(val);  // the same butterfly (common.h)
+    } else {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off, 64);
+      for (int off = 32; off > 0; off >>= 1) val += __shfl_xor(val, off, 64);
+    }
     if (lane == 0) red[i][wv] = val;
   }
   __syncthreads();
