@@ -14,7 +14,7 @@ for v in default lnold; do
   if [ "$v" = default ]; then unset TMVS_LIB_PATH; else export TMVS_LIB_PATH=variants/$v/libtransmvs_hip.so; fi
   STEPS=2 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$v -o run -- python3 scripts/diag/train_step_prof.py > $O/$v.log 2>&1 || exit $?
   echo "== $v" >> $O/summary.txt
-  python3 scripts/diag/kernel_grid_times.py $O/$v/run_results.db wgrad >> $O/summary.txt
+  python3 scripts/diag/kernel_grid_times.py $O/$v/run_results.db layer_norm >> $O/summary.txt
   rm -rf $O/$v
 done
 for v in default lnold default lnold; do
