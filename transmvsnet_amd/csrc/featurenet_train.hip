@@ -228,6 +228,9 @@ __global__ __launch_bounds__(kBlk) void conv2d_wgrad_kernel(const float* __restr
   tile_reduce_any<AP, BC>(v0, v1, la, lb, partial + ((size_t)rb * K * K + k) * AP * BC);
 }
 
+#ifndef TMVS_SMALL_DPP
+#define TMVS_SMALL_DPP 1
+#endif
 // few channels on the gathered side (the image: 3): thread t owns pairs t, t+256, .. of a x b,
 // straight from global memory (L1 hits), fp32 over a block's pixels in 8 interleaved chains, fp64 after
 template <int A, int BC>
@@ -266,8 +269,12 @@ __global__ __launch_bounds__(kBlk) void conv2d_wgrad_small_kernel(const float* _
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
     double x = (double)acc[q];
+    if (TMVS_SMALL_DPP) {
+      x = wave_xor_sum_dpp(x);  // the same butterfly (common.h)
+    } else {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    }
     if (lane == 0) red[q][wv] = x;
   }
   __syncthreads();

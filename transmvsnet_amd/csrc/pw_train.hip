@@ -72,11 +72,11 @@ __device__ __forceinline__ void pw_chain(float s, const float* __restrict__ p, c
 #define TMVS_PW_DPP 1
 #endif
 // fp64 block reduction of NV values per thread into partial[blockIdx.x][NV]: a fixed xor butterfly
-// inside each wave, then the 4 wave sums in a fixed order (deterministic). The DPP moves only for the
-// 160-value pass-2 reduction: with 25 values (pass 1) they raised the kernel to 178 VGPRs (2 waves/SIMD)
+// inside each wave, then the 4 wave sums in a fixed order (deterministic). The DPP moves for the 160-value
+// pass-2 and the 16-value pass-3 / z1 reductions: with 25 values (pass 1) they raised it to 178 VGPRs
 template <typename T, int NV>
 __device__ __forceinline__ void block_reduce_store(const T (&v)[NV], double* __restrict__ partial) {
-  constexpr bool kDpp = TMVS_PW_DPP && NV >= 64;
+  constexpr bool kDpp = TMVS_PW_DPP && (NV >= 64 || NV == 16);
   __shared__ double red[kPwBlock / 64][NV];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
