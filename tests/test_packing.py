@@ -50,3 +50,16 @@ def test_fmt_layer_blocks():
                        "test_fmt")
     for i in range(8):
         assert torch.equal(enc[i], train._pack_enc(params[16 * i:16 * i + 16]))
+
+
+def test_offset_conv_dgrad_pack_one_gather():
+    """featurenet_train.offset_dgrad_pack (one gather from conv_offset_mask.weight) equals the DCN
+    backward's previous build of the same pack: the weight zero-padded to 32 output rows, flipped and
+    transposed (dgrad_same's weight), then device_pack('dcn', .)."""
+    from transmvsnet_amd import featurenet_train as ft
+    g = torch.Generator().manual_seed(1)
+    for _ in range(2):
+        w = torch.randn(27, 32, 3, 3, generator=g)
+        wp = torch.zeros(32, 32, 3, 3)
+        wp[:27] = w
+        assert torch.equal(ft.offset_dgrad_pack(w), ft.device_pack("dcn", ft._flip_t(wp)))

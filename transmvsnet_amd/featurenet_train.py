@@ -61,6 +61,33 @@ def _pack_index(kind, cout, cin, k, device):
     return _PACK_INDEX[key]
 
 
+def _offset_dgrad_index(device):
+    """Gather indices from conv_offset_mask.weight [27][32][3][3] (flattened, plus one trailing zero)
+    straight to the 'dcn' pack of its data-gradient weight: the weight zero-padded to 32 output rows,
+    flipped in both spatial axes and transposed (in <-> out), as dgrad_same builds it -- one gather
+    instead of the pad, flip, transpose and pack launches."""
+    key = ("offdgrad", str(device))
+    if key not in _PACK_INDEX:
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("featurenet_train: offset-conv dgrad index not built yet inside a HIP-graph "
+                               "capture; run the step once eagerly before capturing it")
+        zero = 27 * 32 * 9
+        a, b, kh, kw = np.meshgrid(np.arange(32), np.arange(32), np.arange(3), np.arange(3), indexing="ij")
+        # flipped-transposed padded weight wf[a][b][kh][kw] = W[b][a][2 - kh][2 - kw] (0 for b >= 27)
+        src = np.where(b < 27, ((b * 32 + a) * 3 + (2 - kh)) * 3 + (2 - kw), zero).reshape(-1)
+        src = np.concatenate([src, [zero]])
+        pidx = _pack_index("dcn", 32, 32, 3, "cpu").numpy()
+        _PACK_INDEX[key] = torch.from_numpy(src[pidx].astype(np.int64)).to(device)
+    return _PACK_INDEX[key]
+
+
+def offset_dgrad_pack(w_offset_mask):
+    """device_pack('dcn', _flip_t(W zero-padded to 32 rows)) of conv_offset_mask.weight, one gather."""
+    flat = torch.cat([w_offset_mask.detach().float().reshape(-1),
+                      w_offset_mask.new_zeros(1, dtype=torch.float32)])
+    return flat[_offset_dgrad_index(w_offset_mask.device)]
+
+
 def device_pack(kind, w):
     """The kernels' packed weight layout, gathered on the weight's device ('dcn' or 'conv2d')."""
     co, ci, k, _ = w.shape
@@ -201,10 +228,9 @@ def _dcn_bwd(dcn, x, om, dy, grads):
     dwo = ops.conv2d_wgrad(dom, x, 3, 1, 1)[:, :27].contiguous()
     _acc(grads, com.weight, _untaps(dwo, com.weight.shape))
     _acc(grads, com.bias, ops.colsum(dom)[:27].contiguous())
-    wp = torch.zeros(32, 32, 3, 3, device=x.device)  # [co 27 + 5 zero rows][ci][3][3]
-    wp[:27] = com.weight.detach().float()
-    # dx += its data gradient (dgrad_same's 32 -> 32 3x3 form), added in the conv's epilogue
-    ops.conv3x3_nhwc_acc(dom, device_pack("dcn", _flip_t(wp)), dx)
+    # dx += its data gradient (dgrad_same's 32 -> 32 3x3 form on the weight padded to 32 output rows,
+    # packed by one gather), added in the conv's epilogue
+    ops.conv3x3_nhwc_acc(dom, offset_dgrad_pack(com.weight), dx)
     return dx
 
 
