@@ -247,6 +247,27 @@ def run(args, world, rank, local):
                 raise RuntimeError(f"ranks disagree (steps, depth checksum): {allc}")
             ranks_ok = {"ranks": world, "steps_each": args.steps, "depth_checksum": allc[0][1]}
 
+        eager = None
+        if graphed:
+            # the same K steps launched eagerly from Python, outside the timed region: the form a caller
+            # with per-sample cameras runs (the proj rows are kernel arguments frozen in the captured graph)
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            te = time.perf_counter()
+            for _ in range(args.steps):
+                eager_step()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - te
+            if world > 1:
+                t = torch.tensor([el], device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                el = float(t.item())
+            mps = shard.replicas if shard is not None else (1 if args.mode == "views" else world)
+            eager = {"ms_per_step": round(el / args.steps * 1e3, 3),
+                     "depth_maps_per_s": round(mps * args.steps / el, 3), "steps": args.steps,
+                     "launch": "eager (one Python call per C-ABI entry point per step; not the headline)"}
+
         # instrumented steps (outside the timed region): per-launch HIP-event durations
         timer = EventTimer()
         model.decomposed = True   # same kernels, one C-ABI call each, so each gets its own event pair
@@ -368,6 +389,7 @@ def run(args, world, rank, local):
                                    "outputs (FMT+pathway+stage glue+cost volume+CostRegNet+softmax/WTA)",
                        "global_batch": maps_per_step, "parallelism": f"{args.mode}{world}",
                        "launch": "hip_graph replay" if graphed else "eager"},
+            "eager": eager,
             "roofline": dominant,
             "roofline_kernels": kern,
             "kernel_ms_per_depth_map": breakdown,

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TMVS_ABI_VERSION 7
+#define TMVS_ABI_VERSION 8
 
 #define TMVS_OK 0
 #define TMVS_ERR_ARG (-1)    /* null pointer / non-positive size / bad enum        */
@@ -359,10 +359,12 @@ int tmvs_linattn_bwd_kv(const float* k, const float* v, long tokens, long tokens
 int tmvs_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, double lr,
                    double beta1, double beta2, double eps, double weight_decay, int step, void* stream);
 /* The same with the step number on the device (a captured HIP graph replays it): *step_counter
- * (int, device) is advanced by the launch itself; scalars: 2 device floats of scratch.          */
+ * (int, device) is advanced by the launch itself; scalars: 2 device floats of scratch. lr_dev
+ * (ABI 8): NULL = use lr; else the launch reads the learning rate from that device double when it
+ * runs, so a graph replay follows the schedule the caller writes there (finetune.py:58-72).     */
 int tmvs_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, double lr,
-                       double beta1, double beta2, double eps, double weight_decay, int* step_counter, float* scalars,
-                       void* stream);
+                       const double* lr_dev, double beta1, double beta2, double eps, double weight_decay,
+                       int* step_counter, float* scalars, void* stream);
 
 /* BatchNorm3d in train mode over z [nvox][C] (C divides 256): batch mean and biased variance
  * (fp64 partials, fixed-order combine); y = relu(fmaf(z, a, b)) [+ skip] with a = gamma /
@@ -462,7 +464,7 @@ int tmvs_fusibile(const float* rgbd, const float* cams, int n_views, int height,
                   int consistent_threshold, float depth_threshold, float* coord, float* texture, void* stream);
 
 /* ------------------------------------------------------------------ training losses
- * entropy_loss (models/module.py:495-529) of one stage, as trans_mvsnet_loss / focal_loss_bld
+ * entropy_loss (models/module.py:495-531) of one stage, as trans_mvsnet_loss / focal_loss_bld
  * (:532-588) call it, fused with the backward through the stage's softmax (:prob = softmax(logits)).
  *   prob        [batch][ndepth][H][W]   softmax probability volume (outputs[stage]["prob_volume"])
  *   depth_values [batch][ndepth][H][W] (dv_per_pixel = 1) or [batch][ndepth] (0, module.py:503-504)

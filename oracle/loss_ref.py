@@ -1,5 +1,5 @@
 """CPU oracle for the training losses (TEST INFRASTRUCTURE ONLY: imported by tests/, never by the
-product path). A PyTorch-CPU restatement of models/module.py:495-588; the gradient w.r.t. each
+product path). A PyTorch-CPU restatement of models/module.py:495-592; the gradient w.r.t. each
 stage's logits comes from autograd through F.softmax. Pinned against tests/golden/loss.npz, made by
 tests/golden/make_golden_loss.py from the real reference functions.
 """
@@ -10,7 +10,7 @@ import torch.nn.functional as F
 
 
 def entropy_loss(prob_volume, depth_gt, mask, depth_value, return_prob_map=False):
-    """module.py:495-529."""
+    """module.py:495-531."""
     valid = torch.sum(mask, dim=[1, 2]) + 1e-6                       # :499
     b, h, w = depth_gt.shape
     d = depth_value.shape[1]
@@ -52,12 +52,12 @@ def _stages(inputs, depth_gt_ms, mask_ms, dlossw):
 
 
 def trans_mvsnet_loss(inputs, depth_gt_ms, mask_ms, dlossw=None):
-    """module.py:532-556."""
+    """module.py:534-558."""
     return _stages(inputs, depth_gt_ms, mask_ms, dlossw)
 
 
 def focal_loss_bld(inputs, depth_gt_ms, mask_ms, depth_interval, dlossw=None):
-    """module.py:559-588."""
+    """module.py:561-592."""
     total, depth_loss, _, _ = _stages(inputs, depth_gt_ms, mask_ms, dlossw)
     err = (depth_gt_ms["stage3"] - inputs["stage3"]["depth"]).abs()
     err = err / (depth_interval * 192. / 128.)

@@ -235,3 +235,23 @@ def test_conv2d_wgrad_vs_torch(a, bc, k, stride, h, w):
     got = dw.double().cpu().reshape(k, k, a, bc).permute(2, 3, 0, 1)
     err = float((got - ref).abs().max() / ref.abs().max())
     assert err < 1e-5, err
+
+
+def test_dcn_backward_nonfinite_dy_poisons_dx():
+    """A non-finite upstream gradient (inf / NaN in dy) makes tmvs_dcn_backward's dx and d offset/mask
+    non-finite (the kFixBad path: the fixed-point window cannot hold it, so every window is written
+    as NaN), so the training step's overflow / finiteness checks see it."""
+    from transmvsnet_amd.featurenet_train import _taps
+    torch.manual_seed(3)
+    b, h, w, cout = 1, 24, 40, 32
+    x = torch.randn(b, h, w, 32, device=DEV)
+    om = torch.randn(b, 27, h, w, device=DEV) * 0.3
+    wt = _taps(torch.randn(cout, 32, 3, 3) * 0.06).to(DEV)
+    for bad in (float("inf"), float("nan")):
+        dy = torch.randn(b, h, w, cout, device=DEV)
+        dy[0, 5, 7, 3] = bad
+        dx = torch.zeros(b, h, w, 32, device=DEV)
+        dom, dw = ops.dcn_backward(x, om.contiguous(), wt, dy, dx)
+        torch.cuda.synchronize()
+        assert not bool(torch.isfinite(dx).all()), bad
+        assert not bool(torch.isfinite(dom[..., :27]).all()), bad

@@ -697,6 +697,83 @@ def test_flat_adam_graph_replay_equals_eager_steps():
     assert torch.equal(oa.exp_avg, ob.exp_avg) and torch.equal(oa.exp_avg_sq, ob.exp_avg_sq)
 
 
+def test_flat_adam_graph_replay_follows_lr_schedule():
+    """A captured FlatAdam step reads its learning rate from the device when the replay runs (ABI 8,
+    ADVICE r4): replays with opt.lr changed before each (sync_lr) give bitwise the parameters and
+    moments of eager steps run with the same per-step learning rates (finetune.py:58-72's
+    WarmupMultiStepLR sets the lr every iteration)."""
+    from transmvsnet_amd.train import FlatAdam
+    torch.manual_seed(6)
+    shapes = [(8, 4, 3, 3, 3), (32,)]
+    init = [torch.randn(s) for s in shapes]
+    grads = [torch.randn(s).to(DEV) * 0.1 for s in shapes]
+    lrs = [1e-3, 1e-3, 5e-4, 1e-4, 2e-3]
+    pa = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+    pb = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+    oa = FlatAdam(pa, lr=1e-3, weight_decay=1e-4)
+    ob = FlatAdam(pb, lr=1e-3, weight_decay=1e-4)
+    for lr in lrs:
+        oa.zero_grad()
+        for p, gr in zip(pa, grads):
+            p.grad = gr.clone()
+        oa.step(lr=lr)
+
+    def step_b():
+        ob.zero_grad()
+        for p, gr in zip(pb, grads):
+            p.grad = gr.clone()
+        ob.step()
+    step_b()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step_b()
+    for lr in lrs[1:]:
+        ob.lr = lr
+        ob.sync_lr()
+        graph.replay()
+    torch.cuda.synchronize()
+    assert ob.step_count == len(lrs)
+    assert torch.equal(oa.flat, ob.flat)
+    assert torch.equal(oa.exp_avg, ob.exp_avg) and torch.equal(oa.exp_avg_sq, ob.exp_avg_sq)
+
+
+def test_graph_overflow_flags_are_sticky():
+    """The overflow flag of a warp backward captured in a HIP graph is sticky: a replay
+    whose d similarity is non-finite followed by a clean replay still raises at the next check; the
+    check clears the flags, so a clean replay afterwards passes."""
+    from transmvsnet_amd import ops, synthetic
+    from transmvsnet_amd import train as tr
+    c, d, h, w, nv = 8, 8, 24, 32, 2
+    g = torch.Generator().manual_seed(7)
+    ref = torch.randn(h, w, c, generator=g).to(DEV).requires_grad_()
+    src = torch.randn(nv, h, w, c, generator=g).to(DEV).requires_grad_()
+    rows = ops.proj_rows(synthetic.synthetic_cameras(nv + 1, h * 4, w * 4, seed=3)["stage1"])[0]
+    hyp = torch.linspace(425.0, 935.0, d).view(d, 1, 1).expand(d, h, w).contiguous().to(DEV)
+    clean = torch.randn(nv, d, h, w, generator=g).to(DEV)
+    dsim = clean.clone()
+    tr.warp_corr_views(ref, src, hyp, rows).backward(dsim)  # eager: reserves the flag arena
+    tr.drop_graph_flags()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        tr.warp_corr_views(ref, src, hyp, rows).backward(dsim)
+    assert len(tr.GRAPH_FLAGS) == 1
+    try:
+        graph.replay()
+        tr.check_graph_flags()  # clean
+        dsim[0, 3, 5, 7] = float("inf")
+        graph.replay()  # overflows
+        dsim.copy_(clean)
+        graph.replay()  # clean again: the earlier overflow must not be lost
+        with pytest.raises(RuntimeError, match="non-finite"):
+            tr.check_graph_flags()
+        graph.replay()
+        tr.check_graph_flags()  # cleared by the previous check
+    finally:
+        tr.drop_graph_flags()
+
+
 def test_training_loop_reduces_loss():
     """A C5-style loop on one fixed synthetic sample (128x160, N=3, 8/8/8): FMT -> pathway -> DepthNet
     stages -> focal_loss_bld (dlossw 1,1,1) -> backward -> FlatAdam.step, 8 iterations, all HIP. The

@@ -76,7 +76,7 @@ SIGNATURES = {
     "tmvs_linattn_bwd_q": (I, [P, P, L, L, P, L, P, S, P, P, P]),
     "tmvs_linattn_bwd_kv": (I, [P, P, L, L, P, P, P, P]),
     "tmvs_adam_step": (I, [P, P, P, P, L, D, D, D, D, D, I, P]),
-    "tmvs_adam_step_dev": (I, [P, P, P, P, L, D, D, D, D, D, P, P, P]),
+    "tmvs_adam_step_dev": (I, [P, P, P, P, L, D, P, D, D, D, D, P, P, P]),
     "tmvs_conv3d_generic": (I, [P, I, I, I, I, I, P, I, I, I, I, I, I, P, P]),
     "tmvs_conv3d_mfma": (I, [P, I, I, I, I, I, P, I, I, I, P, P, P]),
     "tmvs_conv3d_wgrad_workspace": (S, [I, I, I, I, I, I]),
@@ -101,7 +101,7 @@ SIGNATURES = {
     "tmvs_softmax_backward": (I, [P, P, I, I, I, I, P, P]),
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 PW_NPARAMS = 201
 ENC_NPARAMS = 8544
 KV_NFLOATS = 160

@@ -412,8 +412,10 @@ __global__ __launch_bounds__(kBlk) void absmax2_kernel(const float* __restrict__
 // CO max|dy| max|W| (m, w_bilinear <= 1), a cell at most kMaxAdds of them: with 2^e above that
 // bound, units of 2^-(62 - e) keep every cell's int64 sum in range, at a resolution 2^-40 or finer
 // relative to the largest possible contribution. A non-finite max|dy| or max|W| (an inf/NaN
-// upstream gradient) returns kFixBad: the window is then written as NaN, so dx propagates the NaN
-// as torch's deform_conv2d backward would, instead of converting inf/NaN to garbage integers.
+// upstream gradient) returns kFixBad: every block's window is then written as NaN, so the WHOLE dx
+// becomes NaN (torch's deform_conv2d backward would poison only the texels the bad values reach);
+// this is deliberate -- a poisoned step must not pass as finite, and the training overflow check sees
+// it -- instead of converting inf/NaN to garbage integers.
 constexpr int kFixBad = -100000;
 __device__ __forceinline__ int dcn_fix_shift(const unsigned* __restrict__ mx, int CO) {
   const double bound = (double)__uint_as_float(mx[0]) * (double)__uint_as_float(mx[1]) * CO * (double)dbw::kMaxAdds;

@@ -540,8 +540,13 @@ extern "C" int tmvs_token_wgrad(const float* dy, int a, const float* x, int b, l
   return TMVS_ERR_SHAPE;
 }
 
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// The LayerNorm kernels move a token's 32 channels as 16-byte quads: x, y, dy and dx must be
+// 16-byte aligned (any row of a contiguous [tokens][32] buffer is when its base is).
 extern "C" int tmvs_layer_norm_fwd(const float* x, long tokens, const float* g, const float* b, float* y, void* stream) {
   if (!x || !g || !b || !y || tokens <= 0) return TMVS_ERR_ARG;
+  if (!aligned16(x) || !aligned16(y)) return TMVS_ERR_ARG;
   hipLaunchKernelGGL(layer_norm_fwd_kernel, dim3((unsigned)((tokens + kTB - 1) / kTB)), dim3(kTB), 0,
                      (hipStream_t)stream, x, tokens, g, b, y);
   TMVS_CHECK_LAUNCH();
@@ -556,6 +561,7 @@ extern "C" size_t tmvs_layer_norm_bwd_workspace(long tokens) {
 extern "C" int tmvs_layer_norm_bwd(const float* dy, const float* x, long tokens, const float* g, void* workspace,
                                    size_t workspace_bytes, float* dx, float* dgb, int accumulate, void* stream) {
   if (!dy || !x || !g || !workspace || !dx || !dgb || tokens <= 0) return TMVS_ERR_ARG;
+  if (!aligned16(dy) || !aligned16(x) || !aligned16(dx)) return TMVS_ERR_ARG;
   if (workspace_bytes < tmvs_layer_norm_bwd_workspace(tokens)) return TMVS_ERR_ARG;
   const long c = tok_chunk(tokens, 1024, 256);
   const int nblk = (int)((tokens + c - 1) / c);

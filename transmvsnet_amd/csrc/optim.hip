@@ -45,10 +45,13 @@ extern "C" int tmvs_adam_step(float* param, const float* grad, float* exp_avg, f
 
 // The same step with the step counter on the device (HIP-graph replays): a one-thread kernel advances
 // *step and writes lr / (1 - beta1^step) and sqrt(1 - beta2^step) (double, as the host form) into
-// scal[0..1], which adam_kernel_dev reads.
-__global__ void adam_prep_kernel(int* __restrict__ step, float* __restrict__ scal, double lr, double beta1,
-                                 double beta2) {
+// scal[0..1], which adam_kernel_dev reads. lr_dev (ABI 8): when non-null the learning rate is read from
+// that device double at run time, so a replayed graph follows the caller's schedule (finetune.py:58-72
+// steps WarmupMultiStepLR every iteration) instead of the lr in effect at capture.
+__global__ void adam_prep_kernel(int* __restrict__ step, float* __restrict__ scal, double lr,
+                                 const double* __restrict__ lr_dev, double beta1, double beta2) {
   const int s = ++step[0];
+  if (lr_dev) lr = lr_dev[0];
   scal[0] = (float)(lr / (1.0 - pow(beta1, (double)s)));
   scal[1] = (float)sqrt(1.0 - pow(beta2, (double)s));
 }
@@ -72,11 +75,11 @@ __global__ __launch_bounds__(256) void adam_kernel_dev(float* __restrict__ p, co
 }
 
 extern "C" int tmvs_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n,
-                                  double lr, double beta1, double beta2, double eps, double weight_decay,
-                                  int* step_counter, float* scalars, void* stream) {
+                                  double lr, const double* lr_dev, double beta1, double beta2, double eps,
+                                  double weight_decay, int* step_counter, float* scalars, void* stream) {
   if (!param || !grad || !exp_avg || !exp_avg_sq || !step_counter || !scalars || n <= 0) return TMVS_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, st, step_counter, scalars, lr, beta1, beta2);
+  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, st, step_counter, scalars, lr, lr_dev, beta1, beta2);
   TMVS_CHECK_LAUNCH();
   hipLaunchKernelGGL(adam_kernel_dev, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, param, grad, exp_avg,
                      exp_avg_sq, n, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,

@@ -5,9 +5,9 @@ return_grad=True it is returned (the seed of a backward chain), and when the out
 train-mode TransMVSNet.forward (their prob_volume carries its logits) the returned total loss is
 connected to those logits, so ``loss.backward()`` works as in the reference's train_sample.
 
-  entropy_loss      models/module.py:495-529
-  trans_mvsnet_loss models/module.py:532-556 (train.py: dlossw default 0.5,1.0,2.0)
-  focal_loss_bld    models/module.py:559-588 (finetune.py: dlossw default 1.0,1.0,1.0)
+  entropy_loss      models/module.py:495-531
+  trans_mvsnet_loss models/module.py:534-558 (train.py: dlossw default 0.5,1.0,2.0)
+  focal_loss_bld    models/module.py:561-592 (finetune.py: dlossw default 1.0,1.0,1.0)
 """
 from __future__ import annotations
 

@@ -521,7 +521,7 @@ def conv2d_bn_relu(x, w_packed, cout, k, stride, bn=None, relu=True, nchw_input=
 
 
 def entropy_loss(prob, depth_values, depth_gt, mask, grad_scale=0.0, want_grad=False):
-    """One stage's entropy_loss (models/module.py:495-529) + smooth-L1 depth loss (:545), and with
+    """One stage's entropy_loss (models/module.py:495-531) + smooth-L1 depth loss (:549), and with
     want_grad the gradient of grad_scale * loss w.r.t. the stage's softmax logits.
     Returns (loss [], depth_loss [], wta_depth [B,H,W], photo_conf [B,H,W], grad_logits or None)."""
     for t, n in ((prob, "prob"), (depth_values, "depth_values"), (depth_gt, "depth_gt"), (mask, "mask")):
@@ -990,17 +990,24 @@ def adam_step(param_flat, grad_flat, exp_avg, exp_avg_sq, lr, betas, eps, weight
                                            float(weight_decay), int(step), _stream()), "tmvs_adam_step")
 
 
-def adam_step_dev(param_flat, grad_flat, exp_avg, exp_avg_sq, lr, betas, eps, weight_decay, step_counter, scalars):
-    """tmvs_adam_step_dev: adam_step with the step number advanced on the device (graph-replayable)."""
+def adam_step_dev(param_flat, grad_flat, exp_avg, exp_avg_sq, lr, betas, eps, weight_decay, step_counter, scalars,
+                  lr_dev=None):
+    """tmvs_adam_step_dev: adam_step with the step number advanced on the device (graph-replayable).
+    lr_dev: an optional device float64 [1] read by the launch when it runs (a replayed graph then
+    follows the value the caller writes there); None = lr by value."""
     for t, n in ((param_flat, "param"), (grad_flat, "grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq"),
                  (scalars, "scalars")):
         _dev(t, n)
     if step_counter.dtype != torch.int32 or not step_counter.is_cuda:
         raise RuntimeError("step_counter must be a device int32 tensor")
+    if lr_dev is not None and (lr_dev.dtype != torch.float64 or not lr_dev.is_cuda or lr_dev.numel() != 1):
+        raise RuntimeError("lr_dev must be a device float64 tensor of one element")
     with _Span("tmvs_adam_step"):
         _lib.check(_lib_h().tmvs_adam_step_dev(_ptr(param_flat), _ptr(grad_flat), _ptr(exp_avg), _ptr(exp_avg_sq),
-                                               param_flat.numel(), float(lr), float(betas[0]), float(betas[1]),
-                                               float(eps), float(weight_decay), _ptr(step_counter), _ptr(scalars),
+                                               param_flat.numel(), float(lr),
+                                               _ptr(lr_dev), float(betas[0]),
+                                               float(betas[1]), float(eps), float(weight_decay), _ptr(step_counter),
+                                               _ptr(scalars),
                                                _stream()), "tmvs_adam_step_dev")
 
 

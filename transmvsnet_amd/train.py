@@ -9,7 +9,7 @@
   fixed-point scatter for the sources, flushed wave-cooperatively).
 * ``costregnet_train``: CostRegNet in train mode with its backward on csrc/costreg_train.hip.
 * ``depth_stages_train``: the three DepthNet stages of a training step (models/TransMVSNet.py:38-109,
-  174-221) from the FMT/pathway features to trans_mvsnet_loss (module.py:532-556) and its backward:
+  174-221) from the FMT/pathway features to trans_mvsnet_loss (module.py:534-558) and its backward:
   hypotheses (tmvs_stage_hypotheses), per-view cost volumes (above), the view aggregation and the
   stage-1 PixelwiseNet in train mode (``aggregate_train``: csrc/pw_train.hip), CostRegNet (above),
   softmax/WTA (tmvs_softmax_wta) and the loss with d loss / d logits (tmvs_entropy_loss); gradients
@@ -69,28 +69,68 @@ class _WarpCorrViews(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dsims):
         ref, src, hyp = ctx.saved_tensors
+        if not torch.cuda.is_current_stream_capturing():
+            reserve_graph_flags(ref.device, 8)
         dref, dsrc, flag = ops.warp_corr_backward(ref, src, ctx.proj12, hyp, dsims.contiguous(), ctx.rot_order,
                                                   planes=ctx.planes)
         if _DEFERRED_FLAGS is not None:  # inside depth_stages_train: one host sync after the whole backward
             _DEFERRED_FLAGS.append(flag.clone())
         elif torch.cuda.is_current_stream_capturing():  # a HIP-graph capture: checked after the replays
-            GRAPH_FLAGS.append(flag.clone())  # a graph-owned copy, not a view into the warp workspace
+            GRAPH_FLAGS.append(_sticky_flag(flag))
         else:
             _check_overflow([flag])
         return dref, dsrc, None, None, None, None
 
 
 _DEFERRED_FLAGS = None
-GRAPH_FLAGS = []  # overflow flags of backwards captured in a HIP graph (check_graph_flags after replaying)
+# Sticky overflow flags of warp backwards captured in a HIP graph: one int32 per captured backward,
+# OR-ed with that backward's flag word on every replay (the warp kernel clears its own flag word per
+# launch, so a plain copy would keep only the last replay's). They live in a zeroed arena allocated
+# outside any capture (a fill recorded inside the graph would clear them per replay).
+GRAPH_FLAGS = []
+_FLAG_ARENA = {}  # device index -> [arena int32 tensor, next free slot]
+_ARENA_SLOTS = 256
+
+
+def reserve_graph_flags(device, n=64):
+    """Make sure >= n sticky-flag slots are free on `device` (call outside a capture; TrainStepGraph
+    does). Eager warp backwards reserve them too, so a capture after an eager step finds them."""
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("reserve_graph_flags: call outside a HIP-graph capture")
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    a = _FLAG_ARENA.get(idx)
+    if a is None or a[0].numel() - a[1] < n:
+        _FLAG_ARENA[idx] = [torch.zeros(max(_ARENA_SLOTS, n), dtype=torch.int32, device=f"cuda:{idx}"), 0]
+
+
+def _sticky_flag(flag):
+    """Inside a capture: a zeroed arena slot that the graph ORs `flag` into on every replay."""
+    idx = flag.device.index
+    a = _FLAG_ARENA.get(idx)
+    if a is None or a[1] >= a[0].numel():
+        raise RuntimeError("warp_corr_backward captured in a HIP graph with no free overflow-flag slot: run one "
+                           "eager step (or train.reserve_graph_flags(device)) before the capture")
+    s = a[0][a[1]:a[1] + 1]
+    a[1] += 1
+    s.bitwise_or_(flag.reshape(1))
+    return s
 
 
 def check_graph_flags():
-    """The overflow check of the warp backwards captured outside a TrainStepGraph (one host sync); the
-    flags are dropped after the check, so a later capture is checked on its own flags only."""
+    """The overflow check of the warp backwards captured outside a TrainStepGraph (one host sync):
+    raises if any of their replays since the last check overflowed. The flags stay registered (later
+    replays are checked by later calls) and are cleared after each check; `drop_graph_flags` forgets
+    them once their graph is gone."""
     try:
         _check_overflow(GRAPH_FLAGS)
     finally:
-        GRAPH_FLAGS.clear()
+        for f in GRAPH_FLAGS:
+            f.zero_()
+
+
+def drop_graph_flags():
+    GRAPH_FLAGS.clear()
 
 
 def _check_overflow(flags):
@@ -631,7 +671,7 @@ def depth_stages_train(model, stage_features, proj_matrix, depth_values, depth_g
         finally:
             _DEFERRED_FLAGS = None
         if torch.cuda.is_current_stream_capturing():
-            GRAPH_FLAGS.extend(flags)
+            GRAPH_FLAGS.extend(_sticky_flag(f) for f in flags)
         else:
             _check_overflow(flags)
     return total, outputs
@@ -695,7 +735,21 @@ class FlatAdam:
         # advances it per replay); eager steps before any capture keep it equal to the host count
         self._step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self._scal_dev = torch.zeros(2, device=dev)
+        # the learning rate a captured step reads when it runs (tmvs_adam_step_dev lr_dev): sync_lr writes
+        # self.lr there before each replay (TrainStepGraph.replay does), so a schedule that sets opt.lr
+        # per iteration (finetune.py:58-72, WarmupMultiStepLR) holds under replays too
+        self._lr_dev = torch.full((1,), float(lr), dtype=torch.float64, device=dev)
+        self._lr_dev_val = float(lr)
         self._gathered = False
+
+    def sync_lr(self, lr=None):
+        """Write lr (default self.lr) to the device scalar a captured step reads (outside a capture)."""
+        lr = float(self.lr if lr is None else lr)
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("FlatAdam.sync_lr: call outside a HIP-graph capture (before replaying)")
+        if lr != self._lr_dev_val:
+            self._lr_dev.fill_(lr)
+            self._lr_dev_val = lr
 
     def zero_grad(self):
         for p in self.params:
@@ -753,13 +807,21 @@ class FlatAdam:
     def step(self, lr=None):
         self._gather()
         lr = self.lr if lr is None else lr
-        if torch.cuda.is_current_stream_capturing() or self._graphed:
+        capturing = torch.cuda.is_current_stream_capturing()
+        if capturing or self._graphed:
             # captured (the launch runs once per replay) or any step after a capture: the step number
             # lives on the device (tmvs_adam_step_dev advances it per launch); the host count is not
-            # touched, so eager steps interleaved with replays use the right bias correction
+            # touched, so eager steps interleaved with replays use the right bias correction. The
+            # learning rate is read from _lr_dev when the launch runs: a captured step takes the value
+            # sync_lr wrote before the replay (CAPTURED_OPTIMIZERS lets TrainStepGraph find this
+            # optimizer); an eager step writes its own lr first.
             self._graphed = True
+            if capturing and _TSG_CAPTURES:
+                CAPTURED_OPTIMIZERS.append(self)
+            else:
+                self.sync_lr(lr)
             ops.adam_step_dev(self.flat, self.grad_flat, self.exp_avg, self.exp_avg_sq, lr, self.betas, self.eps,
-                              self.weight_decay, self._step_dev, self._scal_dev)
+                              self.weight_decay, self._step_dev, self._scal_dev, lr_dev=self._lr_dev)
         else:
             self._host_steps += 1
             ops.adam_step(self.flat, self.grad_flat, self.exp_avg, self.exp_avg_sq, lr, self.betas, self.eps,
@@ -780,12 +842,20 @@ def bump_versions(tensors):
             torch.autograd.graph.increment_version(t)
 
 
+CAPTURED_OPTIMIZERS = []  # FlatAdams whose step a TrainStepGraph captured (it syncs their lr per replay)
+_TSG_CAPTURES = []  # non-empty while a TrainStepGraph captures
+
+
 class TrainStepGraph:
     """A training step captured once as a HIP graph and replayed (finetune.py:144-168's body per replay).
 
-    * The overflow flags of the warp backwards captured in this graph are kept per graph (cloned into
-      graph-owned buffers at capture) and checked by `check_flags`, so one graph's overflow never
-      blocks another's check, and no flag keeps a freed graph's workspace alive.
+    * The overflow flags of the warp backwards captured in this graph are kept per graph as sticky
+      words (every replay ORs its flags in) and checked by `check_flags`, which raises if any replay
+      since the last check overflowed and then clears them; one graph's overflow never blocks
+      another's check.
+    * The learning rate of a FlatAdam step captured in the graph is read from the device when the
+      replay runs: `replay` first writes each such optimizer's current `lr` there (FlatAdam.sync_lr),
+      so a per-iteration schedule (finetune.py:58-72) is followed.
     * `replay` bumps the version counters of the model's parameters and buffers (the replay's Adam step
       and BatchNorm running-statistic updates wrote them without Python seeing it), so an eval forward
       after replays rebuilds the inference caches (TransMVSNet._param_key, FeatureNet's packed
@@ -796,21 +866,36 @@ class TrainStepGraph:
     def __init__(self, fn, model, stream=None):
         self.model = model
         self.graph = torch.cuda.CUDAGraph()
-        n0 = len(GRAPH_FLAGS)
-        with torch.cuda.graph(self.graph, stream=stream):
-            self.out = fn()
-        self.flags = GRAPH_FLAGS[n0:]
-        del GRAPH_FLAGS[n0:]
+        dev = next(model.parameters()).device
+        reserve_graph_flags(dev, 64)
+        n0, o0 = len(GRAPH_FLAGS), len(CAPTURED_OPTIMIZERS)
+        _TSG_CAPTURES.append(self)
+        try:
+            with torch.cuda.graph(self.graph, stream=stream):
+                self.out = fn()
+            self.flags = GRAPH_FLAGS[n0:]
+            self.optimizers = list(dict.fromkeys(CAPTURED_OPTIMIZERS[o0:]))
+        finally:  # a failed capture leaves nothing behind
+            _TSG_CAPTURES.pop()
+            del GRAPH_FLAGS[n0:]
+            del CAPTURED_OPTIMIZERS[o0:]
         self._tensors = list(model.parameters()) + list(model.buffers())
 
     def replay(self):
+        for opt in self.optimizers:
+            opt.sync_lr()
         self.graph.replay()
         bump_versions(self._tensors)
         return self.out
 
     def check_flags(self):
-        """One host sync: raise if any captured warp backward overflowed in the replays so far."""
-        _check_overflow(self.flags)
+        """One host sync: raise if any captured warp backward overflowed in any replay since the last
+        check; the sticky flags are cleared afterwards."""
+        try:
+            _check_overflow(self.flags)
+        finally:
+            for f in self.flags:
+                f.zero_()
 
 
 def allreduce_gradients(params, group=None, bucket_bytes=64 << 20):
