@@ -309,17 +309,24 @@ def stage_hypotheses(depth, depth_values, stage_idx, img_hw, ndepths=NDEPTHS, ra
 
 
 def forward_from_features(sd, features, proj_matrix, depth_values, img_hw, ndepths=NDEPTHS, ratios=DEPTH_RATIOS,
-                          with_view_weights=False, training=False):
+                          with_view_weights=False, training=False, pyramid=None, seed_depth=None):
     """TransMVSNet.forward after feature extraction, models/TransMVSNet.py:162-226 (training: the
     model in train mode -- BatchNorm batch statistics + running-statistic updates; autograd flows
     as in the reference: hypotheses and the next stage's depth detached, stage-1 view weights
-    detached for stages 2/3)."""
-    feats = fmt_with_pathway(sd, features)
+    detached for stages 2/3).
+
+    Test hooks: pyramid = a precomputed fmt_with_pathway(sd, features) (not recomputed);
+    seed_depth = {"stage2": depth, "stage3": depth}: the previous stage's unclamped WTA depth [B,h,w]
+    that stage's hypotheses are built from (TransMVSNet.py:174-213) in place of this run's own -- the
+    reference cascade continued from another implementation's previous-stage depth."""
+    feats = fmt_with_pathway(sd, features) if pyramid is None else pyramid
     outputs = {}
     depth = None
     view_weights = None
     for s in range(len(ndepths)):
         name = f"stage{s + 1}"
+        if seed_depth is not None and name in seed_depth:
+            depth = seed_depth[name]
         hyp = stage_hypotheses(depth, depth_values, s, img_hw, ndepths, ratios)
         if s > 0:
             view_weights = F.interpolate(view_weights, scale_factor=2, mode="nearest")

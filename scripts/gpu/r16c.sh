@@ -1,0 +1,17 @@
+#!/bin/bash
+# r16c: split-K coarse-level convs (conv3d_splitk_kernel) A/B: per-layer times + output diff vs the product
+# kernels, the raw-conv parity test on the variant, and the bench step's kernel trace per variant
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/r16c; mkdir -p $O
+timeout -k 10 200 python scripts/diag/costreg_layers.py --save /tmp/base.pt > $O/layers_base.txt 2>&1 || exit $?
+cat $O/layers_base.txt
+for v in sk15 sk3 sk12 skd skall; do
+  TMVS_LIB_PATH=variants/$v/libtransmvs_hip.so timeout -k 10 200 python scripts/diag/costreg_layers.py --compare /tmp/base.pt > $O/layers_$v.txt 2>&1 || exit $?
+  echo "== $v"; cat $O/layers_$v.txt
+done
+TMVS_LIB_PATH=variants/skall/libtransmvs_hip.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+  tests/test_gpu_train.py -k "conv3d_mfma_raw" > $O/pytest_raw_skall.log 2>&1 || exit $?
+tail -2 $O/pytest_raw_skall.log
+bash scripts/diag/ab_kernels.sh r16c_ab "conv3d deconv3d" skall > $O/ab.txt 2>&1 || exit $?
+cat $O/ab.txt

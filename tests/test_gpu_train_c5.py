@@ -16,8 +16,12 @@ Checked (the 8-GPU DDP part of C5 is covered by tests/test_gpu_distributed.py an
       - loss terms within 1e-4 relative (a near-tie argmax flip moves EPE / less1 / less3 by a pixel);
       - WTA depth of every stage identical wherever the oracle's top-2 log-probability margin exceeds
         max(1e-4, twice the GPU-vs-oracle log-probability spread), the spread itself below 1e-2;
-      - the gradients of the three prob convs (cost_regularization.{s}.prob.weight: d loss / d logits
-        through softmax and the loss, contracted with conv11's output) within 2e-3 of their max;
+      - stages 2/3 of the oracle seeded with the GPU's previous-stage depth, so both sides build the same
+        hypotheses (asserted) and an upstream near-tie flip cannot move a downstream gradient;
+      - EVERY parameter gradient after FeatureNet (FMT, pathway, PixelwiseNet, the three CostRegNets)
+        against a float64 oracle run, within max(1e-4, 2x the fp32 spread) of its max magnitude (the bar
+        of tests/test_gpu_train_ref.py; the spread = the worse distance from float64 of an fp32 oracle run
+        and one with ~1-ulp jittered features);
       - the running statistics of PixelwiseNet and the three CostRegNets within 1e-4 of the oracle's;
   * a HIP-graph replay of the step (train.TrainStepGraph) leaves parameters, Adam moments and the
     running statistics within 1e-5 of eager steps (as tests/test_gpu_train_ref.py at C1).
@@ -85,20 +89,47 @@ def test_c5_train_sample_full_size_vs_oracle():
     # conv's weight and bias are zero-initialised (models/dcn.py:62-64) but do receive gradients
     allowed_zero = {n for n in zero if n.endswith(".bias") and "conv_offset_mask" not in n}
     assert set(zero) <= allowed_zero, sorted(set(zero) - allowed_zero)[:8]
-    # the fp32 oracle from the same features: forward, loss, prob-conv gradients, running statistics
+    # the oracle from the same features (CPU): float64 = the exact value, fp32 (+ one run with ~1-ulp
+    # jittered features) = the reference's own rounding spread. Stages 2/3 are seeded with the GPU's
+    # previous-stage WTA depth (gpu-seeded, as tests/test_gpu_fullsize.py), so both sides build the
+    # same hypotheses and a near-tie flip upstream cannot move a downstream gradient.
     torch.set_num_threads(min(16, torch.get_num_threads()))
-    sd = {k: v.clone() for k, v in sd0.items()}
-    probw = [f"cost_regularization.{s}.prob.weight" for s in range(3)]
-    for k in probw:
-        sd[k].requires_grad_(True)
-    out_ref = oracle.forward_from_features(sd, feats, proj, dv, (H5, W5), training=True)
-    res = loss_ref.focal_loss_bld(out_ref, gt, mask, interval, dlossw=[1.0, 1.0, 1.0])
-    res[0].backward()
+    seed = {}
+    for s in (1, 2):
+        o = outputs[f"stage{s}"]
+        idx = o["prob_volume"].detach().argmax(1, keepdim=True)
+        seed[f"stage{s + 1}"] = torch.gather(o["depth_values"].detach(), 1, idx).squeeze(1).cpu()
+
+    def oracle_step(dt, jitter=None):
+        cast = (lambda t: t.to(dt) if t.is_floating_point() else t)  # noqa: E731
+        sd = {k: cast(v.clone()) for k, v in sd0.items()}
+        for k, v in sd.items():
+            if v.is_floating_point() and not k.startswith("feature.") and not _is_buffer(k):
+                v.requires_grad_(True)
+        if jitter is not None:
+            gen = torch.Generator().manual_seed(jitter)
+            fj = [{k: (v * (1 + 2e-7 * torch.randn(v.shape, generator=gen, dtype=torch.float64))).float()
+                   for k, v in f.items()} for f in feats]
+        else:
+            fj = feats
+        out = oracle.forward_from_features(sd, [{k: cast(v) for k, v in f.items()} for f in fj],
+                                           {k: cast(v) for k, v in proj.items()}, cast(dv), (H5, W5),
+                                           training=True, seed_depth={k: cast(v) for k, v in seed.items()})
+        res = loss_ref.focal_loss_bld(out, {k: cast(v) for k, v in gt.items()}, {k: cast(v) for k, v in mask.items()},
+                                      cast(interval), dlossw=[1.0, 1.0, 1.0])
+        res[0].backward()
+        return res, out, sd
+
+    res, out_ref, sd = oracle_step(torch.float32)
+    _, _, sd_x = oracle_step(torch.float64)
+    _, _, sd_j = oracle_step(torch.float32, jitter=1001)
     ref_terms = [float(t) for t in res]
     rep = {"loss_terms_gpu": gpu_terms, "loss_terms_ref": ref_terms}
     for gv, rv, name in zip(gpu_terms, ref_terms, ("loss", "depth_loss", "epe", "less1", "less3")):
         assert abs(gv - rv) <= 1e-4 * max(abs(rv), 1.0), (name, gv, rv)
     for s in (1, 2, 3):
+        np.testing.assert_array_equal(outputs[f"stage{s}"]["depth_values"].detach().cpu().numpy(),
+                                      out_ref[f"stage{s}"]["depth_values"].detach().numpy())
         prob = out_ref[f"stage{s}"]["prob_volume"].detach().numpy().astype(np.float64)
         lp_ref = np.log(np.maximum(prob, 1e-30))
         lp_gpu = np.log(np.maximum(outputs[f"stage{s}"]["prob_volume"].detach().cpu().numpy().astype(np.float64), 1e-30))
@@ -119,19 +150,51 @@ def test_c5_train_sample_full_size_vs_oracle():
         print(f"stage {s}: flips {rep[f'stage{s}_flips']}", flush=True)
         assert dlp < 1e-2, (s, rep)
         assert not (diff & ~tie).any(), (s, rep)
-    for k in probw:
-        ref = sd[k].grad.numpy().astype(np.float64)
-        err = float(np.abs(grads[k] - ref).max() / np.abs(ref).max())
-        rep[k] = err
-        assert err <= 2e-3, (k, err)
+    # every parameter gradient after FeatureNet (FMT, pathway, PixelwiseNet, 3 CostRegNets; FeatureNet's
+    # own are judged at C1 against the reference's fixtures, tests/test_gpu_train_ref.py): against float64,
+    # within max(1e-4, 2x the fp32 spread) of its max magnitude -- test_gpu_train_ref.py's bar -- the spread
+    # being the worse of the fp32 and jittered-fp32 oracle runs' distances from float64
+    names = sorted(k for k, v in sd_x.items() if v.requires_grad)
+    exact = {n: sd_x[n].grad.numpy() for n in names}
+    scale = float(np.median([np.abs(exact[n]).max() for n in names]))
+    rows, zero_rows = [], []
+    for n in names:
+        got = grads[n].astype(np.float64)
+        ex = exact[n]
+        if float(np.abs(ex).max()) < 1e-7 * scale:  # zero in exact arithmetic (a bias before a BatchNorm)
+            e = float(np.abs(got - ex).max())
+            f = max(float(np.abs(sd[n].grad.numpy() - ex).max()), float(np.abs(sd_j[n].grad.numpy() - ex).max()))
+            zero_rows.append((n, e, f))
+            assert e <= max(3.0 * f, 1e-7 * scale), (n, "exactly-zero gradient", e, f)
+            continue
+        e = _rel(got, ex)
+        spread = max(_rel(sd[n].grad.numpy(), ex), _rel(sd_j[n].grad.numpy(), ex))
+        rows.append((e / max(1e-4, 2.0 * spread), n, e, spread))
+    rows.sort(reverse=True)
+    rep["gradients"] = {"compared": len(rows), "exactly_zero": len(zero_rows),
+                        "worst": [(round(r, 3), n, f"{e:.2e}", f"{f:.2e}") for r, n, e, f in rows[:8]]}
+    print(f"C5 gradients vs float64: {len(rows)} (+{len(zero_rows)} exactly zero); worst (ratio to bar, name, "
+          f"gpu, fp32 spread):", rep["gradients"]["worst"], flush=True)
+    bad = [(n, e, f) for r, n, e, f in rows if r > 1.0]
+    assert not bad, bad[:10]
     bufs = dict(model.named_buffers())
     worst = 0.0
     for k, v in sd.items():
         if k.startswith(("cost_regularization.", "DepthNet.")) and k.endswith(("running_mean", "running_var")):
             worst = max(worst, float(np.abs(bufs[k].cpu().numpy() - v.numpy()).max()))
     rep["running_stats"] = worst
-    print("C5 full size vs fp32 oracle:", rep)
+    print("C5 full size vs oracle:", rep)
     assert worst <= 1e-4, rep
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max()) / max(float(np.abs(b).max()), 1e-30)
+
+
+def _is_buffer(k):
+    return k.endswith(("running_mean", "running_var", "num_batches_tracked"))
 
 
 def test_c5_train_step_graph_replay_equals_eager():

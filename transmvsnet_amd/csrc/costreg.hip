@@ -357,6 +357,130 @@ __global__ __launch_bounds__(256) void conv3d_direct_kernel(const float* __restr
   }
 }
 
+// ---------------------------------------------------------------- conv3d, split-K over the waves
+// The coarse levels (1/4 and 1/8 resolution: conv3..conv6) have few output voxels (15.5 K at the 1/8
+// level of a DTU stage) but long reductions (K = 27 taps x 32..64 channels): one wave per output task
+// ran a single ~900-MFMA chain at ~1 wave per SIMD, its per-tap loads exposed (MFMA busy 0.2-0.3).
+// Here a workgroup is one output task -- NBW rows of 16 voxels x MBW blocks of 16 output channels at
+// one output depth -- and its KS = (CIN/16) x 3 waves split K: wave ks takes channel chunk ks/3 and
+// kd slice ks%3 (9 taps, straight from global/L2, NDHWC so a lane's 4 channels are one 16-byte load);
+// a kd slice wholly in the depth padding is skipped. The partial accumulators meet in LDS and are
+// summed in the fixed slice order (deterministic), then the BN/ReLU epilogue. Many short chains per
+// SIMD instead of one long one: the loads of one wave hide behind the MFMAs of the others.
+template <int CIN, int COUT, int S, int NBW, int MBW>
+__global__ __launch_bounds__(64 * 3 * (CIN / 16)) void conv3d_splitk_kernel(
+    const float* __restrict__ x, const float* __restrict__ wpk, const float* __restrict__ alpha,
+    const float* __restrict__ shift, float* __restrict__ y, Geo g, int n_tasks) {
+  constexpr int NCH = CIN / 16, KS = 3 * NCH;
+  constexpr int MB = (COUT + 15) / 16, MG = MB / MBW;
+  constexpr int NACC = NBW * MBW;  // float4 accumulators per lane
+  static_assert(CIN % 16 == 0 && MB % MBW == 0, "split-K tiling");
+  __shared__ __attribute__((aligned(16))) float4 red[KS][NACC][64];
+  __shared__ int live[KS];
+  const int lane = threadIdx.x & 63, ks = threadIdx.x >> 6;
+  const int task = xcd_remap(blockIdx.x, gridDim.x);
+  if (task >= n_tasks) return;  // whole workgroup
+  int t = task;
+  const int mg = t % MG;
+  t /= MG;
+  const int nws = (g.Wo + 15) / 16;
+  const int wseg = t % nws;
+  t /= nws;
+  const int nhg = (g.Ho + NBW - 1) / NBW;
+  const int hg = t % nhg;
+  t /= nhg;
+  const int od = t % g.Do;
+  const int n = t / g.Do;
+  const int col = lane & 15, kgrp = lane >> 4;
+  const int ch = ks / 3, kd = ks - 3 * ch;
+  const int id = od * S - 1 + kd;
+  const bool kd_ok = id >= 0 && id < g.Di;  // wave-uniform
+  if (lane == 0) live[ks] = kd_ok;
+  floatx4 acc[NBW][MBW];
+#pragma unroll
+  for (int r = 0; r < NBW; ++r)
+#pragma unroll
+    for (int m = 0; m < MBW; ++m) acc[r][m] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (kd_ok) {
+    const int ow = wseg * 16 + col;
+    const size_t in_d = ((size_t)n * g.Di + id) * g.Hi;
+    const int cbase = ch * 16 + kgrp * 4;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      VecN<4> a[3][MBW], b[3][NBW];
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int tap = kd * 9 + kh * 3 + kw;
+#pragma unroll
+        for (int m = 0; m < MBW; ++m) {
+          const int co = (mg * MBW + m) * 16 + col;
+          if (co < COUT)
+            a[kw][m].load(wpk + ((size_t)tap * COUT + co) * CIN + cbase);
+          else
+            a[kw][m].zero();
+        }
+        const int iw = ow * S - 1 + kw;
+        const bool wok = iw >= 0 && iw < g.Wi && ow < g.Wo;
+#pragma unroll
+        for (int r = 0; r < NBW; ++r) {
+          const int oh = hg * NBW + r;
+          const int ih = oh * S - 1 + kh;
+          if (wok && oh < g.Ho && ih >= 0 && ih < g.Hi)
+            b[kw][r].load(x + ((in_d + ih) * g.Wi + iw) * CIN + cbase);
+          else
+            b[kw][r].zero();
+        }
+      }
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < NBW; ++r)
+#pragma unroll
+            for (int m = 0; m < MBW; ++m)
+              acc[r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kw][m].v[j], b[kw][r].v[j], acc[r][m], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // one kh row of taps in flight at a time (VGPR budget)
+    }
+#pragma unroll
+    for (int r = 0; r < NBW; ++r)
+#pragma unroll
+      for (int m = 0; m < MBW; ++m)
+        red[ks][r * MBW + m][lane] = make_float4(acc[r][m][0], acc[r][m][1], acc[r][m][2], acc[r][m][3]);
+  }
+  __syncthreads();
+  // fixed-order combine: element e = (r, m, lane') of the tile, summed over the live slices ks = 0..KS-1
+  const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
+  for (int e = threadIdx.x; e < NACC * 64; e += KS * 64) {
+    const int am = e >> 6, l2 = e & 63;
+    const int r = am / MBW, m = am - r * MBW;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool first = true;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      if (!live[k]) continue;
+      const float4 p = red[k][am][l2];
+      if (first) {
+        s = p;
+        first = false;
+      } else {
+        s = make_float4(s.x + p.x, s.y + p.y, s.z + p.z, s.w + p.w);
+      }
+    }
+    const int ow = wseg * 16 + (l2 & 15), oh = hg * NBW + r;
+    const int co = (mg * MBW + m) * 16 + (l2 >> 4) * 4;
+    if (ow >= g.Wo || oh >= g.Ho || co >= COUT) continue;
+    const float4 al = *reinterpret_cast<const float4*>(alpha + co);
+    const float4 sh = *reinterpret_cast<const float4*>(shift + co);
+    float4 o;
+    o.x = act(fmaf(s.x, al.x, sh.x), g.lo);
+    o.y = act(fmaf(s.y, al.y, sh.y), g.lo);
+    o.z = act(fmaf(s.z, al.z, sh.z), g.lo);
+    o.w = act(fmaf(s.w, al.w, sh.w), g.lo);
+    *reinterpret_cast<float4*>(y + (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co) = o;
+  }
+}
+
 // ---------------------------------------------------------------- ConvTranspose3d k3 s2 p1 op1
 // output o = 2i - 1 + k: parity 0 -> (k=1, i=o/2); parity 1 -> (k=0, i=o/2+1), (k=2, i=o/2).
 // Workgroup tile in input-grid coordinates: 16 columns x THI rows x TDI slices (outputs
@@ -1117,6 +1241,159 @@ static int launch_conv_direct(const float* x, const float* w, const float* al, c
   return TMVS_OK;
 }
 
+// ---------------------------------------------------------------- ConvTranspose3d, split-K over the waves
+// The coarse transposed convs (conv7 64->32, conv9 32->16) the same way: a workgroup is one task of
+// NBW input-grid rows x 16 input columns x MBW output-channel blocks at one input depth md, i.e. all 8
+// output parity classes of those inputs (sub-pixel decomposition, as deconv3d_lds_kernel); its
+// KS = (CIN/16) x 3 waves split K by channel chunk and depth tap: slot 0 = kd 1 (the even output depth,
+// input md), slot 1 = kd 0 (odd output depth, input md+1), slot 2 = kd 2 (odd, input md). Each wave
+// runs its slot's 9 (kh, kw) taps over the 4 (ph, pw) classes. The partials meet in LDS and are summed in
+// a fixed order (chunk ascending; slot 1 before slot 2), then BN/ReLU + skip.
+template <int CIN, int COUT, int NBW, int MBW>
+__global__ __launch_bounds__(64 * 3 * (CIN / 16)) void deconv3d_splitk_kernel(
+    const float* __restrict__ x, const float* __restrict__ wpk, const float* __restrict__ alpha,
+    const float* __restrict__ shift, const float* __restrict__ skip, float* __restrict__ y, Geo g, int n_tasks) {
+  constexpr int NCH = CIN / 16, KS = 3 * NCH;
+  constexpr int MB = (COUT + 15) / 16, MG = MB / MBW;
+  constexpr int NACC = 4 * NBW * MBW;  // (ph, pw) classes x rows x channel blocks
+  static_assert(CIN % 16 == 0 && MB % MBW == 0 && COUT % 16 == 0, "split-K deconv tiling");
+  __shared__ __attribute__((aligned(16))) float4 red[KS][NACC][64];
+  __shared__ int live[KS];
+  const int lane = threadIdx.x & 63, ks = threadIdx.x >> 6;
+  const int task = xcd_remap(blockIdx.x, gridDim.x);
+  if (task >= n_tasks) return;
+  int t = task;
+  const int mg = t % MG;
+  t /= MG;
+  const int nws = (g.Wi + 15) / 16;
+  const int wseg = t % nws;
+  t /= nws;
+  const int nhg = (g.Hi + NBW - 1) / NBW;
+  const int hg = t % nhg;
+  t /= nhg;
+  const int md = t % g.Di;
+  const int n = t / g.Di;
+  const int col = lane & 15, kgrp = lane >> 4;
+  const int ch = ks / 3, slot = ks - 3 * ch;
+  const int kd = slot == 0 ? 1 : (slot == 1 ? 0 : 2);
+  const int id = md + (slot == 1 ? 1 : 0);
+  const bool ok = id < g.Di;  // wave-uniform
+  if (lane == 0) live[ks] = ok;
+  floatx4 acc[4][NBW][MBW];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < NBW; ++r)
+#pragma unroll
+      for (int m = 0; m < MBW; ++m) acc[c][r][m] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (ok) {
+    const int mw = wseg * 16 + col;
+    const size_t in_d = ((size_t)n * g.Di + id) * g.Hi;
+    const int cbase = ch * 16 + kgrp * 4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int ph = c >> 1, pw = c & 1;
+#pragma unroll
+      for (int th = 0; th < 1 + ph; ++th)
+#pragma unroll
+        for (int tw = 0; tw < 1 + pw; ++tw) {
+          const int kh = ph ? (th ? 2 : 0) : 1, oh_off = (ph && !th) ? 1 : 0;
+          const int kw = pw ? (tw ? 2 : 0) : 1, ow_off = (pw && !tw) ? 1 : 0;
+          const int tap = kd * 9 + kh * 3 + kw;
+          VecN<4> a[MBW], b[NBW];
+#pragma unroll
+          for (int m = 0; m < MBW; ++m)
+            a[m].load(wpk + ((size_t)tap * COUT + (mg * MBW + m) * 16 + col) * CIN + cbase);
+          const int iw = mw + ow_off;
+#pragma unroll
+          for (int r = 0; r < NBW; ++r) {
+            const int ih = hg * NBW + r + oh_off;
+            if (iw < g.Wi && ih < g.Hi)
+              b[r].load(x + ((in_d + ih) * g.Wi + iw) * CIN + cbase);
+            else
+              b[r].zero();
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < NBW; ++r)
+#pragma unroll
+              for (int m = 0; m < MBW; ++m)
+                acc[c][r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b[r].v[j], acc[c][r][m], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < NBW; ++r)
+#pragma unroll
+        for (int m = 0; m < MBW; ++m)
+          red[ks][(c * NBW + r) * MBW + m][lane] =
+              make_float4(acc[c][r][m][0], acc[c][r][m][1], acc[c][r][m][2], acc[c][r][m][3]);
+  }
+  __syncthreads();
+  const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
+  for (int e = threadIdx.x; e < 2 * NACC * 64; e += KS * 64) {
+    const int pd = e / (NACC * 64), rem = e - pd * (NACC * 64);
+    const int am = rem >> 6, l2 = rem & 63;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool first = true;
+#pragma unroll
+    for (int c2 = 0; c2 < NCH; ++c2)
+#pragma unroll
+      for (int sl = 0; sl < 3; ++sl) {
+        if ((sl == 0) != (pd == 0)) continue;
+        const int k = 3 * c2 + sl;
+        if (!live[k]) continue;
+        const float4 p = red[k][am][l2];
+        if (first) {
+          s = p;
+          first = false;
+        } else {
+          s = make_float4(s.x + p.x, s.y + p.y, s.z + p.z, s.w + p.w);
+        }
+      }
+    const int c = am / (NBW * MBW), rm = am - c * (NBW * MBW);
+    const int r = rm / MBW, m = rm - r * MBW;
+    const int mw = wseg * 16 + (l2 & 15), mh = hg * NBW + r;
+    if (mw >= g.Wi || mh >= g.Hi) continue;
+    const int co = (mg * MBW + m) * 16 + (l2 >> 4) * 4;
+    const int od = 2 * md + pd, oh = 2 * mh + (c >> 1), ow = 2 * mw + (c & 1);
+    const size_t o = (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co;
+    const float4 al = *reinterpret_cast<const float4*>(alpha + co);
+    const float4 sh = *reinterpret_cast<const float4*>(shift + co);
+    const float4 sk = skip ? *reinterpret_cast<const float4*>(skip + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 v;
+    v.x = sk.x + act(fmaf(s.x, al.x, sh.x), g.lo);
+    v.y = sk.y + act(fmaf(s.y, al.y, sh.y), g.lo);
+    v.z = sk.z + act(fmaf(s.z, al.z, sh.z), g.lo);
+    v.w = sk.w + act(fmaf(s.w, al.w, sh.w), g.lo);
+    *reinterpret_cast<float4*>(y + o) = v;
+  }
+}
+
+template <int CIN, int COUT, int NBW, int MBW>
+static int launch_deconv_splitk(const float* x, const float* w, const float* al, const float* sh, const float* skip,
+                                float* y, int B, const Geo& g, hipStream_t st) {
+  constexpr int MG = ((COUT + 15) / 16) / MBW;
+  const long n_tasks = (long)B * g.Di * ((g.Hi + NBW - 1) / NBW) * ((g.Wi + 15) / 16) * MG;
+  hipLaunchKernelGGL((deconv3d_splitk_kernel<CIN, COUT, NBW, MBW>), dim3((unsigned)n_tasks), dim3(64 * 3 * (CIN / 16)),
+                     0, st, x, w, al, sh, skip, y, g, (int)n_tasks);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
+template <int CIN, int COUT, int S, int NBW, int MBW>
+static int launch_conv_splitk(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
+                              const Geo& g, hipStream_t st) {
+  constexpr int MG = ((COUT + 15) / 16) / MBW;
+  const long n_tasks = (long)B * g.Do * ((g.Ho + NBW - 1) / NBW) * ((g.Wo + 15) / 16) * MG;
+  hipLaunchKernelGGL((conv3d_splitk_kernel<CIN, COUT, S, NBW, MBW>), dim3((unsigned)n_tasks), dim3(64 * 3 * (CIN / 16)),
+                     0, st, x, w, al, sh, y, g, (int)n_tasks);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
 // ---------------------------------------------------------------- deconv 16 -> 8 (conv11)
 // With 8 output channels a 16-row MFMA block would be half empty. Here rows 0-7 and 8-15 hold
 // the two W-parity outputs 2m and 2m+1 of one input column m: for each (d, h) tap the first
@@ -1345,6 +1622,26 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
 #endif
   if (cin == 16 && cout == 16 && stride == 1)
     return launch_conv_c16<TMVS_C16_TD, TMVS_C16_TH>(x, wpk, al, sh, y, B, g, st);
+  // split-K tasks for the coarse levels (bit 0: 16->32 s2, 1: 32->32, 2: 32->64 s2, 3: 64->64); two rows
+  // per task where the level has the voxels to fill the chip, one where it is small
+#ifndef TMVS_CONV_SPLITK
+#define TMVS_CONV_SPLITK 0
+#endif
+#ifndef TMVS_SPLITK_ROWS2
+#define TMVS_SPLITK_ROWS2 32768
+#endif
+  {
+    const bool big = (long)B * g.Do * g.Ho * g.Wo >= TMVS_SPLITK_ROWS2;
+#define TMVS_SPLITK_CASE(BIT, CI, CO, S)                                                            \
+  if ((TMVS_CONV_SPLITK >> BIT & 1) && cin == CI && cout == CO && stride == S)                     \
+    return big ? launch_conv_splitk<CI, CO, S, 2, 2>(x, wpk, al, sh, y, B, g, st)                  \
+               : launch_conv_splitk<CI, CO, S, 1, 2>(x, wpk, al, sh, y, B, g, st);
+    TMVS_SPLITK_CASE(0, 16, 32, 2)
+    TMVS_SPLITK_CASE(1, 32, 32, 1)
+    TMVS_SPLITK_CASE(2, 32, 64, 2)
+    TMVS_SPLITK_CASE(3, 64, 64, 1)
+#undef TMVS_SPLITK_CASE
+  }
   TMVS_CONV_LDS(32, 32, 2, 4, 2)
   TMVS_CONV_LDS(64, 64, 1, 4, 2)
 #undef TMVS_CONV_LDS
@@ -1396,6 +1693,18 @@ static int deconv_dispatch(const float* x, int B, int cin, int d, int h, int w, 
   if (cin == CI && cout == CO) {                                                                  \
     if (g.Di % 2 == 0) return launch_deconv<CI, CO, 2, 2, MBB>(x, wpk, al, sh, skip, y, B, g, st); \
     return launch_deconv<CI, CO, 1, 4, MBB>(x, wpk, al, sh, skip, y, B, g, st);                  \
+  }
+#ifndef TMVS_DECONV_SPLITK
+#define TMVS_DECONV_SPLITK 0
+#endif
+  {  // split-K tasks (bit 0: 64->32, bit 1: 32->16); two input rows per task on the bigger grids
+    const bool big = (long)B * g.Di * g.Hi * g.Wi >= TMVS_SPLITK_ROWS2;
+    if ((TMVS_DECONV_SPLITK & 1) && cin == 64 && cout == 32)
+      return big ? launch_deconv_splitk<64, 32, 2, 1>(x, wpk, al, sh, skip, y, B, g, st)
+                 : launch_deconv_splitk<64, 32, 1, 1>(x, wpk, al, sh, skip, y, B, g, st);
+    if ((TMVS_DECONV_SPLITK & 2) && cin == 32 && cout == 16)
+      return big ? launch_deconv_splitk<32, 16, 2, 1>(x, wpk, al, sh, skip, y, B, g, st)
+                 : launch_deconv_splitk<32, 16, 1, 1>(x, wpk, al, sh, skip, y, B, g, st);
   }
   TMVS_DECONV_CASE(64, 32, 1)
   TMVS_DECONV_CASE(32, 16, 1)

@@ -379,32 +379,36 @@ constexpr long kMaxAdds = (long)TY * TX * 9;
 // max |x| over n floats of two tensors -> atomicMax on the bit patterns (non-negative floats order as
 // unsigned): mx[0] over a (n_a), mx[1] over b (n_b). One atomic per block (a per-wave atomic on one
 // word from ~30K waves serialised to 0.6 ms).
+// The maxima are taken on the bit patterns of |x| as unsigned integers: for non-negative floats that
+// order is the float order, and a NaN (bits above +inf's) wins -- fmaxf would drop it, and a NaN dy
+// would then pass as finite into the fixed-point scatter (garbage integers instead of kFixBad).
+__device__ __forceinline__ unsigned abits(float v) { return __float_as_uint(v) & 0x7fffffffu; }
+__device__ __forceinline__ unsigned amax4(float4 u) {
+  return max(max(abits(u.x), abits(u.y)), max(abits(u.z), abits(u.w)));
+}
 __global__ __launch_bounds__(kBlk) void absmax2_kernel(const float* __restrict__ a, long n_a,
                                                        const float* __restrict__ b, long n_b,
                                                        unsigned* __restrict__ mx) {
-  __shared__ float red[kBlk / 64];
+  __shared__ unsigned red[kBlk / 64];
   const float4* x = reinterpret_cast<const float4*>(blockIdx.y ? b : a);
   const long n4 = (blockIdx.y ? n_b : n_a) / 4;  // a multiple of 4 floats (16-byte aligned tensors)
   const long stride = (long)gridDim.x * kBlk;
-  float m0 = 0.f, m1 = 0.f;
+  unsigned m0 = 0u, m1 = 0u;
   long i = (long)blockIdx.x * kBlk + threadIdx.x;
   for (; i + stride < n4; i += 2 * stride) {  // two independent loads in flight per thread
     const float4 u = x[i], v = x[i + stride];
-    m0 = fmaxf(m0, fmaxf(fmaxf(fabsf(u.x), fabsf(u.y)), fmaxf(fabsf(u.z), fabsf(u.w))));
-    m1 = fmaxf(m1, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    m0 = max(m0, amax4(u));
+    m1 = max(m1, amax4(v));
   }
-  if (i < n4) {
-    const float4 u = x[i];
-    m0 = fmaxf(m0, fmaxf(fmaxf(fabsf(u.x), fabsf(u.y)), fmaxf(fabsf(u.z), fabsf(u.w))));
-  }
-  float m = fmaxf(m0, m1);
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if (i < n4) m0 = max(m0, amax4(x[i]));
+  unsigned m = max(m0, m1);
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0) {
-    float t = red[0];
-    for (int w = 1; w < kBlk / 64; ++w) t = fmaxf(t, red[w]);
-    atomicMax(mx + blockIdx.y, __float_as_uint(t));
+    unsigned t = red[0];
+    for (int w = 1; w < kBlk / 64; ++w) t = max(t, red[w]);
+    atomicMax(mx + blockIdx.y, t);
   }
 }
 

@@ -816,8 +816,9 @@ class FlatAdam:
             # sync_lr wrote before the replay (CAPTURED_OPTIMIZERS lets TrainStepGraph find this
             # optimizer); an eager step writes its own lr first.
             self._graphed = True
-            if capturing and _TSG_CAPTURES:
-                CAPTURED_OPTIMIZERS.append(self)
+            if capturing:
+                if _TSG_CAPTURES:
+                    CAPTURED_OPTIMIZERS.append(self)
             else:
                 self.sync_lr(lr)
             ops.adam_step_dev(self.flat, self.grad_flat, self.exp_avg, self.exp_avg_sq, lr, self.betas, self.eps,
