@@ -58,6 +58,8 @@ def _args():
                     help="timed full forward() passes (images -> depth, FeatureNet included); 0 = skip")
     ap.add_argument("--side-priority", type=int, default=0,
                     help="stream priority of the FMT-pathway side stream (lower = higher; A/B knob)")
+    ap.add_argument("--batch2-steps", type=int, default=10,
+                    help="secondary line: B=2 per step (samples on two concurrent streams), 0 = skip")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the step's kernels from Python every step instead of replaying one HIP graph")
     ap.add_argument("--train-steps", type=int, default=3,
@@ -113,6 +115,37 @@ def make_inputs(device, seed_feat=2):
     proj = synthetic.synthetic_cameras(NVIEWS, H, W, seed=1)
     dv = synthetic.synthetic_depth_values(1)
     return synthetic.stacked_features(NVIEWS, H, W, seed=seed_feat), proj, dv
+
+
+def batch2_timing(model, feats, proj, dv_dev, steps, graphed):
+    """Secondary line (NOT the headline, which is B=1): the same hot path on a batch of 2 depth maps per
+    step -- the bench's sample twice, computed independently -- with the samples on two concurrent
+    streams (TransMVSNet.batch_streams), as a server batching requests would run it."""
+    f2 = {k: torch.cat([v, v], 0).contiguous() for k, v in feats.items()}
+    p2 = {k: torch.cat([v, v], 0) for k, v in proj.items()}
+    d2 = torch.cat([dv_dev, dv_dev], 0)
+
+    def step():
+        return model.forward_features(f2, p2, d2, (H, W))
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    if graphed:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        torch.cuda.synchronize()
+        step = graph.replay  # noqa: F811
+        step()
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"depth_maps_per_s": round(2 * steps / el, 3), "ms_per_step": round(el / steps * 1e3, 3), "steps": steps,
+            "batch": 2, "launch": "hip_graph replay" if graphed else "eager",
+            "note": "secondary: B=2 per step on two concurrent streams; the headline value is B=1"}
 
 
 def resolve_launch(gpus, env):
@@ -291,6 +324,8 @@ def run(args, world, rank, local):
         ospans = otimer.durations()
 
         e2e = end_to_end(model, args.e2e_steps, proj, dv_dev, dev) if args.e2e_steps > 0 and shard is None else None
+        batch2 = (batch2_timing(model, feats, proj, dv_dev, args.batch2_steps, graphed)
+                  if args.batch2_steps > 0 and shard is None else None)
     train = (train_timing(args.train_steps, dev, world, use_graph=not args.no_graph)
              if args.train_steps > 0 and shard is None else None)
 
@@ -400,6 +435,7 @@ def run(args, world, rank, local):
             "cpu_baseline": cpu,
             "abs_depth_l1_vs_ref": l1,
             "end_to_end": e2e,
+            "batch2_concurrent": batch2,
             "train_depth_stages": train,
         }
         if ranks_ok is not None:

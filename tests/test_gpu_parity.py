@@ -475,3 +475,38 @@ def test_e2e_images_batch_of_two_different_depth_ranges(sd, model):
         mean_l1, near, flips = depth_parity(to_np(out[f"stage{s}"]["depth"]), to_np(ref[f"stage{s}"]["depth"]),
                                             to_np(ref[f"stage{s}"]["prob_volume"]))
         assert flips == 0, (s, mean_l1, near, flips)
+
+
+def test_batch_samples_on_concurrent_streams_bitwise(model):
+    """B = 3 from features with the samples on concurrent streams (model.batch_streams, the default) is
+    bitwise the sequential per-sample form (batch_streams False) and each sample's single-sample forward,
+    eagerly and replayed as one HIP graph (the sample streams fork from and join the capturing stream)."""
+    H, W, N = 64, 96, 3
+    fs = [synthetic.synthetic_features(N, H, W, seed=30 + b) for b in range(3)]
+    feats = {k: torch.cat([model.stack_features(f)[k] for f in fs], 0).to(DEV) for k in ("stage1", "stage2", "stage3")}
+    cams = [synthetic.synthetic_cameras(N, H, W, seed=40 + b) for b in range(3)]
+    proj = {k: torch.cat([c[k] for c in cams], 0) for k in cams[0]}
+    dv = torch.cat([synthetic.synthetic_depth_values(1) + 3.0 * b for b in range(3)], 0).to(DEV)
+    keys = ("depth", "photo_confidence", "prob_volume", "depth_values")
+    with torch.no_grad():
+        model.batch_streams = False
+        try:
+            seq = model.forward_features(feats, proj, dv, (H, W))
+        finally:
+            model.batch_streams = True
+        con = model.forward_features(feats, proj, dv, (H, W))
+        # sample 0 alone (later samples take stages 2/3's interval from depth_values[0] in a batch)
+        one = model.forward_features({k: v[0:1] for k, v in feats.items()}, {k: v[0:1] for k, v in proj.items()},
+                                     dv[0:1], (H, W))
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            g_out = model.forward_features(feats, proj, dv, (H, W))
+        graph.replay()
+        torch.cuda.synchronize()
+    for s in (1, 2, 3):
+        for k in keys:
+            a, c, r = seq[f"stage{s}"][k], con[f"stage{s}"][k], g_out[f"stage{s}"][k]
+            assert torch.equal(a, c), (s, k)
+            assert torch.equal(a, r), (s, k, "graph")
+            assert torch.equal(a[0:1], one[f"stage{s}"][k]), (s, k, "single")

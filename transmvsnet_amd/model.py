@@ -247,7 +247,16 @@ class TransMVSNet(nn.Module):
         # (ops.host_rot_order), or 'fma' / 'plain' to pin it (fixtures made on another machine)
         self.warp_rot_order = "auto"
         self._side = {}
+        # B > 1: one stream per sample (sample 0 on the caller's stream), see _forward_features
+        self.batch_streams = True
+        self._sample_streams = {}
         self.register_load_state_dict_post_hook(lambda m, k: m.invalidate())
+
+    def _sample_stream(self, dev, i):
+        key = (dev, i)
+        if key not in self._sample_streams:
+            self._sample_streams[key] = torch.cuda.Stream(dev)
+        return self._sample_streams[key]
 
     def _apply(self, fn, *a, **kw):  # .to() / .cuda() / .float() replace tensors: re-track them
         self._tracked = None
@@ -356,12 +365,36 @@ class TransMVSNet(nn.Module):
         per = []
         vws = []
         # stage 1 samples each sample's own depth range; the stage-2/3 hypothesis interval comes
-        # from depth_values[0] for every sample (models/TransMVSNet.py:146-148)
+        # from depth_values[0] for every sample (models/TransMVSNet.py:146-148). Samples are independent:
+        # with B > 1 each runs on its own stream (sample 0 on the caller's), so one sample's small
+        # coarse-level grids overlap another's kernels; the caller's stream then waits for all of them.
+        concurrent = b > 1 and self.batch_streams and view_shard is None and not self.decomposed
+        main = torch.cuda.current_stream(dev)
+        if concurrent:
+            start = torch.cuda.Event()
+            start.record(main)
+        done = []
         for i in range(b):
-            o, vw = self._forward_one({k: v[i] for k, v in feats.items()}, {k: r[i:i + 1] for k, r in rows.items()},
-                                      dv[i:i + 1], dv[0:1], img_hw, prep, view_shard)
+            st = self._sample_stream(dev, i) if concurrent and i > 0 else main
+            if st is not main:
+                st.wait_event(start)
+            with torch.cuda.stream(st):
+                o, vw = self._forward_one({k: v[i] for k, v in feats.items()}, {k: r[i:i + 1] for k, r in rows.items()},
+                                          dv[i:i + 1], dv[0:1], img_hw, prep, view_shard)
+            if st is not main:
+                ev = torch.cuda.Event()
+                ev.record(st)
+                done.append(ev)
+                if not torch.cuda.is_current_stream_capturing():  # allocator: consumed on the caller's stream
+                    for t in list(o[f"stage{s + 1}"][k] for s in range(self.num_stage) for k in o[f"stage{s + 1}"]) + [vw]:
+                        if t is not None:
+                            t.record_stream(main)
+                    for t in feats.values():
+                        t.record_stream(st)
             per.append(o)
             vws.append(vw)
+        for ev in done:
+            main.wait_event(ev)
         outputs = {}
         for s in range(self.num_stage):
             name = f"stage{s + 1}"
@@ -395,9 +428,10 @@ class TransMVSNet(nn.Module):
             """Launch the pathway on a side stream once stage 1's cost volume is queued, so it runs
             beside stage 1's CostRegNet (whose 1/16-resolution grids leave most CUs idle)."""
             main = torch.cuda.current_stream(s1.device)
-            side = self._side.get(s1.device)
+            key = (s1.device, main.stream_id)  # one pathway side stream per launching stream (B > 1 runs samples concurrently)
+            side = self._side.get(key)
             if side is None:
-                side = self._side[s1.device] = torch.cuda.Stream(s1.device, priority=self.side_priority)
+                side = self._side[key] = torch.cuda.Stream(s1.device, priority=self.side_priority)
             ready = torch.cuda.Event()
             ready.record(main)
             side.wait_event(ready)
