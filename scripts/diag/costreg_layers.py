@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--stages", default="1,2,3")
     ap.add_argument("--layers", default="")
     a = ap.parse_args()
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cpu") if os.environ.get("TMVS_DRYRUN") else torch.device("cuda", 0)
     g = torch.Generator().manual_seed(0)
     outs, total = {}, 0.0
     ref = torch.load(a.compare, weights_only=True) if a.compare else None
@@ -44,6 +44,8 @@ def main():
             dd, hh, ww = d >> lvl, h >> lvl, w >> lvl
             x = torch.randn(1, dd, hh, ww, ci, generator=g).clamp_min(0).to(dev)
             wt = (torch.randn(27, co, ci, generator=g) * (1.0 / (27 * ci) ** 0.5)).to(dev)
+            if (ci, co) == (8, 1):  # prob's packing (ops.prob_pack): [3 kh][72]
+                wt = wt.reshape(3, 72).contiguous()
             sk = None
             if skip:
                 lv = {"conv4": 2, "conv2": 1, "conv0": 0}[skip]
