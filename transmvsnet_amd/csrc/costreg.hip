@@ -683,6 +683,9 @@ __device__ __forceinline__ float lane_from_right(float v) {  // lane l <- lane l
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, false));
 }
 
+#ifndef TMVS_CONV0_XSTORE
+#define TMVS_CONV0_XSTORE 0
+#endif
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, float* __restrict__ y, int D, int H,
                                                     int W, const float* __restrict__ wt,
                                                     const float* __restrict__ alpha,
@@ -704,6 +707,13 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
   const int d0 = dc * kDChunk, d1 = min(D, d0 + kDChunk);
   const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)n * D * HW, (unsigned)(D * HW * 4));
   float* yp = y + ((size_t)n * D * HW + (size_t)h * W + w) * 8;
+#if TMVS_CONV0_XSTORE
+  __shared__ __attribute__((aligned(16))) float4 xs[4][130];
+  const int w0 = seg * kProbCols;
+  float* yrow = y + ((size_t)n * D * HW + (size_t)h * W + w0) * 8;
+  (void)yp;
+  (void)writes;
+#endif
   const unsigned offw = (unsigned)w < (unsigned)W ? (unsigned)w * 4u : kOffOut;
   unsigned offh[3];
 #pragma unroll
@@ -751,11 +761,26 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
       o[2 * cp] = act(fmaf(a[cp].x, al[2 * cp], sh[2 * cp]), lo);
       o[2 * cp + 1] = act(fmaf(a[cp].y, al[2 * cp + 1], sh[2 * cp + 1]), lo);
     }
+#if TMVS_CONV0_XSTORE
+    // the row segment's 62 voxels x 32 B leave as two lane-contiguous store instructions (1 KiB +
+    // 960 B) after an exchange through the wave's LDS rows, instead of two 16-B stores per lane at a
+    // 32-B stride (each instruction half-filling every line it touches)
+    float4* ex = xs[threadIdx.x >> 6];
+    ex[2 * lane] = make_float4(o[0], o[1], o[2], o[3]);
+    ex[2 * lane + 1] = make_float4(o[4], o[5], o[6], o[7]);
+    __builtin_amdgcn_wave_barrier();
+    const float4 s0 = ex[2 + lane], s1 = ex[66 + lane];  // quads j = lane, 64 + lane of columns w0 ..
+    __builtin_amdgcn_wave_barrier();
+    float4* q = reinterpret_cast<float4*>(yrow + (size_t)d * HW * 8);
+    if (w0 + (lane >> 1) < W) q[lane] = s0;
+    if (lane < 60 && w0 + 32 + (lane >> 1) < W) q[64 + lane] = s1;
+#else
     if (writes) {
       float4* q = reinterpret_cast<float4*>(yp + (size_t)d * HW * 8);
       q[0] = make_float4(o[0], o[1], o[2], o[3]);
       q[1] = make_float4(o[4], o[5], o[6], o[7]);
     }
+#endif
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
@@ -843,6 +868,146 @@ __device__ __forceinline__ void prob_walk(__amdgpu_buffer_rsrc_t rx, int w, int 
     plane(i, pa);
     load_plane(i + 2, pa);  // (past the last plane: rows the next chunk reads anyway)
     plane(i + 1, pb);
+  }
+}
+
+// prob_walk for NR consecutive output rows h .. h+NR-1 per wave: input plane i's rows h-1 .. h+NR are
+// loaded once (NR+2 row loads per plane instead of 3 NR: the row re-reads had the kernels address-unit
+// bound) and each row feeds the outputs it borders. Every output keeps prob_walk's FMA chains and
+// order (kd, kh, kw, c), so the logits are bitwise prob_walk's. emit(r, d, logit).
+template <int NR, typename Emit>
+__device__ __forceinline__ void prob_walk_rows(__amdgpu_buffer_rsrc_t rx, int w, int h, int D, int H, int W, int d0,
+                                               const float* __restrict__ wt, Emit emit) {
+  constexpr int NL = NR + 2;
+  const unsigned offw = (unsigned)w < (unsigned)W ? (unsigned)w * 32u : kOffOut;
+  auto load_plane = [&](int i, float4 (&o)[NL][2]) {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int ih = h - 1 + j;
+      const unsigned offr = ((unsigned)i < (unsigned)D && (unsigned)ih < (unsigned)H)
+                                ? ((unsigned)i * (unsigned)H + (unsigned)ih) * (unsigned)W * 32u
+                                : kOffOut;
+      const unsigned off = (offr + offw) | ((offr | offw) & kOffOut);
+      const floatx4 u = buf_load_f32x4(rx, off);
+      const floatx4 v = buf_load_f32x4(rx, off + 16u);
+      o[j][0] = make_float4(u[0], u[1], u[2], u[3]);
+      o[j][1] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  float2_v c12[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) c12[r] = float2_v{0.f, 0.f};
+  auto plane = [&](int i, const float4 (&p)[NL][2]) {
+    float acc_next[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc_next[r] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      int wo = kh * 72;
+      asm volatile("" : "+s"(wo));
+      const float* wk = wt + __builtin_amdgcn_readfirstlane(wo);
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int j = r + kh;  // input row h-1+j feeds output row h+r through weight row kh
+        const float xc[8] = {p[j][0].x, p[j][0].y, p[j][0].z, p[j][0].w, p[j][1].x, p[j][1].y, p[j][1].z, p[j][1].w};
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            const float xv = kw == 0 ? lane_from_left(xc[c]) : kw == 1 ? xc[c] : lane_from_right(xc[c]);
+            const float2_v wp = *reinterpret_cast<const float2_v*>(wk + 2 * (kw * 8 + c));
+            acc_next[r] = fmaf(wk[48 + kw * 8 + c], xv, acc_next[r]);
+            c12[r] = __builtin_elementwise_fma(wp, float2_v{xv, xv}, c12[r]);
+          }
+        }
+        asm volatile("" : "+v"(acc_next[r]), "+v"(c12[r]));
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      if (i - 1 >= d0) emit(r, i - 1, c12[r].y);
+      c12[r] = float2_v{acc_next[r], c12[r].x};
+    }
+  };
+  float4 pa[NL][2], pb[NL][2];
+  load_plane(d0 - 1, pa);
+#pragma unroll 1
+  for (int i = d0 - 1; i < d0 + kDChunk + 1; i += 2) {
+    load_plane(i + 1, pb);
+    plane(i, pa);
+    load_plane(i + 2, pa);
+    plane(i + 1, pb);
+  }
+}
+
+#ifndef TMVS_PROB_ROWS
+#define TMVS_PROB_ROWS 1
+#endif
+
+// prob_kernel with NR output rows per wave (4 waves: 4 NR rows per workgroup)
+template <int NR>
+__global__ __launch_bounds__(256) void prob_rows_kernel(const float* __restrict__ x, float* __restrict__ y, int D, int H,
+                                                        int W, const float* __restrict__ wt) {
+  const int HW = H * W;
+  const int nseg = (W + kProbCols - 1) / kProbCols, nrow = (H + 4 * NR - 1) / (4 * NR), ndc = (D + kDChunk - 1) / kDChunk;
+  int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int seg = lb % nseg;
+  lb /= nseg;
+  const int rowb = lb % nrow;
+  lb /= nrow;
+  const int dc = lb % ndc;
+  const int n = lb / ndc;
+  const int lane = threadIdx.x & 63;
+  const int h = (rowb * 4 + (threadIdx.x >> 6)) * NR;
+  if (h >= H) return;  // whole wave
+  const int w = seg * kProbCols + lane - 1;
+  const bool writes = lane >= 1 && lane <= kProbCols && w < W;
+  const int d0 = dc * kDChunk, d1 = min(D, d0 + kDChunk);
+  const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)n * D * HW * 8, (unsigned)(D * HW * 32));
+  float* yn = y + (size_t)n * D * HW + (size_t)h * W + w;
+  prob_walk_rows<NR>(rx, w, h, D, H, W, d0, wt, [&](int r, int d, float v) {
+    if (d < d1 && writes && h + r < H) yn[(size_t)d * HW + (size_t)r * W] = v;
+  });
+}
+
+// prob_wta_kernel with NR rows per workgroup: wave k walks depth chunk k of all NR rows; after the
+// barrier the first waves run the softmax / WTA of one row each (wave 0 of all rows when D = 8)
+template <int D, int NR>
+__global__ __launch_bounds__(64 * (D / kDChunk)) void prob_wta_rows_kernel(
+    const float* __restrict__ x, const float* __restrict__ wt, const float* __restrict__ hyp, int H, int W, float lo,
+    float hi, float* __restrict__ prob, float* __restrict__ depth, float* __restrict__ depth_raw,
+    float* __restrict__ conf) {
+  constexpr int NW = D / kDChunk;
+  __shared__ float lg[NR][D * 64];
+  const int HW = H * W;
+  const int nseg = (W + kProbCols - 1) / kProbCols, nrow = (H + NR - 1) / NR;
+  int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int seg = lb % nseg;
+  lb /= nseg;
+  const int h0 = (lb % nrow) * NR;
+  const int n = lb / nrow;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int d0 = wv * kDChunk;
+  const int w = seg * kProbCols + lane - 1;
+  const bool writes = lane >= 1 && lane <= kProbCols && w < W;
+  const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)n * D * HW * 8, (unsigned)(D * HW * 32));
+  prob_walk_rows<NR>(rx, w, h0, D, H, W, d0, wt, [&](int r, int d, float v) { lg[r][d * 64 + lane] = v; });
+  __syncthreads();
+  if (!writes) return;
+  for (int r = wv; r < NR; r += NW) {
+    const int h = h0 + r;
+    if (h >= H) break;
+    float xl[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) xl[d] = lg[r][d * 64 + lane];
+    const size_t base = (size_t)n * D * HW + (size_t)h * W + w;
+    float best;
+    const int bi = softmax_first_max<D>(xl, [&](int d, float pr) { prob[base + (size_t)d * HW] = pr; }, best);
+    const size_t o = (size_t)n * HW + (size_t)h * W + w;
+    const float dr = hyp[base + (size_t)bi * HW];
+    depth_raw[o] = dr;
+    depth[o] = fminf(fmaxf(dr, lo), hi);
+    conf[o] = best;
   }
 }
 
@@ -1740,6 +1905,20 @@ static dim3 prob_grid(int batch, int D, int H, int W, int dchunk) {
   return dim3((unsigned)(((W + kProbCols - 1) / kProbCols) * ((H + 3) / 4) * batch * ((D + dchunk - 1) / dchunk)));
 }
 
+// prob (8 -> 1) raw logits: one row per wave (prob_kernel) or TMVS_PROB_ROWS rows per wave
+static int launch_prob(const float* x, float* y, int batch, int D, int H, int W, const float* wt, hipStream_t st) {
+  if constexpr (TMVS_PROB_ROWS > 1) {
+    constexpr int NR = TMVS_PROB_ROWS;
+    const dim3 grid((unsigned)(((W + kProbCols - 1) / kProbCols) * ((H + 4 * NR - 1) / (4 * NR)) * batch *
+                               ((D + kDChunk - 1) / kDChunk)));
+    hipLaunchKernelGGL(prob_rows_kernel<NR>, grid, dim3(256), 0, st, x, y, D, H, W, wt);
+  } else {
+    hipLaunchKernelGGL(prob_kernel, prob_grid(batch, D, H, W, kDChunk), dim3(256), 0, st, x, y, D, H, W, wt);
+  }
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
 // alpha = 1, shift = 0 for the raw (training) form of the MFMA layers (64 = the widest layer)
 __device__ float kUnitAlpha[64] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f,
                                    1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f,
@@ -1775,9 +1954,7 @@ extern "C" int tmvs_conv3d_mfma(const float* x, int batch, int cin, int d, int h
   }
   if (!transposed && stride == 1 && cin == 8 && cout == 1) {  // prob's VALU kernel (prob packing)
     if ((long long)d * h * w * 32 >= (1LL << 31)) return TMVS_ERR_SHAPE;
-    hipLaunchKernelGGL(prob_kernel, prob_grid(batch, d, h, w, kDChunk), dim3(256), 0, st, x, y, d, h, w, wpk);
-    TMVS_CHECK_LAUNCH();
-    return TMVS_OK;
+    return launch_prob(x, y, batch, d, h, w, wpk, st);
   }
   if (transposed) return deconv_dispatch(x, batch, cin, d, h, w, wpk, al, sh, cout, skip, y, st, lo);
   return conv_dispatch(x, batch, cin, d, h, w, wpk, al, sh, cout, stride, y, st, lo);
@@ -1875,10 +2052,7 @@ extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height,
   float *x11, *c0;
   int rc;
   if ((rc = costregnet_trunk(x, batch, depth, height, width, w, workspace, workspace_bytes, st, &x11, &c0))) return rc;
-  hipLaunchKernelGGL(prob_kernel, prob_grid(batch, depth, height, width, kDChunk), dim3(256), 0, st, x11, logits, depth,
-                     height, width, w->w[10]);
-  TMVS_CHECK_LAUNCH();
-  return TMVS_OK;
+  return launch_prob(x11, logits, batch, depth, height, width, w->w[10], st);
 }
 
 extern "C" int tmvs_costregnet_wta(const float* x, const float* hyp, int batch, int depth, int height, int width,
@@ -1898,20 +2072,23 @@ extern "C" int tmvs_costregnet_wta(const float* x, const float* hyp, int batch, 
     // D = 48 (stage 1) fused measured 53.8 us vs 40.1 + 10.3 us split (r07d vs r07b): few columns
     // and a 48-deep softmax tail behind the barrier. Split: the depth-chunked prob kernel, its
     // logits in conv0's buffer (dead once conv11 has consumed it as its skip), then the softmax kernel
-    hipLaunchKernelGGL(prob_kernel, prob_grid(batch, depth, height, width, kDChunk), dim3(256), 0, st, x11, c0, depth,
-                       height, width, w->w[10]);
-    TMVS_CHECK_LAUNCH();
+    if ((rc = launch_prob(x11, c0, batch, depth, height, width, w->w[10], st))) return rc;
     return tmvs_softmax_wta(c0, hyp, batch, depth, height, width, clamp_lo, clamp_hi, prob, depth_out, depth_raw,
                             conf, stream);
   }
   // D <= 32: one workgroup per (sample, row, 62-column segment), its D/8 waves prob_kernel's depth
   // chunks. Measured (r07d vs r07b): D = 32 114.0 vs 108.4 + 15.7 us, D = 8 104.3 vs 90.9 + 18.6 us
-  const dim3 gf((unsigned)(((width + kProbCols - 1) / kProbCols) * height * batch));
+  constexpr int NR = TMVS_PROB_ROWS;
+  const dim3 gf((unsigned)(((width + kProbCols - 1) / kProbCols) * ((height + NR - 1) / NR) * batch));
   const dim3 bf((unsigned)(64 * (depth / kDChunk)));
 #define TMVS_PW_CASE(DD)                                                                                      \
   case DD:                                                                                                    \
-    hipLaunchKernelGGL(prob_wta_kernel<DD>, gf, bf, 0, st, x11, w->w[10], hyp, height, width, clamp_lo,       \
-                       clamp_hi, prob, depth_out, depth_raw, conf);                                           \
+    if constexpr (NR > 1)                                                                                     \
+      hipLaunchKernelGGL((prob_wta_rows_kernel<DD, NR>), gf, bf, 0, st, x11, w->w[10], hyp, height, width,    \
+                         clamp_lo, clamp_hi, prob, depth_out, depth_raw, conf);                               \
+    else                                                                                                      \
+      hipLaunchKernelGGL(prob_wta_kernel<DD>, gf, bf, 0, st, x11, w->w[10], hyp, height, width, clamp_lo,     \
+                         clamp_hi, prob, depth_out, depth_raw, conf);                                         \
     break;
   switch (depth) {
     TMVS_PW_CASE(8)
