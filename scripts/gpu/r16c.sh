@@ -8,7 +8,7 @@ O=gpurun_out/r16c; mkdir -p $O
 soft() { rc=$1; if [ $rc -eq 124 ] || [ $rc -eq 137 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi; [ $rc -ne 0 ] && echo "FAILED rc=$rc"; return 0; }
 timeout -k 10 200 python scripts/diag/costreg_layers.py --save /tmp/base.pt > $O/layers_base.txt 2>&1 || exit $?
 cat $O/layers_base.txt
-for v in sk15 skd skall pr2 c0x; do
+for v in sk15 skd skall pr2 c0x c28 c44; do
   TMVS_LIB_PATH=variants/$v/libtransmvs_hip.so timeout -k 10 200 python scripts/diag/costreg_layers.py --compare /tmp/base.pt > $O/layers_$v.txt 2>&1 || exit $?
   echo "== $v"; cat $O/layers_$v.txt
 done
@@ -18,5 +18,5 @@ tail -2 $O/pytest_raw_skall.log
 TMVS_LIB_PATH=variants/pr2/libtransmvs_hip.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
   tests/test_gpu_parity.py -k "costregnet or e2e_c1 or cascade_48" > $O/pytest_pr2.log 2>&1; soft $?
 tail -2 $O/pytest_pr2.log
-bash scripts/diag/ab_kernels.sh r16c_ab "conv3d deconv3d prob conv0" skall pr2 c0x > $O/ab.txt 2>&1 || exit $?
+bash scripts/diag/ab_kernels.sh r16c_ab "conv3d deconv3d prob conv0" skall pr2 c0x c44 > $O/ab.txt 2>&1 || exit $?
 cat $O/ab.txt

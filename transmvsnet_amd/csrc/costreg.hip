@@ -1085,7 +1085,7 @@ __global__ __launch_bounds__(64 * (D / kDChunk)) void prob_wta_kernel(
 // current tile's 27 taps run on the MFMAs, and committed to LDS between two barriers.
 // Same fragment layouts, tap order and epilogue as conv3d_lds_kernel.
 template <int TD, int TH>
-__global__ __launch_bounds__(256) void conv3d_c16_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv3d_c16_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                          const float* __restrict__ alpha,
                                                          const float* __restrict__ shift, float* __restrict__ y, Geo g,
                                                          int ntiles) {
@@ -1176,7 +1176,7 @@ __global__ __launch_bounds__(256) void conv3d_c16_kernel(const float* __restrict
 #pragma unroll
         for (int r = 0; r < NBW; ++r)
           acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[j], b[r].v[j], acc[r], 0, 0, 0);
-      if (tap % 9 == 8) __builtin_amdgcn_sched_barrier(0);  // bound the fragments in flight
+      if (tap % (NBW > 2 ? 3 : 9) == (NBW > 2 ? 2 : 8)) __builtin_amdgcn_sched_barrier(0);  // bound the fragments in flight
     }
     const int ow = c.ow0 + col;
     const size_t out_n = (size_t)c.n * g.Do * g.Ho * g.Wo;
