@@ -357,130 +357,6 @@ __global__ __launch_bounds__(256) void conv3d_direct_kernel(const float* __restr
   }
 }
 
-// ---------------------------------------------------------------- conv3d, split-K over the waves
-// The coarse levels (1/4 and 1/8 resolution: conv3..conv6) have few output voxels (15.5 K at the 1/8
-// level of a DTU stage) but long reductions (K = 27 taps x 32..64 channels): one wave per output task
-// ran a single ~900-MFMA chain at ~1 wave per SIMD, its per-tap loads exposed (MFMA busy 0.2-0.3).
-// Here a workgroup is one output task -- NBW rows of 16 voxels x MBW blocks of 16 output channels at
-// one output depth -- and its KS = (CIN/16) x 3 waves split K: wave ks takes channel chunk ks/3 and
-// kd slice ks%3 (9 taps, straight from global/L2, NDHWC so a lane's 4 channels are one 16-byte load);
-// a kd slice wholly in the depth padding is skipped. The partial accumulators meet in LDS and are
-// summed in the fixed slice order (deterministic), then the BN/ReLU epilogue. Many short chains per
-// SIMD instead of one long one: the loads of one wave hide behind the MFMAs of the others.
-template <int CIN, int COUT, int S, int NBW, int MBW>
-__global__ __launch_bounds__(64 * 3 * (CIN / 16)) void conv3d_splitk_kernel(
-    const float* __restrict__ x, const float* __restrict__ wpk, const float* __restrict__ alpha,
-    const float* __restrict__ shift, float* __restrict__ y, Geo g, int n_tasks) {
-  constexpr int NCH = CIN / 16, KS = 3 * NCH;
-  constexpr int MB = (COUT + 15) / 16, MG = MB / MBW;
-  constexpr int NACC = NBW * MBW;  // float4 accumulators per lane
-  static_assert(CIN % 16 == 0 && MB % MBW == 0, "split-K tiling");
-  __shared__ __attribute__((aligned(16))) float4 red[KS][NACC][64];
-  __shared__ int live[KS];
-  const int lane = threadIdx.x & 63, ks = threadIdx.x >> 6;
-  const int task = xcd_remap(blockIdx.x, gridDim.x);
-  if (task >= n_tasks) return;  // whole workgroup
-  int t = task;
-  const int mg = t % MG;
-  t /= MG;
-  const int nws = (g.Wo + 15) / 16;
-  const int wseg = t % nws;
-  t /= nws;
-  const int nhg = (g.Ho + NBW - 1) / NBW;
-  const int hg = t % nhg;
-  t /= nhg;
-  const int od = t % g.Do;
-  const int n = t / g.Do;
-  const int col = lane & 15, kgrp = lane >> 4;
-  const int ch = ks / 3, kd = ks - 3 * ch;
-  const int id = od * S - 1 + kd;
-  const bool kd_ok = id >= 0 && id < g.Di;  // wave-uniform
-  if (lane == 0) live[ks] = kd_ok;
-  floatx4 acc[NBW][MBW];
-#pragma unroll
-  for (int r = 0; r < NBW; ++r)
-#pragma unroll
-    for (int m = 0; m < MBW; ++m) acc[r][m] = floatx4{0.f, 0.f, 0.f, 0.f};
-  if (kd_ok) {
-    const int ow = wseg * 16 + col;
-    const size_t in_d = ((size_t)n * g.Di + id) * g.Hi;
-    const int cbase = ch * 16 + kgrp * 4;
-#pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
-      VecN<4> a[3][MBW], b[3][NBW];
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const int tap = kd * 9 + kh * 3 + kw;
-#pragma unroll
-        for (int m = 0; m < MBW; ++m) {
-          const int co = (mg * MBW + m) * 16 + col;
-          if (co < COUT)
-            a[kw][m].load(wpk + ((size_t)tap * COUT + co) * CIN + cbase);
-          else
-            a[kw][m].zero();
-        }
-        const int iw = ow * S - 1 + kw;
-        const bool wok = iw >= 0 && iw < g.Wi && ow < g.Wo;
-#pragma unroll
-        for (int r = 0; r < NBW; ++r) {
-          const int oh = hg * NBW + r;
-          const int ih = oh * S - 1 + kh;
-          if (wok && oh < g.Ho && ih >= 0 && ih < g.Hi)
-            b[kw][r].load(x + ((in_d + ih) * g.Wi + iw) * CIN + cbase);
-          else
-            b[kw][r].zero();
-        }
-      }
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < NBW; ++r)
-#pragma unroll
-            for (int m = 0; m < MBW; ++m)
-              acc[r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kw][m].v[j], b[kw][r].v[j], acc[r][m], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);  // one kh row of taps in flight at a time (VGPR budget)
-    }
-#pragma unroll
-    for (int r = 0; r < NBW; ++r)
-#pragma unroll
-      for (int m = 0; m < MBW; ++m)
-        red[ks][r * MBW + m][lane] = make_float4(acc[r][m][0], acc[r][m][1], acc[r][m][2], acc[r][m][3]);
-  }
-  __syncthreads();
-  // fixed-order combine: element e = (r, m, lane') of the tile, summed over the live slices ks = 0..KS-1
-  const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
-  for (int e = threadIdx.x; e < NACC * 64; e += KS * 64) {
-    const int am = e >> 6, l2 = e & 63;
-    const int r = am / MBW, m = am - r * MBW;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    bool first = true;
-#pragma unroll
-    for (int k = 0; k < KS; ++k) {
-      if (!live[k]) continue;
-      const float4 p = red[k][am][l2];
-      if (first) {
-        s = p;
-        first = false;
-      } else {
-        s = make_float4(s.x + p.x, s.y + p.y, s.z + p.z, s.w + p.w);
-      }
-    }
-    const int ow = wseg * 16 + (l2 & 15), oh = hg * NBW + r;
-    const int co = (mg * MBW + m) * 16 + (l2 >> 4) * 4;
-    if (ow >= g.Wo || oh >= g.Ho || co >= COUT) continue;
-    const float4 al = *reinterpret_cast<const float4*>(alpha + co);
-    const float4 sh = *reinterpret_cast<const float4*>(shift + co);
-    float4 o;
-    o.x = act(fmaf(s.x, al.x, sh.x), g.lo);
-    o.y = act(fmaf(s.y, al.y, sh.y), g.lo);
-    o.z = act(fmaf(s.z, al.z, sh.z), g.lo);
-    o.w = act(fmaf(s.w, al.w, sh.w), g.lo);
-    *reinterpret_cast<float4*>(y + (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co) = o;
-  }
-}
-
 // ---------------------------------------------------------------- ConvTranspose3d k3 s2 p1 op1
 // output o = 2i - 1 + k: parity 0 -> (k=1, i=o/2); parity 1 -> (k=0, i=o/2+1), (k=2, i=o/2).
 // Workgroup tile in input-grid coordinates: 16 columns x THI rows x TDI slices (outputs
@@ -683,9 +559,6 @@ __device__ __forceinline__ float lane_from_right(float v) {  // lane l <- lane l
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, false));
 }
 
-#ifndef TMVS_CONV0_XSTORE
-#define TMVS_CONV0_XSTORE 0
-#endif
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, float* __restrict__ y, int D, int H,
                                                     int W, const float* __restrict__ wt,
                                                     const float* __restrict__ alpha,
@@ -707,13 +580,6 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
   const int d0 = dc * kDChunk, d1 = min(D, d0 + kDChunk);
   const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)n * D * HW, (unsigned)(D * HW * 4));
   float* yp = y + ((size_t)n * D * HW + (size_t)h * W + w) * 8;
-#if TMVS_CONV0_XSTORE
-  __shared__ __attribute__((aligned(16))) float4 xs[4][130];
-  const int w0 = seg * kProbCols;
-  float* yrow = y + ((size_t)n * D * HW + (size_t)h * W + w0) * 8;
-  (void)yp;
-  (void)writes;
-#endif
   const unsigned offw = (unsigned)w < (unsigned)W ? (unsigned)w * 4u : kOffOut;
   unsigned offh[3];
 #pragma unroll
@@ -761,26 +627,11 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
       o[2 * cp] = act(fmaf(a[cp].x, al[2 * cp], sh[2 * cp]), lo);
       o[2 * cp + 1] = act(fmaf(a[cp].y, al[2 * cp + 1], sh[2 * cp + 1]), lo);
     }
-#if TMVS_CONV0_XSTORE
-    // the row segment's 62 voxels x 32 B leave as two lane-contiguous store instructions (1 KiB +
-    // 960 B) after an exchange through the wave's LDS rows, instead of two 16-B stores per lane at a
-    // 32-B stride (each instruction half-filling every line it touches)
-    float4* ex = xs[threadIdx.x >> 6];
-    ex[2 * lane] = make_float4(o[0], o[1], o[2], o[3]);
-    ex[2 * lane + 1] = make_float4(o[4], o[5], o[6], o[7]);
-    __builtin_amdgcn_wave_barrier();
-    const float4 s0 = ex[2 + lane], s1 = ex[66 + lane];  // quads j = lane, 64 + lane of columns w0 ..
-    __builtin_amdgcn_wave_barrier();
-    float4* q = reinterpret_cast<float4*>(yrow + (size_t)d * HW * 8);
-    if (w0 + (lane >> 1) < W) q[lane] = s0;
-    if (lane < 60 && w0 + 32 + (lane >> 1) < W) q[64 + lane] = s1;
-#else
     if (writes) {
       float4* q = reinterpret_cast<float4*>(yp + (size_t)d * HW * 8);
       q[0] = make_float4(o[0], o[1], o[2], o[3]);
       q[1] = make_float4(o[4], o[5], o[6], o[7]);
     }
-#endif
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
@@ -940,8 +791,14 @@ __device__ __forceinline__ void prob_walk_rows(__amdgpu_buffer_rsrc_t rx, int w,
   }
 }
 
+// rows per wave of the raw prob walk (prob_kernel: 1; the 2-row form measured 42.3 -> 44.9 us at stage 1's
+// D = 48, 96.0 -> 92.1 / 90.9 -> 87.8 at stages 2 / 3, r16c) and of the fused prob + softmax/WTA kernel
+// (stages 2 / 3)
 #ifndef TMVS_PROB_ROWS
 #define TMVS_PROB_ROWS 1
+#endif
+#ifndef TMVS_PROB_WTA_ROWS
+#define TMVS_PROB_WTA_ROWS 2
 #endif
 
 // prob_kernel with NR output rows per wave (4 waves: 4 NR rows per workgroup)
@@ -1406,159 +1263,6 @@ static int launch_conv_direct(const float* x, const float* w, const float* al, c
   return TMVS_OK;
 }
 
-// ---------------------------------------------------------------- ConvTranspose3d, split-K over the waves
-// The coarse transposed convs (conv7 64->32, conv9 32->16) the same way: a workgroup is one task of
-// NBW input-grid rows x 16 input columns x MBW output-channel blocks at one input depth md, i.e. all 8
-// output parity classes of those inputs (sub-pixel decomposition, as deconv3d_lds_kernel); its
-// KS = (CIN/16) x 3 waves split K by channel chunk and depth tap: slot 0 = kd 1 (the even output depth,
-// input md), slot 1 = kd 0 (odd output depth, input md+1), slot 2 = kd 2 (odd, input md). Each wave
-// runs its slot's 9 (kh, kw) taps over the 4 (ph, pw) classes. The partials meet in LDS and are summed in
-// a fixed order (chunk ascending; slot 1 before slot 2), then BN/ReLU + skip.
-template <int CIN, int COUT, int NBW, int MBW>
-__global__ __launch_bounds__(64 * 3 * (CIN / 16)) void deconv3d_splitk_kernel(
-    const float* __restrict__ x, const float* __restrict__ wpk, const float* __restrict__ alpha,
-    const float* __restrict__ shift, const float* __restrict__ skip, float* __restrict__ y, Geo g, int n_tasks) {
-  constexpr int NCH = CIN / 16, KS = 3 * NCH;
-  constexpr int MB = (COUT + 15) / 16, MG = MB / MBW;
-  constexpr int NACC = 4 * NBW * MBW;  // (ph, pw) classes x rows x channel blocks
-  static_assert(CIN % 16 == 0 && MB % MBW == 0 && COUT % 16 == 0, "split-K deconv tiling");
-  __shared__ __attribute__((aligned(16))) float4 red[KS][NACC][64];
-  __shared__ int live[KS];
-  const int lane = threadIdx.x & 63, ks = threadIdx.x >> 6;
-  const int task = xcd_remap(blockIdx.x, gridDim.x);
-  if (task >= n_tasks) return;
-  int t = task;
-  const int mg = t % MG;
-  t /= MG;
-  const int nws = (g.Wi + 15) / 16;
-  const int wseg = t % nws;
-  t /= nws;
-  const int nhg = (g.Hi + NBW - 1) / NBW;
-  const int hg = t % nhg;
-  t /= nhg;
-  const int md = t % g.Di;
-  const int n = t / g.Di;
-  const int col = lane & 15, kgrp = lane >> 4;
-  const int ch = ks / 3, slot = ks - 3 * ch;
-  const int kd = slot == 0 ? 1 : (slot == 1 ? 0 : 2);
-  const int id = md + (slot == 1 ? 1 : 0);
-  const bool ok = id < g.Di;  // wave-uniform
-  if (lane == 0) live[ks] = ok;
-  floatx4 acc[4][NBW][MBW];
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int r = 0; r < NBW; ++r)
-#pragma unroll
-      for (int m = 0; m < MBW; ++m) acc[c][r][m] = floatx4{0.f, 0.f, 0.f, 0.f};
-  if (ok) {
-    const int mw = wseg * 16 + col;
-    const size_t in_d = ((size_t)n * g.Di + id) * g.Hi;
-    const int cbase = ch * 16 + kgrp * 4;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int ph = c >> 1, pw = c & 1;
-#pragma unroll
-      for (int th = 0; th < 1 + ph; ++th)
-#pragma unroll
-        for (int tw = 0; tw < 1 + pw; ++tw) {
-          const int kh = ph ? (th ? 2 : 0) : 1, oh_off = (ph && !th) ? 1 : 0;
-          const int kw = pw ? (tw ? 2 : 0) : 1, ow_off = (pw && !tw) ? 1 : 0;
-          const int tap = kd * 9 + kh * 3 + kw;
-          VecN<4> a[MBW], b[NBW];
-#pragma unroll
-          for (int m = 0; m < MBW; ++m)
-            a[m].load(wpk + ((size_t)tap * COUT + (mg * MBW + m) * 16 + col) * CIN + cbase);
-          const int iw = mw + ow_off;
-#pragma unroll
-          for (int r = 0; r < NBW; ++r) {
-            const int ih = hg * NBW + r + oh_off;
-            if (iw < g.Wi && ih < g.Hi)
-              b[r].load(x + ((in_d + ih) * g.Wi + iw) * CIN + cbase);
-            else
-              b[r].zero();
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < NBW; ++r)
-#pragma unroll
-              for (int m = 0; m < MBW; ++m)
-                acc[c][r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b[r].v[j], acc[c][r][m], 0, 0, 0);
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int r = 0; r < NBW; ++r)
-#pragma unroll
-        for (int m = 0; m < MBW; ++m)
-          red[ks][(c * NBW + r) * MBW + m][lane] =
-              make_float4(acc[c][r][m][0], acc[c][r][m][1], acc[c][r][m][2], acc[c][r][m][3]);
-  }
-  __syncthreads();
-  const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
-  for (int e = threadIdx.x; e < 2 * NACC * 64; e += KS * 64) {
-    const int pd = e / (NACC * 64), rem = e - pd * (NACC * 64);
-    const int am = rem >> 6, l2 = rem & 63;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    bool first = true;
-#pragma unroll
-    for (int c2 = 0; c2 < NCH; ++c2)
-#pragma unroll
-      for (int sl = 0; sl < 3; ++sl) {
-        if ((sl == 0) != (pd == 0)) continue;
-        const int k = 3 * c2 + sl;
-        if (!live[k]) continue;
-        const float4 p = red[k][am][l2];
-        if (first) {
-          s = p;
-          first = false;
-        } else {
-          s = make_float4(s.x + p.x, s.y + p.y, s.z + p.z, s.w + p.w);
-        }
-      }
-    const int c = am / (NBW * MBW), rm = am - c * (NBW * MBW);
-    const int r = rm / MBW, m = rm - r * MBW;
-    const int mw = wseg * 16 + (l2 & 15), mh = hg * NBW + r;
-    if (mw >= g.Wi || mh >= g.Hi) continue;
-    const int co = (mg * MBW + m) * 16 + (l2 >> 4) * 4;
-    const int od = 2 * md + pd, oh = 2 * mh + (c >> 1), ow = 2 * mw + (c & 1);
-    const size_t o = (out_n + ((size_t)od * g.Ho + oh) * g.Wo + ow) * COUT + co;
-    const float4 al = *reinterpret_cast<const float4*>(alpha + co);
-    const float4 sh = *reinterpret_cast<const float4*>(shift + co);
-    const float4 sk = skip ? *reinterpret_cast<const float4*>(skip + o) : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 v;
-    v.x = sk.x + act(fmaf(s.x, al.x, sh.x), g.lo);
-    v.y = sk.y + act(fmaf(s.y, al.y, sh.y), g.lo);
-    v.z = sk.z + act(fmaf(s.z, al.z, sh.z), g.lo);
-    v.w = sk.w + act(fmaf(s.w, al.w, sh.w), g.lo);
-    *reinterpret_cast<float4*>(y + o) = v;
-  }
-}
-
-template <int CIN, int COUT, int NBW, int MBW>
-static int launch_deconv_splitk(const float* x, const float* w, const float* al, const float* sh, const float* skip,
-                                float* y, int B, const Geo& g, hipStream_t st) {
-  constexpr int MG = ((COUT + 15) / 16) / MBW;
-  const long n_tasks = (long)B * g.Di * ((g.Hi + NBW - 1) / NBW) * ((g.Wi + 15) / 16) * MG;
-  hipLaunchKernelGGL((deconv3d_splitk_kernel<CIN, COUT, NBW, MBW>), dim3((unsigned)n_tasks), dim3(64 * 3 * (CIN / 16)),
-                     0, st, x, w, al, sh, skip, y, g, (int)n_tasks);
-  TMVS_CHECK_LAUNCH();
-  return TMVS_OK;
-}
-
-template <int CIN, int COUT, int S, int NBW, int MBW>
-static int launch_conv_splitk(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
-                              const Geo& g, hipStream_t st) {
-  constexpr int MG = ((COUT + 15) / 16) / MBW;
-  const long n_tasks = (long)B * g.Do * ((g.Ho + NBW - 1) / NBW) * ((g.Wo + 15) / 16) * MG;
-  hipLaunchKernelGGL((conv3d_splitk_kernel<CIN, COUT, S, NBW, MBW>), dim3((unsigned)n_tasks), dim3(64 * 3 * (CIN / 16)),
-                     0, st, x, w, al, sh, y, g, (int)n_tasks);
-  TMVS_CHECK_LAUNCH();
-  return TMVS_OK;
-}
-
 // ---------------------------------------------------------------- deconv 16 -> 8 (conv11)
 // With 8 output channels a 16-row MFMA block would be half empty. Here rows 0-7 and 8-15 hold
 // the two W-parity outputs 2m and 2m+1 of one input column m: for each (d, h) tap the first
@@ -1572,6 +1276,9 @@ static int launch_conv_splitk(const float* x, const float* w, const float* al, c
 // are requested before the MFMAs too, so neither latency sits between MFMA phases.
 // Tiles are dealt out XCD-contiguously (an XCD's workgroups share one L2: neighbouring tiles
 // share their halo voxels).
+#ifndef TMVS_C8_DIRECT
+#define TMVS_C8_DIRECT 0
+#endif
 template <int TDI, int THI>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void deconv3d_c8_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                           const float* __restrict__ alpha,
@@ -1659,8 +1366,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const int tn = t + per_xcd;
     if (tn < t_hi) fetch(tn);
     // skip rows of this tile: lane (pair) j of a 1 KiB output row, as the epilogue stores it
+    // (TMVS_C8_DIRECT: lane (col, kgrp)'s own MFMA outputs, voxel 2 (mw0 + col) + kgrp / 2, channels
+    // 4 (kgrp & 1) .. +3 -- the whole row segment still one contiguous 1 KiB per instruction, no exchange)
     const size_t out_n = (size_t)c.n * g.Do * g.Ho * g.Wo;
-    const int ow = 2 * c.mw0 + (lane >> 1);
+    const int ow = TMVS_C8_DIRECT ? 2 * (c.mw0 + col) + (kgrp >> 1) : 2 * c.mw0 + (lane >> 1);
     const size_t plane = (size_t)g.Ho * g.Wo * 8, row = (size_t)g.Wo * 8;  // output strides (floats)
     float4 sk[NBW][4];
     size_t oo[NBW];
@@ -1670,7 +1379,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const int rr = wv * NBW + r;
       const int md = c.md0 + rr / THI, mh = c.mh0 + rr % THI;
       ok[r] = md < g.Di && mh < g.Hi && ow < 2 * g.Wi;
-      oo[r] = (out_n + ((size_t)(2 * md) * g.Ho + 2 * mh) * g.Wo + ow) * 8 + (lane & 1) * 4;
+      oo[r] = (out_n + ((size_t)(2 * md) * g.Ho + 2 * mh) * g.Wo + ow) * 8 + (TMVS_C8_DIRECT ? cq : (lane & 1) * 4);
 #pragma unroll
       for (int pdh = 0; pdh < 4; ++pdh)
         sk[r][pdh] = (ok[r] && skip) ? *reinterpret_cast<const float4*>(skip + oo[r] + (pdh >> 1) * plane + (pdh & 1) * row)
@@ -1722,12 +1431,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
       for (int pdh = 0; pdh < 4; ++pdh) {
         const floatx4 a = acc[r][pdh];
-        *reinterpret_cast<float4*>(eb + (2 * col + (kgrp >> 1)) * 8 + cq) =
-            make_float4(act(fmaf(a[0], al.x, sh.x), g.lo), act(fmaf(a[1], al.y, sh.y), g.lo), act(fmaf(a[2], al.z, sh.z), g.lo),
-                        act(fmaf(a[3], al.w, sh.w), g.lo));
-        __builtin_amdgcn_wave_barrier();
-        const float4 v = *reinterpret_cast<const float4*>(eb + lane * 4);
-        __builtin_amdgcn_wave_barrier();
+        float4 v = make_float4(act(fmaf(a[0], al.x, sh.x), g.lo), act(fmaf(a[1], al.y, sh.y), g.lo),
+                               act(fmaf(a[2], al.z, sh.z), g.lo), act(fmaf(a[3], al.w, sh.w), g.lo));
+        if constexpr (!TMVS_C8_DIRECT) {
+          *reinterpret_cast<float4*>(eb + (2 * col + (kgrp >> 1)) * 8 + cq) = v;
+          __builtin_amdgcn_wave_barrier();
+          v = *reinterpret_cast<const float4*>(eb + lane * 4);
+          __builtin_amdgcn_wave_barrier();
+        }
         const float4 sv = sk[r][pdh];
         if (ok[r])
           *reinterpret_cast<float4*>(y + oo[r] + (pdh >> 1) * plane + (pdh & 1) * row) =
@@ -1787,26 +1498,6 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
 #endif
   if (cin == 16 && cout == 16 && stride == 1)
     return launch_conv_c16<TMVS_C16_TD, TMVS_C16_TH>(x, wpk, al, sh, y, B, g, st);
-  // split-K tasks for the coarse levels (bit 0: 16->32 s2, 1: 32->32, 2: 32->64 s2, 3: 64->64); two rows
-  // per task where the level has the voxels to fill the chip, one where it is small
-#ifndef TMVS_CONV_SPLITK
-#define TMVS_CONV_SPLITK 0
-#endif
-#ifndef TMVS_SPLITK_ROWS2
-#define TMVS_SPLITK_ROWS2 32768
-#endif
-  {
-    const bool big = (long)B * g.Do * g.Ho * g.Wo >= TMVS_SPLITK_ROWS2;
-#define TMVS_SPLITK_CASE(BIT, CI, CO, S)                                                            \
-  if ((TMVS_CONV_SPLITK >> BIT & 1) && cin == CI && cout == CO && stride == S)                     \
-    return big ? launch_conv_splitk<CI, CO, S, 2, 2>(x, wpk, al, sh, y, B, g, st)                  \
-               : launch_conv_splitk<CI, CO, S, 1, 2>(x, wpk, al, sh, y, B, g, st);
-    TMVS_SPLITK_CASE(0, 16, 32, 2)
-    TMVS_SPLITK_CASE(1, 32, 32, 1)
-    TMVS_SPLITK_CASE(2, 32, 64, 2)
-    TMVS_SPLITK_CASE(3, 64, 64, 1)
-#undef TMVS_SPLITK_CASE
-  }
   TMVS_CONV_LDS(32, 32, 2, 4, 2)
   TMVS_CONV_LDS(64, 64, 1, 4, 2)
 #undef TMVS_CONV_LDS
@@ -1858,18 +1549,6 @@ static int deconv_dispatch(const float* x, int B, int cin, int d, int h, int w, 
   if (cin == CI && cout == CO) {                                                                  \
     if (g.Di % 2 == 0) return launch_deconv<CI, CO, 2, 2, MBB>(x, wpk, al, sh, skip, y, B, g, st); \
     return launch_deconv<CI, CO, 1, 4, MBB>(x, wpk, al, sh, skip, y, B, g, st);                  \
-  }
-#ifndef TMVS_DECONV_SPLITK
-#define TMVS_DECONV_SPLITK 0
-#endif
-  {  // split-K tasks (bit 0: 64->32, bit 1: 32->16); two input rows per task on the bigger grids
-    const bool big = (long)B * g.Di * g.Hi * g.Wi >= TMVS_SPLITK_ROWS2;
-    if ((TMVS_DECONV_SPLITK & 1) && cin == 64 && cout == 32)
-      return big ? launch_deconv_splitk<64, 32, 2, 1>(x, wpk, al, sh, skip, y, B, g, st)
-                 : launch_deconv_splitk<64, 32, 1, 1>(x, wpk, al, sh, skip, y, B, g, st);
-    if ((TMVS_DECONV_SPLITK & 2) && cin == 32 && cout == 16)
-      return big ? launch_deconv_splitk<32, 16, 2, 1>(x, wpk, al, sh, skip, y, B, g, st)
-                 : launch_deconv_splitk<32, 16, 1, 1>(x, wpk, al, sh, skip, y, B, g, st);
   }
   TMVS_DECONV_CASE(64, 32, 1)
   TMVS_DECONV_CASE(32, 16, 1)
@@ -2078,7 +1757,7 @@ extern "C" int tmvs_costregnet_wta(const float* x, const float* hyp, int batch, 
   }
   // D <= 32: one workgroup per (sample, row, 62-column segment), its D/8 waves prob_kernel's depth
   // chunks. Measured (r07d vs r07b): D = 32 114.0 vs 108.4 + 15.7 us, D = 8 104.3 vs 90.9 + 18.6 us
-  constexpr int NR = TMVS_PROB_ROWS;
+  constexpr int NR = TMVS_PROB_WTA_ROWS;
   const dim3 gf((unsigned)(((width + kProbCols - 1) / kProbCols) * ((height + NR - 1) / NR) * batch));
   const dim3 bf((unsigned)(64 * (depth / kDChunk)));
 #define TMVS_PW_CASE(DD)                                                                                      \
