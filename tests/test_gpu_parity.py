@@ -479,8 +479,8 @@ def test_e2e_images_batch_of_two_different_depth_ranges(sd, model):
 
 def test_batch_samples_on_concurrent_streams_bitwise(model):
     """B = 3 from features with the samples on concurrent streams (model.batch_streams, the default) is
-    bitwise the sequential per-sample form (batch_streams False) and each sample's single-sample forward,
-    eagerly and replayed as one HIP graph (the sample streams fork from and join the capturing stream)."""
+    bitwise the sequential per-sample form (batch_streams False) and each sample's single-sample forward;
+    a HIP-graph capture of the B = 3 step (samples in order on the capturing stream) replays the same bits."""
     H, W, N = 64, 96, 3
     fs = [synthetic.synthetic_features(N, H, W, seed=30 + b) for b in range(3)]
     feats = {k: torch.cat([model.stack_features(f)[k] for f in fs], 0).to(DEV) for k in ("stage1", "stage2", "stage3")}

@@ -1097,6 +1097,9 @@ static int launch_conv_c16(const float* x, const float* w, const float* al, cons
 // taps are taken in pairs (a, b): lanes kgrp 0/1 read channel quads 0/1 of tap a, lanes 2/3
 // of tap b, one 16-byte read each; MFMA j contracts k = (tap, quad) over channel j of each
 // quad, and the A fragments are laid out to match (the 14th pair is half empty).
+#ifndef TMVS_S2C8_SW
+#define TMVS_S2C8_SW 17
+#endif
 template <int TD, int TH>
 __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ wpk,
@@ -1104,7 +1107,9 @@ __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __re
                                                                const float* __restrict__ shift, float* __restrict__ y,
                                                                Geo g, int ntiles) {
   constexpr int CIN = 8, COUT = 16, NBW = TD * TH / 4;
-  constexpr int LW = 33, LH = 2 * TH + 1, LD = 2 * TD + 1, SW = 17;
+  // SW: voxel slots per parity half-row; 20 (not 17) puts a staging write's odd-column voxels 32 banks
+  // from its even ones (the commit's ds_write_b128 had 2-way conflicts, PMC ldsconf 0.24)
+  constexpr int LW = 33, LH = 2 * TH + 1, LD = 2 * TD + 1, SW = TMVS_S2C8_SW;
   constexpr int NROW = LD * LH, NQ = NROW * LW * 2;  // float4 quads per tile
   constexpr int NLD = (NQ + 255) / 256;
   __shared__ __attribute__((aligned(16))) float tile[NROW * 2 * SW * 8];

@@ -368,7 +368,12 @@ class TransMVSNet(nn.Module):
         # from depth_values[0] for every sample (models/TransMVSNet.py:146-148). Samples are independent:
         # with B > 1 each runs on its own stream (sample 0 on the caller's), so one sample's small
         # coarse-level grids overlap another's kernels; the caller's stream then waits for all of them.
-        concurrent = b > 1 and self.batch_streams and view_shard is None and not self.decomposed
+        # (not inside a HIP-graph capture: a multi-stream fork/join of the samples there crashed the
+        # capture's end on the box, r16g -- a captured B > 1 step runs its samples in order on the
+        # capturing stream; to replay samples concurrently, capture one graph per sample and replay them
+        # on separate streams, as bench.py's batch2_concurrent line does)
+        concurrent = (b > 1 and self.batch_streams and view_shard is None and not self.decomposed
+                      and not torch.cuda.is_current_stream_capturing())
         main = torch.cuda.current_stream(dev)
         if concurrent:
             start = torch.cuda.Event()
@@ -380,7 +385,8 @@ class TransMVSNet(nn.Module):
                 st.wait_event(start)
             with torch.cuda.stream(st):
                 o, vw = self._forward_one({k: v[i] for k, v in feats.items()}, {k: r[i:i + 1] for k, r in rows.items()},
-                                          dv[i:i + 1], dv[0:1], img_hw, prep, view_shard)
+                                          dv[i:i + 1], dv[0:1], img_hw, prep, view_shard,
+                                          slot=i if st is not main else 0)
             if st is not main:
                 ev = torch.cuda.Event()
                 ev.record(st)
@@ -412,7 +418,7 @@ class TransMVSNet(nn.Module):
         n, c, h1, w1 = s1.shape
         return ops.fmt_forward(s1, self._pe_slice(h1, w1, s1.device), prep["enc"])
 
-    def _forward_one(self, f, rows, dv, dv0, img_hw, prep, view_shard):
+    def _forward_one(self, f, rows, dv, dv0, img_hw, prep, view_shard, slot=0):
         s1, s2, s3 = f["stage1"], f["stage2"], f["stage3"]
         n, _, h1, w1 = s1.shape
         tokens = self._fmt(s1, prep)
@@ -428,7 +434,7 @@ class TransMVSNet(nn.Module):
             """Launch the pathway on a side stream once stage 1's cost volume is queued, so it runs
             beside stage 1's CostRegNet (whose 1/16-resolution grids leave most CUs idle)."""
             main = torch.cuda.current_stream(s1.device)
-            key = (s1.device, main.stream_id)  # one pathway side stream per launching stream (B > 1 runs samples concurrently)
+            key = (s1.device, slot)  # one pathway side stream per sample stream (B > 1 runs samples concurrently)
             side = self._side.get(key)
             if side is None:
                 side = self._side[key] = torch.cuda.Stream(s1.device, priority=self.side_priority)
