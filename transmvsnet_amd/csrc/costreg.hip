@@ -1097,9 +1097,6 @@ static int launch_conv_c16(const float* x, const float* w, const float* al, cons
 // taps are taken in pairs (a, b): lanes kgrp 0/1 read channel quads 0/1 of tap a, lanes 2/3
 // of tap b, one 16-byte read each; MFMA j contracts k = (tap, quad) over channel j of each
 // quad, and the A fragments are laid out to match (the 14th pair is half empty).
-#ifndef TMVS_S2C8_SW
-#define TMVS_S2C8_SW 17
-#endif
 template <int TD, int TH>
 __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ wpk,
@@ -1107,9 +1104,8 @@ __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __re
                                                                const float* __restrict__ shift, float* __restrict__ y,
                                                                Geo g, int ntiles) {
   constexpr int CIN = 8, COUT = 16, NBW = TD * TH / 4;
-  // SW: voxel slots per parity half-row; 20 (not 17) puts a staging write's odd-column voxels 32 banks
-  // from its even ones (the commit's ds_write_b128 had 2-way conflicts, PMC ldsconf 0.24)
-  constexpr int LW = 33, LH = 2 * TH + 1, LD = 2 * TD + 1, SW = TMVS_S2C8_SW;
+  // (SW = 20, which offsets the staging writes' odd-column voxels by 32 banks, measured the same: r16g)
+  constexpr int LW = 33, LH = 2 * TH + 1, LD = 2 * TD + 1, SW = 17;
   constexpr int NROW = LD * LH, NQ = NROW * LW * 2;  // float4 quads per tile
   constexpr int NLD = (NQ + 255) / 256;
   __shared__ __attribute__((aligned(16))) float tile[NROW * 2 * SW * 8];
@@ -1281,9 +1277,6 @@ static int launch_conv_direct(const float* x, const float* w, const float* al, c
 // are requested before the MFMAs too, so neither latency sits between MFMA phases.
 // Tiles are dealt out XCD-contiguously (an XCD's workgroups share one L2: neighbouring tiles
 // share their halo voxels).
-#ifndef TMVS_C8_DIRECT
-#define TMVS_C8_DIRECT 0
-#endif
 template <int TDI, int THI>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void deconv3d_c8_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                           const float* __restrict__ alpha,
@@ -1370,11 +1363,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const TileCoord c = coord(t);
     const int tn = t + per_xcd;
     if (tn < t_hi) fetch(tn);
-    // skip rows of this tile: lane (pair) j of a 1 KiB output row, as the epilogue stores it
-    // (TMVS_C8_DIRECT: lane (col, kgrp)'s own MFMA outputs, voxel 2 (mw0 + col) + kgrp / 2, channels
-    // 4 (kgrp & 1) .. +3 -- the whole row segment still one contiguous 1 KiB per instruction, no exchange)
+    // skip rows of this tile: lane (pair) j of a 1 KiB output row, as the epilogue stores it (storing each
+    // lane's own MFMA outputs without the exchange measured 110.2 -> 112.6 us in the step, r16g)
     const size_t out_n = (size_t)c.n * g.Do * g.Ho * g.Wo;
-    const int ow = TMVS_C8_DIRECT ? 2 * (c.mw0 + col) + (kgrp >> 1) : 2 * c.mw0 + (lane >> 1);
+    const int ow = 2 * c.mw0 + (lane >> 1);
     const size_t plane = (size_t)g.Ho * g.Wo * 8, row = (size_t)g.Wo * 8;  // output strides (floats)
     float4 sk[NBW][4];
     size_t oo[NBW];
@@ -1384,7 +1376,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const int rr = wv * NBW + r;
       const int md = c.md0 + rr / THI, mh = c.mh0 + rr % THI;
       ok[r] = md < g.Di && mh < g.Hi && ow < 2 * g.Wi;
-      oo[r] = (out_n + ((size_t)(2 * md) * g.Ho + 2 * mh) * g.Wo + ow) * 8 + (TMVS_C8_DIRECT ? cq : (lane & 1) * 4);
+      oo[r] = (out_n + ((size_t)(2 * md) * g.Ho + 2 * mh) * g.Wo + ow) * 8 + (lane & 1) * 4;
 #pragma unroll
       for (int pdh = 0; pdh < 4; ++pdh)
         sk[r][pdh] = (ok[r] && skip) ? *reinterpret_cast<const float4*>(skip + oo[r] + (pdh >> 1) * plane + (pdh & 1) * row)
@@ -1436,14 +1428,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
       for (int pdh = 0; pdh < 4; ++pdh) {
         const floatx4 a = acc[r][pdh];
-        float4 v = make_float4(act(fmaf(a[0], al.x, sh.x), g.lo), act(fmaf(a[1], al.y, sh.y), g.lo),
-                               act(fmaf(a[2], al.z, sh.z), g.lo), act(fmaf(a[3], al.w, sh.w), g.lo));
-        if constexpr (!TMVS_C8_DIRECT) {
-          *reinterpret_cast<float4*>(eb + (2 * col + (kgrp >> 1)) * 8 + cq) = v;
-          __builtin_amdgcn_wave_barrier();
-          v = *reinterpret_cast<const float4*>(eb + lane * 4);
-          __builtin_amdgcn_wave_barrier();
-        }
+        *reinterpret_cast<float4*>(eb + (2 * col + (kgrp >> 1)) * 8 + cq) =
+            make_float4(act(fmaf(a[0], al.x, sh.x), g.lo), act(fmaf(a[1], al.y, sh.y), g.lo), act(fmaf(a[2], al.z, sh.z), g.lo),
+                        act(fmaf(a[3], al.w, sh.w), g.lo));
+        __builtin_amdgcn_wave_barrier();
+        const float4 v = *reinterpret_cast<const float4*>(eb + lane * 4);
+        __builtin_amdgcn_wave_barrier();
         const float4 sv = sk[r][pdh];
         if (ok[r])
           *reinterpret_cast<float4*>(y + oo[r] + (pdh >> 1) * plane + (pdh & 1) * row) =
