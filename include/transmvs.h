@@ -88,8 +88,6 @@ int tmvs_stage_hypotheses(const float* depth_values, int n_values, const float* 
 #define TMVS_WARP_PARTIAL 1
 #define TMVS_WARP_ROT_PLAIN 2
 #define TMVS_WARP_BWD_PLANES 4 /* tmvs_warp_corr_backward: hyp[d] is one depth per plane (stage 1) */
-#define TMVS_WARP_SRC_PAIRED 8 /* tmvs_warp_corr, C = 8 / 16 with given view weights: src_fea holds tap pairs
-                                  [n_src][H][W+1][2C], P[i] = (f[i-1], f[i]) (tmvs_pair_rows); ABI 8 */
 #define TMVS_PW_NPARAMS 201 /* w0[16] a0[16] s0[16] w1[8][16] a1[8] s1[8] w2[8] b2 */
 int tmvs_warp_corr(const float* ref_fea, const float* src_fea, const float* proj, const float* hyp,
                    const float* view_w_in, int vw_shift, int vw_offset, int vw_total, const float* pw_params,
@@ -354,10 +352,6 @@ int tmvs_linattn_bwd_q(const float* q, const float* dmsg, long tokens, long toke
                        void* stream);
 int tmvs_linattn_bwd_kv(const float* k, const float* v, long tokens, long tokens_per_group, const float* dkv,
                         float* dk, float* dv, void* stream);
-
-/* [nv][h][w][c] NHWC features -> [nv][h][w+1][2c] tap pairs P[i] = (f[i-1], f[i]) (zeros beyond the
- * image): the source layout of TMVS_WARP_SRC_PAIRED (c % 4 == 0). */
-int tmvs_pair_rows(const float* src, int nv, int height, int width, int channels, float* out, void* stream);
 
 /* Adam over one flat fp32 buffer (finetune.py:324: torch.optim.Adam, L2 weight decay, no amsgrad),
  * torch's single-tensor update order; step >= 1 is the 1-based step count (bias corrections).

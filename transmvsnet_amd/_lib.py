@@ -25,7 +25,6 @@ SIGNATURES = {
     "tmvs_stage_hypotheses": (I, [P, I, P, I, I, I, I, F, I, I, I, P, P]),
     "tmvs_warp_corr": (I, [P, P, P, P, P, I, I, I, P, I, I, I, I, I, I, I, P, P, P, P]),
     "tmvs_aggregate_finalize": (I, [P, P, I, I, I, I, P]),
-    "tmvs_pair_rows": (I, [P, I, I, I, I, P, P]),
     "tmvs_homo_warping": (I, [P, P, P, I, I, I, I, I, I, P, P]),
     "tmvs_costregnet_workspace": (S, [I, I, I, I, I]),
     "tmvs_costregnet": (I, [P, I, I, I, I, P, P, S, P, P]),
@@ -108,7 +107,6 @@ ENC_NPARAMS = 8544
 KV_NFLOATS = 160
 WARP_PARTIAL = 1
 WARP_ROT_PLAIN = 2
-WARP_SRC_PAIRED = 8
 WARP_BWD_PLANES = 4
 CONV_TRANSPOSED = 1
 CONV_ACCUMULATE = 2

@@ -479,12 +479,7 @@ __device__ __forceinline__ Geom geom_round(const Geom& own, int t) {
 // Row-pair rounds R0..R0+N-1 (see warp_pair_kernel): in round t the group samples plane t;
 // this lane loads its tap column's two rows (one 16-byte channel quad each); all loads of the
 // batch are issued before any is consumed.
-// PAIRED (TMVS_WARP_SRC_PAIRED): the source rows hold tap pairs P[i] = (f[i-1], f[i]), i = 0 .. W
-// (zeros beyond the image), 2C floats each, so the two taps (x0, x0+1) of a row are the aligned pair
-// P[x0+1]: a C = 8 span never straddles a 128-byte line (32-byte alignment did, for x0 = 3 mod 4) and a
-// C = 16 span is one whole line (64-byte alignment straddled two for odd x0); the lane's tap column is
-// folded into vbase.
-template <int C, int R0, int N, bool PAIRED = false>
+template <int C, int R0, int N>
 __device__ __forceinline__ void pair_rounds(const __amdgpu_buffer_rsrc_t rsrc, unsigned vbase, unsigned rowb, int W,
                                             int H, const Geom& own, const float4* r4, int tx, float* part) {
   constexpr int LPS = C / 2;
@@ -493,14 +488,8 @@ __device__ __forceinline__ void pair_rounds(const __amdgpu_buffer_rsrc_t rsrc, u
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const Geom g = geom_round<LPS>(own, R0 + i);
-    unsigned ox;
-    if constexpr (PAIRED) {
-      const int P = g.x0 + 1;
-      ox = (unsigned)P <= (unsigned)W ? (unsigned)P * (unsigned)(2 * C * 4) : kAxisOut;
-    } else {
-      const int X = g.x0 + tx;
-      ox = (unsigned)X < (unsigned)W ? (unsigned)X * (unsigned)(C * 4) : kAxisOut;
-    }
+    const int X = g.x0 + tx;
+    const unsigned ox = (unsigned)X < (unsigned)W ? (unsigned)X * (unsigned)(C * 4) : kAxisOut;
     const unsigned yrow = vbase + (unsigned)g.y0 * rowb;
     const unsigned oa = (unsigned)g.y0 < (unsigned)H ? yrow : kAxisOut;
     const unsigned ob = (unsigned)(g.y0 + 1) < (unsigned)H ? yrow + rowb : kAxisOut;
@@ -567,7 +556,7 @@ __device__ __forceinline__ float reduce_scatter(const float* p, int k) {
 #define TMVS_WARP_PMAJOR 1
 #endif
 
-template <int C, int D, bool PARTIAL, bool PAIRED = false>
+template <int C, int D, bool PARTIAL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void warp_pair_kernel(
     const float* __restrict__ ref, const float* __restrict__ src, const float* __restrict__ hyp,
     const float* __restrict__ vw_in, float* __restrict__ sim_out, float* __restrict__ wsum_out, int V, int H, int W,
@@ -613,25 +602,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const int Ws = W >> vw_shift, Hs = H >> vw_shift;
   const float* wv = vw_in + (size_t)vw_offset * Hs * Ws + (py >> vw_shift) * Ws + (px >> vw_shift);
   float wsum = PARTIAL ? 0.f : 1e-5f;
-  const unsigned rowb = (unsigned)(PAIRED ? (W + 1) * 2 : W) * C * 4;
   const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)((unsigned)V * H * rowb), kRsrcWord3);
+      __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, V * HW * C * 4, kRsrcWord3);
+  const unsigned rowb = (unsigned)W * C * 4;
   for (int v = 0; v < V; ++v) {
     const float* R = args.proj[v];
     const float rx = rot_row(R, fxp, fyp, args.rot_plain);
     const float ry = rot_row(R + 4, fxp, fyp, args.rot_plain);
     const float rz = rot_row(R + 8, fxp, fyp, args.rot_plain);
-    const unsigned vbase = (unsigned)v * H * rowb + 16u * q + (PAIRED ? (unsigned)tx * C * 4 : 0u);
+    const unsigned vbase = (unsigned)(v * HW * C * 4 + 16 * q);
     const float w = wv[(size_t)v * Hs * Ws];
 #pragma unroll 1
     for (int j = 0; j < DPT; ++j) {
       Geom own;
       project(rx, ry, rz, R[3], R[7], R[11], dep_lds[j][tid], halfw, halfh, own.x0, own.y0, own.fx, own.fy);
       float part[LPS];
-      pair_rounds<C, 0, (LPS < 4 ? LPS : 4), PAIRED>(rsrc, vbase, rowb, W, H, own, r4, tx, part);
+      pair_rounds<C, 0, (LPS < 4 ? LPS : 4)>(rsrc, vbase, rowb, W, H, own, r4, tx, part);
       if constexpr (LPS == 8) {
         __builtin_amdgcn_sched_barrier(0);
-        pair_rounds<C, 4, 4, PAIRED>(rsrc, vbase, rowb, W, H, own, r4, tx, part);
+        pair_rounds<C, 4, 4>(rsrc, vbase, rowb, W, H, own, r4, tx, part);
       }
       float tot = reduce_scatter<LPS>(part, k);
       acc_lds[j][tid] = acc_lds[j][tid] + (tot * (1.f / (float)C)) * w;
@@ -650,20 +639,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 template <int C, int D, bool PW, bool PARTIAL>
 static int launch_warp(const float* ref, const float* src, const float* hyp, const float* vw_in, float* sim,
                        float* wsum, float* vw_out, int V, int H, int W, int vw_shift, int vw_offset, int vw_total,
-                       const WarpArgs& args, hipStream_t st, bool paired) {
+                       const WarpArgs& args, hipStream_t st) {
   if constexpr ((C == 8 || C == 16) && !PW) {
     constexpr int PIXP = 4 * (64 / (C / 2));
     const int nblk = (H * W + PIXP - 1) / PIXP;
-    if (paired)
-      hipLaunchKernelGGL((warp_pair_kernel<C, D, PARTIAL, true>), dim3(nblk), dim3(256), 0, st, ref, src, hyp, vw_in,
-                         sim, wsum, V, H, W, vw_shift, vw_offset, args);
-    else
-      hipLaunchKernelGGL((warp_pair_kernel<C, D, PARTIAL>), dim3(nblk), dim3(256), 0, st, ref, src, hyp, vw_in, sim,
-                         wsum, V, H, W, vw_shift, vw_offset, args);
+    hipLaunchKernelGGL((warp_pair_kernel<C, D, PARTIAL>), dim3(nblk), dim3(256), 0, st, ref, src, hyp, vw_in, sim,
+                       wsum, V, H, W, vw_shift, vw_offset, args);
     TMVS_CHECK_LAUNCH();
     return TMVS_OK;
   }
-  if (paired) return TMVS_ERR_ARG;  // the paired source layout is read by the row-pair kernel (C = 8 / 16, given weights)
   constexpr int PIX = 4 * (64 / (C / 4));
   const int nblk = (H * W + PIX - 1) / PIX;
   hipLaunchKernelGGL((warp_corr_kernel<C, D, PW, PARTIAL>), dim3(nblk), dim3(256), 0, st, ref, src, hyp, vw_in, sim,
@@ -675,11 +659,11 @@ static int launch_warp(const float* ref, const float* src, const float* hyp, con
 template <int C, bool PW, bool PARTIAL>
 static int dispatch_depth(int D, const float* ref, const float* src, const float* hyp, const float* vw_in, float* sim,
                           float* wsum, float* vw_out, int V, int H, int W, int vw_shift, int vw_offset, int vw_total,
-                          const WarpArgs& a, hipStream_t st, bool paired) {
+                          const WarpArgs& a, hipStream_t st) {
 #define TMVS_WARP_CASE(DD)                                                                                        \
   if (D == DD)                                                                                                    \
     return launch_warp<C, DD, PW, PARTIAL>(ref, src, hyp, vw_in, sim, wsum, vw_out, V, H, W, vw_shift, vw_offset, \
-                                           vw_total, a, st, paired);
+                                           vw_total, a, st);
   TMVS_WARP_CASE(48)
   TMVS_WARP_CASE(32)
   TMVS_WARP_CASE(16)
@@ -693,18 +677,18 @@ static int dispatch_depth(int D, const float* ref, const float* src, const float
 template <int C>
 static int dispatch_mode(bool pw, bool partial, int D, const float* ref, const float* src, const float* hyp,
                          const float* vw_in, float* sim, float* wsum, float* vw_out, int V, int H, int W, int vw_shift,
-                         int vw_offset, int vw_total, const WarpArgs& a, hipStream_t st, bool paired) {
+                         int vw_offset, int vw_total, const WarpArgs& a, hipStream_t st) {
   if (pw && partial)
     return dispatch_depth<C, true, true>(D, ref, src, hyp, vw_in, sim, wsum, vw_out, V, H, W, vw_shift, vw_offset,
-                                         vw_total, a, st, paired);
+                                         vw_total, a, st);
   if (pw)
     return dispatch_depth<C, true, false>(D, ref, src, hyp, vw_in, sim, wsum, vw_out, V, H, W, vw_shift, vw_offset,
-                                          vw_total, a, st, paired);
+                                          vw_total, a, st);
   if (partial)
     return dispatch_depth<C, false, true>(D, ref, src, hyp, vw_in, sim, wsum, vw_out, V, H, W, vw_shift, vw_offset,
-                                          vw_total, a, st, paired);
+                                          vw_total, a, st);
   return dispatch_depth<C, false, false>(D, ref, src, hyp, vw_in, sim, wsum, vw_out, V, H, W, vw_shift, vw_offset,
-                                         vw_total, a, st, paired);
+                                         vw_total, a, st);
 }
 
 
@@ -1087,10 +1071,8 @@ extern "C" int tmvs_warp_corr(const float* ref_fea, const float* src_fea, const 
   if (pw && (!pw_params || !view_w_out)) return TMVS_ERR_ARG;
   if (partial && !wsum_out) return TMVS_ERR_ARG;
   if (vw_offset < 0 || vw_offset + n_src > vw_total || vw_shift < 0) return TMVS_ERR_ARG;
-  const bool paired = (flags & TMVS_WARP_SRC_PAIRED) != 0;
-  const long long src_row = paired ? (long long)(width + 1) * 2 * channels : (long long)width * channels;
   // the kernel addresses one sample's source views with 32-bit byte offsets (< 2^30)
-  if ((long long)n_src * height * src_row * 4 >= (1LL << 30)) return TMVS_ERR_SHAPE;
+  if ((long long)n_src * height * width * channels * 4 >= (1LL << 30)) return TMVS_ERR_SHAPE;
   if (width > 32766 || height > 32766) return TMVS_ERR_SHAPE;
   hipStream_t st = (hipStream_t)stream;
   const size_t HW = (size_t)height * width;
@@ -1104,7 +1086,7 @@ extern "C" int tmvs_warp_corr(const float* ref_fea, const float* src_fea, const 
     else
       for (int k = 0; k < TMVS_PW_NPARAMS; ++k) a.pw[k] = 0.f;
     const float* rb = ref_fea + (size_t)b * HW * channels;
-    const float* sb = src_fea + (size_t)b * n_src * height * src_row;
+    const float* sb = src_fea + (size_t)b * n_src * HW * channels;
     const float* hb = hyp + (size_t)b * ndepth * HW;
     const size_t hs = (size_t)(height >> vw_shift) * (width >> vw_shift);
     const float* vib = pw ? nullptr : view_w_in + (size_t)b * vw_total * hs;
@@ -1115,44 +1097,21 @@ extern "C" int tmvs_warp_corr(const float* ref_fea, const float* src_fea, const 
     switch (channels) {
       case 32:
         rc = dispatch_mode<32>(pw, partial, ndepth, rb, sb, hb, vib, sob, wob, vob, n_src, height, width, vw_shift,
-                               vw_offset, vw_total, a, st, paired);
+                               vw_offset, vw_total, a, st);
         break;
       case 16:
         rc = dispatch_mode<16>(pw, partial, ndepth, rb, sb, hb, vib, sob, wob, vob, n_src, height, width, vw_shift,
-                               vw_offset, vw_total, a, st, paired);
+                               vw_offset, vw_total, a, st);
         break;
       case 8:
         rc = dispatch_mode<8>(pw, partial, ndepth, rb, sb, hb, vib, sob, wob, vob, n_src, height, width, vw_shift,
-                               vw_offset, vw_total, a, st, paired);
+                              vw_offset, vw_total, a, st);
         break;
       default:
         return TMVS_ERR_SHAPE;
     }
     if (rc != TMVS_OK) return rc;
   }
-  return TMVS_OK;
-}
-
-// [nv][h][w][c] NHWC -> [nv][h][w+1][2c] tap pairs P[i] = (f[i-1], f[i]) (zeros outside), the source
-// layout of TMVS_WARP_SRC_PAIRED; one thread per output float4
-__global__ __launch_bounds__(256) void pair_rows_kernel(const float4* __restrict__ src, float4* __restrict__ out,
-                                                        long n_out4, int w, int c4) {
-  const long o = (long)blockIdx.x * 256 + threadIdx.x;
-  if (o >= n_out4) return;
-  const int q = (int)(o % (2 * c4));
-  const long rp = o / (2 * c4);  // (view, row) * (w + 1) + pair
-  const int i = (int)(rp % (w + 1));
-  const long row = rp / (w + 1);
-  const int x = q < c4 ? i - 1 : i;
-  out[o] = (x >= 0 && x < w) ? src[(row * w + x) * c4 + (q % c4)] : make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-extern "C" int tmvs_pair_rows(const float* src, int nv, int height, int width, int channels, float* out, void* stream) {
-  if (!src || !out || nv <= 0 || height <= 0 || width <= 0 || channels <= 0 || channels % 4) return TMVS_ERR_ARG;
-  const long n4 = (long)nv * height * (width + 1) * 2 * (channels / 4);
-  hipLaunchKernelGGL(pair_rows_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     reinterpret_cast<const float4*>(src), reinterpret_cast<float4*>(out), n4, width, channels / 4);
-  TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
 

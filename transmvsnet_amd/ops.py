@@ -168,32 +168,16 @@ def stage_hypotheses(depth_values, prev_depth, ndepth, ratio, full_hw, stage_sca
     return out
 
 
-def pair_rows(src_nhwc):
-    """tmvs_pair_rows: [V,H,W,C] -> [V,H,W+1,2C] tap pairs P[i] = (f[i-1], f[i]) (the src_paired layout)."""
-    _dev(src_nhwc, "src")
-    v, h, w, c = src_nhwc.shape
-    out = torch.empty(v, h, w + 1, 2 * c, device=src_nhwc.device)
-    with _Span("tmvs_pair_rows"):
-        _lib.check(_lib_h().tmvs_pair_rows(_ptr(src_nhwc), v, h, w, c, _ptr(out), _stream()), "tmvs_pair_rows")
-    return out
-
-
 def warp_corr(ref_nhwc, src_nhwc, proj12, hyp, view_w_in=None, vw_shift=0, vw_offset=0, vw_total=None,
-              pw_params=None, partial=False, view_w_out=None, sim_out=None, wsum_out=None, rot_order="auto",
-              src_paired=False):
+              pw_params=None, partial=False, view_w_out=None, sim_out=None, wsum_out=None, rot_order="auto"):
     """Fused cost volume (models/TransMVSNet.py:58-93). ref [B,H,W,C], src [B,V,H,W,C], proj12 HOST [B,V,12].
 
     Returns sim [B,D,H,W] (and w_sum [B,H,W] when partial) ; stage 1 writes view_w_out [B,vw_total,H,W].
     rot_order: the reference's rounding of rot·(x, y, 1) ('auto' = this host's torch, host_rot_order).
-    src_paired: src is [B,V,H,W+1,2C] tap pairs (pair_rows; C = 8 / 16 with given view weights).
     """
     for t, n in ((ref_nhwc, "ref"), (src_nhwc, "src"), (hyp, "hyp"), (view_w_in, "view_w_in"), (view_w_out, "view_w_out")):
         _dev(t, n)
     b, v, h, w, c = src_nhwc.shape
-    if src_paired:
-        w, c = w - 1, c // 2
-        if tuple(ref_nhwc.shape[-3:]) != (h, w, c):
-            raise ValueError("warp_corr: src_paired wants src [B,V,H,W+1,2C] for ref [B,H,W,C]")
     d = hyp.shape[1]
     vw_total = v if vw_total is None else vw_total
     proj = np.ascontiguousarray(proj12, np.float32).reshape(b, v, 12)
@@ -214,8 +198,7 @@ def warp_corr(ref_nhwc, src_nhwc, proj12, hyp, view_w_in=None, vw_shift=0, vw_of
     with _Span("tmvs_warp_corr"):
         _lib.check(_lib_h().tmvs_warp_corr(_ptr(ref_nhwc), _ptr(src_nhwc), proj.ctypes.data, _ptr(hyp), _ptr(view_w_in),
                                            vw_shift, vw_offset, vw_total, pw_ptr, b, v, c, d, h, w,
-                                           (_lib.WARP_PARTIAL if partial else 0) | warp_flags(rot_order, h * w)
-                                           | (_lib.WARP_SRC_PAIRED if src_paired else 0),
+                                           (_lib.WARP_PARTIAL if partial else 0) | warp_flags(rot_order, h * w),
                                            _ptr(sim), _ptr(wsum),
                                            _ptr(view_w_out if view_w_in is None else None), _stream()), "tmvs_warp_corr")
     return sim, wsum, (view_w_out if view_w_in is None else None)
@@ -585,7 +568,7 @@ def depth_metrics(depth, depth_gt, mask, depth_interval):
     return out
 
 
-for _name in ("stage_hypotheses", "warp_corr", "pair_rows", "aggregate_finalize", "homo_warping", "softmax_wta", "costregnet",
+for _name in ("stage_hypotheses", "warp_corr", "aggregate_finalize", "homo_warping", "softmax_wta", "costregnet",
               "costregnet_wta",
               "conv3d_bn_relu", "deconv3d_bn_relu_add", "fmt_embed", "fmt_kv", "fmt_apply", "fmt_pathway",
               "fmt_forward", "depth_stage", "deform_conv2d", "dcn_fused", "conv3x3_nhwc", "fpn_merge",
