@@ -1097,9 +1097,6 @@ static int launch_conv_c16(const float* x, const float* w, const float* al, cons
 // taps are taken in pairs (a, b): lanes kgrp 0/1 read channel quads 0/1 of tap a, lanes 2/3
 // of tap b, one 16-byte read each; MFMA j contracts k = (tap, quad) over channel j of each
 // quad, and the A fragments are laid out to match (the 14th pair is half empty).
-#ifndef TMVS_S2C8_SW
-#define TMVS_S2C8_SW 17
-#endif
 template <int TD, int TH>
 __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ wpk,
@@ -1107,11 +1104,8 @@ __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __re
                                                                const float* __restrict__ shift, float* __restrict__ y,
                                                                Geo g, int ntiles) {
   constexpr int CIN = 8, COUT = 16, NBW = TD * TH / 4;
-  // SW: voxel slots per parity half-row. ds_write_b128 banks are (a/4) mod 32 over 8-lane groups = 4 voxels
-  // of a staged row, alternating parity halves: with SW = 18 (SW * 32 B = 64 mod 128) the odd half-row sits
-  // 64 B off the even one and the group's 4 voxels fill 128 distinct bytes; SW = 17 put two of them on the
-  // same 32 B (PMC: 24 % of the LDS cycles were conflicts; SW = 20 kept them, r16g)
-  constexpr int LW = 33, LH = 2 * TH + 1, LD = 2 * TD + 1, SW = TMVS_S2C8_SW;
+  // (SW = 20, which offsets the staging writes' odd-column voxels by 32 banks, measured the same: r16g)
+  constexpr int LW = 33, LH = 2 * TH + 1, LD = 2 * TD + 1, SW = 17;
   constexpr int NROW = LD * LH, NQ = NROW * LW * 2;  // float4 quads per tile
   constexpr int NLD = (NQ + 255) / 256;
   __shared__ __attribute__((aligned(16))) float tile[NROW * 2 * SW * 8];
@@ -1283,9 +1277,6 @@ static int launch_conv_direct(const float* x, const float* w, const float* al, c
 // are requested before the MFMAs too, so neither latency sits between MFMA phases.
 // Tiles are dealt out XCD-contiguously (an XCD's workgroups share one L2: neighbouring tiles
 // share their halo voxels).
-#ifndef TMVS_C8_XSWZ
-#define TMVS_C8_XSWZ 0
-#endif
 template <int TDI, int THI>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void deconv3d_c8_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                           const float* __restrict__ alpha,
@@ -1437,17 +1428,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
       for (int pdh = 0; pdh < 4; ++pdh) {
         const floatx4 a = acc[r][pdh];
-        // the row's float4 f = 4 col + kgrp (voxel 2 col + kgrp / 2, channel half kgrp & 1) goes to slot
-        // kgrp * 16 + (col ^ 4 kgrp) (TMVS_C8_XSWZ): each 8-lane ds_write_b128 group then fills 128
-        // distinct bytes (f * 16 put 8 lanes on 2 slots: 4-way conflicts, PMC 31 % of the LDS cycles) and
-        // each 16-lane ds_read_b128 group of the lane-contiguous read-back still covers 16 distinct slots
-        const int wslot = TMVS_C8_XSWZ ? kgrp * 16 + (col ^ (4 * kgrp)) : 4 * col + kgrp;
-        const int rslot = TMVS_C8_XSWZ ? (lane & 3) * 16 + ((lane >> 2) ^ (4 * (lane & 3))) : lane;
-        *reinterpret_cast<float4*>(eb + wslot * 4) =
+        *reinterpret_cast<float4*>(eb + (2 * col + (kgrp >> 1)) * 8 + cq) =
             make_float4(act(fmaf(a[0], al.x, sh.x), g.lo), act(fmaf(a[1], al.y, sh.y), g.lo), act(fmaf(a[2], al.z, sh.z), g.lo),
                         act(fmaf(a[3], al.w, sh.w), g.lo));
         __builtin_amdgcn_wave_barrier();
-        const float4 v = *reinterpret_cast<const float4*>(eb + rslot * 4);
+        const float4 v = *reinterpret_cast<const float4*>(eb + lane * 4);
         __builtin_amdgcn_wave_barrier();
         const float4 sv = sk[r][pdh];
         if (ok[r])
