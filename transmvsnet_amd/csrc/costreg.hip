@@ -51,6 +51,37 @@ struct VecN<2> {
   __device__ __forceinline__ void zero() { v[0] = v[1] = 0.f; }
 };
 
+// Range-checked raw buffer over one tensor: a lane whose 32-bit byte offset is out of range reads
+// zeros (the buffer unit's bound check), so padding taps need no exec-mask branch and no 64-bit
+// address per load; the wave-uniform part of an offset goes in the scalar offset. Branch-free load
+// streams keep the compiler's vmcnt waits exact (a branch per load made it wait vmcnt(0)).
+struct Buf {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ Buf(const float* base, uint32_t nbytes)
+      : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)nbytes, 0x00020000)) {}
+  static constexpr int kOOB = (int)0x80000000u;  // any offset >= the range reads zeros
+  __device__ __forceinline__ float4 ld4(int voff, int soff = 0) const {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+  }
+  __device__ __forceinline__ float2 ld2(int voff, int soff = 0) const {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+    return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+  }
+};
+template <int N>
+__device__ __forceinline__ void buf_load(VecN<N>& d, const Buf& b, int voff, int soff = 0);
+template <>
+__device__ __forceinline__ void buf_load<4>(VecN<4>& d, const Buf& b, int voff, int soff) {
+  const float4 t = b.ld4(voff, soff);
+  d.v[0] = t.x, d.v[1] = t.y, d.v[2] = t.z, d.v[3] = t.w;
+}
+template <>
+__device__ __forceinline__ void buf_load<2>(VecN<2>& d, const Buf& b, int voff, int soff) {
+  const float2 t = b.ld2(voff, soff);
+  d.v[0] = t.x, d.v[1] = t.y;
+}
+
 struct Geo {
   int Di, Hi, Wi;  // input dims
   int Do, Ho, Wo;  // output dims
@@ -112,6 +143,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
 
   // channel chunk ch's tile: global -> registers (issued one chunk ahead) -> LDS
   constexpr int NCH = CIN / CK, NLD = (NVOX * PL + 255) / 256;
+  const Buf xb(x + in_n * CIN, (uint32_t)g.Di * g.Hi * g.Wi * CIN * 4);  // this sample (host: < 2 GB)
+  const Buf wb(wpk, 27u * COUT * CIN * 4);
   float4 pf[NLD];
   auto fetch = [&](int ch) {
 #pragma unroll
@@ -120,9 +153,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
       const int vox = idx / PL, q = idx - vox * PL;
       const int lw = vox % LW, rest = vox / LW, lh = rest % LH, ld = rest / LH;
       const int iw = iw0 + lw, ih = ih0 + lh, id = id0 + ld;
-      pf[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (idx < NVOX * PL && iw >= 0 && iw < g.Wi && ih >= 0 && ih < g.Hi && id >= 0 && id < g.Di)
-        pf[k] = *reinterpret_cast<const float4*>(x + (in_n + ((size_t)id * g.Hi + ih) * g.Wi + iw) * CIN + ch * CK + 4 * q);
+      // branch-free: padding lanes load x[0..3] and select zero, so the loads stay in one basic
+      // block and the compiler's vmcnt waits count them exactly (a branch per load made it wait
+      // vmcnt(0) every third tap, exposing the L2 latency of the two-tap-ahead weight loads)
+      const bool ok = idx < NVOX * PL && iw >= 0 && iw < g.Wi && ih >= 0 && ih < g.Hi && id >= 0 && id < g.Di;
+      pf[k] = xb.ld4(ok ? (((id * g.Hi + ih) * g.Wi + iw) * CIN + 4 * q) * 4 : Buf::kOOB, ch * CK * 4);
     }
   };
   auto commit = [&]() {
@@ -147,89 +182,93 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
     kd_hi = g.Di - 1 - id_base < 2 ? g.Di - 1 - id_base : 2;
     if (od >= g.Do) kd_hi = -1;  // rows past the volume: nothing to compute
   }
+  // A fragments (chunk ch, tap) from global/L2, requested two taps ahead of their MFMAs; the
+  // chunk's last two taps request the next chunk's first two
+  auto wload = [&](int ch, int tap, VecN<PL>(&a)[MBB]) {
+#pragma unroll
+    for (int m = 0; m < MBB; ++m) {
+      const int co = (mg * MBB + m) * 16 + col;  // channels >= COUT read zeros
+      buf_load(a[m], wb, (co < COUT ? co * CIN + kgrp * PL : Buf::kOOB / 4) * 4, (tap * COUT * CIN + ch * CK) * 4);
+    }
+  };
+  VecN<PL> aw[3][MBB];
+  // one tap: B fragments from the LDS tile, NBW x MBB x PL MFMAs
+  auto tap_mfma = [&](int kd, int kh, int kw, const VecN<PL>* a) {
+    VecN<PL> b[NBW];
+#pragma unroll
+    for (int r = 0; r < NBW; ++r) {
+      const int rr = wv * NBW + r;
+      const int odl = rr / TH, ohl = rr - odl * TH;
+      const int lvox = ((odl * S + kd) * LH + ohl * S + kh) * LW + col * S + kw;
+      const int qs = SWZ ? (kgrp ^ ((lvox >> 1) & 3)) : kgrp;
+      b[r].load(tile + lvox * VST + qs * PL);
+    }
+#pragma unroll
+    for (int j = 0; j < PL; ++j)
+#pragma unroll
+      for (int r = 0; r < NBW; ++r)
+#pragma unroll
+        for (int m = 0; m < MBB; ++m)
+          acc[r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b[r].v[j], acc[r][m], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);  // keep the 2-tap-ahead schedule (and the VGPR budget)
+  };
+  // The next chunk's tile is requested right after the chunk's last weight load (3 taps before
+  // its end), not ahead of the chunk's first: vmcnt retires loads in issue order, so any weight
+  // load issued behind the tile loads waits for them (fetching at the chunk's start measured the
+  // same, r17a).
   fetch(0);
   commit();
   __syncthreads();
-#pragma unroll 1
-  for (int ch = 0; ch < NCH; ++ch) {
-    if (ch + 1 < NCH) fetch(ch + 1);  // lands during this chunk's MFMAs
-    // A fragments from global/L2, requested two taps ahead of their MFMAs
-    auto wload = [&](int tap, VecN<PL>(&a)[MBB]) {
-#pragma unroll
-      for (int m = 0; m < MBB; ++m) {
-        const int co = (mg * MBB + m) * 16 + col;
-        if (co < COUT)
-          a[m].load(wpk + ((size_t)tap * COUT + co) * CIN + ch * CK + kgrp * PL);
-        else
-          a[m].zero();
-      }
-    };
-    VecN<PL> aw[3][MBB];
-    // one tap: B fragments from the LDS tile, NBW x MBB x PL MFMAs
-    auto tap_mfma = [&](int kd, int kh, int kw, const VecN<PL>* a) {
-      VecN<PL> b[NBW];
-#pragma unroll
-      for (int r = 0; r < NBW; ++r) {
-        const int rr = wv * NBW + r;
-        const int odl = rr / TH, ohl = rr - odl * TH;
-        const int lvox = ((odl * S + kd) * LH + ohl * S + kh) * LW + col * S + kw;
-        const int qs = SWZ ? (kgrp ^ ((lvox >> 1) & 3)) : kgrp;
-        b[r].load(tile + lvox * VST + qs * PL);
-      }
-#pragma unroll
-      for (int j = 0; j < PL; ++j)
-#pragma unroll
-        for (int r = 0; r < NBW; ++r)
-#pragma unroll
-          for (int m = 0; m < MBB; ++m)
-            acc[r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b[r].v[j], acc[r][m], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);  // keep the 2-tap-ahead schedule (and the VGPR budget)
-    };
+  if constexpr (KDSKIP) {
+    if (kd_lo <= kd_hi) {
+      wload(0, kd_lo * 9, aw[0]);
+      wload(0, kd_lo * 9 + 1, aw[1]);
+    }
+  } else {
+    wload(0, 0, aw[0]);
+    wload(0, 1, aw[1]);
+  }
+  // one channel chunk; MORE (compile time, so no branch splits the load stream and the vmcnt
+  // waits stay exact): the next chunk's first weights and tile are requested at its end
+  auto chunk = [&](int ch, auto more_c) {
+    constexpr bool MORE = decltype(more_c)::value;
+    if (MORE && KDSKIP && kd_lo > kd_hi) fetch(ch + 1);  // a wave with no slices still stages its share
     if constexpr (KDSKIP) {
-      if (kd_lo <= kd_hi) {
-        wload(kd_lo * 9, aw[0]);
-        wload(kd_lo * 9 + 1, aw[1]);
-      }
 #pragma unroll 1
       for (int kd = kd_lo; kd <= kd_hi; ++kd)
 #pragma unroll
         for (int k9 = 0; k9 < 9; ++k9) {
-          if (k9 + 2 < 9 || kd < kd_hi) wload(kd * 9 + k9 + 2, aw[(k9 + 2) % 3]);
+          if (k9 + 2 < 9) {
+            wload(ch, kd * 9 + k9 + 2, aw[(k9 + 2) % 3]);
+          } else {  // uniform branch: the next slice's first taps, or the next chunk's
+            if (kd < kd_hi)
+              wload(ch, kd * 9 + k9 + 2, aw[(k9 + 2) % 3]);
+            else if (MORE)
+              wload(ch + 1, kd_lo * 9 + k9 - 7, aw[(k9 + 2) % 3]);
+          }
+          if (MORE && k9 == 6 && kd == kd_hi) fetch(ch + 1);
           tap_mfma(kd, k9 / 3, k9 % 3, aw[k9 % 3]);
         }
     } else {
-    wload(0, aw[0]);
-    wload(1, aw[1]);
 #pragma unroll
-    for (int tap = 0; tap < 27; ++tap) {
-      const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
-      if (tap + 2 < 27) wload(tap + 2, aw[(tap + 2) % 3]);
-      const VecN<PL>* a = aw[tap % 3];
-      VecN<PL> b[NBW];
-#pragma unroll
-      for (int r = 0; r < NBW; ++r) {
-        const int rr = wv * NBW + r;
-        const int odl = rr / TH, ohl = rr - odl * TH;
-        const int lvox = ((odl * S + kd) * LH + ohl * S + kh) * LW + col * S + kw;
-        const int qs = SWZ ? (kgrp ^ ((lvox >> 1) & 3)) : kgrp;
-        b[r].load(tile + lvox * VST + qs * PL);
+      for (int tap = 0; tap < 27; ++tap) {
+        if (tap + 2 < 27)
+          wload(ch, tap + 2, aw[(tap + 2) % 3]);
+        else if (MORE)
+          wload(ch + 1, tap - 25, aw[(tap + 2) % 3]);
+        if (MORE && tap == 24) fetch(ch + 1);
+        tap_mfma(tap / 9, (tap / 3) % 3, tap % 3, aw[tap % 3]);
       }
-#pragma unroll
-      for (int j = 0; j < PL; ++j)
-#pragma unroll
-        for (int r = 0; r < NBW; ++r)
-#pragma unroll
-          for (int m = 0; m < MBB; ++m)
-            acc[r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b[r].v[j], acc[r][m], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);  // keep the 2-tap-ahead schedule (and the VGPR budget)
     }
-    }
-    if (ch + 1 < NCH) {
+    if (MORE) {
       __syncthreads();
       commit();
       __syncthreads();
     }
-  }
+  };
+#pragma unroll 1
+  for (int ch = 0; ch + 1 < NCH; ++ch) chunk(ch, std::true_type{});
+  chunk(NCH - 1, std::false_type{});
   const int ow = ow0 + col;
   if (ow >= g.Wo) return;
   const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
@@ -256,6 +295,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
 
 // ---------------------------------------------------------------- conv3d, direct (no LDS)
 // Used for the stride-2 layers: no LDS footprint, high occupancy hides the per-tap L1/L2 latency.
+// (Branch-free buffer loads with a one-step-ahead register prefetch measured the same, r17a.)
 template <int CIN, int COUT, int S, int NBW, int MBW>
 __global__ __launch_bounds__(256) void conv3d_direct_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                           const float* __restrict__ alpha,
@@ -1482,6 +1522,8 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
     g.Ho = (h - 1) / 2 + 1;
     g.Wo = (w - 1) / 2 + 1;
   }
+  // the MFMA kernels address one sample's input through a buffer with 32-bit byte offsets
+  if ((long long)d * h * w * cin * 4 >= (1LL << 31)) return TMVS_ERR_SHAPE;
   // stride 1: LDS-staged tiles, one output depth slice x 8 rows x 16 columns per workgroup
 #define TMVS_CONV_LDS(CI, CO, TD, TH, MBB)                                                      \
   if (cin == CI && cout == CO && stride == 1) {                                               \

@@ -289,7 +289,9 @@ __global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __rest
   __shared__ float red[4][kKV];
   __shared__ __attribute__((aligned(16))) float frag[2 * 32 * 32];  // Wk, Wv fragments (see stage_afrag)
   const int v = blockIdx.y;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // wave index wave-uniform (readfirstlane): the tile loop is then scalar control flow, not a divergent
+  // loop whose per-lane exits make the compiler wait vmcnt(0) (stores included) at its head
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
   stage_afrag<32, 32, true>(w + TMVS_ENC_WK, frag);
   stage_afrag<32, 32, true>(w + TMVS_ENC_WV, frag + 1024);
@@ -312,28 +314,26 @@ __global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __rest
   __syncthreads();
   const float* sv = src + (size_t)v * S * kD;
   const int tile0 = (blockIdx.x * 4 + wv) * tpw;
-  floatx4 xnext[2];  // the next tile's tokens, loaded while this tile computes
+  floatx4 xa[2], xb[2];  // this tile's tokens, the next tile's (loaded while this one computes)
   if (tile0 * 16 < S) {
     const int t = tile0 * 16 + (lane & 15);
-    load_token_frag(sv + (size_t)(t < S ? t : S - 1) * kD, xnext, lane);
+    load_token_frag(sv + (size_t)(t < S ? t : S - 1) * kD, xa, lane);
   }
-#pragma unroll 1
-  for (int it = 0; it < tpw; ++it) {
-    if ((tile0 + it) * 16 >= S) break;  // wave-uniform
+  auto tile = [&](int it, floatx4 (&cur)[2], floatx4 (&nxt)[2]) {
     int salt = 0;  // opaque offset: fragment reads stay in the loop (not hoisted back into VGPRs)
-    asm volatile("" : "+v"(salt));
+    asm volatile("" : "+s"(salt));  // an SGPR: a VGPR here could alias a pending load (vmcnt wait)
     const float* fr = frag + salt;
     bool okp[1];
     floatx4 xin[1][2], kk[1][2], vv[1][2];
     {
       const int t = (tile0 + it) * 16 + (lane & 15);
       okp[0] = t < S;
-      xin[0][0] = xnext[0];
-      xin[0][1] = xnext[1];
-      if (it + 1 < tpw && (tile0 + it + 1) * 16 < S) {
-        const int tn = t + 16;
-        load_token_frag(sv + (size_t)(tn < S ? tn : S - 1) * kD, xnext, lane);
-      }
+      xin[0][0] = cur[0];
+      xin[0][1] = cur[1];
+      // unconditional (clamped row; past the wave's range the value is never used): a branch here
+      // made the compiler wait vmcnt(0) for this prefetch before the tile's first MFMA
+      const int tn = t + 16;
+      load_token_frag(sv + (size_t)(tn < S ? tn : S - 1) * kD, nxt, lane);
     }
     mfma_linear_lds<32, 32, 1>(fr, xin, kk, lane);
     mfma_linear_lds<32, 32, 1>(fr + 1024, xin, vv, lane);
@@ -355,6 +355,14 @@ __global__ __launch_bounds__(256) void fmt_kv_partial_kernel(const float* __rest
 #pragma unroll
       for (int d = 0; d < 4; ++d) ks[mb][d] += kh[d];
     }
+  };
+  // (unrolled by two like the apply it needed 144 VGPRs, 3 waves/SIMD: one buffer, copied per tile)
+#pragma unroll 1
+  for (int it = 0; it < tpw; ++it) {
+    if ((tile0 + it) * 16 >= S) break;  // wave-uniform
+    tile(it, xa, xb);
+    xa[0] = xb[0];
+    xa[1] = xb[1];
   }
   // sum over the 16 token lanes of each lane group (fixed butterfly)
 #pragma unroll
@@ -419,7 +427,9 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
   constexpr int kVB2 = 128, kVLN = 160;
   __shared__ __attribute__((aligned(16))) float vec[288];
   const int v = blockIdx.y;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // wave index wave-uniform (readfirstlane): the tile loop is then scalar control flow, not a divergent
+  // loop whose per-lane exits make the compiler wait vmcnt(0) (stores included) at its head
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
   if (threadIdx.x < kKV) kvs[threadIdx.x] = kvg[(size_t)v * kv_stride + threadIdx.x];
   for (int i = threadIdx.x; i < 288; i += blockDim.x)
@@ -434,17 +444,17 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
   float* xv = x + (size_t)v * L * kD;
   const int tile0 = (blockIdx.x * 4 + wv) * tpw;
   constexpr int NT = kApplyNT;
-  floatx4 xnext[NT][2];  // the next group's tokens, loaded while this group computes
+  // two token buffers used alternately (the loop unrolled by two, so they swap by name: a
+  // loop-carried copy made the compiler wait vmcnt(0) -- this tile's stores included -- at the latch)
+  floatx4 xa[NT][2], xb[NT][2];
 #pragma unroll
   for (int p = 0; p < NT; ++p) {
     const int t = (tile0 + p) * 16 + (lane & 15);
-    if (p < tpw) load_token_frag(xv + (size_t)(t < L ? t : L - 1) * kD, xnext[p], lane);
+    if (p < tpw) load_token_frag(xv + (size_t)(t < L ? t : L - 1) * kD, xa[p], lane);
   }
-#pragma unroll 1
-  for (int it = 0; it < tpw; it += NT) {
-    if ((tile0 + it) * 16 >= L) break;  // wave-uniform
+  auto tile = [&](int it, floatx4 (&cur)[NT][2], floatx4 (&nxt)[NT][2]) {
     int salt = 0;  // opaque offset: fragment reads stay in the loop (not hoisted back into VGPRs)
-    asm volatile("" : "+v"(salt));
+    asm volatile("" : "+s"(salt));  // an SGPR: a VGPR here could alias a pending load (vmcnt wait)
     const float* fr = frag + salt;
     const float* vb = vec + salt;
     float* row[NT];
@@ -455,10 +465,12 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
       const int t = (tile0 + it + p) * 16 + (lane & 15);
       ok[p] = t < L && it + p < tpw;
       row[p] = xv + (size_t)(t < L ? t : L - 1) * kD;
-      xs[p][0] = xnext[p][0];
-      xs[p][1] = xnext[p][1];
+      xs[p][0] = cur[p][0];
+      xs[p][1] = cur[p][1];
       const int tn = t + 16 * NT;
-      if (it + NT + p < tpw) load_token_frag(xv + (size_t)(tn < L ? tn : L - 1) * kD, xnext[p], lane);
+      // unconditional (clamped row; a prefetch past the wave's range is never used): a branch here made
+      // the compiler wait vmcnt(0) for this prefetch before the tile's first MFMA
+      load_token_frag(xv + (size_t)(tn < L ? tn : L - 1) * kD, nxt[p], lane);
     }
     floatx4 q[NT][2], msg[NT][2];
     mfma_linear_lds<32, 32, NT>(fr, xs, q, lane);
@@ -535,6 +547,13 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
               make_float4(xs[p][mb][0], xs[p][mb][1], xs[p][mb][2], xs[p][mb][3]);
       }
     }
+  };
+#pragma unroll 1
+  for (int it = 0; it < tpw; it += 2 * NT) {
+    if ((tile0 + it) * 16 >= L) break;  // wave-uniform
+    tile(it, xa, xb);
+    if (it + NT >= tpw || (tile0 + it + NT) * 16 >= L) break;
+    tile(it + NT, xb, xa);
   }
 }
 
