@@ -97,7 +97,16 @@ __device__ __forceinline__ float act(float v, float lo) { return v > lo ? v : lo
 // its NBW = TD*TH/4 rows through the 27 taps: A (weights) from global/L2, requested two taps
 // ahead, B from LDS. The next chunk's tile is fetched into registers during the current
 // chunk's MFMAs.
-template <int CIN, int COUT, int S, int TD, int TH, int MBB, bool KDSKIP = false>
+#ifndef TMVS_LDS_BPF
+#define TMVS_LDS_BPF 1
+#endif
+#ifndef TMVS_LDS_ABL
+#define TMVS_LDS_ABL 0  // timing ablations (scripts/gpu/r17f.sh): 1 no weight loads, 2 no next-chunk fetch,
+#endif                  // 4 no chunk barriers / commit, 8 no MFMAs -- wrong results, never the product
+#ifndef TMVS_LDS_SGB
+#define TMVS_LDS_SGB 1
+#endif
+template <int CIN, int COUT, int S, int TD, int TH, int MBB, int WS = 1, bool KDSKIP = false>
 #ifndef TMVS_LDS_WPE
 #define TMVS_LDS_WPE 3
 #endif
@@ -109,14 +118,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
   constexpr int PL = CK / 4;
   constexpr int MB = (COUT + 15) / 16;
   constexpr int MG = MB / MBB;
-  constexpr int NBW = TD * TH / 4;
+  // WS: the 4 waves are WS block groups x 4/WS row groups; a wave runs NBW rows x MBW blocks (WS = 1:
+  // every wave all MBB blocks of TD*TH/4 rows -- the 4 waves then request identical weight fragments)
+  static_assert(WS == 1 || WS == 2 || WS == 4, "WS");
+  static_assert(MBB % WS == 0 && (TD * TH * WS) % 4 == 0, "wave split");
+  constexpr int NBW = TD * TH * WS / 4, MBW = MBB / WS;
   constexpr int LW = 15 * S + 3, LH = (TH - 1) * S + 3, LD = (TD - 1) * S + 3;
   // voxel stride / quad swizzle chosen so the 4 lane groups of every ds_read_b128 are
   // bank-conflict free (exhaustive search over the gfx950 b128 lane grouping)
   constexpr bool SWZ = (CK == 16);  // (stride 2 included: conv3's instance)
   constexpr int VST = SWZ ? 16 : CK + 4;
   constexpr int NVOX = LD * LH * LW;
-  static_assert(MB % MBB == 0 && (TD * TH) % 4 == 0, "tile");
+  static_assert(MB % MBB == 0, "tile");
   __shared__ __attribute__((aligned(16))) float tile[NVOX * VST];
 
   const int nws = (g.Wo + 15) / 16, nhs = (g.Ho + TH - 1) / TH, nds = (g.Do + TD - 1) / TD;
@@ -133,13 +146,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
   const int iw0 = ow0 * S - 1, ih0 = oh0 * S - 1, id0 = od0 * S - 1;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int col = lane & 15, kgrp = lane >> 4;
+  const int rg = __builtin_amdgcn_readfirstlane(wv / WS), bg = __builtin_amdgcn_readfirstlane(wv % WS);
+  const int mb0 = mg * MBB + bg * MBW;  // the wave's first 16-channel output block
   const size_t in_n = (size_t)n * g.Di * g.Hi * g.Wi;
 
-  floatx4 acc[NBW][MBB];
+  floatx4 acc[NBW][MBW];
 #pragma unroll
   for (int r = 0; r < NBW; ++r)
 #pragma unroll
-    for (int m = 0; m < MBB; ++m) acc[r][m] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m < MBW; ++m) acc[r][m] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // channel chunk ch's tile: global -> registers (issued one chunk ahead) -> LDS
   constexpr int NCH = CIN / CK, NLD = (NVOX * PL + 255) / 256;
@@ -176,7 +191,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
   static_assert(!KDSKIP || TH % NBW == 0, "KDSKIP needs one output slice per wave");
   int kd_lo = 0, kd_hi = 2;
   if constexpr (KDSKIP) {
-    const int od = od0 + (__builtin_amdgcn_readfirstlane(wv) * NBW) / TH;
+    const int od = od0 + (rg * NBW) / TH;
     const int id_base = od * S - 1;  // input slice of kd = 0
     kd_lo = id_base < 0 ? -id_base : 0;
     kd_hi = g.Di - 1 - id_base < 2 ? g.Di - 1 - id_base : 2;
@@ -184,34 +199,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
   }
   // A fragments (chunk ch, tap) from global/L2, requested two taps ahead of their MFMAs; the
   // chunk's last two taps request the next chunk's first two
-  auto wload = [&](int ch, int tap, VecN<PL>(&a)[MBB]) {
+  auto wload = [&](int ch, int tap, VecN<PL>(&a)[MBW]) {
 #pragma unroll
-    for (int m = 0; m < MBB; ++m) {
-      const int co = (mg * MBB + m) * 16 + col;  // channels >= COUT read zeros
+    for (int m = 0; m < MBW; ++m) {
+      const int co = (mb0 + m) * 16 + col;  // channels >= COUT read zeros
+      if (TMVS_LDS_ABL & 1) {  // timing ablation only: no weight loads
+#pragma unroll
+        for (int i = 0; i < PL; ++i) a[m].v[i] = (float)(tap * PL + i + ch) * 1e-3f;
+        continue;
+      }
       buf_load(a[m], wb, (co < COUT ? co * CIN + kgrp * PL : Buf::kOOB / 4) * 4, (tap * COUT * CIN + ch * CK) * 4);
     }
   };
-  VecN<PL> aw[3][MBB];
+  VecN<PL> aw[3][MBW];
   // one tap: B fragments from the LDS tile, NBW x MBB x PL MFMAs
-  auto tap_mfma = [&](int kd, int kh, int kw, const VecN<PL>* a) {
-    VecN<PL> b[NBW];
+  // B fragments of one tap from the LDS tile
+  auto bload = [&](int kd, int kh, int kw, VecN<PL>(&b)[NBW]) {
 #pragma unroll
     for (int r = 0; r < NBW; ++r) {
-      const int rr = wv * NBW + r;
+      const int rr = rg * NBW + r;
       const int odl = rr / TH, ohl = rr - odl * TH;
       const int lvox = ((odl * S + kd) * LH + ohl * S + kh) * LW + col * S + kw;
       const int qs = SWZ ? (kgrp ^ ((lvox >> 1) & 3)) : kgrp;
       b[r].load(tile + lvox * VST + qs * PL);
+    }
+  };
+  // one tap: NBW x MBB x PL MFMAs on fragments already in registers
+  auto tap_mfma = [&](const VecN<PL>* a, const VecN<PL>* b) {
+    if (TMVS_LDS_ABL & 8) {  // timing ablation only: no MFMAs (one FMA keeps the loads live)
+#pragma unroll
+      for (int r = 0; r < NBW; ++r)
+#pragma unroll
+        for (int m = 0; m < MBW; ++m) acc[r][m][0] = fmaf(a[m].v[0], b[r].v[0], acc[r][m][0]);
+      return;
     }
 #pragma unroll
     for (int j = 0; j < PL; ++j)
 #pragma unroll
       for (int r = 0; r < NBW; ++r)
 #pragma unroll
-        for (int m = 0; m < MBB; ++m)
+        for (int m = 0; m < MBW; ++m)
           acc[r][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b[r].v[j], acc[r][m], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);  // keep the 2-tap-ahead schedule (and the VGPR budget)
+    // one-MFMA schedule groups keep the accumulators' chains interleaved as written (the scheduler
+    // otherwise issued each accumulator's PL dependent MFMAs back to back: 40-cycle dependent issue
+    // against 32 for an independent one)
+    if constexpr (TMVS_LDS_SGB)
+#pragma unroll
+      for (int i = 0; i < PL * NBW * MBW; ++i) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_barrier(0);  // keep the lookahead schedule (and the VGPR budget)
   };
+  // B of tap t + 1 is read from LDS before tap t's MFMAs (TMVS_LDS_BPF; read right before its own
+  // MFMAs its latency sat between every tap's MFMA groups)
+  VecN<PL> bw[2][NBW];
   // The next chunk's tile is requested right after the chunk's last weight load (3 taps before
   // its end), not ahead of the chunk's first: vmcnt retires loads in issue order, so any weight
   // load issued behind the tile loads waits for them (fetching at the chunk's start measured the
@@ -246,8 +285,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
             else if (MORE)
               wload(ch + 1, kd_lo * 9 + k9 - 7, aw[(k9 + 2) % 3]);
           }
-          if (MORE && k9 == 6 && kd == kd_hi) fetch(ch + 1);
-          tap_mfma(kd, k9 / 3, k9 % 3, aw[k9 % 3]);
+          if (MORE && !(TMVS_LDS_ABL & 2) && k9 == 6 && kd == kd_hi) fetch(ch + 1);
+          // B prefetch within the slice (9 taps: the parity would flip across the rolled kd loop)
+          if (!TMVS_LDS_BPF || k9 == 0) bload(kd, k9 / 3, k9 % 3, bw[k9 & 1]);
+          if (TMVS_LDS_BPF && k9 + 1 < 9) bload(kd, (k9 + 1) / 3, (k9 + 1) % 3, bw[(k9 + 1) & 1]);
+          tap_mfma(aw[k9 % 3], bw[k9 & 1]);
         }
     } else {
 #pragma unroll
@@ -256,11 +298,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
           wload(ch, tap + 2, aw[(tap + 2) % 3]);
         else if (MORE)
           wload(ch + 1, tap - 25, aw[(tap + 2) % 3]);
-        if (MORE && tap == 24) fetch(ch + 1);
-        tap_mfma(tap / 9, (tap / 3) % 3, tap % 3, aw[tap % 3]);
+        if (MORE && !(TMVS_LDS_ABL & 2) && tap == 24) fetch(ch + 1);
+        if (!TMVS_LDS_BPF || tap == 0) bload(tap / 9, (tap / 3) % 3, tap % 3, bw[tap & 1]);
+        if (TMVS_LDS_BPF && tap + 1 < 27) bload((tap + 1) / 9, ((tap + 1) / 3) % 3, (tap + 1) % 3, bw[(tap + 1) & 1]);
+        tap_mfma(aw[tap % 3], bw[tap & 1]);
       }
     }
-    if (MORE) {
+    if (MORE && !(TMVS_LDS_ABL & 4)) {
       __syncthreads();
       commit();
       __syncthreads();
@@ -273,14 +317,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
   if (ow >= g.Wo) return;
   const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
 #pragma unroll
-  for (int m = 0; m < MBB; ++m) {
-    const int co = (mg * MBB + m) * 16 + kgrp * 4;
+  for (int m = 0; m < MBW; ++m) {
+    const int co = (mb0 + m) * 16 + kgrp * 4;
     if (co >= COUT) continue;
     const float4 al = *reinterpret_cast<const float4*>(alpha + co);
     const float4 sh = *reinterpret_cast<const float4*>(shift + co);
 #pragma unroll
     for (int r = 0; r < NBW; ++r) {
-      const int rr = wv * NBW + r;
+      const int rr = rg * NBW + r;
       const int od = od0 + rr / TH, oh = oh0 + rr % TH;
       if (od >= g.Do || oh >= g.Ho) continue;
       float4 o;
@@ -1276,18 +1320,18 @@ static int launch_conv_s2c8_tile(const float* x, const float* w, const float* al
 #ifndef TMVS_KDSKIP_MAX_DO
 #define TMVS_KDSKIP_MAX_DO 2
 #endif
-template <int CIN, int COUT, int S, int TD, int TH, int MBB>
+template <int CIN, int COUT, int S, int TD, int TH, int MBB, int WS = 1>
 static int launch_conv(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
                        const Geo& g, hipStream_t st) {
   constexpr int MG = ((COUT + 15) / 16) / MBB;
   const long nblk = (long)B * ((g.Do + TD - 1) / TD) * ((g.Ho + TH - 1) / TH) * ((g.Wo + 15) / 16) * MG;
   // output depth <= 2 (the coarse levels of a D = 8 stage): every wave has a depth-padding kd slice
   if (g.Do <= TMVS_KDSKIP_MAX_DO)
-    hipLaunchKernelGGL((conv3d_lds_kernel<CIN, COUT, S, TD, TH, MBB, true>), dim3((unsigned)nblk), dim3(256), 0, st, x,
-                       w, al, sh, y, g);
+    hipLaunchKernelGGL((conv3d_lds_kernel<CIN, COUT, S, TD, TH, MBB, WS, true>), dim3((unsigned)nblk), dim3(256), 0, st,
+                       x, w, al, sh, y, g);
   else
-    hipLaunchKernelGGL((conv3d_lds_kernel<CIN, COUT, S, TD, TH, MBB>), dim3((unsigned)nblk), dim3(256), 0, st, x, w, al,
-                       sh, y, g);
+    hipLaunchKernelGGL((conv3d_lds_kernel<CIN, COUT, S, TD, TH, MBB, WS>), dim3((unsigned)nblk), dim3(256), 0, st, x, w,
+                       al, sh, y, g);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -1525,9 +1569,9 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
   // the MFMA kernels address one sample's input through a buffer with 32-bit byte offsets
   if ((long long)d * h * w * cin * 4 >= (1LL << 31)) return TMVS_ERR_SHAPE;
   // stride 1: LDS-staged tiles, one output depth slice x 8 rows x 16 columns per workgroup
-#define TMVS_CONV_LDS(CI, CO, TD, TH, MBB)                                                      \
+#define TMVS_CONV_LDS(CI, CO, ...)                                                              \
   if (cin == CI && cout == CO && stride == 1) {                                               \
-    return launch_conv<CI, CO, 1, TD, TH, MBB>(x, wpk, al, sh, y, B, g, st);                 \
+    return launch_conv<CI, CO, 1, __VA_ARGS__>(x, wpk, al, sh, y, B, g, st);                 \
   }
 #ifndef TMVS_C16_TD
 #define TMVS_C16_TD 2
@@ -1535,8 +1579,20 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
 #endif
   if (cin == 16 && cout == 16 && stride == 1)
     return launch_conv_c16<TMVS_C16_TD, TMVS_C16_TH>(x, wpk, al, sh, y, B, g, st);
-  TMVS_CONV_LDS(32, 32, 2, 4, 2)
-  TMVS_CONV_LDS(64, 64, 1, 4, 2)
+#ifndef TMVS_C4_CFG
+#define TMVS_C4_CFG 2, 2, 2, 2     // (TD, TH, MBB, WS) of conv4 (32 -> 32); output depth > 2 (r17h)
+#define TMVS_C4_CFG_KD 2, 4, 2, 1  // output depth <= 2 (the depth-padding-skipping instance)
+#endif
+  if (cin == 32 && cout == 32 && stride == 1 && g.Do <= TMVS_KDSKIP_MAX_DO)
+    return launch_conv<32, 32, 1, TMVS_C4_CFG_KD>(x, wpk, al, sh, y, B, g, st);
+#ifndef TMVS_C6_CFG
+#define TMVS_C6_CFG 1, 2, 4, 4  // and of conv6 (64 -> 64): each wave one output block (r17g)
+#endif
+#ifndef TMVS_C3_CFG
+#define TMVS_C3_CFG 1, 4, 2, 1  // and of conv3 (16 -> 32, stride 2)
+#endif
+  TMVS_CONV_LDS(32, 32, TMVS_C4_CFG)
+  TMVS_CONV_LDS(64, 64, TMVS_C6_CFG)
 #undef TMVS_CONV_LDS
   // stride 2, 8 -> 16 (full-resolution input): tap pairs, 16-byte loads
 #ifndef TMVS_S2C8_TD
@@ -1554,7 +1610,7 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
   // pattern half-fills every cache line it touches); same accumulation order as the direct kernel.
   // 63.8 -> 54.2 us per stage-2/3 call (r12k). conv5 (32 -> 64, two chunks) stays direct: the LDS
   // kernel's chunk-outer order changes its sums, and it measured no faster (58.0 vs 56.9 us).
-  if (cin == 16 && cout == 32 && stride == 2) return launch_conv<16, 32, 2, 1, 4, 2>(x, wpk, al, sh, y, B, g, st);
+  if (cin == 16 && cout == 32 && stride == 2) return launch_conv<16, 32, 2, TMVS_C3_CFG>(x, wpk, al, sh, y, B, g, st);
 #endif
   // stride 2: direct
 #define TMVS_CONV_DIRECT(CI, CO, NBW, MBW) \
@@ -1565,8 +1621,11 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
   // often) on the stage-2/3 grids (15.5 K output voxels): 58.1 -> 51.4 / 29.8 -> 27.0 us; the
   // stage-1 grid (5.8 K voxels) is faster at 2 x 1 (26.6 vs 35.3 us). 1 x 1 and 4 x 1 measured slower
   // (r12r, r12s). Both tilings keep every output's accumulation order.
+#ifndef TMVS_C5_CFG
+#define TMVS_C5_CFG 2, 2  // (NBW, MBW) of conv5 on the stage-2/3 grids
+#endif
   if (cin == 32 && cout == 64 && stride == 2 && (long)g.Do * g.Ho * g.Wo >= 8192)
-    return launch_conv_direct<32, 64, 2, 2, 2>(x, wpk, al, sh, y, B, g, st);
+    return launch_conv_direct<32, 64, 2, TMVS_C5_CFG>(x, wpk, al, sh, y, B, g, st);
   TMVS_CONV_DIRECT(32, 64, 2, 1)
 #undef TMVS_CONV_DIRECT
   return TMVS_ERR_SHAPE;
@@ -1582,10 +1641,14 @@ static int deconv_dispatch(const float* x, int B, int cin, int d, int h, int w, 
   g.Do = 2 * d;
   g.Ho = 2 * h;
   g.Wo = 2 * w;
-#define TMVS_DECONV_CASE(CI, CO, MBB)                                                              \
-  if (cin == CI && cout == CO) {                                                                  \
-    if (g.Di % 2 == 0) return launch_deconv<CI, CO, 2, 2, MBB>(x, wpk, al, sh, skip, y, B, g, st); \
-    return launch_deconv<CI, CO, 1, 4, MBB>(x, wpk, al, sh, skip, y, B, g, st);                  \
+#ifndef TMVS_DECONV_EVEN
+#define TMVS_DECONV_EVEN 2, 2  // (TDI, THI) input tile for an even input depth
+#define TMVS_DECONV_ODD 1, 4   // and for an odd one
+#endif
+#define TMVS_DECONV_CASE(CI, CO, MBB)                                                                       \
+  if (cin == CI && cout == CO) {                                                                           \
+    if (g.Di % 2 == 0) return launch_deconv<CI, CO, TMVS_DECONV_EVEN, MBB>(x, wpk, al, sh, skip, y, B, g, st); \
+    return launch_deconv<CI, CO, TMVS_DECONV_ODD, MBB>(x, wpk, al, sh, skip, y, B, g, st);                  \
   }
   TMVS_DECONV_CASE(64, 32, 1)
   TMVS_DECONV_CASE(32, 16, 1)
