@@ -1608,8 +1608,8 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
   // conv3 (16 -> 32, stride 2, one 16-channel chunk): the LDS-staged kernel -- each input voxel is
   // fetched once per tile instead of once per tap that reads it (the direct form's stride-2 lane
   // pattern half-fills every cache line it touches); same accumulation order as the direct kernel.
-  // 63.8 -> 54.2 us per stage-2/3 call (r12k). conv5 (32 -> 64, two chunks) stays direct: the LDS
-  // kernel's chunk-outer order changes its sums, and it measured no faster (58.0 vs 56.9 us).
+  // 63.8 -> 54.2 us per stage-2/3 call (r12k). (conv5 through the LDS kernel measured no faster
+  // before the wave split, 58.0 vs 56.9 us, r12k; with it, below, it is.)
   if (cin == 16 && cout == 32 && stride == 2) return launch_conv<16, 32, 2, TMVS_C3_CFG>(x, wpk, al, sh, y, B, g, st);
 #endif
   // stride 2: direct
@@ -1617,16 +1617,14 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
   if (cin == CI && cout == CO && stride == 2) return launch_conv_direct<CI, CO, 2, NBW, MBW>(x, wpk, al, sh, y, B, g, st);
   TMVS_CONV_DIRECT(8, 16, 4, 1)
   TMVS_CONV_DIRECT(16, 32, 4, 1)
-  // conv5: 2 rows x 2 output blocks per wave (half the waves, each weight fragment used twice as
-  // often) on the stage-2/3 grids (15.5 K output voxels): 58.1 -> 51.4 / 29.8 -> 27.0 us; the
-  // stage-1 grid (5.8 K voxels) is faster at 2 x 1 (26.6 vs 35.3 us). 1 x 1 and 4 x 1 measured slower
-  // (r12r, r12s). Both tilings keep every output's accumulation order.
-#ifndef TMVS_C5_CFG
-#define TMVS_C5_CFG 2, 2  // (NBW, MBW) of conv5 on the stage-2/3 grids
+#ifndef TMVS_C5_LDS
+#define TMVS_C5_LDS 1, 2, 4, 4  // conv5 (32 -> 64, stride 2) through the LDS-tiled kernel, (TD, TH, MBB, WS)
 #endif
-  if (cin == 32 && cout == 64 && stride == 2 && (long)g.Do * g.Ho * g.Wo >= 8192)
-    return launch_conv_direct<32, 64, 2, TMVS_C5_CFG>(x, wpk, al, sh, y, B, g, st);
-  TMVS_CONV_DIRECT(32, 64, 2, 1)
+  // conv5 through the wave-split LDS kernel: 52.6 -> 30.4 / 24.0 -> 15.5 / 24.2 -> 19.1 us (stages 2 / 1 / 3)
+  // against the direct kernel's best tilings (2 rows x 2 blocks per wave on the stage-2/3 grids, 2 x 1 on
+  // stage 1; r12r, r12s, r17j); chunk-outer K order, so its sums differ from the direct form's in the
+  // last bits (3e-6)
+  if (cin == 32 && cout == 64 && stride == 2) return launch_conv<32, 64, 2, TMVS_C5_LDS>(x, wpk, al, sh, y, B, g, st);
 #undef TMVS_CONV_DIRECT
   return TMVS_ERR_SHAPE;
 }
