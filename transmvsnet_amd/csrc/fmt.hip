@@ -180,18 +180,23 @@ __device__ __forceinline__ void mfma_linear_lds(const float* __restrict__ fl, co
   for (int p = 0; p < NT; ++p)
 #pragma unroll
     for (int mb = 0; mb < OUT / 16; ++mb) acc[p][mb] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // per s4: every output block's fragment first, then the MFMAs block-interleaved (each accumulator's
+  // own order unchanged), so consecutive MFMAs feed different accumulators
 #pragma unroll
-  for (int s4 = 0; s4 < IN / 16; ++s4)
+  for (int s4 = 0; s4 < IN / 16; ++s4) {
+    float4 a4[OUT / 16];
 #pragma unroll
-    for (int mb = 0; mb < OUT / 16; ++mb) {
-      const float4 a4 = *reinterpret_cast<const float4*>(fl + ((mb * (IN / 16) + s4) * 64 + lane) * 4);
-      const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+    for (int mb = 0; mb < OUT / 16; ++mb)
+      a4[mb] = *reinterpret_cast<const float4*>(fl + ((mb * (IN / 16) + s4) * 64 + lane) * 4);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int mb = 0; mb < OUT / 16; ++mb)
 #pragma unroll
         for (int p = 0; p < NT; ++p)
-          acc[p][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], in[p][s4][j], acc[p][mb], 0, 0, 0);
-    }
+          acc[p][mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(j == 0 ? a4[mb].x : j == 1 ? a4[mb].y : j == 2 ? a4[mb].z : a4[mb].w,
+                                                            in[p][s4][j], acc[p][mb], 0, 0, 0);
+  }
 }
 
 // NT independent tiles interleaved: NT x OUT/16 independent accumulation chains in flight
