@@ -1581,6 +1581,8 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
     return launch_conv_c16<TMVS_C16_TD, TMVS_C16_TH>(x, wpk, al, sh, y, B, g, st);
 #ifndef TMVS_C4_CFG
 #define TMVS_C4_CFG 2, 2, 2, 2     // (TD, TH, MBB, WS) of conv4 (32 -> 32); output depth > 2 (r17h)
+#endif
+#ifndef TMVS_C4_CFG_KD
 #define TMVS_C4_CFG_KD 2, 4, 2, 1  // output depth <= 2 (the depth-padding-skipping instance)
 #endif
   if (cin == 32 && cout == 32 && stride == 1 && g.Do <= TMVS_KDSKIP_MAX_DO)
@@ -1589,7 +1591,7 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
 #define TMVS_C6_CFG 1, 2, 4, 4  // and of conv6 (64 -> 64): each wave one output block (r17g)
 #endif
 #ifndef TMVS_C3_CFG
-#define TMVS_C3_CFG 1, 4, 2, 1  // and of conv3 (16 -> 32, stride 2)
+#define TMVS_C3_CFG 2, 2, 2, 2  // and of conv3 (16 -> 32, stride 2): 50.4 -> 46.0 us at stage 3 (r17n)
 #endif
   TMVS_CONV_LDS(32, 32, TMVS_C4_CFG)
   TMVS_CONV_LDS(64, 64, TMVS_C6_CFG)
