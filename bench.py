@@ -646,8 +646,11 @@ def host_cores():
 def parity_report(gpu_out, ref, margin=1e-4):
     """Abs depth L1 vs the reference restatement, per stage, with every differing pixel
     classified: a near-tie has a top-2 log-prob margin < `margin` in the reference's prob volume
-    (SURVEY.md 8c); a flip elsewhere is a real mismatch."""
+    (SURVEY.md 8c); a cascaded pixel (stages 2/3) lies within 2 px of where the previous stage's
+    depth already differed (up-sampled x2), so its depth hypotheses differ from the reference's;
+    a flip elsewhere is a real mismatch."""
     rep = {}
+    prev = None
     for s in (1, 2, 3):
         g = gpu_out[f"stage{s}"]["depth"].float().cpu().numpy().astype(np.float64)
         r = ref[f"stage{s}"]["depth"].numpy().astype(np.float64)
@@ -655,9 +658,18 @@ def parity_report(gpu_out, ref, margin=1e-4):
         srt = np.sort(pr, axis=1)
         near = (np.log(np.maximum(srt[:, -1], 1e-30)) - np.log(np.maximum(srt[:, -2], 1e-30))) < margin
         diff = np.abs(g - r) > 1e-3
+        casc = np.zeros_like(diff)
+        if prev is not None and prev.any():  # the previous stage's differing pixels, x2 and dilated by 2 px
+            up = prev.repeat(2, axis=-2).repeat(2, axis=-1)[..., :diff.shape[-2], :diff.shape[-1]]
+            pad = np.pad(up, [(0, 0)] * (up.ndim - 2) + [(2, 2), (2, 2)])
+            for dy in range(5):
+                for dx in range(5):
+                    casc |= pad[..., dy:dy + diff.shape[-2], dx:dx + diff.shape[-1]]
         rep[f"stage{s}"] = {"mean_abs_mm": float(np.abs(g - r).mean()), "max_abs_mm": float(np.abs(g - r).max()),
                             "pixels_differing": int(diff.sum()), "near_tie_flips": int((diff & near).sum()),
-                            "other_flips": int((diff & ~near).sum())}
+                            "cascaded": int((diff & ~near & casc).sum()),
+                            "other_flips": int((diff & ~near & ~casc).sum())}
+        prev = diff
     d3 = rep["stage3"]
     return {"stage3_mean_abs_mm": d3["mean_abs_mm"], "stage3_max_abs_mm": d3["max_abs_mm"],
             "stage3_frac_pixels_differing": d3["pixels_differing"] / gpu_out["depth"].numel(),
