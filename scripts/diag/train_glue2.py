@@ -1,7 +1,7 @@
 """Which Python call sites issue torch's own device ops (copies, fills, index, elementwise) in one eager C5
 training step (bench._train_setup's full_step): a TorchDispatchMode records every aten op with the innermost
 transmvsnet_amd / bench frame of the Python stack (forward, loss and the custom Functions' backward).
-Ops that launch no device work (views, metadata) are skipped.
+Ops on host tensors and ops that launch no device work (views, metadata) are skipped.
 
     python scripts/diag/train_glue2.py [top]
 """
@@ -12,6 +12,7 @@ import traceback
 
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
 import torch  # noqa: E402
+import torch.utils._pytree  # noqa: E402,F401
 from torch.utils._python_dispatch import TorchDispatchMode  # noqa: E402
 
 import bench  # noqa: E402
@@ -28,7 +29,9 @@ class Rec(TorchDispatchMode):
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         name = str(func)
-        if not any(s in name for s in SKIP):
+        on_gpu = any(isinstance(a, torch.Tensor) and a.is_cuda
+                     for a in torch.utils._pytree.tree_flatten((args, kwargs or {}))[0])
+        if on_gpu and not any(s in name for s in SKIP):
             site = "?"
             for fr in reversed(traceback.extract_stack()[:-1]):
                 f = fr.filename

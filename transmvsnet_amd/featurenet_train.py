@@ -20,11 +20,14 @@ gradients tmvs_colsum, the FPN merges' nearest x2 adjoint tmvs_nearest_up2_backw
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
 from . import ops
 from .bn_running import update_running_stats
+from .packing import gather_packs
 
 BN_MOMENTUM = 0.1
 _PACK_INDEX = {}
@@ -95,6 +98,90 @@ def device_pack(kind, w):
     return flat[_pack_index(kind, co, ci, k, w.device)].contiguous()
 
 
+# ------------------------------------------------------------------------- the step's weight packs
+# Every weight re-layout a FeatureNet step needs (forward packs, data-gradient packs, tap transposes) is
+# gathered ONCE per forward by _prepare_packs (packing.gather_packs: one cat + one index gather instead of
+# ~130 small cat / index / flip / permute launches); the layer functions look their packs up here and
+# fall back to packing on the spot for a weight not in the table.
+_STEP_PACKS = {}
+
+
+def _pk(key):
+    return _STEP_PACKS.get(key)
+
+
+def _pack_fn(kind, co, ci, k):
+    return lambda t: torch.cat([t.reshape(-1), t.new_zeros(1)])[_pack_index(kind, co, ci, k, t.device)]
+
+
+def _dgrad_kind(co, ci, k):
+    """The data-gradient form dgrad_same takes for a stride-1 conv weight [co][ci][k][k]."""
+    if ci == 32 and co == 32 and k == 3:
+        return "dcn"
+    if (co, ci, k) in _MFMA_DGRAD:
+        return "conv2d"
+    return "taps_t"
+
+
+def _prepare_packs(fnet):
+    """Fill _STEP_PACKS with one gather_packs call for the whole FeatureNet (TMVS_NO_STEP_PACKS=1: leave it
+    empty -- every layer packs on the spot, the previous form; for bitwise A/Bs)."""
+    _STEP_PACKS.clear()
+    if os.environ.get("TMVS_NO_STEP_PACKS") == "1":
+        return
+    tensors, specs, keys = [], [], []
+
+    def add(t, fn, key):
+        tensors.append(t)
+        specs.append((len(tensors) - 1, fn))
+        keys.append(key)
+
+    def block(blk, k, stride, head3x3=False, need_dx=True):
+        w = blk.conv.weight
+        co, ci = w.shape[0], w.shape[1]
+        add(w, _pack_fn("dcn" if head3x3 else "conv2d", co, ci, k), ("fwd", id(w)))
+        if not need_dx:
+            return
+        kind = _dgrad_kind(co, ci, k) if stride == 1 else "taps_t"
+        if kind == "taps_t":
+            add(w, lambda t, k=k, co=co, ci=ci: t.permute(2, 3, 1, 0).reshape(k * k, ci, co), ("taps_t", id(w)))
+        else:
+            add(w, lambda t, kind=kind, k=k, co=co, ci=ci: _pack_fn(kind, ci, co, k)(t.flip(2, 3).transpose(0, 1)),
+                ("dgrad", id(w)))
+
+    def dcn(d):
+        com, w = d.conv_offset_mask, d.weight
+        cout = w.shape[0]
+        add(com.weight, _pack_fn("dcn", 27, 32, 3), ("fwd", id(com.weight)))
+        add(w, _pack_fn("dcn", cout, 32, 3), ("fwd", id(w)))
+        add(w, lambda t, cout=cout: t.reshape(cout, 32, 9).permute(2, 0, 1), ("wtaps", id(w)))
+        add(com.weight, lambda t: _pack_fn("dcn", 32, 32, 3)(torch.cat([t, t.new_zeros(5, 32, 3, 3)]).flip(2, 3)
+                                                                  .transpose(0, 1)), ("offdgrad", id(com.weight)))
+
+    block(fnet.conv0[0], 3, 1, need_dx=False)
+    block(fnet.conv0[1], 3, 1)
+    block(fnet.conv1[0], 5, 2)
+    block(fnet.conv1[1], 3, 1)
+    block(fnet.conv1[2], 3, 1)
+    block(fnet.conv2[0], 5, 2)
+    block(fnet.conv2[1], 3, 1)
+    block(fnet.conv2[2], 3, 1)
+    for seq, k in ((fnet.out1, 1), (fnet.out2, 3), (fnet.out3, 3)):
+        block(seq[0], k, 1, head3x3=k == 3)
+        dcn(seq[1])
+        dcn(seq[4])
+        dcn(seq[7])
+    for conv in (fnet.inner1, fnet.inner2):
+        w = conv.weight
+        co, ci = w.shape[0], w.shape[1]
+        add(w, lambda t, co=co, ci=ci: t.permute(2, 3, 1, 0).reshape(1, ci, co), ("taps_t", id(w)))
+    # a parameter appearing twice (forward and data-gradient packs) is passed twice: gather_packs keys
+    # its index on the tensors' shapes, and the specs name their own tensor
+    outs = gather_packs(tensors, specs, "featurenet_train")
+    for key, o in zip(keys, outs):
+        _STEP_PACKS[key] = o
+
+
 def _taps(w):
     """Conv2d weight [Co][Ci][k][k] -> [k*k][Co][Ci] (the forward gather)."""
     co, ci, k, _ = w.shape
@@ -140,20 +227,23 @@ def _block_fwd(tape, blk, x, k, stride, nchw_input=False, head3x3=False):
     """Conv2d (no bias) + BatchNorm (train) + ReLU (models/module.py:24-61) -> (y NHWC, record)."""
     w = blk.conv.weight
     cout = w.shape[0]
+    pw = _pk(("fwd", id(w)))
     if head3x3:
-        _, z = ops.conv3x3_nhwc(x, device_pack("dcn", w), bn=None, relu=False)
+        _, z = ops.conv3x3_nhwc(x, pw if pw is not None else device_pack("dcn", w), bn=None, relu=False)
     else:
-        z = ops.conv2d_bn_relu(x, device_pack("conv2d", w), cout, k, stride, bn=None, relu=False,
-                               nchw_input=nchw_input)
+        z = ops.conv2d_bn_relu(x, pw if pw is not None else device_pack("conv2d", w), cout, k, stride, bn=None,
+                               relu=False, nchw_input=nchw_input)
     y, per = _bn_relu_views(tape, z, blk.bn)
     return y, ("block", blk, x, z, per, k, stride, nchw_input)
 
 
 def _dcn_fwd(dcn, x, want_nchw=False):
     com = dcn.conv_offset_mask
-    u, om, out = ops.dcn_forward_train(x, device_pack("dcn", com.weight), com.bias.detach().float().contiguous(),
-                                       device_pack("dcn", dcn.weight), dcn.bias.detach().float().contiguous(),
-                                       dcn.cout, want_nchw=want_nchw)
+    pwo, pw = _pk(("fwd", id(com.weight))), _pk(("fwd", id(dcn.weight)))
+    u, om, out = ops.dcn_forward_train(x, pwo if pwo is not None else device_pack("dcn", com.weight),
+                                       com.bias.detach().float().contiguous(),
+                                       pw if pw is not None else device_pack("dcn", dcn.weight),
+                                       dcn.bias.detach().float().contiguous(), dcn.cout, want_nchw=want_nchw)
     return u, om, out
 
 
@@ -173,6 +263,29 @@ def _acc(grads, p, g):
     grads[id(p)] = g if id(p) not in grads else grads[id(p)] + g
 
 
+def _defer(grads, p, raw, fn):
+    """A weight gradient in a kernel's layout, re-laid out by fn at the end of the backward together with
+    all the others (one packing.gather_packs call instead of a permute/slice launch each)."""
+    if os.environ.get("TMVS_NO_STEP_PACKS") == "1":
+        _acc(grads, p, fn(raw).contiguous())
+        return
+    grads.setdefault("__defer__", []).append((p, raw, fn))
+
+
+def _flush_deferred(grads):
+    pend = grads.pop("__defer__", [])
+    if not pend:
+        return
+    outs = gather_packs([r for _, r, _ in pend], [(i, fn) for i, (_, _, fn) in enumerate(pend)], "featurenet_grads")
+    for (p, _, _), o in zip(pend, outs):
+        _acc(grads, p, o)
+
+
+def _untaps_fn(shape):
+    co, ci, k, _ = shape
+    return lambda t: t.reshape(k, k, co, ci).permute(2, 3, 0, 1)
+
+
 def _flip_t(w):
     """The data gradient of a stride-1 'same' conv is a forward conv of dz with the weight transposed
     (in <-> out) and flipped in both spatial axes: W'[ci][co][kh][kw] = W[co][ci][k-1-kh][k-1-kw]."""
@@ -188,12 +301,14 @@ def dgrad_same(dz, w, out_hw):
     the MFMA inference kernels (tmvs_conv3x3_nhwc for 32 -> 32 3x3, tmvs_conv2d_bn_relu otherwise),
     falling back to the VALU transposed gather for shapes those kernels do not take."""
     co, ci, k, _ = w.shape
-    wf = _flip_t(w)
-    if ci == 32 and co == 32 and k == 3:
-        return ops.conv3x3_nhwc(dz, device_pack("dcn", wf), bn=None, relu=False)[1]
-    if (co, ci, k) in _MFMA_DGRAD:
-        return ops.conv2d_bn_relu(dz, device_pack("conv2d", wf), ci, k, 1, bn=None, relu=False)
-    return ops.conv2d_generic(dz, _taps_t(w), ci, out_hw, k, 1, k // 2, transposed=True)
+    kind = _dgrad_kind(co, ci, k)
+    pd = _pk(("dgrad", id(w))) if kind != "taps_t" else _pk(("taps_t", id(w)))
+    if kind == "dcn":
+        return ops.conv3x3_nhwc(dz, pd if pd is not None else device_pack("dcn", _flip_t(w)), bn=None, relu=False)[1]
+    if kind == "conv2d":
+        return ops.conv2d_bn_relu(dz, pd if pd is not None else device_pack("conv2d", _flip_t(w)), ci, k, 1, bn=None,
+                                  relu=False)
+    return ops.conv2d_generic(dz, pd if pd is not None else _taps_t(w), ci, out_hw, k, 1, k // 2, transposed=True)
 
 
 def _block_bwd(rec, dy, grads, need_dx=True):
@@ -204,12 +319,14 @@ def _block_bwd(rec, dy, grads, need_dx=True):
     w = blk.conv.weight
     pad = k // 2
     xg = x.permute(0, 2, 3, 1).contiguous() if nchw_input else x
-    _acc(grads, w, _untaps(ops.conv2d_wgrad(dz, xg, k, stride, pad), w.shape))
+    _defer(grads, w, ops.conv2d_wgrad(dz, xg, k, stride, pad), _untaps_fn(w.shape))
     if not need_dx:
         return None
     if stride == 1:
         return dgrad_same(dz, w, (xg.shape[1], xg.shape[2]))
-    return ops.conv2d_generic(dz, _taps_t(w), w.shape[1], (xg.shape[1], xg.shape[2]), k, stride, pad, transposed=True)
+    pt = _pk(("taps_t", id(w)))
+    return ops.conv2d_generic(dz, pt if pt is not None else _taps_t(w), w.shape[1], (xg.shape[1], xg.shape[2]), k,
+                              stride, pad, transposed=True)
 
 
 def _dcn_bwd(dcn, x, om, dy, grads):
@@ -218,19 +335,22 @@ def _dcn_bwd(dcn, x, om, dy, grads):
     w = dcn.weight
     cout = w.shape[0]
     dx = torch.zeros_like(x)
-    w_taps = w.detach().float().reshape(cout, 32, 9).permute(2, 0, 1).contiguous()
+    w_taps = _pk(("wtaps", id(w)))
+    if w_taps is None:
+        w_taps = w.detach().float().reshape(cout, 32, 9).permute(2, 0, 1).contiguous()
     dom, dw = ops.dcn_backward(x, om, w_taps, dy, dx)
-    _acc(grads, w, dw.permute(1, 2, 0).reshape(cout, 32, 3, 3).contiguous())
+    _defer(grads, w, dw, lambda t, cout=cout: t.permute(1, 2, 0).reshape(cout, 32, 3, 3))
     _acc(grads, dcn.bias, ops.colsum(dy))
     # the offset/mask conv (3x3, 32 -> 27, bias) on dom padded to 32 channels (27..31 zero): its
     # weight gradient rows 27..31 are dropped, its data gradient reads them against zero weights
     com = dcn.conv_offset_mask
-    dwo = ops.conv2d_wgrad(dom, x, 3, 1, 1)[:, :27].contiguous()
-    _acc(grads, com.weight, _untaps(dwo, com.weight.shape))
-    _acc(grads, com.bias, ops.colsum(dom)[:27].contiguous())
+    _defer(grads, com.weight, ops.conv2d_wgrad(dom, x, 3, 1, 1),
+           lambda t: t[:, :27].reshape(3, 3, 27, 32).permute(2, 3, 0, 1))
+    _defer(grads, com.bias, ops.colsum(dom), lambda t: t[:27])
     # dx += its data gradient (dgrad_same's 32 -> 32 3x3 form on the weight padded to 32 output rows,
     # packed by one gather), added in the conv's epilogue
-    ops.conv3x3_nhwc_acc(dom, offset_dgrad_pack(com.weight), dx)
+    po = _pk(("offdgrad", id(com.weight)))
+    ops.conv3x3_nhwc_acc(dom, po if po is not None else offset_dgrad_pack(com.weight), dx)
     return dx
 
 
@@ -252,14 +372,16 @@ def _head_bwd(rec, dout_nchw, grads):
 def _inner_bwd(conv, d, lat, grads):
     """inner{1,2} = Conv2d(cl, 32, 1, bias) of the FPN merge: grads, and d lat [N,h,w,cl]."""
     w = conv.weight
-    _acc(grads, w, _untaps(ops.conv2d_wgrad(d, lat, 1, 1, 0), w.shape))
+    _defer(grads, w, ops.conv2d_wgrad(d, lat, 1, 1, 0), _untaps_fn(w.shape))
     _acc(grads, conv.bias, ops.colsum(d))
-    return ops.conv2d_generic(d, _taps_t(w), w.shape[1], (lat.shape[1], lat.shape[2]), 1, 1, 0)
+    pt = _pk(("taps_t", id(w)))
+    return ops.conv2d_generic(d, pt if pt is not None else _taps_t(w), w.shape[1], (lat.shape[1], lat.shape[2]), 1, 1, 0)
 
 
 class _FeatureNetTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, imgs, fnet, tape, *params):
+        _prepare_packs(fnet)
         x = imgs.float().contiguous()
         c00, r00 = _block_fwd(tape, fnet.conv0[0], x, 3, 1, nchw_input=True)
         conv0, r01 = _block_fwd(tape, fnet.conv0[1], c00, 3, 1)
@@ -316,6 +438,7 @@ class _FeatureNetTrain(torch.autograd.Function):
         d = d if dconv0 is None else d.add_(dconv0)
         d = _block_bwd(r01, d, grads)
         _block_bwd(r00, d, grads, need_dx=False)
+        _flush_deferred(grads)
         return (None, None, None, *[grads.get(i) for i in ctx.param_ids])
 
 
