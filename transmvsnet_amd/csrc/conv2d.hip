@@ -47,8 +47,14 @@ __global__ __launch_bounds__(512) void conv2d_bn_relu_kernel(const float* __rest
   using C = Conv2dCfg<CI, CO, K, S, NCHW>;
   __shared__ floatx4_t wl[C::NA4];
   __shared__ floatx4_t win[C::WIN4];
+  // BN alpha / shift in LDS for the epilogue (from global there, each was a serialised L2 round trip per unit)
+  __shared__ __attribute__((aligned(16))) float cst[2][C::MT * 16];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int i = tid; i < C::NA4; i += 512) wl[i] = reinterpret_cast<const floatx4_t*>(wpk)[i];
+  if (tid < C::MT * 16) {
+    cst[0][tid] = alpha && tid < CO ? alpha[tid] : 1.f;
+    cst[1][tid] = alpha && tid < CO ? shift[tid] : 0.f;
+  }
   const int nbx = (Wo + 15) / 16, nby = (Ho + 7) / 8, nunits = B * nby * nbx;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int u_begin = (int)((long long)nunits * bid / gridDim.x);
@@ -95,17 +101,27 @@ __global__ __launch_bounds__(512) void conv2d_bn_relu_kernel(const float* __rest
     floatx4_t acc[C::MT];
 #pragma unroll
     for (int m = 0; m < C::MT; ++m) acc[m] = floatx4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < C::NB; ++kb) {
+    // k-block kb + 1's fragments are read during kb's MFMAs
+    floatx4_t fb[2], fa[2][C::MT];
+    auto frag = [&](int kb, int bf) {
       const int idx = min(4 * kb + j, C::NIDX - 1);  // padded pairs carry zero weights
       const int tap = idx / C::G, ch = idx - tap * C::G, ki = tap / K, kj = tap - ki * K;
       const int P = (wv * S + ki) * C::WC + n * S + kj;
-      const floatx4_t bv = win[c2_slot<C::G, C::SH>(P, ch)];
+      fb[bf] = win[c2_slot<C::G, C::SH>(P, ch)];
+#pragma unroll
+      for (int m = 0; m < C::MT; ++m) fa[bf][m] = wl[(kb * C::MT + m) * 64 + lane];
+    };
+    frag(0, 0);
+#pragma unroll
+    for (int kb = 0; kb < C::NB; ++kb) {
+      if (kb + 1 < C::NB) frag(kb + 1, (kb + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const floatx4_t bv = fb[kb & 1];
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int m = 0; m < C::MT; ++m)
-          acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wl[(kb * C::MT + m) * 64 + lane][e], bv[e], acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[kb & 1][m][e], bv[e], acc[m], 0, 0, 0);
     }
     if (n < nvalid) {
       float* o = out + (((size_t)b * Ho + row) * Wo + x0 + n) * CO;
@@ -113,11 +129,13 @@ __global__ __launch_bounds__(512) void conv2d_bn_relu_kernel(const float* __rest
       for (int m = 0; m < C::MT; ++m) {
         const int co0 = 16 * m + 4 * j;
         if (co0 >= CO) continue;
+        const floatx4_t ca = *reinterpret_cast<const floatx4_t*>(&cst[0][co0]);
+        const floatx4_t cs = *reinterpret_cast<const floatx4_t*>(&cst[1][co0]);
         float r[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float y = acc[m][i];
-          if (alpha) y = fmaf(y, alpha[co0 + i], shift[co0 + i]);
+          if (alpha) y = fmaf(y, ca[i], cs[i]);
           if (relu) y = fmaxf(y, 0.f);
           r[i] = y;
         }

@@ -447,6 +447,9 @@ __global__ __launch_bounds__(256) void conv3d_direct_kernel(const float* __restr
 // 32 x 2THI x 2TDI). Each wave owns TDI*THI/4 input-grid rows and all 8 output parity
 // classes of them (a class = 16 outputs with one parity per dimension = one tap set of
 // 1, 2, 4 or 8 taps), so the waves carry equal work. Input tile (+1 halo) staged in LDS.
+#ifndef TMVS_DECONV_ABL
+#define TMVS_DECONV_ABL 0  // timing ablations (wrong results): 1 no weight staging, 2 no tile staging, 4 no MFMAs
+#endif
 template <int CIN, int COUT, int TDI, int THI, int MBB>
 __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restrict__ x,
                                                            const float* __restrict__ wpk,
@@ -498,7 +501,7 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
 #pragma unroll 1
   for (int ch = 0; ch < CIN / CK; ++ch) {
     if (ch) __syncthreads();
-    for (int idx = threadIdx.x; idx < NVOX * PL; idx += 256) {
+    for (int idx = threadIdx.x; idx < ((TMVS_DECONV_ABL & 2) ? 0 : NVOX * PL); idx += 256) {
       const int vox = idx / PL, q = idx - vox * PL;
       const int lw = vox % LW, rest = vox / LW, lh = rest % LH, ld = rest / LH;
       const int iw = mw0 + lw, ih = mh0 + lh, id = md0 + ld;
@@ -508,7 +511,7 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
       const int qs = SWZ ? (q ^ ((vox >> 1) & 3)) : q;
       *reinterpret_cast<float4*>(tile + vox * VST + 4 * qs) = v;
     }
-    for (int idx = threadIdx.x; idx < 27 * RM * 4; idx += 256) {
+    for (int idx = threadIdx.x; idx < ((TMVS_DECONV_ABL & 1) ? 0 : 27 * RM * 4); idx += 256) {
       const int q = idx & 3, row = (idx >> 2) % RM, tap = (idx >> 2) / RM;
       const float4 v = *reinterpret_cast<const float4*>(wpk + ((size_t)tap * COUT + mg * 16 + row) * CIN + ch * CK + 4 * q);
       *reinterpret_cast<float4*>(wts + (tap * RM + row) * 16 + 4 * (q ^ ((row >> 1) & 3))) = v;
@@ -543,8 +546,12 @@ __global__ __launch_bounds__(256) void deconv3d_lds_kernel(const float* __restri
 #pragma unroll
               for (int j = 0; j < PL; ++j)
 #pragma unroll
-                for (int m = 0; m < MBB; ++m)
-                  acc[r][cls][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b.v[j], acc[r][cls][m], 0, 0, 0);
+                for (int m = 0; m < MBB; ++m) {
+                  if (TMVS_DECONV_ABL & 4)  // timing ablation: no MFMAs (one FMA keeps the reads live)
+                    acc[r][cls][m][0] = fmaf(a[m].v[j], b.v[j], acc[r][cls][m][0]);
+                  else
+                    acc[r][cls][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m].v[j], b.v[j], acc[r][cls][m], 0, 0, 0);
+                }
             }
           }
     }

@@ -44,8 +44,19 @@ static_assert(WIN4 % (WAVES * 64) == 0, "window copy must split evenly over the 
 constexpr int NREC = 9 * TW;                               // (tap, pixel) records per wave
 }  // namespace dcn
 
+typedef float float2_t __attribute__((ext_vector_type(2)));
+
 // Window slot of chunk c of window pixel P.
 __device__ __forceinline__ int dcn_slot(int P, int c) { return P * 8 + (c ^ (P & 7)); }
+
+// Timing ablations (wrong outputs by construction; A/B builds only): bit 1 drops the offset-conv MFMAs,
+// 2 the bilinear blend (a tap's B operand is its first corner), 4 the tap MFMAs, 8 the window stores.
+#ifndef TMVS_DCN_ABL
+#define TMVS_DCN_ABL 0
+#endif
+#ifndef TMVS_DCN_PK
+#define TMVS_DCN_PK 1  // the bilinear blend on packed fp32 (A/B: 0 = scalar)
+#endif
 
 // The 9 taps of one wave-unit: gather (window LDS; beyond it, global, unless FAST), blend,
 // modulate, MT x 8 MFMAs per tap.
@@ -58,11 +69,18 @@ __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* 
   floatx4_t alt = floatx4_t{0.f, 0.f, 0.f, 0.f};
   floatx4_t v[2][4][2], w4[2];
   float mk[2];
-  // gathers of tap k into buffer bb (issued one tap ahead of their use)
-  auto gather = [&](int k, int bb) {
-    const int rr = k * dcn::TW + n;
-    w4[bb] = recw[rr];
-    const int2 bm = recb[rr];  // (window pixel of corner (y0, x0) | fallback code, mask bits)
+  // the records of the next tap to gather, read one tap before its gathers (their addresses come from
+  // them: read just before, each tap had waited out an LDS round trip between its MFMA blocks)
+  floatx4_t rw;
+  int2 rb;  // (window pixel of corner (y0, x0) | fallback code, mask bits)
+  auto rec = [&](int k) {
+    rw = recw[k * dcn::TW + n];
+    rb = recb[k * dcn::TW + n];
+  };
+  // gathers of the tap whose records are in (rw, rb) into buffer bb (issued one tap ahead of their use)
+  auto gather = [&](int bb) {
+    w4[bb] = rw;
+    const int2 bm = rb;
     mk[bb] = __int_as_float(bm.y);
     if (FAST || bm.x >= 0) {
 #pragma unroll
@@ -83,31 +101,69 @@ __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* 
       }
     }
   };
-  gather(0, 0);
+  // A fragments of tap k into buffer ab, read one tap ahead too: in LDS order they then precede the
+  // tap's gathers, so the MFMAs never wait on the gathers issued just before them
+  floatx4_t af[2][MT][2];
+  auto lda = [&](int k, int ab) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      af[ab][m][0] = wl[((k * MT + m) * 2 + 0) * 64 + lane];
+      af[ab][m][1] = wl[((k * MT + m) * 2 + 1) * 64 + lane];
+    }
+  };
+  rec(0);
+  lda(0, 0);
+  gather(0);
+  rec(1);
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
     const int bb = k & 1;
-    floatx4_t a[MT][2];
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      a[m][0] = wl[((k * MT + m) * 2 + 0) * 64 + lane];
-      a[m][1] = wl[((k * MT + m) * 2 + 1) * 64 + lane];
-    }
+    const floatx4_t(&a)[MT][2] = af[bb];
     float b[8];
+    // two channels per packed fp32 instruction (v_pk_mul_f32 / v_pk_add_f32: the same IEEE operations
+    // per element as the scalar form, half the VALU issue)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float val = w4[bb][0] * v[bb][0][e >> 2][e & 3];
-      val = val + w4[bb][1] * v[bb][1][e >> 2][e & 3];
-      val = val + w4[bb][2] * v[bb][2][e >> 2][e & 3];
-      val = val + w4[bb][3] * v[bb][3][e >> 2][e & 3];
-      b[e] = mk[bb] * val;
+    for (int e = 0; e < 8; e += 2) {
+      if (TMVS_DCN_ABL & 2) {
+        b[e] = v[bb][0][e >> 2][e & 3];
+        b[e + 1] = v[bb][0][e >> 2][(e & 3) + 1];
+        continue;
+      }
+      if (!TMVS_DCN_PK) {
+#pragma unroll
+        for (int f = e; f < e + 2; ++f) {
+          float val = w4[bb][0] * v[bb][0][f >> 2][f & 3];
+          val = val + w4[bb][1] * v[bb][1][f >> 2][f & 3];
+          val = val + w4[bb][2] * v[bb][2][f >> 2][f & 3];
+          val = val + w4[bb][3] * v[bb][3][f >> 2][f & 3];
+          b[f] = mk[bb] * val;
+        }
+        continue;
+      }
+      auto pr = [&](int c) { return float2_t{v[bb][c][e >> 2][e & 3], v[bb][c][e >> 2][(e & 3) + 1]}; };
+      auto bc = [](float t) { return float2_t{t, t}; };
+      float2_t val = bc(w4[bb][0]) * pr(0);
+      val = val + bc(w4[bb][1]) * pr(1);
+      val = val + bc(w4[bb][2]) * pr(2);
+      val = val + bc(w4[bb][3]) * pr(3);
+      const float2_t r = bc(mk[bb]) * val;
+      b[e] = r.x;
+      b[e + 1] = r.y;
     }
-    if (k < 8) gather(k + 1, bb ^ 1);
+    if (k < 8) {
+      lda(k + 1, bb ^ 1);
+      gather(bb ^ 1);
+      if (k < 7) rec(k + 2);
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
+        if (TMVS_DCN_ABL & 4) {
+          acc[m][0] += b[s];
+          continue;
+        }
         if (MT == 1 && (s & 1))  // one output tile: two interleaved chains hide the dependent latency
           alt = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s >> 2][s & 3], b[s], alt, 0, 0, 0);
         else
@@ -140,7 +196,16 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
   __shared__ floatx4_t recw[dcn::WAVES][dcn::NREC];     // [tap][px] bilinear weights (0 outside)
                                                         // (FUSED: first the [px][32] offset/mask tile)
   __shared__ int2 recb[dcn::WAVES][dcn::NREC];          // [tap][px] (window pixel | fallback code, mask bits)
+  // per-channel constants: bias, BN alpha, BN shift (CO), offset-conv bias (27): read from LDS in the
+  // epilogues (read from global there, each was a serialised L2 round trip per unit)
+  __shared__ __attribute__((aligned(16))) float cst[4][32];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid < 32) {
+    cst[0][tid] = tid < CO ? bias[tid] : 0.f;
+    cst[1][tid] = alpha && tid < CO ? alpha[tid] : 1.f;
+    cst[2][tid] = alpha && tid < CO ? shift[tid] : 0.f;
+    cst[3][tid] = FUSED && tid < 27 ? bom[tid] : 0.f;
+  }
   for (int i = tid; i < NA4; i += 512) wl[i] = reinterpret_cast<const floatx4_t*>(wpk)[i];
   if (FUSED)
     for (int i = tid; i < NO4; i += 512) wo[i] = reinterpret_cast<const floatx4_t*>(wom)[i];
@@ -191,7 +256,7 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
 #pragma unroll
     for (int i = 0; i < dcn::STAGE; ++i) {
       const int idx = tid + 512 * i;
-      win[dcn_slot(idx >> 3, idx & 7)] = stg[i];
+      if (!(TMVS_DCN_ABL & 8) || u == u_begin) win[dcn_slot(idx >> 3, idx & 7)] = stg[i];
     }
     __syncthreads();
     if (u + 1 < u_end) fetch(u + 1);  // next window in flight during this unit's work
@@ -201,24 +266,38 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
     if (FUSED) {
       // conv_offset_mask of this wave's 16 pixels from the window: B lane (j, n) = chunks j, j+4 of
       // window pixel (wv + HALO + ki - 1, HALO + n + kj - 1); D lane (j, n) = channels 16m + 4j + i
+      // (tap k + 1's fragments are read during tap k's MFMAs)
       floatx4_t ao[2] = {floatx4_t{0.f, 0.f, 0.f, 0.f}, floatx4_t{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
+      floatx4_t fb[2][2], fa[2][2][2];
+      auto frag = [&](int k, int bf) {
         const int ki = k / 3, kj = k - 3 * ki;
         const int P = (wv + dcn::HALO + ki - 1) * dcn::WC + dcn::HALO + n + kj - 1;
-        const floatx4_t b0 = win[dcn_slot(P, j)], b1 = win[dcn_slot(P, j + 4)];
-        floatx4_t a[2][2];
+        fb[bf][0] = win[dcn_slot(P, j)];
+        fb[bf][1] = win[dcn_slot(P, j + 4)];
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
-          a[m][0] = wo[((k * 2 + m) * 2 + 0) * 64 + lane];
-          a[m][1] = wo[((k * 2 + m) * 2 + 1) * 64 + lane];
+          fa[bf][m][0] = wo[((k * 2 + m) * 2 + 0) * 64 + lane];
+          fa[bf][m][1] = wo[((k * 2 + m) * 2 + 1) * 64 + lane];
         }
+      };
+      frag(0, 0);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        if (k < 8) frag(k + 1, (k + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);  // keep those reads ahead of this tap's MFMAs
+        const floatx4_t b0 = fb[k & 1][0], b1 = fb[k & 1][1];
+        const floatx4_t(&a)[2][2] = fa[k & 1];
 #pragma unroll
         for (int s = 0; s < 8; ++s)
 #pragma unroll
-          for (int m = 0; m < 2; ++m)
+          for (int m = 0; m < 2; ++m) {
+            if (TMVS_DCN_ABL & 1) {
+              ao[m][0] += (s < 4 ? b0[s] : b1[s - 4]) * a[m][s >> 2][s & 3];
+              continue;
+            }
             ao[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s >> 2][s & 3], s < 4 ? b0[s] : b1[s - 4], ao[m], 0,
                                                          0, 0);
+          }
       }
       // [px][33] tile (odd row stride: the record builders' column reads hit 16 distinct banks),
       // consumed before the records overwrite it
@@ -229,7 +308,7 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
         for (int i = 0; i < 4; ++i) {
           const int c = 16 * m + 4 * j + i;
           if (c < 27) {
-            const float o = ao[m][i] + bom[c];
+            const float o = ao[m][i] + cst[3][c];
             omt[n * 33 + c] = o;
             // training: the offset/mask tensor the backward needs ([B][27][H][W])
             if (om_out && n < nvalid) om_out[((size_t)b * 27 + c) * HW + (size_t)row * W + x0t + n] = o;
@@ -289,11 +368,14 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
       for (int m = 0; m < MT; ++m) {
         const int co0 = 16 * m + 4 * j;
         if (co0 >= CO) continue;
+        const floatx4_t cb = *reinterpret_cast<const floatx4_t*>(&cst[0][co0]);
+        const floatx4_t ca = *reinterpret_cast<const floatx4_t*>(&cst[1][co0]);
+        const floatx4_t cs = *reinterpret_cast<const floatx4_t*>(&cst[2][co0]);
         float r[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          float y = acc[m][i] + bias[co0 + i];
-          if (alpha) y = fmaf(y, alpha[co0 + i], shift[co0 + i]);
+          float y = acc[m][i] + cb[i];
+          if (alpha) y = fmaf(y, ca[i], cs[i]);
           if (relu) y = fmaxf(y, 0.f);
           r[i] = y;
           if (out) out[((size_t)b * CO + co0 + i) * HW + pq] = y;
@@ -327,8 +409,14 @@ __global__ __launch_bounds__(512) void conv3x3_window_kernel(const float* __rest
   constexpr int NA4 = 9 * 2 * 2 * 64;
   __shared__ floatx4_t wl[NA4];
   __shared__ floatx4_t win[c3::WIN4];
+  __shared__ __attribute__((aligned(16))) float cst[3][32];  // bias, BN alpha, BN shift (as the DCN's)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int i = tid; i < NA4; i += 512) wl[i] = reinterpret_cast<const floatx4_t*>(wpk)[i];
+  if (tid < 32) {
+    cst[0][tid] = bias ? bias[tid] : 0.f;
+    cst[1][tid] = alpha ? alpha[tid] : 1.f;
+    cst[2][tid] = alpha ? shift[tid] : 0.f;
+  }
   const int HW = H * W, nbx = (W + dcn::TW - 1) / dcn::TW, nby = (H + dcn::WAVES - 1) / dcn::WAVES;
   const int nunits = B * nby * nbx;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -364,17 +452,26 @@ __global__ __launch_bounds__(512) void conv3x3_window_kernel(const float* __rest
     const int x0t = xs * dcn::TW, nvalid = min(dcn::TW, W - x0t);
     if (row >= H) continue;
     floatx4_t acc[2] = {floatx4_t{0.f, 0.f, 0.f, 0.f}, floatx4_t{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
+    // tap k + 1's fragments are read during tap k's MFMAs (the DCN's offset conv does the same)
+    floatx4_t fb[2][2], fa[2][2][2];
+    auto frag = [&](int k, int bf) {
       const int ki = k / 3, kj = k - 3 * ki;
       const int P = (wv + c3::HALO + ki - 1) * c3::WC + c3::HALO + n + kj - 1;
-      const floatx4_t b0 = win[dcn_slot(P, j)], b1 = win[dcn_slot(P, j + 4)];
-      floatx4_t a[2][2];
+      fb[bf][0] = win[dcn_slot(P, j)];
+      fb[bf][1] = win[dcn_slot(P, j + 4)];
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
-        a[m][0] = wl[((k * 2 + m) * 2 + 0) * 64 + lane];
-        a[m][1] = wl[((k * 2 + m) * 2 + 1) * 64 + lane];
+        fa[bf][m][0] = wl[((k * 2 + m) * 2 + 0) * 64 + lane];
+        fa[bf][m][1] = wl[((k * 2 + m) * 2 + 1) * 64 + lane];
       }
+    };
+    frag(0, 0);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      if (k < 8) frag(k + 1, (k + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const floatx4_t b0 = fb[k & 1][0], b1 = fb[k & 1][1];
+      const floatx4_t(&a)[2][2] = fa[k & 1];
 #pragma unroll
       for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -387,12 +484,15 @@ __global__ __launch_bounds__(512) void conv3x3_window_kernel(const float* __rest
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
         const int co0 = 16 * m + 4 * j;
+        const floatx4_t cb = *reinterpret_cast<const floatx4_t*>(&cst[0][co0]);
+        const floatx4_t ca = *reinterpret_cast<const floatx4_t*>(&cst[1][co0]);
+        const floatx4_t cs = *reinterpret_cast<const floatx4_t*>(&cst[2][co0]);
         float r[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float y = acc[m][i];
-          if (bias) y = y + bias[co0 + i];
-          if (alpha) y = fmaf(y, alpha[co0 + i], shift[co0 + i]);
+          if (bias) y = y + cb[i];
+          if (alpha) y = fmaf(y, ca[i], cs[i]);
           if (relu & 1) y = fmaxf(y, 0.f);
           r[i] = y;
           if (out) out[((size_t)b * 32 + co0 + i) * HW + pq] = y;
