@@ -111,15 +111,8 @@ __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* 
       af[ab][m][1] = wl[((k * MT + m) * 2 + 1) * 64 + lane];
     }
   };
-  rec(0);
-  lda(0, 0);
-  gather(0);
-  rec(1);
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    const int bb = k & 1;
-    const floatx4_t(&a)[MT][2] = af[bb];
-    float b[8];
+  // bilinear blend and modulation of the gathers in buffer bb into the tap's B operands
+  auto blend = [&](int bb, float (&b)[8]) {
     // two channels per packed fp32 instruction (v_pk_mul_f32 / v_pk_add_f32: the same IEEE operations
     // per element as the scalar form, half the VALU issue)
 #pragma unroll
@@ -150,12 +143,8 @@ __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* 
       b[e] = r.x;
       b[e + 1] = r.y;
     }
-    if (k < 8) {
-      lda(k + 1, bb ^ 1);
-      gather(bb ^ 1);
-      if (k < 7) rec(k + 2);
-    }
-    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mfmas = [&](const floatx4_t(&a)[MT][2], const float (&b)[8]) {
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -169,6 +158,23 @@ __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* 
         else
           acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s >> 2][s & 3], b[s], acc[m], 0, 0, 0);
       }
+  };
+  rec(0);
+  lda(0, 0);
+  gather(0);
+  rec(1);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int bb = k & 1;
+    float b[8];
+    blend(bb, b);
+    if (k < 8) {
+      lda(k + 1, bb ^ 1);
+      gather(bb ^ 1);
+      if (k < 7) rec(k + 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(af[bb], b);
     __builtin_amdgcn_sched_barrier(0);
   }
   if (MT == 1) acc[0] = acc[0] + alt;
