@@ -337,6 +337,11 @@ int tmvs_upsample2_backward_nhwc(const float* du, int n, int h, int w, int chann
 int tmvs_token_linear(const float* x, long tokens, int in_features, int out_features, const float* w,
                       const float* b, int transpose_w, const float* relu_of, int accumulate, float* y,
                       void* stream);
+/* tmvs_token_linear_res: y = residual + tmvs_token_linear(x) (the residual [T][out] read, y written: the
+ *   accumulate form without first copying the residual into y; residual must not alias y). */
+int tmvs_token_linear_res(const float* x, long tokens, int in_features, int out_features, const float* w,
+                          const float* b, int transpose_w, const float* relu_of, const float* residual, float* y,
+                          void* stream);
 size_t tmvs_token_wgrad_workspace(long tokens, int a, int b);
 int tmvs_token_wgrad(const float* dy, int a, const float* x, int b, long tokens, void* workspace,
                      size_t workspace_bytes, float* dw, float* db, int accumulate, void* stream);
@@ -510,6 +515,11 @@ int tmvs_depth_metrics(const float* depth, const float* depth_gt, const float* m
  *                                27..31 are written 0 (aligned rows for the offset/mask conv's gradients)
  *     dw_taps  [9][cout][32]   = the weight gradient (the bias gradient is tmvs_colsum of dy).
  *   cout in {8, 16, 32}. The offset/mask conv's gradients are tmvs_conv2d_wgrad / _generic of dom.
+ * tmvs_dcn_backward_set: the same, but dx_nhwc is WRITTEN (need not be initialised): the corners
+ *   beyond the LDS windows are added with fp32 atomics into far_zeroed [B][H][W][32], which must be all
+ *   zero on entry and is all zero again on return (the gather pass folds it into dx and clears it, only
+ *   when a far corner occurred) -- so the caller keeps one zeroed buffer instead of a zero fill of dx per
+ *   call. One far buffer per stream: concurrent calls must not share it.
  * tmvs_nearest_up2_backward_nhwc: dprev [n][h][w][C] (+)= the 2x2 sums of d [n][2h][2w][C] (the
  *   adjoint of interpolate(scale 2, nearest), models/module.py:413,417).
  * tmvs_softmax_backward: dlogits = prob * (dprob - sum_d prob * dprob), [B][D][H][W].            */
@@ -529,6 +539,9 @@ size_t tmvs_dcn_backward_workspace(int batch, int cout, int height, int width);
 int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, const float* w_taps, const float* dy_nhwc,
                       int batch, int cin, int cout, int height, int width, void* workspace, size_t workspace_bytes,
                       float* dx_nhwc, float* dom_nhwc, float* dw_taps, void* stream);
+int tmvs_dcn_backward_set(const float* x_nhwc, const float* offset_mask, const float* w_taps, const float* dy_nhwc,
+                          int batch, int cin, int cout, int height, int width, void* workspace, size_t workspace_bytes,
+                          float* dx_nhwc, float* dom_nhwc, float* dw_taps, float* far_zeroed, void* stream);
 int tmvs_nearest_up2_backward_nhwc(const float* d, int n, int h, int w, int channels, int accumulate, float* dprev,
                                    void* stream);
 int tmvs_softmax_backward(const float* prob, const float* dprob, int batch, int ndepth, int height, int width,

@@ -237,6 +237,34 @@ def test_conv2d_wgrad_vs_torch(a, bc, k, stride, h, w):
     assert err < 1e-5, err
 
 
+@pytest.mark.parametrize("scale", [0.3, 4.0])
+def test_dcn_backward_set_matches_accumulate_form(scale):
+    """tmvs_dcn_backward_set (dx written; the corners beyond the windows through the self-clearing far buffer)
+    against tmvs_dcn_backward into a zeroed dx: bitwise when no corner leaves the window (0.3 px), within fp32
+    atomic-order rounding otherwise (4 px), and the far buffer is all zero again after each call (twice)."""
+    from transmvsnet_amd.featurenet_train import _taps
+    torch.manual_seed(11)
+    b, h, w, cout = 2, 30, 44, 32
+    x = torch.randn(b, h, w, 32, device=DEV)
+    om = torch.randn(b, 27, h, w, device=DEV)
+    om[:, :18] *= scale
+    wt = _taps(torch.randn(cout, 32, 3, 3) * 0.06).to(DEV)
+    dy = torch.randn(b, h, w, cout, device=DEV)
+    dx_ref = torch.zeros(b, h, w, 32, device=DEV)
+    dom_ref, dw_ref = ops.dcn_backward(x, om.contiguous(), wt, dy, dx_ref)
+    for _ in range(2):
+        dx, dom, dw = ops.dcn_backward_set(x, om.contiguous(), wt, dy)
+        torch.cuda.synchronize()
+        far = ops._DCN_FAR[(str(x.device), tuple(x.shape))]
+        assert float(far.abs().max()) == 0.0
+        assert torch.equal(dom, dom_ref) and torch.equal(dw, dw_ref)
+        if scale <= 0.3:
+            assert torch.equal(dx, dx_ref)
+        else:
+            err = float((dx - dx_ref).abs().max()) / float(dx_ref.abs().max())
+            assert err <= 1e-6, err
+
+
 def test_dcn_backward_nonfinite_dy_poisons_dx():
     """A non-finite upstream gradient (inf / NaN in dy) makes tmvs_dcn_backward's dx and d offset/mask
     non-finite (the kFixBad path: the fixed-point window cannot hold it, so every window is written

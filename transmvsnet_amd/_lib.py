@@ -66,6 +66,7 @@ SIGNATURES = {
     "tmvs_upsample2_add_nhwc": (I, [P, P, I, I, I, I, P, P]),
     "tmvs_upsample2_backward_nhwc": (I, [P, I, I, I, I, P, P]),
     "tmvs_token_linear": (I, [P, L, I, I, P, P, I, P, I, P, P]),
+    "tmvs_token_linear_res": (I, [P, L, I, I, P, P, I, P, P, P, P]),
     "tmvs_token_wgrad_workspace": (S, [L, I, I]),
     "tmvs_token_wgrad": (I, [P, I, P, I, L, P, S, P, P, I, P]),
     "tmvs_layer_norm_fwd": (I, [P, L, P, P, P, P]),
@@ -97,6 +98,7 @@ SIGNATURES = {
     "tmvs_dcn_forward_train": (I, [P, P, P, P, P, I, I, I, I, I, P, P, P, P]),
     "tmvs_dcn_backward_workspace": (S, [I, I, I, I]),
     "tmvs_dcn_backward": (I, [P, P, P, P, I, I, I, I, I, P, S, P, P, P, P]),
+    "tmvs_dcn_backward_set": (I, [P, P, P, P, I, I, I, I, I, P, S, P, P, P, P, P]),
     "tmvs_nearest_up2_backward_nhwc": (I, [P, I, I, I, I, I, P, P]),
     "tmvs_softmax_backward": (I, [P, P, I, I, I, I, P, P]),
 }

@@ -528,6 +528,8 @@ void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ 
     asm volatile("" ::: "memory");  // one wave's LDS operations complete in order
   };
   const float* xb = x + (size_t)b * HW * 32;
+  // corners beyond the window go to dx: the caller's dx (accumulate form) or the zeroed far buffer
+  // (overwrite form, tmvs_dcn_backward_set); either way they raise the flag word after absmax[0..1]
   float* dxb = dx + (size_t)b * HW * 32;
   const float* omp = om + (size_t)b * 27 * HW + (size_t)(live ? y : 0) * W + (live ? xq : 0);
   float aY[9], aX[9], aM[9];
@@ -614,6 +616,8 @@ void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ 
                                                                : __double2ll_rn(ldexp((double)(f * dc[c]), kfix))));
           } else {  // an offset beyond the window: straight to global memory
             float* gp = dxb + ((size_t)cy * W + cx) * 32 + cc * CC;
+            // the gather pass must read `far` (every writer stores the same 1; the word follows the two maxima)
+            const_cast<unsigned*>(absmax)[2] = 1u;
 #pragma unroll
             for (int c = 0; c < CC; ++c) unsafeAtomicAdd(gp + c, f * dc[c]);
           }
@@ -649,8 +653,12 @@ void dcn_bwd_data_kernel(const float* __restrict__ x, const float* __restrict__ 
 // dx[q][c] += sum over the blocks whose windows cover texel q (block rows / columns ascending) of their
 // window value: one thread per (texel, channel); grid (ceil(32 W / 256), H, B), so a thread's texel comes
 // from its block coordinates (a flat index had cost two 64-bit divisions per element)
+// Overwrite form (far != nullptr): dx[q][c] = far[q][c] + (the window sum), where far holds the corners
+// beyond the windows when the data kernel raised far_flag (else 0), and far is cleared again for the next call.
 __global__ __launch_bounds__(kBlk) void dcn_gather_windows_kernel(const float* __restrict__ scratch, int B, int H,
-                                                                 int W, float* __restrict__ dx) {
+                                                                 int W, float* __restrict__ dx,
+                                                                 float* __restrict__ far,
+                                                                 const unsigned* __restrict__ far_flag) {
   using namespace dbw;
   const int j = blockIdx.x * kBlk + threadIdx.x;
   if (j >= W * 32) return;
@@ -675,7 +683,9 @@ __global__ __launch_bounds__(kBlk) void dcn_gather_windows_kernel(const float* _
       const size_t blk = ((size_t)b * nty + by) * ntx + bx;
       v[r][q] = ok[r][q] ? scratch[(blk * (WR * WC) + cell) * 32 + c] : 0.f;
     }
-  const float d0 = dx[i];
+  const bool fr = far && *far_flag;
+  const float d0 = far ? (fr ? far[i] : 0.f) : dx[i];
+  if (fr) far[i] = 0.f;
   float s = 0.f;
 #pragma unroll
   for (int r = 0; r < 2; ++r)
@@ -905,9 +915,10 @@ extern "C" size_t tmvs_dcn_backward_workspace(int batch, int cout, int height, i
   return dcn_partials_bytes(batch, cout, height, width) + dcn_scratch_bytes(batch, height, width) + 256;
 }
 
-extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, const float* w_taps, const float* dy_nhwc,
-                                 int batch, int cin, int cout, int height, int width, void* workspace,
-                                 size_t workspace_bytes, float* dx_nhwc, float* dom_nhwc, float* dw_taps, void* stream) {
+static int dcn_backward_impl(const float* x_nhwc, const float* offset_mask, const float* w_taps, const float* dy_nhwc,
+                             int batch, int cin, int cout, int height, int width, void* workspace,
+                             size_t workspace_bytes, float* dx_nhwc, float* dom_nhwc, float* dw_taps, float* far,
+                             void* stream) {
   if (!x_nhwc || !offset_mask || !w_taps || !dy_nhwc || !workspace || !dx_nhwc || !dom_nhwc || !dw_taps)
     return TMVS_ERR_ARG;
   if (batch <= 0 || height <= 0 || width <= 0) return TMVS_ERR_ARG;
@@ -921,18 +932,19 @@ extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, 
   double* part = (double*)workspace;
   float* scratch = (float*)((char*)workspace + dcn_partials_bytes(batch, cout, height, width));
   unsigned* absmax = (unsigned*)((char*)scratch + dcn_scratch_bytes(batch, height, width));
-  if (hipMemsetAsync(absmax, 0, 2 * sizeof(unsigned), st) != hipSuccess) return TMVS_ERR_HIP;
+  unsigned* far_flag = absmax + 2;
+  if (hipMemsetAsync(absmax, 0, 3 * sizeof(unsigned), st) != hipSuccess) return TMVS_ERR_HIP;
   hipLaunchKernelGGL(absmax2_kernel, dim3((unsigned)std::min<long>(512, (np * cout / 4 + kBlk - 1) / kBlk), 2),
                      dim3(kBlk), 0, st, dy_nhwc, np * cout, w_taps, 9L * cout * 32, absmax);
   TMVS_CHECK_LAUNCH();
 #define TMVS_DCNB(CO)                                                                                             \
   case CO:                                                                                                        \
     hipLaunchKernelGGL(dcn_bwd_data_kernel<CO>, dim3(nbd), dim3(kBlk), 0, st, x_nhwc, offset_mask, w_taps, dy_nhwc, \
-                       batch, height, width, (const unsigned*)absmax, dx_nhwc, dom_nhwc, scratch);                \
+                       batch, height, width, (const unsigned*)absmax, far ? far : dx_nhwc, dom_nhwc, scratch);    \
     TMVS_CHECK_LAUNCH();                                                                                          \
     hipLaunchKernelGGL(dcn_gather_windows_kernel, dim3((unsigned)((width * 32 + kBlk - 1) / kBlk), height, batch),  \
                        dim3(kBlk), 0, st,                                                                         \
-                       (const float*)scratch, batch, height, width, dx_nhwc);                                     \
+                       (const float*)scratch, batch, height, width, dx_nhwc, far, (const unsigned*)far_flag);     \
     TMVS_CHECK_LAUNCH();                                                                                          \
     hipLaunchKernelGGL(dcn_bwd_weight_kernel<CO>, xcd_range_tap_grid(9, nblk), dim3(kBlk), 0, st, x_nhwc,          \
                        offset_mask, dy_nhwc, batch, height, width, ppb, nblk, part);                            \
@@ -949,6 +961,22 @@ extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, 
                      nblk, n, dw_taps);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
+}
+
+extern "C" int tmvs_dcn_backward(const float* x_nhwc, const float* offset_mask, const float* w_taps, const float* dy_nhwc,
+                                 int batch, int cin, int cout, int height, int width, void* workspace,
+                                 size_t workspace_bytes, float* dx_nhwc, float* dom_nhwc, float* dw_taps, void* stream) {
+  return dcn_backward_impl(x_nhwc, offset_mask, w_taps, dy_nhwc, batch, cin, cout, height, width, workspace,
+                           workspace_bytes, dx_nhwc, dom_nhwc, dw_taps, nullptr, stream);
+}
+
+extern "C" int tmvs_dcn_backward_set(const float* x_nhwc, const float* offset_mask, const float* w_taps,
+                                     const float* dy_nhwc, int batch, int cin, int cout, int height, int width,
+                                     void* workspace, size_t workspace_bytes, float* dx_nhwc, float* dom_nhwc,
+                                     float* dw_taps, float* far_zeroed, void* stream) {
+  if (!far_zeroed) return TMVS_ERR_ARG;
+  return dcn_backward_impl(x_nhwc, offset_mask, w_taps, dy_nhwc, batch, cin, cout, height, width, workspace,
+                           workspace_bytes, dx_nhwc, dom_nhwc, dw_taps, far_zeroed, stream);
 }
 
 extern "C" int tmvs_nearest_up2_backward_nhwc(const float* d, int n, int h, int w, int channels, int accumulate,

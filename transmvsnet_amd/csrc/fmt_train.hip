@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void token_linear_mfma_kernel(const float* __r
                                                                 const float* __restrict__ W,
                                                                 const float* __restrict__ b,
                                                                 const float* __restrict__ relu_of, int accumulate,
-                                                                float* __restrict__ y) {
+                                                                const float* __restrict__ res, float* __restrict__ y) {
   constexpr int NI = IN / 16, NB = OUT / 16;
   const int lane = threadIdx.x & 63, kg = lane >> 4, col = lane & 15;
   float afr[NB][NI][4];
@@ -86,8 +86,8 @@ __global__ __launch_bounds__(256) void token_linear_mfma_kernel(const float* __r
           v.z = m.z > 0.f ? v.z : 0.f;
           v.w = m.w > 0.f ? v.w : 0.f;
         }
-        if (accumulate) {
-          const float4 pr = *reinterpret_cast<const float4*>(y + t * OUT + o0);
+        if (accumulate || res) {  // y += v, or y = res + v (the same addition without a copy of res into y)
+          const float4 pr = *reinterpret_cast<const float4*>((res ? res : y) + t * OUT + o0);
           v.x = pr.x + v.x;
           v.y = pr.y + v.y;
           v.z = pr.z + v.z;
@@ -491,9 +491,9 @@ static long tok_chunk(long T, long maxblk, long c = 1024) {
 
 using namespace tmvs;
 
-extern "C" int tmvs_token_linear(const float* x, long tokens, int in_features, int out_features, const float* w,
-                                 const float* b, int transpose_w, const float* relu_of, int accumulate, float* y,
-                                 void* stream) {
+static int token_linear_impl(const float* x, long tokens, int in_features, int out_features, const float* w,
+                             const float* b, int transpose_w, const float* relu_of, int accumulate, const float* res,
+                             float* y, void* stream) {
   if (!x || !w || !y || tokens <= 0) return TMVS_ERR_ARG;
   const dim3 grid((unsigned)((tokens + 16L * 4 * kLinTiles - 1) / (16L * 4 * kLinTiles)));
   hipStream_t st = (hipStream_t)stream;
@@ -501,16 +501,30 @@ extern "C" int tmvs_token_linear(const float* x, long tokens, int in_features, i
   if (in_features == I && out_features == O) {                                                                    \
     if (transpose_w)                                                                                              \
       hipLaunchKernelGGL((token_linear_mfma_kernel<I, O, true>), grid, dim3(256), 0, st, x, tokens, w, b,         \
-                         relu_of, accumulate, y);                                                                 \
+                         relu_of, accumulate, res, y);                                                            \
     else                                                                                                          \
       hipLaunchKernelGGL((token_linear_mfma_kernel<I, O, false>), grid, dim3(256), 0, st, x, tokens, w, b,        \
-                         relu_of, accumulate, y);                                                                 \
+                         relu_of, accumulate, res, y);                                                            \
     TMVS_CHECK_LAUNCH();                                                                                          \
     return TMVS_OK;                                                                                               \
   }
   TMVS_TL(32, 32) TMVS_TL(32, 64) TMVS_TL(64, 32)
 #undef TMVS_TL
   return TMVS_ERR_SHAPE;
+}
+
+extern "C" int tmvs_token_linear(const float* x, long tokens, int in_features, int out_features, const float* w,
+                                 const float* b, int transpose_w, const float* relu_of, int accumulate, float* y,
+                                 void* stream) {
+  return token_linear_impl(x, tokens, in_features, out_features, w, b, transpose_w, relu_of, accumulate, nullptr, y,
+                           stream);
+}
+
+extern "C" int tmvs_token_linear_res(const float* x, long tokens, int in_features, int out_features, const float* w,
+                                     const float* b, int transpose_w, const float* relu_of, const float* residual,
+                                     float* y, void* stream) {
+  if (!residual || residual == y) return TMVS_ERR_ARG;
+  return token_linear_impl(x, tokens, in_features, out_features, w, b, transpose_w, relu_of, 0, residual, y, stream);
 }
 
 extern "C" size_t tmvs_token_wgrad_workspace(long tokens, int a, int b) {

@@ -334,11 +334,10 @@ def _dcn_bwd(dcn, x, om, dy, grads):
     conv (3x3, 32 -> 27, bias). Returns dx [N,h,w,32]."""
     w = dcn.weight
     cout = w.shape[0]
-    dx = torch.zeros_like(x)
     w_taps = _pk(("wtaps", id(w)))
     if w_taps is None:
         w_taps = w.detach().float().reshape(cout, 32, 9).permute(2, 0, 1).contiguous()
-    dom, dw = ops.dcn_backward(x, om, w_taps, dy, dx)
+    dx, dom, dw = ops.dcn_backward_set(x, om, w_taps, dy)  # dx written: no zero fill per call
     _defer(grads, w, dw, lambda t, cout=cout: t.permute(1, 2, 0).reshape(cout, 32, 3, 3))
     _acc(grads, dcn.bias, ops.colsum(dy))
     # the offset/mask conv (3x3, 32 -> 27, bias) on dom padded to 32 channels (27..31 zero): its

@@ -859,13 +859,28 @@ def _tokens(x, name, c=None):
     return x.shape[0]
 
 
-def token_linear(x, w, b=None, transpose_w=False, relu_of=None, out=None):
+def token_linear(x, w, b=None, transpose_w=False, relu_of=None, out=None, residual=None):
     """tmvs_token_linear: x [T,in] -> x w^T + b (w [out,in]) or, transpose_w, x w (w [in',out'] -> out = in').
 
-    relu_of [T,out] masks the result where relu_of <= 0; out (given) is accumulated into."""
+    relu_of [T,out] masks the result where relu_of <= 0; out (given) is accumulated into; residual (given,
+    tmvs_token_linear_res) -> a new residual + result (the same additions as out=residual.clone())."""
     t = _tokens(x, "x")
-    for a, n in ((w, "w"), (b, "b"), (relu_of, "relu_of"), (out, "out")):
+    for a, n in ((w, "w"), (b, "b"), (relu_of, "relu_of"), (out, "out"), (residual, "residual")):
         _dev(a, n)
+    if residual is not None:
+        if out is not None:
+            raise ValueError("token_linear: give out or residual, not both")
+        o_f = w.shape[0] if not transpose_w else w.shape[1]
+        if x.shape[1] != (w.shape[1] if not transpose_w else w.shape[0]) or tuple(residual.shape) != (t, o_f) or \
+                (relu_of is not None and tuple(relu_of.shape) != (t, o_f)):
+            raise ValueError("token_linear: shape mismatch")
+        y = torch.empty(t, o_f, device=x.device)
+        with _Span("tmvs_token_linear_res"):
+            _lib.check(_lib_h().tmvs_token_linear_res(_ptr(x), t, x.shape[1], o_f, _ptr(w),
+                                                      _ptr(b) if b is not None else None, int(transpose_w),
+                                                      _ptr(relu_of) if relu_of is not None else None, _ptr(residual),
+                                                      _ptr(y), _stream()), "tmvs_token_linear_res")
+        return y
     o_f = w.shape[0] if not transpose_w else w.shape[1]
     if x.shape[1] != (w.shape[1] if not transpose_w else w.shape[0]):
         raise ValueError("token_linear: x / w feature mismatch")
@@ -1103,6 +1118,35 @@ def dcn_backward(x_nhwc, offset_mask, w_taps, dy_nhwc, dx_nhwc):
     return dom, dw
 
 
+_DCN_FAR = {}
+
+
+def dcn_backward_set(x_nhwc, offset_mask, w_taps, dy_nhwc):
+    """tmvs_dcn_backward_set: -> (dx [B,H,W,32] written, not accumulated; dom; dw_taps). The corners beyond the
+    LDS windows go through a zeroed far buffer kept per (device, shape) and cleared again by the call, so no
+    activation-sized zero fill runs per call (one buffer per shape: calls on one stream only)."""
+    for t, n in ((x_nhwc, "x_nhwc"), (offset_mask, "offset_mask"), (w_taps, "w_taps"), (dy_nhwc, "dy_nhwc")):
+        _dev(t, n)
+    b, h, w, cin = x_nhwc.shape
+    cout = dy_nhwc.shape[-1]
+    if tuple(offset_mask.shape) != (b, 27, h, w) or tuple(dy_nhwc.shape) != (b, h, w, cout) or \
+            tuple(w_taps.shape) != (9, cout, cin):
+        raise ValueError("dcn_backward_set: shape mismatch")
+    key = (str(x_nhwc.device), tuple(x_nhwc.shape))
+    far = _DCN_FAR.get(key)
+    if far is None:
+        far = _DCN_FAR[key] = torch.zeros_like(x_nhwc)
+    ws = torch.empty(_lib_h().tmvs_dcn_backward_workspace(b, cout, h, w) // 4 + 64, device=x_nhwc.device)
+    dx = torch.empty_like(x_nhwc)
+    dom = torch.empty(b, h, w, 32, device=x_nhwc.device)
+    dw = torch.empty(9, cout, cin, device=x_nhwc.device)
+    with _Span("tmvs_dcn_backward_set"):
+        _lib.check(_lib_h().tmvs_dcn_backward_set(_ptr(x_nhwc), _ptr(offset_mask), _ptr(w_taps), _ptr(dy_nhwc), b, cin,
+                                                  cout, h, w, _ptr(ws), ws.numel() * 4, _ptr(dx), _ptr(dom), _ptr(dw),
+                                                  _ptr(far), _stream()), "tmvs_dcn_backward_set")
+    return dx, dom, dw
+
+
 def nearest_up2_backward_nhwc(d, out=None):
     """tmvs_nearest_up2_backward_nhwc: d [n,2h,2w,C] -> [n,h,w,C] (accumulated into `out` when given)."""
     _dev(d, "d")
@@ -1126,7 +1170,8 @@ def softmax_backward(prob, dprob):
     return out
 
 
-for _name in ("conv2d_generic", "conv2d_wgrad", "colsum", "dcn_forward_train", "dcn_backward", "conv3x3_nhwc_acc",
+for _name in ("conv2d_generic", "conv2d_wgrad", "colsum", "dcn_forward_train", "dcn_backward", "dcn_backward_set",
+              "conv3x3_nhwc_acc",
               "nearest_up2_backward_nhwc", "softmax_backward"):
     globals()[_name] = _on_tensor_device(globals()[_name])
 del _name

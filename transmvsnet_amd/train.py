@@ -221,16 +221,16 @@ def _encoder_layer_backward(p, enc_w, x, src, dy, tpg, spg, self_attn):
     v = ops.token_linear(src, wv, bv)
     kv = ops.fmt_kv(src.view(groups, spg, 32), enc_w)
     msg = ops.linattn_fwd(q, kv, tpg)
-    xp1 = ops.token_linear(msg, wo, bo, out=x.clone())                     # x + out_projection(msg)
+    xp1 = ops.token_linear(msg, wo, bo, residual=x)                        # x + out_projection(msg)
     x1 = ops.layer_norm_fwd(xp1, g1, n1)
     hp = ops.token_linear(x1, w1, b1)
     hdn = ops.token_linear(x1, w1, b1, relu_of=hp)                         # relu(linear1(x1))
-    xp2 = ops.token_linear(hdn, w2, b2, out=x1.clone())                    # x1 + linear2(hdn)
+    xp2 = ops.token_linear(hdn, w2, b2, residual=x1)                       # x1 + linear2(hdn)
     dxp2, dgb2 = ops.layer_norm_bwd(dy, xp2, g2)
     dw2, db2 = ops.token_wgrad(dxp2, hdn)
     dhp = ops.token_linear(dxp2, w2, transpose_w=True, relu_of=hp)
     dw1, db1 = ops.token_wgrad(dhp, x1)
-    dx1 = ops.token_linear(dhp, w1, transpose_w=True, out=dxp2.clone())
+    dx1 = ops.token_linear(dhp, w1, transpose_w=True, residual=dxp2)
     dxp1, dgb1 = ops.layer_norm_bwd(dx1, xp1, g1)
     dwo, dbo = ops.token_wgrad(dxp1, msg)
     dmsg = ops.token_linear(dxp1, wo, transpose_w=True)
