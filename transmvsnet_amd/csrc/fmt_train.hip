@@ -491,6 +491,8 @@ static long tok_chunk(long T, long maxblk, long c = 1024) {
 
 using namespace tmvs;
 
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 static int token_linear_impl(const float* x, long tokens, int in_features, int out_features, const float* w,
                              const float* b, int transpose_w, const float* relu_of, int accumulate, const float* res,
                              float* y, void* stream) {
@@ -523,7 +525,7 @@ extern "C" int tmvs_token_linear(const float* x, long tokens, int in_features, i
 extern "C" int tmvs_token_linear_res(const float* x, long tokens, int in_features, int out_features, const float* w,
                                      const float* b, int transpose_w, const float* relu_of, const float* residual,
                                      float* y, void* stream) {
-  if (!residual || residual == y) return TMVS_ERR_ARG;
+  if (!residual || residual == y || !aligned16(residual) || !aligned16(y)) return TMVS_ERR_ARG;  // float4 rows
   return token_linear_impl(x, tokens, in_features, out_features, w, b, transpose_w, relu_of, 0, residual, y, stream);
 }
 
@@ -554,7 +556,6 @@ extern "C" int tmvs_token_wgrad(const float* dy, int a, const float* x, int b, l
   return TMVS_ERR_SHAPE;
 }
 
-static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // The LayerNorm kernels move a token's 32 channels as 16-byte quads: x, y, dy and dx must be
 // 16-byte aligned (any row of a contiguous [tokens][32] buffer is when its base is).
