@@ -15,17 +15,17 @@
 // pixel n itself and holds channels {4j..4j+3} (k-steps 0-3) and {16+4j..16+4j+3} (k-steps 4-7)
 // of the tap: the weights are packed in that K order, as the kernel's LDS image.
 //
-// Work unit = (image, 8-row band, 16-pixel column step); wave w of the 512-thread block owns row
-// 8*band + w of the unit. Per unit the block stages the source window rows [8*band - 4, +16) x
-// columns [x0 - 4, +24) x 32 channels (48 KB) in LDS, so the 4 bilinear corners of every tap whose
-// offsets stay within the window (|offset| up to ~2 px; the reference's zero-initialised offsets,
-// models/dcn.py:62-64, always) are LDS reads; a wave whose unit has a sample beyond the window runs
-// the same taps with per-lane global fallback gathers. The next unit's window is fetched into
-// registers during the current unit's taps. Window layout: 16-byte chunk c of window pixel P at
-// P*8 + (c ^ (P & 7)), which makes both the staging writes (one 128-byte pixel row per 8 lanes)
-// and the B-layout reads (chunks j and j+4 of 16 pixels per lane group) bank-conflict-free.
-// Per (tap, pixel) sampling records (window index, 4 bilinear weights, mask) are built once per
-// unit and shared by the 4 lanes of a pixel.
+// Work unit = (image, NW-row band, 16-pixel column step); wave w of the NW*64-thread block owns row
+// NW*band + w of the unit (NW = 12 by default: 3 waves/SIMD). Per unit the block stages the source
+// window rows [NW*band - HL, +NW+2HL) x columns [x0 - HL, +16+2HL) x 32 channels in LDS (HL = 3:
+// 50 KB), so the 4 bilinear corners of every tap whose offsets stay within the window (|offset| up to
+// ~HL - 1 px; the reference's zero-initialised offsets, models/dcn.py:62-64, always) are LDS reads; a
+// wave whose unit has a sample beyond the window runs the same taps with per-lane global fallback
+// gathers (dcn_taps_slow). The next unit's window is fetched into registers during the current unit's
+// taps. Window layout: 16-byte chunk c of window pixel P at P*8 + (c ^ (P & 7)), which makes both the
+// staging writes (one 128-byte pixel row per 8 lanes) and the B-layout reads (chunks j and j+4 of 16
+// pixels per lane group) bank-conflict-free. Per (tap, pixel) 16-byte sampling records (the bilinear
+// fractions, window index, mask) are built once per unit and shared by the 4 lanes of a pixel.
 #include "common.h"
 
 #include <algorithm>
@@ -34,15 +34,20 @@ namespace tmvs {
 
 namespace dcn {
 constexpr int CI = 32;     // input channels (FeatureNet heads: 4 * base_channels)
-constexpr int WAVES = 8;   // waves per block = rows per unit
+constexpr int WAVES = 8;   // waves per block = rows per unit (the 3x3 conv's unit; the DCN's: DcnWin)
 constexpr int TW = 16;     // pixels per wave row
-constexpr int HALO = 4;    // window margin (pixels) on every side
-constexpr int WR = WAVES + 2 * HALO, WC = TW + 2 * HALO;  // window rows, columns
-constexpr int WIN4 = WR * WC * 8;                          // window float4s (8 per pixel)
-constexpr int STAGE = WIN4 / (WAVES * 64);                 // float4 per thread per window copy
-static_assert(WIN4 % (WAVES * 64) == 0, "window copy must split evenly over the block");
 constexpr int NREC = 9 * TW;                               // (tap, pixel) records per wave
 }  // namespace dcn
+
+// The DCN's unit / window geometry: NW waves = NW rows of 16 pixels per unit, a window margin of HL
+// pixels on every side (samples whose 4 corners stay inside it read LDS; others take the global path)
+template <int NW, int HL>
+struct DcnWin {
+  static constexpr int WAVES = NW, HALO = HL, NT = NW * 64;
+  static constexpr int WR = NW + 2 * HL, WC = dcn::TW + 2 * HL;  // window rows, columns
+  static constexpr int WIN4 = WR * WC * 8;                       // window float4s (8 per pixel)
+  static constexpr int STAGE = (WIN4 + NT - 1) / NT;             // float4 per thread per window copy
+};
 
 typedef float float2_t __attribute__((ext_vector_type(2)));
 
@@ -60,32 +65,36 @@ __device__ __forceinline__ int dcn_slot(int P, int c) { return P * 8 + (c ^ (P &
 
 // The 9 taps of one wave-unit: gather (window LDS; beyond it, global, unless FAST), blend,
 // modulate, MT x 8 MFMAs per tap.
-template <int MT, bool FAST>
+// SB: one gather / A-fragment buffer (a tap's blend consumes the gathers before the next tap's refill
+// them; the next tap's A fragments are read after this tap's MFMAs): the register budget of 3 waves/SIMD
+template <int MT, bool FAST, int WC, bool SB = false>
 __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* __restrict__ wl,
-                                         const floatx4_t* __restrict__ win, const floatx4_t* __restrict__ recw,
-                                         const int2* __restrict__ recb, __amdgpu_buffer_rsrc_t rx, int H, int W,
-                                         int lane) {
+                                         const floatx4_t* __restrict__ win, const floatx4_t* __restrict__ recs,
+                                         __amdgpu_buffer_rsrc_t rx, int H, int W, int lane) {
   const int j = lane >> 4, n = lane & 15;
   floatx4_t alt = floatx4_t{0.f, 0.f, 0.f, 0.f};
-  floatx4_t v[2][4][2], w4[2];
-  float mk[2];
+  constexpr int NB = SB ? 1 : 2;
+  floatx4_t v[NB][4][2], w4[NB];
+  float mk[NB];
   // the records of the next tap to gather, read one tap before its gathers (their addresses come from
   // them: read just before, each tap had waited out an LDS round trip between its MFMA blocks)
+  // record = (ly, lx, window pixel of corner (y0, x0) | fallback code, mask); a sample outside the
+  // image has ly = lx = 0 and mask 0, so its B operand is 0
   floatx4_t rw;
-  int2 rb;  // (window pixel of corner (y0, x0) | fallback code, mask bits)
-  auto rec = [&](int k) {
-    rw = recw[k * dcn::TW + n];
-    rb = recb[k * dcn::TW + n];
-  };
-  // gathers of the tap whose records are in (rw, rb) into buffer bb (issued one tap ahead of their use)
+  auto rec = [&](int k) { rw = recs[k * dcn::TW + n]; };
+  // gathers of the tap whose record is in rw into buffer bb (issued one tap ahead of their use); the
+  // bilinear weights are formed here from the fractions, the same products the record builder formed
   auto gather = [&](int bb) {
-    w4[bb] = rw;
-    const int2 bm = rb;
-    mk[bb] = __int_as_float(bm.y);
+    {
+      const float ly = rw[0], lx = rw[1], hy = 1.f - ly, hx = 1.f - lx;
+      w4[bb] = floatx4_t{hy * hx, hy * lx, ly * hx, ly * lx};
+    }
+    const int2 bm = make_int2(__float_as_int(rw[2]), 0);
+    mk[bb] = rw[3];
     if (FAST || bm.x >= 0) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const int Pc = bm.x + (c >> 1) * dcn::WC + (c & 1);
+        const int Pc = bm.x + (c >> 1) * WC + (c & 1);
         v[bb][c][0] = win[dcn_slot(Pc, j)];
         v[bb][c][1] = win[dcn_slot(Pc, j + 4)];
       }
@@ -103,7 +112,7 @@ __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* 
   };
   // A fragments of tap k into buffer ab, read one tap ahead too: in LDS order they then precede the
   // tap's gathers, so the MFMAs never wait on the gathers issued just before them
-  floatx4_t af[2][MT][2];
+  floatx4_t af[NB][MT][2];
   auto lda = [&](int k, int ab) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
@@ -165,17 +174,82 @@ __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* 
   rec(1);
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    const int bb = k & 1;
+    const int bb = SB ? 0 : k & 1;
     float b[8];
     blend(bb, b);
     if (k < 8) {
-      lda(k + 1, bb ^ 1);
-      gather(bb ^ 1);
+      if (!SB) lda(k + 1, bb ^ 1);
+      gather(SB ? 0 : bb ^ 1);
       if (k < 7) rec(k + 2);
     }
     __builtin_amdgcn_sched_barrier(0);
     mfmas(af[bb], b);
     __builtin_amdgcn_sched_barrier(0);
+    if (SB && k < 8) lda(k + 1, 0);
+  }
+  if (MT == 1) acc[0] = acc[0] + alt;
+}
+
+// The taps of a wave-unit with a sample beyond the window (rare: offsets over ~HALO - 1 px), in the
+// simplest form -- one tap at a time, no read-ahead -- so it does not raise the kernel's register
+// budget: the same gathers (window or global), blend and MFMA chains as dcn_taps, so the same results.
+template <int MT, int WC>
+__device__ __forceinline__ void dcn_taps_slow(floatx4_t (&acc)[MT], const floatx4_t* __restrict__ wl,
+                                           const floatx4_t* __restrict__ win, const floatx4_t* __restrict__ recs,
+                                           __amdgpu_buffer_rsrc_t rx, int H, int W, int lane) {
+  const int j = lane >> 4, n = lane & 15;
+  floatx4_t alt = floatx4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int k = 0; k < 9; ++k) {
+    const floatx4_t rw = recs[k * dcn::TW + n];
+    const float ly = rw[0], lx = rw[1], hy = 1.f - ly, hx = 1.f - lx;
+    const floatx4_t w4 = floatx4_t{hy * hx, hy * lx, ly * hx, ly * lx};
+    const int code = __float_as_int(rw[2]);
+    const float mk = rw[3];
+    floatx4_t v[4][2];
+    if (code >= 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int Pc = code + (c >> 1) * WC + (c & 1);
+        v[c][0] = win[dcn_slot(Pc, j)];
+        v[c][1] = win[dcn_slot(Pc, j + 4)];
+      }
+    } else {
+      const int cd = -1 - code, y0 = (cd >> 15) - 1, x0 = (cd & 32767) - 1;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int cy = y0 + (c >> 1), cx = x0 + (c & 1);
+        const bool ok = (unsigned)cy < (unsigned)H && (unsigned)cx < (unsigned)W;
+        const unsigned off = ok ? ((unsigned)(cy * W + cx) * dcn::CI + 4u * j) * 4u : kOffOut;
+        v[c][0] = buf_load_f32x4(rx, off);
+        v[c][1] = buf_load_f32x4(rx, off == kOffOut ? kOffOut : off + 64u);
+      }
+    }
+    float b[8];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      auto pr = [&](int c) { return float2_t{v[c][e >> 2][e & 3], v[c][e >> 2][(e & 3) + 1]}; };
+      auto bc = [](float t) { return float2_t{t, t}; };
+      float2_t val = bc(w4[0]) * pr(0);
+      val = val + bc(w4[1]) * pr(1);
+      val = val + bc(w4[2]) * pr(2);
+      val = val + bc(w4[3]) * pr(3);
+      const float2_t r = bc(mk) * val;
+      b[e] = r.x;
+      b[e + 1] = r.y;
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const floatx4_t a0 = wl[((k * MT + m) * 2 + 0) * 64 + lane], a1 = wl[((k * MT + m) * 2 + 1) * 64 + lane];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const float a = s < 4 ? a0[s] : a1[s - 4];
+        if (MT == 1 && (s & 1))
+          alt = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[s], alt, 0, 0, 0);
+        else
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[s], acc[m], 0, 0, 0);
+      }
+    }
   }
   if (MT == 1) acc[0] = acc[0] + alt;
 }
@@ -183,8 +257,8 @@ __device__ __forceinline__ void dcn_taps(floatx4_t (&acc)[MT], const floatx4_t* 
 // FUSED: the DCN's offset/mask conv (conv_offset_mask, models/dcn.py:58-64: 3x3, 32 -> 27, bias)
 // is computed in-kernel from the same LDS window (implicit GEMM on MFMA, M = 27 padded to 32), so
 // the [27][H][W] offset/mask tensor never exists in HBM; otherwise `om` is read from global.
-template <int CO, bool FUSED>
-__global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict__ x, const float* __restrict__ om,
+template <int CO, bool FUSED, int NW, int HL>
+__global__ __launch_bounds__(NW * 64) void dcn_window_kernel(const float* __restrict__ x, const float* __restrict__ om,
                                                          const float* __restrict__ wom, const float* __restrict__ bom,
                                                          const float* __restrict__ wpk,
                                                          const float* __restrict__ bias,
@@ -193,15 +267,16 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
                                                          int W, float* __restrict__ out,
                                                          float* __restrict__ out_nhwc,
                                                          float* __restrict__ om_out) {
+  using Cfg = DcnWin<NW, HL>;
+  constexpr int NT = Cfg::NT;
   constexpr int MT = (CO + 15) / 16;
   constexpr int NA4 = 9 * MT * 2 * 64;  // A fragments [tap][mt][half][lane] float4
   constexpr int NO4 = FUSED ? 9 * 2 * 2 * 64 : 1;  // offset-conv A fragments (27 rows padded to 32)
   __shared__ floatx4_t wl[NA4];
   __shared__ floatx4_t wo[NO4];
-  __shared__ floatx4_t win[dcn::WIN4];                  // swizzled [row][col] pixels of 8 chunks
-  __shared__ floatx4_t recw[dcn::WAVES][dcn::NREC];     // [tap][px] bilinear weights (0 outside)
-                                                        // (FUSED: first the [px][32] offset/mask tile)
-  __shared__ int2 recb[dcn::WAVES][dcn::NREC];          // [tap][px] (window pixel | fallback code, mask bits)
+  __shared__ floatx4_t win[Cfg::WIN4];                  // swizzled [row][col] pixels of 8 chunks
+  __shared__ floatx4_t recs[NW][dcn::NREC];             // [tap][px] sampling records (16 B)
+                                                        // (FUSED: first the [px][33] offset/mask tile)
   // per-channel constants: bias, BN alpha, BN shift (CO), offset-conv bias (27): read from LDS in the
   // epilogues (read from global there, each was a serialised L2 round trip per unit)
   __shared__ __attribute__((aligned(16))) float cst[4][32];
@@ -212,10 +287,10 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
     cst[2][tid] = alpha && tid < CO ? shift[tid] : 0.f;
     cst[3][tid] = FUSED && tid < 27 ? bom[tid] : 0.f;
   }
-  for (int i = tid; i < NA4; i += 512) wl[i] = reinterpret_cast<const floatx4_t*>(wpk)[i];
+  for (int i = tid; i < NA4; i += NT) wl[i] = reinterpret_cast<const floatx4_t*>(wpk)[i];
   if (FUSED)
-    for (int i = tid; i < NO4; i += 512) wo[i] = reinterpret_cast<const floatx4_t*>(wom)[i];
-  const int HW = H * W, nbx = (W + dcn::TW - 1) / dcn::TW, nby = (H + dcn::WAVES - 1) / dcn::WAVES;
+    for (int i = tid; i < NO4; i += NT) wo[i] = reinterpret_cast<const floatx4_t*>(wom)[i];
+  const int HW = H * W, nbx = (W + dcn::TW - 1) / dcn::TW, nby = (H + NW - 1) / NW;
   const int nunits = B * nby * nbx;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int u_begin = (int)((long long)nunits * bid / gridDim.x);
@@ -225,22 +300,22 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
 
   // global -> register copy of a unit's window (zeros outside the image) and (not FUSED) of the
   // offsets/mask logits of the (tap, pixel) records this lane builds (r = lane + 64 i < 144)
-  floatx4_t stg[dcn::STAGE];
+  floatx4_t stg[Cfg::STAGE];
   float omv[9];
   auto fetch = [&](int u) {
     const int b = u / (nby * nbx), rem = u - b * (nby * nbx), band = rem / nbx, xs = rem - band * nbx;
-    const int wy0 = band * dcn::WAVES - dcn::HALO, wx0 = xs * dcn::TW - dcn::HALO;
+    const int wy0 = band * NW - HL, wx0 = xs * dcn::TW - HL;
     const __amdgpu_buffer_rsrc_t rx = raw_rsrc(x + (size_t)b * HW * dcn::CI, (unsigned)HW * dcn::CI * 4);
 #pragma unroll
-    for (int i = 0; i < dcn::STAGE; ++i) {
-      const int idx = tid + 512 * i, pix = idx >> 3, ch = idx & 7;
-      const int r = pix / dcn::WC, c = pix - r * dcn::WC;
+    for (int i = 0; i < Cfg::STAGE; ++i) {
+      const int idx = min(tid + NT * i, Cfg::WIN4 - 1), pix = idx >> 3, ch = idx & 7;
+      const int r = pix / Cfg::WC, c = pix - r * Cfg::WC;
       const int gy = wy0 + r, gx = wx0 + c;
       const bool ok = (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
       stg[i] = buf_load_f32x4(rx, ok ? ((unsigned)(gy * W + gx) * dcn::CI + 4u * ch) * 4u : kOffOut);
     }
     if (!FUSED) {
-      const int row = min(band * dcn::WAVES + wv, H - 1), x0t = xs * dcn::TW;
+      const int row = min(band * NW + wv, H - 1), x0t = xs * dcn::TW;
       const float* omb = om + (size_t)b * 27 * HW + (size_t)row * W + x0t;
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
@@ -257,16 +332,17 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
   if (u_begin < u_end) fetch(u_begin);
   for (int u = u_begin; u < u_end; ++u) {
     const int b = u / (nby * nbx), rem = u - b * (nby * nbx), band = rem / nbx, xs = rem - band * nbx;
-    const int wy0 = band * dcn::WAVES - dcn::HALO, wx0 = xs * dcn::TW - dcn::HALO;
+    const int wy0 = band * NW - HL, wx0 = xs * dcn::TW - HL;
     __syncthreads();  // previous unit's window reads are done (and, first time, the weights are staged)
 #pragma unroll
-    for (int i = 0; i < dcn::STAGE; ++i) {
-      const int idx = tid + 512 * i;
-      if (!(TMVS_DCN_ABL & 8) || u == u_begin) win[dcn_slot(idx >> 3, idx & 7)] = stg[i];
+    for (int i = 0; i < Cfg::STAGE; ++i) {
+      const int idx = tid + NT * i;
+      if ((Cfg::WIN4 % NT == 0 || idx < Cfg::WIN4) && (!(TMVS_DCN_ABL & 8) || u == u_begin))
+        win[dcn_slot(idx >> 3, idx & 7)] = stg[i];
     }
     __syncthreads();
     if (u + 1 < u_end) fetch(u + 1);  // next window in flight during this unit's work
-    const int row = band * dcn::WAVES + wv;
+    const int row = band * NW + wv;
     const int x0t = xs * dcn::TW, nvalid = min(dcn::TW, W - x0t);
     if (row >= H) continue;
     if (FUSED) {
@@ -274,10 +350,11 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
       // window pixel (wv + HALO + ki - 1, HALO + n + kj - 1); D lane (j, n) = channels 16m + 4j + i
       // (tap k + 1's fragments are read during tap k's MFMAs)
       floatx4_t ao[2] = {floatx4_t{0.f, 0.f, 0.f, 0.f}, floatx4_t{0.f, 0.f, 0.f, 0.f}};
-      floatx4_t fb[2][2], fa[2][2][2];
+      constexpr int OB = NW > 8 ? 1 : 2;  // 3 waves/SIMD: read each tap's fragments just before it
+      floatx4_t fb[OB][2], fa[OB][2][2];
       auto frag = [&](int k, int bf) {
         const int ki = k / 3, kj = k - 3 * ki;
-        const int P = (wv + dcn::HALO + ki - 1) * dcn::WC + dcn::HALO + n + kj - 1;
+        const int P = (wv + HL + ki - 1) * Cfg::WC + HL + n + kj - 1;
         fb[bf][0] = win[dcn_slot(P, j)];
         fb[bf][1] = win[dcn_slot(P, j + 4)];
 #pragma unroll
@@ -286,13 +363,17 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
           fa[bf][m][1] = wo[((k * 2 + m) * 2 + 1) * 64 + lane];
         }
       };
-      frag(0, 0);
+      if (OB == 2) frag(0, 0);
 #pragma unroll
       for (int k = 0; k < 9; ++k) {
-        if (k < 8) frag(k + 1, (k + 1) & 1);
+        if (OB == 1)
+          frag(k, 0);
+        else if (k < 8)
+          frag(k + 1, (k + 1) & 1);
         __builtin_amdgcn_sched_barrier(0);  // keep those reads ahead of this tap's MFMAs
-        const floatx4_t b0 = fb[k & 1][0], b1 = fb[k & 1][1];
-        const floatx4_t(&a)[2][2] = fa[k & 1];
+        const int ob = OB == 1 ? 0 : k & 1;
+        const floatx4_t b0 = fb[ob][0], b1 = fb[ob][1];
+        const floatx4_t(&a)[2][2] = fa[ob];
 #pragma unroll
         for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -307,7 +388,8 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
       }
       // [px][33] tile (odd row stride: the record builders' column reads hit 16 distinct banks),
       // consumed before the records overwrite it
-      float* omt = reinterpret_cast<float*>(recw[wv]);
+      float* omt = reinterpret_cast<float*>(recs[wv]);
+      static_assert(16 * 33 <= 4 * dcn::NREC, "offset tile fits a wave's records");
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -348,13 +430,14 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
         const float hy = 1.f - ly, hx = 1.f - lx;
         const int y0i = (int)fmaxf(fminf(y0, 32766.f), -2.f), x0i = (int)fmaxf(fminf(x0, 32766.f), -2.f);
         const int ry = y0i - wy0, rxw = x0i - wx0;
-        const bool inwin = (unsigned)ry < (unsigned)(dcn::WR - 1) && (unsigned)rxw < (unsigned)(dcn::WC - 1);
+        const bool inwin = (unsigned)ry < (unsigned)(Cfg::WR - 1) && (unsigned)rxw < (unsigned)(Cfg::WC - 1);
         lane_fast = lane_fast && (inwin || !inside);
         const float mk = __frcp_rn(1.f + __expf(-omv[3 * i + 2]));  // sigmoid (fast exp / rcp)
         // inside => y0 in [-1, H-1], x0 in [-1, W-1]: the fallback code fits 30 bits
-        const int code = !inside ? 0 : inwin ? ry * dcn::WC + rxw : -1 - (((y0i + 1) << 15) | (x0i + 1));
-        recb[wv][r] = make_int2(code, __float_as_int(mk));
-        recw[wv][r] = inside ? floatx4_t{hy * hx, hy * lx, ly * hx, ly * lx} : floatx4_t{0.f, 0.f, 0.f, 0.f};
+        const int code = !inside ? 0 : inwin ? ry * Cfg::WC + rxw : -1 - (((y0i + 1) << 15) | (x0i + 1));
+        (void)hy;
+        (void)hx;
+        recs[wv][r] = inside ? floatx4_t{ly, lx, __int_as_float(code), mk} : floatx4_t{0.f, 0.f, __int_as_float(0), 0.f};
       }
     }
     // every sample of the wave's unit inside the window: the branch-free tap loop
@@ -363,10 +446,13 @@ __global__ __launch_bounds__(512) void dcn_window_kernel(const float* __restrict
     floatx4_t acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+    constexpr bool SB = NW > 8;  // 3 waves/SIMD: single buffers
     if (fast)
-      dcn_taps<MT, true>(acc, wl, win, recw[wv], recb[wv], rx, H, W, lane);
+      dcn_taps<MT, true, Cfg::WC, SB>(acc, wl, win, recs[wv], rx, H, W, lane);
+    else if (SB)
+      dcn_taps_slow<MT, Cfg::WC>(acc, wl, win, recs[wv], rx, H, W, lane);
     else
-      dcn_taps<MT, false>(acc, wl, win, recw[wv], recb[wv], rx, H, W, lane);
+      dcn_taps<MT, false, Cfg::WC, SB>(acc, wl, win, recs[wv], rx, H, W, lane);
     // D fragment: lane (j, n) holds output channels 16m + 4j .. +3 of pixel (row, x0t + n)
     if (n < nvalid) {
       const int pq = row * W + x0t + n;
@@ -590,24 +676,31 @@ extern "C" int tmvs_deform_conv2d_pack(const float* weight, int cout, int cin, f
 
 namespace {
 
+// The DCN unit: TMVS_DCN_NW waves (rows) per workgroup with a TMVS_DCN_HALO-pixel window margin
+#ifndef TMVS_DCN_NW
+#define TMVS_DCN_NW 12
+#endif
+#ifndef TMVS_DCN_HALO
+#define TMVS_DCN_HALO 3
+#endif
 template <int CO, bool FUSED>
 int dcn_launch(const float* x, const float* om, const float* wom, const float* bom, const float* w,
                const float* bias, const float* alpha, const float* shift, int relu, int batch, int height, int width,
                float* out, float* out_nhwc, hipStream_t st, float* om_out = nullptr) {
+  constexpr int NW = TMVS_DCN_NW, HL = TMVS_DCN_HALO;
   // persistent grid: one block per CU slot the kernel's LDS/VGPR footprint allows
   static int grid = 0;
   if (!grid) {
     int dev = 0, ncu = 0, occ = 0;
     if (hipGetDevice(&dev) != hipSuccess) return TMVS_ERR_HIP;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dcn_window_kernel<CO, FUSED>, 512, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dcn_window_kernel<CO, FUSED, NW, HL>, NW * 64, 0);
     grid = std::max(1, ncu * std::max(occ, 1));
   }
-  const long long nunits =
-      (long long)batch * ((height + dcn::WAVES - 1) / dcn::WAVES) * ((width + dcn::TW - 1) / dcn::TW);
+  const long long nunits = (long long)batch * ((height + NW - 1) / NW) * ((width + dcn::TW - 1) / dcn::TW);
   const int nblk = (int)std::min<long long>(grid, nunits);
-  hipLaunchKernelGGL((dcn_window_kernel<CO, FUSED>), dim3(nblk), dim3(512), 0, st, x, om, wom, bom, w, bias, alpha,
-                     shift, relu, batch, height, width, out, out_nhwc, om_out);
+  hipLaunchKernelGGL((dcn_window_kernel<CO, FUSED, NW, HL>), dim3(nblk), dim3(NW * 64), 0, st, x, om, wom, bom, w,
+                     bias, alpha, shift, relu, batch, height, width, out, out_nhwc, om_out);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
