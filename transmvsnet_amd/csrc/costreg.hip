@@ -1584,6 +1584,9 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
 #define TMVS_C16_TD 2
 #define TMVS_C16_TH 4
 #endif
+#ifdef TMVS_C16_LDS  // A/B: conv2 through the general LDS kernel (weights from L2) with this (TD, TH, MBB, WS)
+  TMVS_CONV_LDS(16, 16, TMVS_C16_LDS)
+#endif
   if (cin == 16 && cout == 16 && stride == 1)
     return launch_conv_c16<TMVS_C16_TD, TMVS_C16_TH>(x, wpk, al, sh, y, B, g, st);
 #ifndef TMVS_C4_CFG
