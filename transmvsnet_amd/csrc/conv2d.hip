@@ -39,6 +39,9 @@ __device__ __forceinline__ int c2_slot(int P, int c) {
   return G == 1 ? P : P * G + (c ^ ((P >> SH) & (G - 1)));
 }
 
+#ifndef TMVS_C2D_ABL
+#define TMVS_C2D_ABL 0
+#endif
 template <int CI, int CO, int K, int S, bool NCHW>
 __global__ __launch_bounds__(512) void conv2d_bn_relu_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                              const float* __restrict__ alpha,
@@ -120,8 +123,13 @@ __global__ __launch_bounds__(512) void conv2d_bn_relu_kernel(const float* __rest
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int m = 0; m < C::MT; ++m)
+        for (int m = 0; m < C::MT; ++m) {
+          if (TMVS_C2D_ABL) {  // timing ablation (wrong outputs): no MFMAs
+            acc[m][0] += fa[kb & 1][m][e] * bv[e];
+            continue;
+          }
           acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[kb & 1][m][e], bv[e], acc[m], 0, 0, 0);
+        }
     }
     if (n < nvalid) {
       float* o = out + (((size_t)b * Ho + row) * Wo + x0 + n) * CO;
