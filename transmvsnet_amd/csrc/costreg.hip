@@ -1032,15 +1032,18 @@ __global__ __launch_bounds__(64 * (D / kDChunk)) void prob_wta_kernel(
 // 2x4x16-voxel output tiles; the next tile's input is fetched into registers while the
 // current tile's 27 taps run on the MFMAs, and committed to LDS between two barriers.
 // Same fragment layouts, tap order and epilogue as conv3d_lds_kernel.
-template <int TD, int TH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv3d_c16_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
+// NWV waves per workgroup (4, or 8 = two workgroups' rows in one: the staged weights shared by twice
+// the waves, 4 waves/SIMD at <= 128 VGPRs instead of 2 workgroups x 4 waves at 2 waves/SIMD)
+template <int TD, int TH, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV == 8 ? 4 : 2))) void conv3d_c16_kernel(const float* __restrict__ x, const float* __restrict__ wpk,
                                                          const float* __restrict__ alpha,
                                                          const float* __restrict__ shift, float* __restrict__ y, Geo g,
                                                          int ntiles) {
-  constexpr int C = 16, PL = 4, NBW = TD * TH / 4;
+  constexpr int C = 16, PL = 4, NBW = TD * TH / NWV, NTH = NWV * 64;
+  static_assert(TD * TH % NWV == 0, "rows split evenly over the waves");
   constexpr int LW = 18, LH = TH + 2, LD = TD + 2, VST = 16;
   constexpr int NVOX = LD * LH * LW;
-  constexpr int NLD = (NVOX * 4 + 255) / 256;
+  constexpr int NLD = (NVOX * 4 + NTH - 1) / NTH;
   __shared__ __attribute__((aligned(16))) float tile[NVOX * VST];
   __shared__ __attribute__((aligned(16))) float wts[27 * 16 * 16];
   const int nws = (g.Wo + 15) / 16, nhs = (g.Ho + TH - 1) / TH, nds = (g.Do + TD - 1) / TD;
@@ -1069,7 +1072,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const size_t in_n = (size_t)c.n * g.Di * g.Hi * g.Wi;
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
-      const int idx = threadIdx.x + 256 * k;
+      const int idx = threadIdx.x + NTH * k;
       const int vox = idx >> 2, q = idx & 3;
       const int lw = vox % LW, rest = vox / LW, lh = rest % LH, ld = rest / LH;
       const int iw = c.ow0 - 1 + lw, ih = c.oh0 - 1 + lh, id = c.od0 - 1 + ld;
@@ -1081,12 +1084,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   auto commit = [&]() {
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
-      const int idx = threadIdx.x + 256 * k;
+      const int idx = threadIdx.x + NTH * k;
       const int vox = idx >> 2, q = idx & 3;
       if (vox < NVOX) *reinterpret_cast<float4*>(tile + vox * VST + 4 * (q ^ ((vox >> 1) & 3))) = pf[k];
     }
   };
-  for (int idx = threadIdx.x; idx < 27 * 16 * 4; idx += 256) {
+  for (int idx = threadIdx.x; idx < 27 * 16 * 4; idx += NTH) {
     const int q = idx & 3, row = (idx >> 2) & 15, tap = idx >> 6;
     const float4 v = *reinterpret_cast<const float4*>(wpk + ((size_t)tap * C + row) * C + 4 * q);
     *reinterpret_cast<float4*>(wts + (tap * 16 + row) * 16 + 4 * (q ^ ((row >> 1) & 3))) = v;
@@ -1148,7 +1151,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 
 // residency of a persistent kernel: resident workgroups per CU x CUs (queried once per kernel)
 template <typename K>
-static int persistent_grid(K kernel, long ntiles) {
+static int persistent_grid(K kernel, long ntiles, int block = 256) {
   struct Entry {
     const void* fn;
     int dev, cap;
@@ -1161,18 +1164,23 @@ static int persistent_grid(K kernel, long ntiles) {
     if (cache[i].fn == (const void*)kernel && cache[i].dev == dev) return (int)std::min<long>(ntiles, cache[i].cap);
   int cus = 0, per = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, 0);
   const int cap = std::max(8, cus * std::max(per, 1));
   if (used < 16) cache[used++] = Entry{(const void*)kernel, dev, cap};
   return (int)std::min<long>(ntiles, cap);
 }
 
+#ifndef TMVS_C16_NWV
+#define TMVS_C16_NWV 4
+#endif
 template <int TD, int TH>
 static int launch_conv_c16(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
                            const Geo& g, hipStream_t st) {
+  constexpr int NWV = TMVS_C16_NWV;
   const long ntiles = (long)B * ((g.Do + TD - 1) / TD) * ((g.Ho + TH - 1) / TH) * ((g.Wo + 15) / 16);
-  const int grid = persistent_grid(conv3d_c16_kernel<TD, TH>, ntiles);
-  hipLaunchKernelGGL((conv3d_c16_kernel<TD, TH>), dim3(grid), dim3(256), 0, st, x, w, al, sh, y, g, (int)ntiles);
+  const int grid = persistent_grid(conv3d_c16_kernel<TD, TH, NWV>, ntiles, NWV * 64);
+  hipLaunchKernelGGL((conv3d_c16_kernel<TD, TH, NWV>), dim3(grid), dim3(NWV * 64), 0, st, x, w, al, sh, y, g,
+                     (int)ntiles);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
 }
@@ -1188,17 +1196,18 @@ static int launch_conv_c16(const float* x, const float* w, const float* al, cons
 // taps are taken in pairs (a, b): lanes kgrp 0/1 read channel quads 0/1 of tap a, lanes 2/3
 // of tap b, one 16-byte read each; MFMA j contracts k = (tap, quad) over channel j of each
 // quad, and the A fragments are laid out to match (the 14th pair is half empty).
-template <int TD, int TH>
-__global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __restrict__ x,
+template <int TD, int TH, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV == 8 ? 4 : 1))) void conv3d_s2c8_tile_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ wpk,
                                                                const float* __restrict__ alpha,
                                                                const float* __restrict__ shift, float* __restrict__ y,
                                                                Geo g, int ntiles) {
-  constexpr int CIN = 8, COUT = 16, NBW = TD * TH / 4;
+  constexpr int CIN = 8, COUT = 16, NBW = TD * TH / NWV, NTH = NWV * 64;
+  static_assert(TD * TH % NWV == 0, "rows split evenly over the waves");
   // (SW = 20, which offsets the staging writes' odd-column voxels by 32 banks, measured the same: r16g)
   constexpr int LW = 33, LH = 2 * TH + 1, LD = 2 * TD + 1, SW = 17;
   constexpr int NROW = LD * LH, NQ = NROW * LW * 2;  // float4 quads per tile
-  constexpr int NLD = (NQ + 255) / 256;
+  constexpr int NLD = (NQ + NTH - 1) / NTH;
   __shared__ __attribute__((aligned(16))) float tile[NROW * 2 * SW * 8];
   __shared__ __attribute__((aligned(16))) float wts[28 * 16 * 8];
   const int nws = (g.Wo + 15) / 16, nhs = (g.Ho + TH - 1) / TH, nds = (g.Do + TD - 1) / TD;
@@ -1228,7 +1237,7 @@ __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __re
     const size_t in_n = (size_t)c.n * g.Di * g.Hi * g.Wi;
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
-      const int idx = threadIdx.x + 256 * k;
+      const int idx = threadIdx.x + NTH * k;
       const int q = idx & 1, v = idx >> 1;
       const int lw = v % LW, row = v / LW, lh = row % LH, ld = row / LH;
       const int iw = 2 * c.ow0 - 1 + lw, ih = 2 * c.oh0 - 1 + lh, id = 2 * c.od0 - 1 + ld;
@@ -1240,13 +1249,13 @@ __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __re
   auto commit = [&]() {
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
-      const int idx = threadIdx.x + 256 * k;
+      const int idx = threadIdx.x + NTH * k;
       const int q = idx & 1, v = idx >> 1;
       const int lw = v % LW, row = v / LW;
       if (idx < NQ) *reinterpret_cast<float4*>(tile + ((row * 2 + (lw & 1)) * SW + (lw >> 1)) * 8 + 4 * q) = pf[k];
     }
   };
-  for (int idx = threadIdx.x; idx < 28 * 16 * 2; idx += 256) {  // tap 27: zero (the empty half of pair 13)
+  for (int idx = threadIdx.x; idx < 28 * 16 * 2; idx += NTH) {  // tap 27: zero (the empty half of pair 13)
     const int q = idx & 1, row = (idx >> 1) & 15, tap = idx >> 5;
     const float4 v = tap < 27 ? *reinterpret_cast<const float4*>(wpk + ((size_t)tap * COUT + row) * CIN + 4 * q)
                               : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1312,12 +1321,16 @@ __global__ __launch_bounds__(256) void conv3d_s2c8_tile_kernel(const float* __re
   }
 }
 
+#ifndef TMVS_S2C8_NWV
+#define TMVS_S2C8_NWV 4
+#endif
 template <int TD, int TH>
 static int launch_conv_s2c8_tile(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
                                  const Geo& g, hipStream_t st) {
   const long ntiles = (long)B * ((g.Do + TD - 1) / TD) * ((g.Ho + TH - 1) / TH) * ((g.Wo + 15) / 16);
-  const int grid = persistent_grid(conv3d_s2c8_tile_kernel<TD, TH>, ntiles);
-  hipLaunchKernelGGL((conv3d_s2c8_tile_kernel<TD, TH>), dim3(grid), dim3(256), 0, st, x, w, al, sh, y, g,
+  constexpr int NWV = TMVS_S2C8_NWV;
+  const int grid = persistent_grid(conv3d_s2c8_tile_kernel<TD, TH, NWV>, ntiles, NWV * 64);
+  hipLaunchKernelGGL((conv3d_s2c8_tile_kernel<TD, TH, NWV>), dim3(grid), dim3(NWV * 64), 0, st, x, w, al, sh, y, g,
                      (int)ntiles);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
