@@ -59,6 +59,12 @@ __device__ __forceinline__ int dcn_slot(int P, int c) { return P * 8 + (c ^ (P &
 #ifndef TMVS_DCN_ABL
 #define TMVS_DCN_ABL 0
 #endif
+#ifndef TMVS_DCN_OB12
+#define TMVS_DCN_OB12 1  // offset-conv fragment buffers at 12 waves (A/B: 2 = read one tap ahead)
+#endif
+#ifndef TMVS_DCN_SB12
+#define TMVS_DCN_SB12 1  // single tap buffers at 12 waves (A/B: 0 = double)
+#endif
 #ifndef TMVS_DCN_PK
 #define TMVS_DCN_PK 1  // the bilinear blend on packed fp32 (A/B: 0 = scalar)
 #endif
@@ -350,7 +356,7 @@ __global__ __launch_bounds__(NW * 64) void dcn_window_kernel(const float* __rest
       // window pixel (wv + HALO + ki - 1, HALO + n + kj - 1); D lane (j, n) = channels 16m + 4j + i
       // (tap k + 1's fragments are read during tap k's MFMAs)
       floatx4_t ao[2] = {floatx4_t{0.f, 0.f, 0.f, 0.f}, floatx4_t{0.f, 0.f, 0.f, 0.f}};
-      constexpr int OB = NW > 8 ? 1 : 2;  // 3 waves/SIMD: read each tap's fragments just before it
+      constexpr int OB = NW > 8 ? TMVS_DCN_OB12 : 2;  // 3 waves/SIMD: read each tap's fragments just before it
       floatx4_t fb[OB][2], fa[OB][2][2];
       auto frag = [&](int k, int bf) {
         const int ki = k / 3, kj = k - 3 * ki;
@@ -446,7 +452,7 @@ __global__ __launch_bounds__(NW * 64) void dcn_window_kernel(const float* __rest
     floatx4_t acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = floatx4_t{0.f, 0.f, 0.f, 0.f};
-    constexpr bool SB = NW > 8;  // 3 waves/SIMD: single buffers
+    constexpr bool SB = NW > 8 && TMVS_DCN_SB12;  // 3 waves/SIMD: single buffers
     if (fast)
       dcn_taps<MT, true, Cfg::WC, SB>(acc, wl, win, recs[wv], rx, H, W, lane);
     else if (SB)
