@@ -50,16 +50,12 @@ def _pack_index(kind, cout, cin, k, device):
                                            indexing="ij")
             co, ci = 16 * m + (lane & 15), 16 * h + 4 * (lane >> 4) + e
             idx = np.where(co < cout, (co * cin + ci) * 9 + t, zero)
-        else:  # conv2d: [k-block b][m-tile][lane][e], pair idx = 4b + (l >> 4) -> (tap, channel chunk)
-            cip = max(cin, 4)
-            g = cip // 4
-            nidx = k * k * g
-            nb, mt = (nidx + 3) // 4, (cout + 15) // 16
-            b, m, lane, e = np.meshgrid(np.arange(nb), np.arange(mt), np.arange(64), np.arange(4), indexing="ij")
-            pair, co = 4 * b + (lane >> 4), 16 * m + (lane & 15)
-            tap, c = pair // g, 4 * (pair % g) + e
-            ok = (pair < nidx) & (co < cout) & (c < cin)
-            idx = np.where(ok, (co * cin + np.minimum(c, cin - 1)) * k * k + np.minimum(tap, k * k - 1), zero)
+        else:  # conv2d: the host packer itself on an index-valued weight (value i + 1 at flat index i; a
+            # packed 0 is a padding slot), so the layout -- incl. the 8-channel row-pair form -- is the C one
+            from . import ops
+            w_idx = torch.arange(1, zero + 1, dtype=torch.float32).reshape(cout, cin, k, k)  # exact below 2^24
+            packed = ops.conv2d_pack(w_idx).numpy().astype(np.int64)
+            idx = np.where(packed > 0, packed - 1, zero)
         _PACK_INDEX[key] = torch.from_numpy(idx.reshape(-1).astype(np.int64)).to(device)
     return _PACK_INDEX[key]
 
