@@ -555,6 +555,9 @@ __device__ __forceinline__ float reduce_scatter(const float* p, int k) {
 #ifndef TMVS_WARP_PMAJOR
 #define TMVS_WARP_PMAJOR 1
 #endif
+#ifndef TMVS_WARP_PAD
+#define TMVS_WARP_PAD 0
+#endif
 
 template <int C, int D, bool PARTIAL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void warp_pair_kernel(
@@ -573,6 +576,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   __shared__ float acc_lds[DPT][256];
   const int tid = threadIdx.x;
   const int HW = H * W;
+#if TMVS_WARP_PAD
+  __shared__ float pad_lds[TMVS_WARP_PAD];  // A/B only: dead LDS that caps blocks per CU
+  if (H < 0) pad_lds[tid] = 0.f;
+#endif
   const int nblk = (HW + PIX - 1) / PIX;
   const int tile = xcd_remap(blockIdx.x, nblk);
   const int lane = tid & 63;
