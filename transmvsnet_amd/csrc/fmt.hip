@@ -128,6 +128,7 @@ __global__ __launch_bounds__(256) void fmt_embed_kernel(const float* __restrict_
 // are summed in that permuted order (an exact fp32 FMA chain; the reference's BLAS order is
 // unknown anyway). VALU version of this file's history: bound by weight delivery (PMC).
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned uint4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int kfeat(int s, int g) { return 16 * (s >> 2) + 4 * g + (s & 3); }
 
@@ -421,6 +422,9 @@ __global__ __launch_bounds__(1024) void fmt_kv_combine_kernel(const float* __res
 #define TMVS_APPLY_NT 1
 #endif
 constexpr int kApplyNT = TMVS_APPLY_NT;
+#ifndef TMVS_APPLY_BUFST
+#define TMVS_APPLY_BUFST 0
+#endif
 // (amdgpu_waves_per_eu(5) fits it in 94 VGPRs without AGPRs, 5 waves/SIMD instead of 4: the 8 applies
 // measured 456.6 vs 448.1 us per step, 6 waves (80 VGPRs + scratch) 472.0 -- profiles/r11n: not kept)
 __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, int L, const float* __restrict__ kvg,
@@ -447,6 +451,7 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
   stage_afrag<32, 64, true>(w + TMVS_ENC_W2T, frag + 4096);
   __syncthreads();
   float* xv = x + (size_t)v * L * kD;
+  const auto xr = raw_rsrc(xv, (unsigned)L * kD * 4);
   const int tile0 = (blockIdx.x * 4 + wv) * tpw;
   constexpr int NT = kApplyNT;
   // two token buffers used alternately (the loop unrolled by two, so they swap by name: a
@@ -464,11 +469,13 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
     const float* vb = vec + salt;
     float* row[NT];
     bool ok[NT];
+    unsigned soff[NT];  // byte offset of the lane's token row in the view, or out of range
     floatx4 xs[NT][2];
 #pragma unroll
     for (int p = 0; p < NT; ++p) {
       const int t = (tile0 + it + p) * 16 + (lane & 15);
       ok[p] = t < L && it + p < tpw;
+      soff[p] = ok[p] ? (unsigned)t * (kD * 4) : kOffOut;
       row[p] = xv + (size_t)(t < L ? t : L - 1) * kD;
       xs[p][0] = cur[p][0];
       xs[p][1] = cur[p][1];
@@ -545,7 +552,15 @@ __global__ __launch_bounds__(256) void fmt_apply_kernel(float* __restrict__ x, i
         for (int r = 0; r < 4; ++r) xs[p][mb][r] = xs[p][mb][r] + (ff[p][mb][r] + b2[r]);
       }
       layer_norm_frag(xs[p], vb + kVLN + 2 * kD, vb + kVLN + 3 * kD, lane);
-      if (ok[p]) {
+      if (TMVS_APPLY_BUFST) {
+        // unconditional buffer stores, rows outside the wave's range at an out-of-range offset (dropped):
+        // no branch around the stores, so the next tile's wait for its prefetched tokens does not merge
+        // with a path where those loads were the last VMEM ops (which made it wait for these stores too)
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4_t, xs[p][mb]), xr,
+                                                 soff[p] == kOffOut ? kOffOut : soff[p] + (16 * mb + 4 * g) * 4, 0, 0);
+      } else if (ok[p]) {
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb)
           *reinterpret_cast<float4*>(row[p] + 16 * mb + 4 * g) =
