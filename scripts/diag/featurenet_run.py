@@ -1,5 +1,6 @@
 """FeatureNet over the 5 DTU views (batched, as TransMVSNet.forward does), K times: the command
-profiled by rocprofv3 to see where FeatureNet's time goes; prints the median HIP-event time of one forward.
+profiled by rocprofv3 to see where FeatureNet's time goes; prints the median HIP-event time of one forward
+(FNET_SAVE=path also saves the outputs).
 Usage: featurenet_run.py [K]"""
 import os, sys
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
@@ -23,5 +24,8 @@ with torch.no_grad():
         if i >= 2:
             ts.append(e0.elapsed_time(e1))
 ts.sort()
-print(os.environ.get("TMVS_LIB_PATH") or "default", f"FeatureNet {ts[len(ts) // 2]:.3f} ms (median of {K})",
+if os.environ.get("FNET_SAVE"):
+    torch.save({k: v.cpu() for k, v in f.items()}, os.environ["FNET_SAVE"])
+print(os.environ.get("TMVS_LIB_PATH") or "default", "side" if os.environ.get("TMVS_FNET_SIDE", "1") != "0" else "serial",
+      f"FeatureNet {ts[len(ts) // 2]:.3f} ms (median of {K})",
       {k: tuple(v.shape) for k, v in f.items()})
