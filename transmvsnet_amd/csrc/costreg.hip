@@ -813,6 +813,12 @@ __device__ __forceinline__ void prob_walk(__amdgpu_buffer_rsrc_t rx, int w, int 
   }
 }
 
+// prob_walk_rows' plane loop: 0 = divergent loop on the per-lane d0 (the latch copied the prefetched
+// plane between buffers after a vmcnt(0)), 1 = d0 made wave-uniform, 2 = uniform and fully unrolled
+// (r18z, bitwise the same: stage 3 89.6 -> 86.0 us, stage 2 94.7 -> 93.5 us; 1 alone 89.8 / 96.3)
+#ifndef TMVS_PROB_UNIFORM
+#define TMVS_PROB_UNIFORM 2
+#endif
 // prob_walk for NR consecutive output rows h .. h+NR-1 per wave: input plane i's rows h-1 .. h+NR are
 // loaded once (NR+2 row loads per plane instead of 3 NR: the row re-reads had the kernels address-unit
 // bound) and each row feeds the outputs it borders. Every output keeps prob_walk's FMA chains and
@@ -821,6 +827,11 @@ template <int NR, typename Emit>
 __device__ __forceinline__ void prob_walk_rows(__amdgpu_buffer_rsrc_t rx, int w, int h, int D, int H, int W, int d0,
                                                const float* __restrict__ wt, Emit emit) {
   constexpr int NL = NR + 2;
+#if TMVS_PROB_UNIFORM
+  // d0 is the wave's depth chunk: wave-uniform, but derived from threadIdx.x, so without this the plane
+  // loop is a divergent (exec-mask) loop whose latch waits vmcnt(0) for the prefetched plane
+  d0 = __builtin_amdgcn_readfirstlane(d0);
+#endif
   const unsigned offw = (unsigned)w < (unsigned)W ? (unsigned)w * 32u : kOffOut;
   auto load_plane = [&](int i, float4 (&o)[NL][2]) {
 #pragma unroll
@@ -873,8 +884,15 @@ __device__ __forceinline__ void prob_walk_rows(__amdgpu_buffer_rsrc_t rx, int w,
   };
   float4 pa[NL][2], pb[NL][2];
   load_plane(d0 - 1, pa);
+#if TMVS_PROB_UNIFORM >= 2
+  // unrolled: no loop-carried plane buffers, whose register copies at the latch waited vmcnt(0)
+#pragma unroll
+  for (int j = 0; j < kDChunk + 2; j += 2) {
+    const int i = d0 - 1 + j;
+#else
 #pragma unroll 1
   for (int i = d0 - 1; i < d0 + kDChunk + 1; i += 2) {
+#endif
     load_plane(i + 1, pb);
     plane(i, pa);
     load_plane(i + 2, pa);
