@@ -756,6 +756,10 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
 // Planes d0-1 .. d0+8 (kDChunk + 2), double-buffered: plane i+1's three rows are in flight while
 // plane i is consumed (with one row of lookahead a wave had a single load outstanding and the
 // kernels ran at 2.3-2.5 TB/s). emit(d, logit) for d = d0 .. d0+7 (the caller bounds d by D).
+// the same for prob_walk's plane loop (prob_kernel, stage 1: 38.6 -> 37.2 us, bitwise the same, r18z2)
+#ifndef TMVS_PROB1_UNIFORM
+#define TMVS_PROB1_UNIFORM 1
+#endif
 template <typename Emit>
 __device__ __forceinline__ void prob_walk(__amdgpu_buffer_rsrc_t rx, int w, int h, int D, int H, int W, int d0,
                                           const float* __restrict__ wt, Emit emit) {
@@ -803,9 +807,18 @@ __device__ __forceinline__ void prob_walk(__amdgpu_buffer_rsrc_t rx, int w, int 
     c12 = float2_v{acc_next, c12.x};
   };
   float4 pa[3][2], pb[3][2];
+#if TMVS_PROB1_UNIFORM
+  d0 = __builtin_amdgcn_readfirstlane(d0);  // as in prob_walk_rows (TMVS_PROB_UNIFORM)
+#endif
   load_plane(d0 - 1, pa);
+#if TMVS_PROB1_UNIFORM
+#pragma unroll
+  for (int j = 0; j < kDChunk + 2; j += 2) {
+    const int i = d0 - 1 + j;
+#else
 #pragma unroll 1
   for (int i = d0 - 1; i < d0 + kDChunk + 1; i += 2) {  // planes i (in pa) and i + 1 (in pb)
+#endif
     load_plane(i + 1, pb);
     plane(i, pa);
     load_plane(i + 2, pa);  // (past the last plane: rows the next chunk reads anyway)
@@ -815,7 +828,8 @@ __device__ __forceinline__ void prob_walk(__amdgpu_buffer_rsrc_t rx, int w, int 
 
 // prob_walk_rows' plane loop: 0 = divergent loop on the per-lane d0 (the latch copied the prefetched
 // plane between buffers after a vmcnt(0)), 1 = d0 made wave-uniform, 2 = uniform and fully unrolled
-// (r18z, bitwise the same: stage 3 89.6 -> 86.0 us, stage 2 94.7 -> 93.5 us; 1 alone 89.8 / 96.3)
+// (r18z, bitwise the same: stage 3 89.6 -> 86.0 us, stage 2 94.7 -> 93.5 us; 1 alone 89.8 / 96.3; the
+// same build re-run on another box in r18z2: 89.2 / 93.0 -- box-to-box spread of about 3 %)
 #ifndef TMVS_PROB_UNIFORM
 #define TMVS_PROB_UNIFORM 2
 #endif
