@@ -106,7 +106,11 @@ __device__ __forceinline__ float act(float v, float lo) { return v > lo ? v : lo
 #ifndef TMVS_LDS_SGB
 #define TMVS_LDS_SGB 1
 #endif
-template <int CIN, int COUT, int S, int TD, int TH, int MBB, int WS = 1, bool KDSKIP = false>
+// TAPOUT: every channel chunk's tile is staged at once and the K walk runs taps outer, chunks inner --
+// conv3d_direct_kernel's order (tap, chunk, lane channel), so the sums are that kernel's bit for bit; the
+// default walks chunks outer (one chunk's tile in LDS at a time), which re-associates the K sum when
+// CIN > 16. TAPOUT needs TD = 1 (the kd slices in the depth padding are skipped per workgroup, exact zeros).
+template <int CIN, int COUT, int S, int TD, int TH, int MBB, int WS = 1, bool KDSKIP = false, bool TAPOUT = false>
 #ifndef TMVS_LDS_WPE
 #define TMVS_LDS_WPE 3
 #endif
@@ -130,7 +134,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
   constexpr int VST = SWZ ? 16 : CK + 4;
   constexpr int NVOX = LD * LH * LW;
   static_assert(MB % MBB == 0, "tile");
-  __shared__ __attribute__((aligned(16))) float tile[NVOX * VST];
+  static_assert(!TAPOUT || (TD == 1 && !KDSKIP), "TAPOUT: one output slice per workgroup, its own kd skip");
+  __shared__ __attribute__((aligned(16))) float tile[(TAPOUT ? CIN / CK : 1) * NVOX * VST];
 
   const int nws = (g.Wo + 15) / 16, nhs = (g.Ho + TH - 1) / TH, nds = (g.Do + TD - 1) / TD;
   int t = xcd_remap(blockIdx.x, gridDim.x);  // contiguous tiles per XCD: halos share an L2
@@ -161,7 +166,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
   const Buf xb(x + in_n * CIN, (uint32_t)g.Di * g.Hi * g.Wi * CIN * 4);  // this sample (host: < 2 GB)
   const Buf wb(wpk, 27u * COUT * CIN * 4);
   float4 pf[NLD];
-  auto fetch = [&](int ch) {
+  auto fetch_to = [&](int ch, float4(&dst)[NLD]) {
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
       const int idx = threadIdx.x + 256 * k;
@@ -172,18 +177,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
       // block and the compiler's vmcnt waits count them exactly (a branch per load made it wait
       // vmcnt(0) every third tap, exposing the L2 latency of the two-tap-ahead weight loads)
       const bool ok = idx < NVOX * PL && iw >= 0 && iw < g.Wi && ih >= 0 && ih < g.Hi && id >= 0 && id < g.Di;
-      pf[k] = xb.ld4(ok ? (((id * g.Hi + ih) * g.Wi + iw) * CIN + 4 * q) * 4 : Buf::kOOB, ch * CK * 4);
+      dst[k] = xb.ld4(ok ? (((id * g.Hi + ih) * g.Wi + iw) * CIN + 4 * q) * 4 : Buf::kOOB, ch * CK * 4);
     }
   };
-  auto commit = [&]() {
+  auto fetch = [&](int ch) { fetch_to(ch, pf); };
+  auto commit_from = [&](const float4(&src)[NLD], float* base) {
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
       const int idx = threadIdx.x + 256 * k;
       const int vox = idx / PL, q = idx - vox * PL;
       const int qs = SWZ ? (q ^ ((vox >> 1) & 3)) : q;
-      if (idx < NVOX * PL) *reinterpret_cast<float4*>(tile + vox * VST + 4 * qs) = pf[k];
+      if (idx < NVOX * PL) *reinterpret_cast<float4*>(base + vox * VST + 4 * qs) = src[k];
     }
   };
+  auto commit = [&]() { commit_from(pf, tile); };
   // KDSKIP (launched only for output depth <= 2, where every wave has one): the kd slices whose
   // input plane lies wholly in the depth padding of the wave's output slice are not run (their
   // products are exact zeros). The taps then run as a loop over the kept slices (9 unrolled taps
@@ -214,16 +221,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
   VecN<PL> aw[3][MBW];
   // one tap: B fragments from the LDS tile, NBW x MBB x PL MFMAs
   // B fragments of one tap from the LDS tile
-  auto bload = [&](int kd, int kh, int kw, VecN<PL>(&b)[NBW]) {
+  auto bload_at = [&](const float* base, int kd, int kh, int kw, VecN<PL>(&b)[NBW]) {
 #pragma unroll
     for (int r = 0; r < NBW; ++r) {
       const int rr = rg * NBW + r;
       const int odl = rr / TH, ohl = rr - odl * TH;
       const int lvox = ((odl * S + kd) * LH + ohl * S + kh) * LW + col * S + kw;
       const int qs = SWZ ? (kgrp ^ ((lvox >> 1) & 3)) : kgrp;
-      b[r].load(tile + lvox * VST + qs * PL);
+      b[r].load(base + lvox * VST + qs * PL);
     }
   };
+  auto bload = [&](int kd, int kh, int kw, VecN<PL>(&b)[NBW]) { bload_at(tile, kd, kh, kw, b); };
   // one tap: NBW x MBB x PL MFMAs on fragments already in registers
   auto tap_mfma = [&](const VecN<PL>* a, const VecN<PL>* b) {
     if (TMVS_LDS_ABL & 8) {  // timing ablation only: no MFMAs (one FMA keeps the loads live)
@@ -251,6 +259,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
   // B of tap t + 1 is read from LDS before tap t's MFMAs (TMVS_LDS_BPF; read right before its own
   // MFMAs its latency sat between every tap's MFMA groups)
   VecN<PL> bw[2][NBW];
+  if constexpr (TAPOUT) {
+    // all chunks staged (every chunk's loads in flight before the first commit), then per kept kd slice
+    // 9 taps x NCH chunks as one step sequence with the same two-step weight / one-step B lookahead
+    float4 pfc[NCH][NLD];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) fetch_to(ch, pfc[ch]);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) commit_from(pfc[ch], tile + ch * NVOX * VST);
+    __syncthreads();
+    const int id_base = od0 * S - 1;  // input slice of kd = 0 (workgroup-uniform: TD = 1)
+    const int klo = id_base < 0 ? -id_base : 0;
+    const int khi = od0 >= g.Do ? -1 : (g.Di - 1 - id_base < 2 ? g.Di - 1 - id_base : 2);
+    constexpr int NS = 9 * NCH;  // steps per slice; a multiple of 3, so the weight ring lines up across slices
+    auto wstep = [&](int kd, int s, VecN<PL>(&a)[MBW]) { wload(s % NCH, kd * 9 + s / NCH, a); };
+    auto bstep = [&](int kd, int s, VecN<PL>(&b)[NBW]) {
+      const int t9 = s / NCH;
+      bload_at(tile + (s % NCH) * NVOX * VST, kd, t9 / 3, t9 % 3, b);
+    };
+    if (klo <= khi) {
+      wstep(klo, 0, aw[0]);
+      wstep(klo, 1, aw[1]);
+    }
+#pragma unroll 1
+    for (int kd = klo; kd <= khi; ++kd) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        if (s + 2 < NS)
+          wstep(kd, s + 2, aw[(s + 2) % 3]);
+        else if (kd < khi)  // uniform: the next slice's first two steps
+          wstep(kd + 1, s + 2 - NS, aw[(s + 2) % 3]);
+        if (s == 0) bstep(kd, 0, bw[0]);
+        if (s + 1 < NS) bstep(kd, s + 1, bw[(s + 1) & 1]);
+        tap_mfma(aw[s % 3], bw[s & 1]);
+      }
+    }
+  } else {
   // The next chunk's tile is requested right after the chunk's last weight load (3 taps before
   // its end), not ahead of the chunk's first: vmcnt retires loads in issue order, so any weight
   // load issued behind the tile loads waits for them (fetching at the chunk's start measured the
@@ -313,6 +357,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMVS_LDS_WP
 #pragma unroll 1
   for (int ch = 0; ch + 1 < NCH; ++ch) chunk(ch, std::true_type{});
   chunk(NCH - 1, std::false_type{});
+  }
   const int ow = ow0 + col;
   if (ow >= g.Wo) return;
   const size_t out_n = (size_t)n * g.Do * g.Ho * g.Wo;
@@ -1388,6 +1433,17 @@ static int launch_conv(const float* x, const float* w, const float* al, const fl
   return TMVS_OK;
 }
 
+template <int CIN, int COUT, int S, int TD, int TH, int MBB, int WS>
+static int launch_conv_tapout(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
+                              const Geo& g, hipStream_t st) {
+  constexpr int MG = ((COUT + 15) / 16) / MBB;
+  const long nblk = (long)B * ((g.Do + TD - 1) / TD) * ((g.Ho + TH - 1) / TH) * ((g.Wo + 15) / 16) * MG;
+  hipLaunchKernelGGL((conv3d_lds_kernel<CIN, COUT, S, TD, TH, MBB, WS, false, true>), dim3((unsigned)nblk), dim3(256), 0,
+                     st, x, w, al, sh, y, g);
+  TMVS_CHECK_LAUNCH();
+  return TMVS_OK;
+}
+
 template <int CIN, int COUT, int S, int NBW, int MBW>
 static int launch_conv_direct(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
                               const Geo& g, hipStream_t st) {
@@ -1679,9 +1735,17 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
 #endif
   // conv5 through the wave-split LDS kernel: 52.6 -> 30.4 / 24.0 -> 15.5 / 24.2 -> 19.1 us (stages 2 / 1 / 3)
   // against the direct kernel's best tilings (2 rows x 2 blocks per wave on the stage-2/3 grids, 2 x 1 on
-  // stage 1; r12r, r12s, r17j); chunk-outer K order, so its sums differ from the direct form's in the
-  // last bits (3e-6)
-  if (cin == 32 && cout == 64 && stride == 2) return launch_conv<32, 64, 2, TMVS_C5_LDS>(x, wpk, al, sh, y, B, g, st);
+  // stage 1; r12r, r12s, r17j). TMVS_C5_MODE 2 (default): both 16-channel chunks staged, taps outer -- the
+  // direct kernel's K order, so its sums bit for bit (round 6); 1: chunk-outer (round 5: re-associated
+  // sums, one stage-2 near-tie flip at C2 cascading into 23 stage-3 pixels); 0: the direct kernel.
+#ifndef TMVS_C5_MODE
+#define TMVS_C5_MODE 2
+#endif
+  if (cin == 32 && cout == 64 && stride == 2) {
+    if constexpr (TMVS_C5_MODE == 2) return launch_conv_tapout<32, 64, 2, TMVS_C5_LDS>(x, wpk, al, sh, y, B, g, st);
+    if constexpr (TMVS_C5_MODE == 1) return launch_conv<32, 64, 2, TMVS_C5_LDS>(x, wpk, al, sh, y, B, g, st);
+  }
+  TMVS_CONV_DIRECT(32, 64, 2, 1)
 #undef TMVS_CONV_DIRECT
   return TMVS_ERR_SHAPE;
 }

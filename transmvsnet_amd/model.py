@@ -368,12 +368,13 @@ class TransMVSNet(nn.Module):
         # from depth_values[0] for every sample (models/TransMVSNet.py:146-148). Samples are independent:
         # with B > 1 each runs on its own stream (sample 0 on the caller's), so one sample's small
         # coarse-level grids overlap another's kernels; the caller's stream then waits for all of them.
-        # (not inside a HIP-graph capture: a multi-stream fork/join of the samples there crashed the
-        # capture's end on the box, r16g -- a captured B > 1 step runs its samples in order on the
-        # capturing stream; to replay samples concurrently, capture one graph per sample and replay them
-        # on separate streams, as bench.py's batch2_concurrent line does)
-        concurrent = (b > 1 and self.batch_streams and view_shard is None and not self.decomposed
-                      and not torch.cuda.is_current_stream_capturing())
+        # Inside a HIP-graph capture the fork/join is captured too: each sample stream joins the capture by
+        # waiting on an event of the capturing stream, its pathway side stream (one per sample slot) by
+        # waiting on the sample stream, and every one of them is joined back before the capture ends.
+        # (Round 5 turned this off after a segfault of `rocprofv3 --kernel-trace -- bench.py` while the
+        # bench captured a B = 2 step, gpurun_out/r16c/ab.txt; round 6 re-enabled it behind
+        # test_batch2_full_size_capture_equals_eager)
+        concurrent = b > 1 and self.batch_streams and view_shard is None and not self.decomposed
         main = torch.cuda.current_stream(dev)
         if concurrent:
             start = torch.cuda.Event()
