@@ -255,7 +255,7 @@ def test_dcn_backward_set_matches_accumulate_form(scale):
     for _ in range(2):
         dx, dom, dw = ops.dcn_backward_set(x, om.contiguous(), wt, dy)
         torch.cuda.synchronize()
-        far = ops._DCN_FAR[(str(x.device), tuple(x.shape))]
+        far = ops._DCN_FAR[(str(x.device), tuple(x.shape))][0]
         assert float(far.abs().max()) == 0.0
         assert torch.equal(dom, dom_ref) and torch.equal(dw, dw_ref)
         if scale <= 0.3:
@@ -263,6 +263,32 @@ def test_dcn_backward_set_matches_accumulate_form(scale):
         else:
             err = float((dx - dx_ref).abs().max()) / float(dx_ref.abs().max())
             assert err <= 1e-6, err
+
+
+def test_dcn_backward_set_first_call_inside_capture_raises():
+    """The far buffer of a new shape is allocated and zeroed outside any HIP-graph capture: a first call for a
+    shape inside a capture raises (a fill recorded in the graph would run per replay, and an eager call before
+    the first replay would read an unfilled buffer); after one eager call the same shape captures."""
+    from transmvsnet_amd.featurenet_train import _taps
+    torch.manual_seed(12)
+    b, h, w, cout = 1, 14, 22, 8
+    x = torch.randn(b, h, w, 32, device=DEV)
+    om = torch.randn(b, 27, h, w, device=DEV).contiguous()
+    wt = _taps(torch.randn(cout, 32, 3, 3) * 0.06).to(DEV)
+    dy = torch.randn(b, h, w, cout, device=DEV)
+    assert (str(x.device), tuple(x.shape)) not in ops._DCN_FAR
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(RuntimeError, match="outside any capture"):
+        with torch.cuda.graph(g):
+            ops.dcn_backward_set(x, om, wt, dy)
+    dx0, _, _ = ops.dcn_backward_set(x, om, wt, dy)  # eager: creates the buffer
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        dx1, _, _ = ops.dcn_backward_set(x, om, wt, dy)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1)
 
 
 def test_dcn_backward_nonfinite_dy_poisons_dx():

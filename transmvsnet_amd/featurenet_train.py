@@ -97,13 +97,30 @@ def device_pack(kind, w):
 # ------------------------------------------------------------------------- the step's weight packs
 # Every weight re-layout a FeatureNet step needs (forward packs, data-gradient packs, tap transposes) is
 # gathered ONCE per forward by _prepare_packs (packing.gather_packs: one cat + one index gather instead of
-# ~130 small cat / index / flip / permute launches); the layer functions look their packs up here and
-# fall back to packing on the spot for a weight not in the table.
+# ~130 small cat / index / flip / permute launches); the layer functions look their packs up in the active
+# table and fall back to packing on the spot for a weight not in it. Each forward's table is kept on its
+# autograd context and made active again for its own backward (_active_packs), so a backward always uses the
+# packs of the weights its forward ran with, whatever other forwards ran in between.
 _STEP_PACKS = {}
 
 
 def _pk(key):
     return _STEP_PACKS.get(key)
+
+
+class _active_packs:
+    """with _active_packs(table): the layer functions' _pk lookups read `table` (restored on exit)."""
+
+    def __init__(self, table):
+        self.table = table
+
+    def __enter__(self):
+        global _STEP_PACKS
+        self.prev, _STEP_PACKS = _STEP_PACKS, self.table
+
+    def __exit__(self, *a):
+        global _STEP_PACKS
+        _STEP_PACKS = self.prev
 
 
 def _pack_fn(kind, co, ci, k):
@@ -120,11 +137,12 @@ def _dgrad_kind(co, ci, k):
 
 
 def _prepare_packs(fnet):
-    """Fill _STEP_PACKS with one gather_packs call for the whole FeatureNet (TMVS_NO_STEP_PACKS=1: leave it
-    empty -- every layer packs on the spot, the previous form; for bitwise A/Bs)."""
-    _STEP_PACKS.clear()
+    """A new pack table (one gather_packs call for the whole FeatureNet) made active for the forward
+    (TMVS_NO_STEP_PACKS=1: empty -- every layer packs on the spot, the previous form; for bitwise A/Bs)."""
+    global _STEP_PACKS
+    table = _STEP_PACKS = {}
     if os.environ.get("TMVS_NO_STEP_PACKS") == "1":
-        return
+        return table
     tensors, specs, keys = [], [], []
 
     def add(t, fn, key):
@@ -175,7 +193,8 @@ def _prepare_packs(fnet):
     # its index on the tensors' shapes, and the specs name their own tensor
     outs = gather_packs(tensors, specs, "featurenet_train")
     for key, o in zip(keys, outs):
-        _STEP_PACKS[key] = o
+        table[key] = o
+    return table
 
 
 def _taps(w):
@@ -376,7 +395,7 @@ def _inner_bwd(conv, d, lat, grads):
 class _FeatureNetTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, imgs, fnet, tape, *params):
-        _prepare_packs(fnet)
+        ctx.packs = _prepare_packs(fnet)
         x = imgs.float().contiguous()
         c00, r00 = _block_fwd(tape, fnet.conv0[0], x, 3, 1, nchw_input=True)
         conv0, r01 = _block_fwd(tape, fnet.conv0[1], c00, 3, 1)
@@ -399,6 +418,11 @@ class _FeatureNetTrain(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, d1, d2, d3):
+        with _active_packs(ctx.packs):  # this forward's packs, not the most recent forward's
+            return _FeatureNetTrain._backward(ctx, d1, d2, d3)
+
+    @staticmethod
+    def _backward(ctx, d1, d2, d3):
         r00, r01, r10, r11, r12, r20, r21, r22, h1, h2, h3 = ctx.recs
         conv0, conv1 = ctx.lat
         fnet = ctx.fnet

@@ -1124,7 +1124,9 @@ _DCN_FAR = {}
 def dcn_backward_set(x_nhwc, offset_mask, w_taps, dy_nhwc):
     """tmvs_dcn_backward_set: -> (dx [B,H,W,32] written, not accumulated; dom; dw_taps). The corners beyond the
     LDS windows go through a zeroed far buffer kept per (device, shape) and cleared again by the call, so no
-    activation-sized zero fill runs per call (one buffer per shape: calls on one stream only)."""
+    activation-sized zero fill runs per call. One buffer per shape: an eager call on another stream waits for
+    the previous call's stream (event), and the buffer is created outside any HIP-graph capture (raises if a
+    shape is first seen while capturing)."""
     for t, n in ((x_nhwc, "x_nhwc"), (offset_mask, "offset_mask"), (w_taps, "w_taps"), (dy_nhwc, "dy_nhwc")):
         _dev(t, n)
     b, h, w, cin = x_nhwc.shape
@@ -1133,9 +1135,18 @@ def dcn_backward_set(x_nhwc, offset_mask, w_taps, dy_nhwc):
             tuple(w_taps.shape) != (9, cout, cin):
         raise ValueError("dcn_backward_set: shape mismatch")
     key = (str(x_nhwc.device), tuple(x_nhwc.shape))
-    far = _DCN_FAR.get(key)
-    if far is None:
-        far = _DCN_FAR[key] = torch.zeros_like(x_nhwc)
+    capturing = torch.cuda.is_current_stream_capturing()
+    ent = _DCN_FAR.get(key)
+    if ent is None:
+        if capturing:  # a zero fill recorded in the graph would run per replay, and an eager call before the
+            # first replay would read an unfilled buffer: the buffer must exist before the capture
+            raise RuntimeError("dcn_backward_set: first call for this shape inside a HIP-graph capture; run one eager "
+                               "step first (the far buffer is allocated and zeroed outside any capture)")
+        ent = _DCN_FAR[key] = [torch.zeros_like(x_nhwc), None, None]  # buffer, last stream, its done event
+    far = ent[0]
+    cur = torch.cuda.current_stream(x_nhwc.device)
+    if not capturing and ent[1] is not None and ent[1] != cur:  # a call on another stream: order after its use
+        cur.wait_event(ent[2])
     ws = torch.empty(_lib_h().tmvs_dcn_backward_workspace(b, cout, h, w) // 4 + 64, device=x_nhwc.device)
     dx = torch.empty_like(x_nhwc)
     dom = torch.empty(b, h, w, 32, device=x_nhwc.device)
@@ -1144,6 +1155,10 @@ def dcn_backward_set(x_nhwc, offset_mask, w_taps, dy_nhwc):
         _lib.check(_lib_h().tmvs_dcn_backward_set(_ptr(x_nhwc), _ptr(offset_mask), _ptr(w_taps), _ptr(dy_nhwc), b, cin,
                                                   cout, h, w, _ptr(ws), ws.numel() * 4, _ptr(dx), _ptr(dom), _ptr(dw),
                                                   _ptr(far), _stream()), "tmvs_dcn_backward_set")
+    if not capturing:
+        ev = ent[2] or torch.cuda.Event()
+        ev.record(cur)
+        ent[1], ent[2] = cur, ev
     return dx, dom, dw
 
 

@@ -37,7 +37,6 @@ Tensor layout is NDHWC throughout; weight re-layouts are index permutations (pac
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 
 from . import ops
 from .bn_running import update_running_stats
@@ -817,6 +816,10 @@ class FlatAdam:
             # optimizer); an eager step writes its own lr first.
             self._graphed = True
             if capturing:
+                # an explicit lr becomes the optimizer's: TrainStepGraph.replay syncs opt.lr into _lr_dev before
+                # every replay, so the captured step keeps applying it (a raw torch.cuda.graph replay must call
+                # sync_lr itself: the launch reads whatever _lr_dev holds)
+                self.lr = lr
                 if _TSG_CAPTURES:
                     CAPTURED_OPTIMIZERS.append(self)
             else:
