@@ -369,11 +369,10 @@ class TransMVSNet(nn.Module):
         # with B > 1 each runs on its own stream (sample 0 on the caller's), so one sample's small
         # coarse-level grids overlap another's kernels; the caller's stream then waits for all of them.
         # Inside a HIP-graph capture the fork/join is captured too: each sample stream joins the capture by
-        # waiting on an event of the capturing stream, its pathway side stream (one per sample slot) by
-        # waiting on the sample stream, and every one of them is joined back before the capture ends.
-        # (Round 5 turned this off after a segfault of `rocprofv3 --kernel-trace -- bench.py` while the
-        # bench captured a B = 2 step, gpurun_out/r16c/ab.txt; round 6 re-enabled it behind
-        # test_batch2_full_size_capture_equals_eager)
+        # waiting on an event of the capturing stream and is joined back before the capture ends; only the
+        # caller's stream forks the FMT pathway's side stream (one fork level, _forward_one). (Round 5 turned
+        # this off after a segfault at capture end; round 6 located it -- a two-level fork, the sample stream's
+        # own pathway side stream, crashes hipStreamEndCapture -- DESIGN.md 7, tests/test_gpu_batch.py.)
         concurrent = b > 1 and self.batch_streams and view_shard is None and not self.decomposed
         main = torch.cuda.current_stream(dev)
         if concurrent:
@@ -424,7 +423,11 @@ class TransMVSNet(nn.Module):
         n, _, h1, w1 = s1.shape
         tokens = self._fmt(s1, prep)
         st1 = tokens.view(n, h1, w1, 32)
-        overlap = self.overlap_pathway and not self.decomposed
+        # the pathway's side stream forks only from the caller's stream (slot 0): a sample on its own stream
+        # (slot > 0, B > 1) runs the pathway in line, so no stream forks from an already-forked stream -- a
+        # HIP-graph capture of such a two-level fork (sample stream -> its side stream) segfaulted inside
+        # hipStreamEndCapture on the box (r20a); the samples themselves still overlap each other
+        overlap = self.overlap_pathway and not self.decomposed and slot == 0
         lateral = {}
 
         def pathway():
