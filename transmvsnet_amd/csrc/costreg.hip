@@ -1675,6 +1675,9 @@ static int launch_deconv_c8(const float* x, const float* w, const float* al, con
 #ifndef TMVS_FUSE_DP
 #define TMVS_FUSE_DP 1
 #endif
+#ifndef TMVS_DP_ROLE
+#define TMVS_DP_ROLE 0
+#endif
 template <int THI>
 __global__ __launch_bounds__(THI * 128) void deconv_prob_kernel(
     const float* __restrict__ x, const float* __restrict__ wpk, const float* __restrict__ alpha,
@@ -1696,8 +1699,12 @@ __global__ __launch_bounds__(THI * 128) void deconv_prob_kernel(
   const int band = t % nb;
   const int n = t / nb;
   const int mh0 = band * (THI - 1) - 1, m0 = cs * 15 - 1;  // first input row / column (may be -1)
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool mfma_role = wv < THI;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // role and index within it: TMVS_DP_ROLE 0 = waves 0..THI-1 MFMA, the rest walk; 1 = even / odd waves;
+  // 2 = alternating groups of 4 waves (the placement that puts both roles on every SIMD, scripts/micro/wave_simd)
+  const bool mfma_role = TMVS_DP_ROLE == 0 ? wid < THI : TMVS_DP_ROLE == 1 ? !(wid & 1) : !((wid >> 2) & 1);
+  const int wv = TMVS_DP_ROLE == 0 ? (wid < THI ? wid : wid - THI)
+                 : TMVS_DP_ROLE == 1 ? wid >> 1 : ((wid >> 3) << 2) + (wid & 3);
   const size_t plane_sz = (size_t)Hr * Wr;
 
   for (int idx = threadIdx.x; idx < 27 * 8 * 4; idx += 2 * NTM) {
@@ -1713,7 +1720,7 @@ __global__ __launch_bounds__(THI * 128) void deconv_prob_kernel(
     auto fetch = [&](int md) {  // input plane md (zeros outside the volume) -> registers
 #pragma unroll
       for (int k = 0; k < NLD; ++k) {
-        const int idx = threadIdx.x + NTM * k;
+        const int idx = wv * 64 + lane + NTM * k;  // the role-local thread index
         const int vox = idx >> 2, q = idx & 3;
         const int lw = vox % LW, lh = vox / LW;
         const int iw = m0 + lw, ih = mh0 + lh;
@@ -1725,7 +1732,7 @@ __global__ __launch_bounds__(THI * 128) void deconv_prob_kernel(
     auto commit = [&](float* buf) {
 #pragma unroll
       for (int k = 0; k < NLD; ++k) {
-        const int idx = threadIdx.x + NTM * k;
+        const int idx = wv * 64 + lane + NTM * k;  // the role-local thread index
         const int vox = idx >> 2, q = idx & 3;
         if (vox < NVP) *reinterpret_cast<float4*>(buf + vox * VST + 4 * (q ^ ((vox >> 1) & 3))) = pf[k];
       }
@@ -1809,7 +1816,7 @@ __global__ __launch_bounds__(THI * 128) void deconv_prob_kernel(
     }
   } else {
     // ------------------------------------------------------------ the prob walk role
-    const int vw = wv - THI;
+    const int vw = wv;
     const int lr = 1 + 2 * vw + (lane >> 5), c = lane & 31;  // logit row of the band, x11 column
     const int grow = 2 * mh0 + lr, gcol = 2 * m0 + c;
     const bool emits = vw < THI - 1 && c >= 1 && c <= 30 && (unsigned)grow < (unsigned)Hr && (unsigned)gcol < (unsigned)Wr;
