@@ -1678,6 +1678,9 @@ static int launch_deconv_c8(const float* x, const float* w, const float* al, con
 #ifndef TMVS_DP_ROLE
 #define TMVS_DP_ROLE 0
 #endif
+#ifndef TMVS_DP_ABL
+#define TMVS_DP_ABL 0  // timing ablations only (wrong results): 1 no prob walk, 2 no MFMAs, 4 no skip loads
+#endif
 template <int THI>
 __global__ __launch_bounds__(THI * 128) void deconv_prob_kernel(
     const float* __restrict__ x, const float* __restrict__ wpk, const float* __restrict__ alpha,
@@ -1764,7 +1767,7 @@ __global__ __launch_bounds__(THI * 128) void deconv_prob_kernel(
         for (int pdh = 0; pdh < 4; ++pdh) {  // skip (conv0) at planes 2md + pd, rows 2mh + ph, this column
           const int orow = 2 * mh + (pdh & 1);
           ok[pdh] = col_ok && (unsigned)orow < (unsigned)Hr;
-          sk[pdh] = ok[pdh] ? *reinterpret_cast<const float4*>(
+          sk[pdh] = ok[pdh] && !(TMVS_DP_ABL & 4) ? *reinterpret_cast<const float4*>(
                                   skip + (out_n + ((size_t)(2 * md + (pdh >> 1)) * Hr + orow) * Wr + ocol) * 8 + cq)
                             : make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -1792,6 +1795,10 @@ __global__ __launch_bounds__(THI * 128) void deconv_prob_kernel(
               VecN<PL> b1, b2;
               b1.load(cur + lv * VST + 4 * (kgrp ^ ((lv >> 1) & 3)));
               b2.load(cur + (lv + 1) * VST + 4 * (kgrp ^ (((lv + 1) >> 1) & 3)));
+              if (TMVS_DP_ABL & 2) {
+                acc[pdh][0] += a1.v[0] * b1.v[0] + a2.v[0] * b2.v[0];
+                continue;
+              }
 #pragma unroll
               for (int j = 0; j < PL; ++j)
                 acc[pdh] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.v[j], b1.v[j], acc[pdh], 0, 0, 0);
@@ -1854,7 +1861,7 @@ __global__ __launch_bounds__(THI * 128) void deconv_prob_kernel(
     __syncthreads();  // the MFMA role's initial staging
 #pragma unroll 1
     for (int md = 0; md <= g.Di; ++md) {
-      if (md >= 1 && vw < THI - 1) {
+      if (md >= 1 && vw < THI - 1 && !(TMVS_DP_ABL & 1)) {
         const int sb = (md - 1) & 1;
         walk_plane(xo[sb][0], 2 * md - 2, false);
         walk_plane(xo[sb][1], 2 * md - 1, false);
