@@ -275,10 +275,9 @@ def test_deconv3d_layers(sd, model, layer, idx):
                                      (64, 16, 72, 1), (16, 40, 128, 1), (24, 8, 8, 2), (32, 432, 576, 1),
                                      (8, 864, 1152, 1)])
 def test_costregnet_wta_equals_costregnet_then_softmax(model, d, h, w, b):
-    """tmvs_costregnet_wta (D <= 32: conv11 + skip + prob conv in one kernel, deconv_prob_kernel -- x11 never
-    written -- then the softmax/WTA kernel; D = 48/64: conv11, the depth-chunked prob kernel, softmax) ==
-    tmvs_costregnet (conv11 written by deconv3d_c8_kernel, read by the prob kernel) -> tmvs_softmax_wta, bit for
-    bit; ragged bands / column segments, tiny volumes, B = 2 and the DTU stage-2/3 sizes."""
+    """tmvs_costregnet_wta (prob conv + softmax/WTA in one kernel for D <= 32; the depth-chunked
+    prob kernel + softmax kernel for 48/64) == tmvs_costregnet -> tmvs_softmax_wta, bit for bit (ragged
+    shapes, tiny volumes, B = 2 and the DTU stage-2/3 sizes)."""
     g = torch.Generator().manual_seed(d * 1000 + h)
     x = torch.randn(b, d, h, w, generator=g).to(DEV)
     hyp = (425.0 + torch.rand(b, d, h, w, generator=g).mul(510.0)).sort(dim=1).values.to(DEV)

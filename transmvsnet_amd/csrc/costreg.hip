@@ -1647,242 +1647,6 @@ static int launch_deconv_c8(const float* x, const float* w, const float* al, con
   return TMVS_OK;
 }
 
-// ---------------------------------------------------------------- conv11 + skip + prob, fused (stages 2/3)
-// models/module.py:452-455: x11 = conv0 + conv11(x9) (ConvTranspose3d 16 -> 8 + BN + ReLU), then the
-// 8 -> 1 prob conv. The 8-channel full-resolution x11 (255 MB per DTU stage-2/3 call, written by
-// deconv3d_c8_kernel and read back by the prob walk) never reaches HBM: a workgroup owns a band of rows x
-// a 32-column segment of x11 and walks the whole depth, two x11 planes per step (one input plane md:
-// outputs 2md, 2md+1), x11 held in LDS; the prob walk of the band's logits consumes each plane after it is
-// produced, its FMA chain state (prob_walk's c12 / acc_next) carried in registers from step to step.
-// Bands overlap by one x11 row / column on each side (the prob conv's halo, recomputed: 2 THI rows and
-// 32 columns of x11 for (2 THI - 2) x 30 logits), so the logits of every pixel come from one workgroup.
-// Per output, the deconv's MFMA sequence is deconv3d_c8_kernel's and the prob chain is prob_walk's, so
-// x11 and the logits are bit for bit those of the two-kernel form; the logits go to HBM ([D][H][W], 1/8 of
-// x11) for the softmax / WTA kernel.
-// Two wave roles, software-pipelined by one step so the matrix cores and the vector ALUs of a SIMD work at
-// the same time (one barrier per step; x11 double-buffered):
-//   * THI "MFMA" waves: wave w runs input row mh0 + w of step md through the MFMAs (all 8 output parity
-//     classes of it, as deconv3d_c8_kernel's row r), adds the skip and writes its x11 rows to xo[md & 1];
-//     they also stage the input planes (a 3-plane ring) and read the skip;
-//   * THI "walk" waves: wave v < THI - 1 walks the x11 planes of step md - 1 from xo[(md - 1) & 1] for logit
-//     rows 1 + 2v, 2 + 2v of the band (lanes 0-31 / 32-63 = one row each, lane & 31 = x11 column; kw
-//     neighbours by wave-wide DPP shifts, whose wrap between the two rows lands on halo columns only).
-// (The first form ran both roles on every wave in barrier-separated phases: 219 / 188 us at stages 2 / 3
-// against 112 + 93 / 112 + 85 us for the two kernels, r20b.)
-#ifndef TMVS_DP_THI
-#define TMVS_DP_THI 8
-#endif
-#ifndef TMVS_FUSE_DP
-#define TMVS_FUSE_DP 1
-#endif
-#ifndef TMVS_DP_ROLE
-#define TMVS_DP_ROLE 0
-#endif
-#ifndef TMVS_DP_ABL
-#define TMVS_DP_ABL 0  // timing ablations only (wrong results): 1 no prob walk, 2 no MFMAs, 4 no skip loads
-#endif
-template <int THI>
-__global__ __launch_bounds__(THI * 128) void deconv_prob_kernel(
-    const float* __restrict__ x, const float* __restrict__ wpk, const float* __restrict__ alpha,
-    const float* __restrict__ shift, const float* __restrict__ skip, const float* __restrict__ wprob,
-    float* __restrict__ logits, Geo g) {
-  constexpr int CIN = 16, COUT = 8, PL = 4, NTM = THI * 64;  // threads of the MFMA role
-  constexpr int LW = 17, LH = THI + 1, VST = 16, NVP = LH * LW;  // one staged input plane
-  constexpr int NLD = (NVP * 4 + NTM - 1) / NTM;
-  constexpr int XR = 2 * THI;  // x11 rows per band (logit rows 1 .. XR - 2)
-  __shared__ __attribute__((aligned(16))) float xin[3][NVP * VST];  // input planes md, md+1, md+2 (ring)
-  __shared__ __attribute__((aligned(16))) float wts[27 * 8 * 16];
-  __shared__ __attribute__((aligned(16))) float xo[2][2][XR][2][32][4];  // x11: [step & 1][pd][row][quad][col][4]
-
-  const int Hr = g.Ho, Wr = g.Wo, Do = g.Do;
-  const int R = XR - 2, nb = (Hr + 1 + R - 1) / R, ncs = (Wr + 1 + 29) / 30;
-  int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int cs = t % ncs;
-  t /= ncs;
-  const int band = t % nb;
-  const int n = t / nb;
-  const int mh0 = band * (THI - 1) - 1, m0 = cs * 15 - 1;  // first input row / column (may be -1)
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // role and index within it: TMVS_DP_ROLE 0 = waves 0..THI-1 MFMA, the rest walk; 1 = even / odd waves;
-  // 2 = alternating groups of 4 waves (the placement that puts both roles on every SIMD, scripts/micro/wave_simd)
-  const bool mfma_role = TMVS_DP_ROLE == 0 ? wid < THI : TMVS_DP_ROLE == 1 ? !(wid & 1) : !((wid >> 2) & 1);
-  const int wv = TMVS_DP_ROLE == 0 ? (wid < THI ? wid : wid - THI)
-                 : TMVS_DP_ROLE == 1 ? wid >> 1 : ((wid >> 3) << 2) + (wid & 3);
-  const size_t plane_sz = (size_t)Hr * Wr;
-
-  for (int idx = threadIdx.x; idx < 27 * 8 * 4; idx += 2 * NTM) {
-    const int q = idx & 3, row = (idx >> 2) & 7, tap = idx >> 5;
-    const float4 v = *reinterpret_cast<const float4*>(wpk + ((size_t)tap * COUT + row) * CIN + 4 * q);
-    *reinterpret_cast<float4*>(wts + (tap * 8 + row) * 16 + 4 * (q ^ ((row >> 1) & 3))) = v;
-  }
-  if (mfma_role) {
-    // ------------------------------------------------------------ the deconv (+ skip) role
-    const int col = lane & 15, kgrp = lane >> 4;
-    const size_t in_n = (size_t)n * g.Di * g.Hi * g.Wi;
-    float4 pf[NLD];
-    auto fetch = [&](int md) {  // input plane md (zeros outside the volume) -> registers
-#pragma unroll
-      for (int k = 0; k < NLD; ++k) {
-        const int idx = wv * 64 + lane + NTM * k;  // the role-local thread index
-        const int vox = idx >> 2, q = idx & 3;
-        const int lw = vox % LW, lh = vox / LW;
-        const int iw = m0 + lw, ih = mh0 + lh;
-        pf[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (vox < NVP && (unsigned)iw < (unsigned)g.Wi && (unsigned)ih < (unsigned)g.Hi && (unsigned)md < (unsigned)g.Di)
-          pf[k] = *reinterpret_cast<const float4*>(x + (in_n + ((size_t)md * g.Hi + ih) * g.Wi + iw) * CIN + 4 * q);
-      }
-    };
-    auto commit = [&](float* buf) {
-#pragma unroll
-      for (int k = 0; k < NLD; ++k) {
-        const int idx = wv * 64 + lane + NTM * k;  // the role-local thread index
-        const int vox = idx >> 2, q = idx & 3;
-        if (vox < NVP) *reinterpret_cast<float4*>(buf + vox * VST + 4 * (q ^ ((vox >> 1) & 3))) = pf[k];
-      }
-    };
-    const int co = col & 7;    // A row -> output channel
-    const bool hi = col >= 8;  // rows 8-15: the odd-w output
-    const int cq = 4 * (kgrp & 1);
-    const float4 al = *reinterpret_cast<const float4*>(alpha + cq);
-    const float4 sh = *reinterpret_cast<const float4*>(shift + cq);
-    auto wfrag = [&](int tap, VecN<PL>& a) { a.load(wts + (tap * 8 + co) * 16 + 4 * (kgrp ^ ((co >> 1) & 3))); };
-    // this lane's x11 voxel column (the prob conv's zero padding outside the volume)
-    const int ocol = 2 * (m0 + col) + (kgrp >> 1);
-    const bool col_ok = (unsigned)ocol < (unsigned)Wr;
-    const size_t out_n = (size_t)n * Do * plane_sz;
-    const int mh = mh0 + wv;
-    fetch(0);
-    commit(xin[0]);
-    fetch(1);
-    commit(xin[1]);
-    __syncthreads();
-#pragma unroll 1
-    for (int md = 0; md <= g.Di; ++md) {
-      if (md < g.Di) {
-        fetch(md + 2);  // the ring's third slot (read last in step md - 1); committed after the MFMAs
-        const int s0 = md % 3, s1 = (md + 1) % 3;
-        float4 sk[4];
-        bool ok[4];
-#pragma unroll
-        for (int pdh = 0; pdh < 4; ++pdh) {  // skip (conv0) at planes 2md + pd, rows 2mh + ph, this column
-          const int orow = 2 * mh + (pdh & 1);
-          ok[pdh] = col_ok && (unsigned)orow < (unsigned)Hr;
-          sk[pdh] = ok[pdh] && !(TMVS_DP_ABL & 4) ? *reinterpret_cast<const float4*>(
-                                  skip + (out_n + ((size_t)(2 * md + (pdh >> 1)) * Hr + orow) * Wr + ocol) * 8 + cq)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        floatx4 acc[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int pdh = 0; pdh < 4; ++pdh) {
-          const int pd = pdh >> 1, ph = pdh & 1;
-#pragma unroll
-          for (int td = 0; td < 1 + pd; ++td)
-#pragma unroll
-            for (int th = 0; th < 1 + ph; ++th) {
-              const int kd = pd ? (td ? 2 : 0) : 1, od_off = (pd && !td) ? 1 : 0;
-              const int kh = ph ? (th ? 2 : 0) : 1, oh_off = (ph && !th) ? 1 : 0;
-              const int tap_base = kd * 9 + kh * 3;
-              VecN<PL> a1, a2;
-              wfrag(tap_base + (hi ? 2 : 1), a1);  // rows 0-7: kw=1, rows 8-15: kw=2 (input column m)
-              if (hi)
-                wfrag(tap_base + 0, a2);           // rows 8-15: kw=0 (input column m+1)
-              else
-                a2.zero();
-              const float* cur = xin[od_off ? s1 : s0];
-              const int lv = (wv + oh_off) * LW + col;
-              VecN<PL> b1, b2;
-              b1.load(cur + lv * VST + 4 * (kgrp ^ ((lv >> 1) & 3)));
-              b2.load(cur + (lv + 1) * VST + 4 * (kgrp ^ (((lv + 1) >> 1) & 3)));
-              if (TMVS_DP_ABL & 2) {
-                acc[pdh][0] += a1.v[0] * b1.v[0] + a2.v[0] * b2.v[0];
-                continue;
-              }
-#pragma unroll
-              for (int j = 0; j < PL; ++j)
-                acc[pdh] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.v[j], b1.v[j], acc[pdh], 0, 0, 0);
-#pragma unroll
-              for (int j = 0; j < PL; ++j)
-                acc[pdh] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2.v[j], b2.v[j], acc[pdh], 0, 0, 0);
-            }
-        }
-        commit(xin[(md + 2) % 3]);
-        // x11 = conv0 + relu(bn(conv11)) (deconv3d_c8_kernel's epilogue: skip + value), 0 outside the volume
-#pragma unroll
-        for (int pdh = 0; pdh < 4; ++pdh) {
-          const floatx4 a = acc[pdh];
-          const float4 sv = sk[pdh];
-          float4 o = make_float4(sv.x + act(fmaf(a[0], al.x, sh.x), g.lo), sv.y + act(fmaf(a[1], al.y, sh.y), g.lo),
-                                 sv.z + act(fmaf(a[2], al.z, sh.z), g.lo), sv.w + act(fmaf(a[3], al.w, sh.w), g.lo));
-          if (!ok[pdh]) o = make_float4(0.f, 0.f, 0.f, 0.f);
-          *reinterpret_cast<float4*>(&xo[md & 1][pdh >> 1][2 * wv + (pdh & 1)][kgrp & 1][2 * col + (kgrp >> 1)][0]) = o;
-        }
-      }
-      __syncthreads();
-    }
-  } else {
-    // ------------------------------------------------------------ the prob walk role
-    const int vw = wv;
-    const int lr = 1 + 2 * vw + (lane >> 5), c = lane & 31;  // logit row of the band, x11 column
-    const int grow = 2 * mh0 + lr, gcol = 2 * m0 + c;
-    const bool emits = vw < THI - 1 && c >= 1 && c <= 30 && (unsigned)grow < (unsigned)Hr && (unsigned)gcol < (unsigned)Wr;
-    float* lgp = logits + (size_t)n * Do * plane_sz + (size_t)(emits ? grow : 0) * Wr + (emits ? gcol : 0);
-    float2_v c12 = {0.f, 0.f};  // prob_walk's chains: {output p (kd = 1 next), output p - 1 (kd = 2 next)}
-    // one x11 plane p through the prob chains: prob_walk's plane() with the rows from LDS (zero: plane Do)
-    auto walk_plane = [&](const float (*xp)[2][32][4], int p, bool zero) {
-      float acc_next = 0.f;
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        float4 u = make_float4(0.f, 0.f, 0.f, 0.f), v = u;
-        if (!zero) {
-          u = *reinterpret_cast<const float4*>(&xp[lr - 1 + kh][0][c][0]);
-          v = *reinterpret_cast<const float4*>(&xp[lr - 1 + kh][1][c][0]);
-        }
-        const float xc[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-        int wo = kh * 72;
-        asm volatile("" : "+s"(wo));
-        const float* wk = wprob + __builtin_amdgcn_readfirstlane(wo);
-#pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-#pragma unroll
-          for (int ch = 0; ch < 8; ++ch) {
-            const float xv = kw == 0 ? lane_from_left(xc[ch]) : kw == 1 ? xc[ch] : lane_from_right(xc[ch]);
-            const float2_v wp = *reinterpret_cast<const float2_v*>(wk + 2 * (kw * 8 + ch));
-            acc_next = fmaf(wk[48 + kw * 8 + ch], xv, acc_next);
-            c12 = __builtin_elementwise_fma(wp, float2_v{xv, xv}, c12);
-          }
-        }
-        asm volatile("" : "+v"(acc_next), "+v"(c12));
-      }
-      if (p >= 1 && emits) lgp[(size_t)(p - 1) * plane_sz] = c12.y;  // output p - 1 complete
-      c12 = float2_v{acc_next, c12.x};
-    };
-    __syncthreads();  // the MFMA role's initial staging
-#pragma unroll 1
-    for (int md = 0; md <= g.Di; ++md) {
-      if (md >= 1 && vw < THI - 1 && !(TMVS_DP_ABL & 1)) {
-        const int sb = (md - 1) & 1;
-        walk_plane(xo[sb][0], 2 * md - 2, false);
-        walk_plane(xo[sb][1], 2 * md - 1, false);
-      }
-      __syncthreads();
-    }
-    if (vw < THI - 1) walk_plane(xo[0][0], Do, true);  // plane Do: the depth padding, completes output Do - 1
-  }
-}
-
-template <int THI>
-static int launch_deconv_prob(const float* x, const float* w, const float* al, const float* sh, const float* skip,
-                              const float* wprob, float* logits, int B, const Geo& g, hipStream_t st) {
-  constexpr int R = 2 * THI - 2;
-  const long nblk = (long)B * ((g.Ho + 1 + R - 1) / R) * ((g.Wo + 1 + 29) / 30);
-  hipLaunchKernelGGL((deconv_prob_kernel<THI>), dim3((unsigned)nblk), dim3(THI * 128), 0, st, x, w, al, sh, skip, wprob,
-                     logits, g);
-  TMVS_CHECK_LAUNCH();
-  return TMVS_OK;
-}
-
 template <int CIN, int COUT, int TDI, int THI, int MBB>
 static int launch_deconv(const float* x, const float* w, const float* al, const float* sh, const float* skip,
                          float* y, int B, const Geo& g, hipStream_t st) {
@@ -2114,11 +1878,9 @@ extern "C" size_t tmvs_costregnet_workspace(int batch, int depth, int height, in
 
 // CostRegNet up to conv11 + skip (models/module.py:447-455); *x11_out = the 8-channel
 // full-resolution NDHWC volume the prob conv reads, *c0_out = conv0's (dead once x11 exists).
-// fuse_prob: stop before conv11 -- *x11_out = x9 (the input of the fused conv11 + prob kernel), and the
-// x11 workspace slot is returned in *spare_out (free: x11 is never materialised then)
 static int costregnet_trunk(const float* x, int batch, int depth, int height, int width, const TmvsCostRegWeights* w,
                             void* workspace, size_t workspace_bytes, hipStream_t st, float** x11_out,
-                            float** c0_out, bool fuse_prob = false, float** spare_out = nullptr) {
+                            float** c0_out) {
   if (!x || !w || !workspace || batch <= 0) return TMVS_ERR_ARG;
   if (depth % 8 || height % 8 || width % 8) return TMVS_ERR_SHAPE;
   if (w->base_ch != 8) return TMVS_ERR_SHAPE;
@@ -2172,33 +1934,12 @@ static int costregnet_trunk(const float* x, int batch, int depth, int height, in
     return rc;
   if ((rc = deconv_dispatch(x7, batch, 4 * c, D2, H2, W2, w->w[8], w->alpha[8], w->shift[8], 2 * c, c2, x9, st)))
     return rc;
-  if (fuse_prob) {
-    *x11_out = x9;
-    *c0_out = c0;
-    *spare_out = x11;
-    return TMVS_OK;
-  }
   if ((rc = deconv_dispatch(x9, batch, 2 * c, D1, H1, W1, w->w[9], w->alpha[9], w->shift[9], c, c0, x11, st)))
     return rc;
   *x11_out = x11;
   *c0_out = c0;
   return TMVS_OK;
 }
-
-// conv11 + skip + prob through deconv_prob_kernel: logits [B][D][H][W] (x9 at half resolution, c0 the skip)
-static int conv11_prob_fused(const float* x9, const float* c0, const TmvsCostRegWeights* w, int batch, int depth,
-                             int height, int width, float* logits, hipStream_t st) {
-  Geo g;
-  g.lo = 0.f;
-  g.Di = depth / 2;
-  g.Hi = height / 2;
-  g.Wi = width / 2;
-  g.Do = depth;
-  g.Ho = height;
-  g.Wo = width;
-  return launch_deconv_prob<TMVS_DP_THI>(x9, w->w[9], w->alpha[9], w->shift[9], c0, w->w[10], logits, batch, g, st);
-}
-
 
 extern "C" int tmvs_costregnet(const float* x, int batch, int depth, int height, int width,
                                const TmvsCostRegWeights* w, void* workspace, size_t workspace_bytes, float* logits,
@@ -2223,16 +1964,6 @@ extern "C" int tmvs_costregnet_wta(const float* x, const float* hyp, int batch, 
   hipStream_t st = (hipStream_t)stream;
   float *x11, *c0;
   int rc;
-  // TMVS_FUSE_DP: conv11 + prob in one kernel (deconv_prob_kernel: x11 never written) for D <= 32 (1) or
-  // every D (2), then the softmax / WTA kernel on the logits; 0 = conv11, then the prob (+ WTA) kernels
-  if (TMVS_FUSE_DP == 2 || (TMVS_FUSE_DP == 1 && depth <= 32)) {
-    float* lg;
-    if ((rc = costregnet_trunk(x, batch, depth, height, width, w, workspace, workspace_bytes, st, &x11, &c0, true, &lg)))
-      return rc;
-    if ((rc = conv11_prob_fused(x11, c0, w, batch, depth, height, width, lg, st))) return rc;
-    return tmvs_softmax_wta(lg, hyp, batch, depth, height, width, clamp_lo, clamp_hi, prob, depth_out, depth_raw,
-                            conf, stream);
-  }
   if ((rc = costregnet_trunk(x, batch, depth, height, width, w, workspace, workspace_bytes, st, &x11, &c0))) return rc;
   if (depth > 32) {
     // D = 48 (stage 1) fused measured 53.8 us vs 40.1 + 10.3 us split (r07d vs r07b): few columns
