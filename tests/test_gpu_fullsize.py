@@ -251,9 +251,10 @@ def _as_stages(arrs):
 
 
 def _check_sharded(res, single, world, n_src):
-    """Every rank bitwise equal to rank 0; rank 0 against the single-rank forward with the same classifier as
-    against the oracle (the partial sums re-associate the view sum: near ties may flip; upstream ones
-    cascade), and its cascaded stage 3 within 1e-4 mm of it when stages 1-2 agree on every pixel."""
+    """Every rank bitwise equal to rank 0; rank 0 against the single-rank forward with the classifier used
+    against the oracle (the partial sums re-associate the view sum: near ties -- up to the measured top-2
+    spread -- may flip; upstream ones cascade), and its cascaded stage 3 within 1e-4 mm of it when stages
+    1-2 agree on every pixel."""
     from transmvsnet_amd.distributed import partition_views, view_groups
     g, _ = view_groups(world, n_src)
     for r in range(world):
@@ -263,7 +264,7 @@ def _check_sharded(res, single, world, n_src):
         for s in STAGES:
             for k in ("depth", "prob_volume", "depth_values"):
                 np.testing.assert_array_equal(res[r][f"{s}_{k}"], res[0][f"{s}_{k}"], err_msg=f"rank {r} {s} {k}")
-    rep = parity.cascade_report(_as_stages(res[0]), single)
+    rep = parity.cascade_report(_as_stages(res[0]), single, spread=True)
     for s in (1, 2, 3):
         c = rep[f"cascade_stage{s}"]
         c["prob_max_abs"] = float(np.abs(res[0][f"stage{s}_prob_volume"] - single[f"stage{s}"]["prob_volume"].numpy()).max())
