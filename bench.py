@@ -343,6 +343,7 @@ def run(args, world, rank, local):
         ops.set_timer(None)
         ospans = otimer.durations()
 
+        coherent = coherent_warp_timing(model, feats, proj, dv_dev) if args.profile_steps > 0 and shard is None else None
         e2e = end_to_end(model, args.e2e_steps, proj, dv_dev, dev) if args.e2e_steps > 0 and shard is None else None
         batch2 = (batch2_timing(model, feats, proj, dv_dev, args.batch2_steps, graphed)
                   if args.batch2_steps > 0 and shard is None else None)
@@ -395,6 +396,8 @@ def run(args, world, rank, local):
                      "per": "depth map (3 tmvs_costregnet_wta calls: 11 CostRegNet kernels each, the prob conv fused with softmax/WTA at stages 2/3, + the softmax kernel at stage 1)",
                      "algorithmic_flop": int(sum(cr_flop)),
                      "per_stage_ms": [round(float(x), 4) for x in per_launch]})
+    if coherent is not None:
+        kern.append(coherent)
     # headline roofline: the north-star kernel (warp_corr_kernel, one launch per stage; its
     # rocprofv3 average over the 3 launches of a step is avg_launch_us); CostRegNet (11
     # kernels per stage) is listed beside it in roofline_kernels
@@ -465,6 +468,68 @@ def run(args, world, rank, local):
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def coherent_warp_timing(model, feats, proj, dv_dev, reps=20):
+    """Secondary workload (roofline_kernels, not the headline): the stage-2/3 cost-volume launches
+    (tmvs_warp_corr) on COHERENT hypotheses next to the bench's own. The bench's random features make its
+    stage-1/2 WTA depth -- which the stage-2/3 hypotheses are built from (models/TransMVSNet.py:174-190) --
+    spatially incoherent, so neighbouring pixels' bilinear taps land in unrelated source neighbourhoods;
+    real scenes give smooth depth. Same stage features, cameras, view weights and kernels, with the
+    hypotheses built by tmvs_stage_hypotheses from a slanted plane 600 + 150 x/W + 100 y/H mm instead of the
+    GPU's own previous-stage depth. Per stage: HIP-event median of `reps` launches; tap bytes 16 C D P V over
+    the address unit's rate, algorithmic HBM bytes over 8 TB/s."""
+    from transmvsnet_amd import ops
+    from transmvsnet_amd.model import STAGE_SCALES
+    dev = dv_dev.device
+    with torch.no_grad():
+        out, vw = model.forward_features(feats, proj, dv_dev, (H, W), return_view_weights=True)
+        prep = model._prepared(dev)
+        s1, s2, s3 = feats["stage1"][0], feats["stage2"][0], feats["stage3"][0]
+        n, _, h1, w1 = s1.shape
+        st1 = model._fmt(s1, prep).view(n, h1, w1, 32)
+        st2 = ops.fmt_pathway(st1, s2, prep["red1"], prep["sm1"])
+        fs = (st1, st2, ops.fmt_pathway(st2, s3, prep["red2"], prep["sm2"]))
+        rows = {k: ops.proj_rows(proj[k]) for k in ("stage2", "stage3")}
+        per = {}
+        for s in (1, 2):
+            name = f"stage{s + 1}"
+            hp, wp = H // STAGE_SCALES[s - 1], W // STAGE_SCALES[s - 1]
+            yy, xx = torch.meshgrid(torch.arange(hp, dtype=torch.float32), torch.arange(wp, dtype=torch.float32),
+                                    indexing="ij")
+            plane = (600.0 + 150.0 * xx / wp + 100.0 * yy / hp)[None].to(dev).contiguous()
+            hyps = {"bench": out[name]["depth_values"].contiguous(),
+                    "coherent": ops.stage_hypotheses(dv_dev[0:1], plane, model.ndepths[s], model.depth_interals_ratio[s],
+                                                     (H, W), STAGE_SCALES[s])}
+            f = fs[s]
+            _, h, w, c = f.shape
+            d, v, p = model.ndepths[s], NVIEWS - 1, h * w
+            tap, alg = 16 * c * d * p * v, 4 * p * (c * (1 + v) + 2 * d + v)
+            row = {}
+            for kind, hyp in hyps.items():
+                for _ in range(3):
+                    ops.warp_corr(f[0:1], f[1:].unsqueeze(0), rows[name], hyp, view_w_in=vw, vw_shift=s)
+                ts = []
+                for _ in range(reps):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    ops.warp_corr(f[0:1], f[1:].unsqueeze(0), rows[name], hyp, view_w_in=vw, vw_shift=s)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ts.append(e0.elapsed_time(e1) * 1e3)
+                us = float(np.median(ts))
+                row[kind] = {"us": round(us, 2), "ta_frac": round(tap / (us * 1e-6) / 1e9 / PEAK_TA_GBS, 4),
+                             "hbm_frac": round(alg / (us * 1e-6) / 1e9 / PEAK_HBM_GBS, 4)}
+            per[name] = row
+    us = sum(per[k]["coherent"]["us"] for k in per)
+    tap = sum(gather_bytes()[1:])
+    return {"kernel": "tmvs_warp_corr (gather, coherent stage-2/3 hypotheses)", "bound": "ta",
+            "achieved": round(tap / (us * 1e-6) / 1e9, 1), "peak": PEAK_TA_GBS, "unit": "GB/s",
+            "frac": round(tap / (us * 1e-6) / 1e9 / PEAK_TA_GBS, 4), "traffic": None,
+            "per": "stages 2+3 of one depth map, one launch each (HIP events, median of %d); secondary workload: "
+                   "hypotheses from a slanted plane (600 + 150 x/W + 100 y/H mm) instead of the bench's incoherent "
+                   "WTA depth" % reps,
+            "per_stage": per}
 
 
 def end_to_end(model, steps, proj, dv_dev, dev):
