@@ -100,3 +100,33 @@ def test_oracle_stage_glue():
         prev = torch.from_numpy(g[f"glue{s}_prev"])
         hyp = oracle.stage_hypotheses(prev, dv, s - 1, (hh, ww), ndepths=(48, 32, 8))
         np.testing.assert_array_equal(hyp.numpy(), g[f"glue{s}_hyp"])
+
+
+@pytest.mark.parametrize("scale", [0.7, 3.0])
+def test_oracle_deform_conv2d_matches_grid_sample_formulation(scale):
+    """The oracle's torchvision.ops.deform_conv2d restatement (models/dcn.py:71-80's call; torchvision is
+    absent here, so no reference output holds it at nonzero offsets) against an independent formulation of
+    the same operator: per tap k, the input sampled at p + p_k + (dy_k, dx_k) by F.grid_sample (bilinear,
+    zeros padding, align_corners=True: corners outside the image contribute 0, as torchvision's
+    bilinear_interpolate), times the mask, contracted with the weights by einsum. Float64, offsets of up to a
+    few pixels (many samples leave the image), two channel / output counts."""
+    torch.manual_seed(int(scale * 10))
+    for b, c, co, h, w in ((2, 5, 3, 9, 11), (1, 8, 6, 7, 13)):
+        x = torch.randn(b, c, h, w, dtype=torch.float64)
+        off = torch.randn(b, 18, h, w, dtype=torch.float64) * scale
+        mask = torch.rand(b, 9, h, w, dtype=torch.float64)
+        wt = torch.randn(co, c, 3, 3, dtype=torch.float64)
+        bias = torch.randn(co, dtype=torch.float64)
+        got = oracle.deform_conv2d(x, off, wt, bias, 1, mask)
+        ys = torch.arange(h, dtype=torch.float64).view(1, h, 1)
+        xs = torch.arange(w, dtype=torch.float64).view(1, 1, w)
+        cols = []
+        for k in range(9):
+            i, j = divmod(k, 3)
+            py = ys + (i - 1) + off[:, 2 * k]
+            px = xs + (j - 1) + off[:, 2 * k + 1]
+            grid = torch.stack([2 * px / (w - 1) - 1, 2 * py / (h - 1) - 1], dim=-1)
+            s = torch.nn.functional.grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
+            cols.append(s * mask[:, k:k + 1])
+        ref = torch.einsum("ocij,bcijhw->bohw", wt, torch.stack(cols, 2).view(b, c, 3, 3, h, w)) + bias.view(1, -1, 1, 1)
+        torch.testing.assert_close(got, ref, rtol=1e-10, atol=1e-10)
