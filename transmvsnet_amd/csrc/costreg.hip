@@ -86,9 +86,6 @@ struct Geo {
   int Di, Hi, Wi;  // input dims
   int Do, Ho, Wo;  // output dims
   float lo;        // epilogue floor: 0 = ReLU, -inf = none
-  // row range of the launch (conv3d_s2c8_tile_kernel: output rows; deconv3d_c8_kernel: input rows): the
-  // row-chunked producer / consumer pairs of tmvs_costregnet_wta (TMVS_MALL_CHUNKS); default all rows
-  int r0 = 0, r1 = 0x7fffffff;
 };
 
 __device__ __forceinline__ float act(float v, float lo) { return v > lo ? v : lo; }
@@ -698,13 +695,12 @@ __device__ __forceinline__ float lane_from_right(float v) {  // lane l <- lane l
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, false));
 }
 
-// rows [r0, r1) of the volume (the row-chunked launches of tmvs_costregnet_wta; all rows otherwise)
 __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, float* __restrict__ y, int D, int H,
                                                     int W, const float* __restrict__ wt,
                                                     const float* __restrict__ alpha,
-                                                    const float* __restrict__ shift, float lo, int r0, int r1) {
+                                                    const float* __restrict__ shift, float lo) {
   const int HW = H * W;
-  const int nseg = (W + kProbCols - 1) / kProbCols, nrow = (r1 - r0 + 3) / 4, ndc = (D + kDChunk - 1) / kDChunk;
+  const int nseg = (W + kProbCols - 1) / kProbCols, nrow = (H + 3) / 4, ndc = (D + kDChunk - 1) / kDChunk;
   int lb = xcd_remap(blockIdx.x, gridDim.x);
   const int seg = lb % nseg;
   lb /= nseg;
@@ -713,8 +709,8 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
   const int dc = lb % ndc;
   const int n = lb / ndc;
   const int lane = threadIdx.x & 63;
-  const int h = r0 + rowb * 4 + (threadIdx.x >> 6);
-  if (h >= r1) return;  // whole wave
+  const int h = rowb * 4 + (threadIdx.x >> 6);
+  if (h >= H) return;  // whole wave
   const int w = seg * kProbCols + lane - 1;
   const bool writes = lane >= 1 && lane <= kProbCols && w < W;
   const int d0 = dc * kDChunk, d1 = min(D, d0 + kDChunk);
@@ -972,12 +968,6 @@ __device__ __forceinline__ void prob_walk_rows(__amdgpu_buffer_rsrc_t rx, int w,
 #ifndef TMVS_PROB_WTA_ROWS
 #define TMVS_PROB_WTA_ROWS 2
 #endif
-#ifndef TMVS_MALL_CHUNKS
-#define TMVS_MALL_CHUNKS 2  // row chunks of the full-resolution producer / consumer pairs (tmvs_costregnet_wta)
-#endif
-#ifndef TMVS_MALL_MIN_MB
-#define TMVS_MALL_MIN_MB 128  // ... applied when the 8-channel full-resolution volume is at least this large
-#endif
 
 // prob_kernel with NR output rows per wave (4 waves: 4 NR rows per workgroup)
 template <int NR>
@@ -1011,15 +1001,15 @@ template <int D, int NR>
 __global__ __launch_bounds__(64 * (D / kDChunk)) void prob_wta_rows_kernel(
     const float* __restrict__ x, const float* __restrict__ wt, const float* __restrict__ hyp, int H, int W, float lo,
     float hi, float* __restrict__ prob, float* __restrict__ depth, float* __restrict__ depth_raw,
-    float* __restrict__ conf, int r0, int r1) {
+    float* __restrict__ conf) {
   constexpr int NW = D / kDChunk;
   __shared__ float lg[NR][D * 64];
   const int HW = H * W;
-  const int nseg = (W + kProbCols - 1) / kProbCols, nrow = (r1 - r0 + NR - 1) / NR;
+  const int nseg = (W + kProbCols - 1) / kProbCols, nrow = (H + NR - 1) / NR;
   int lb = xcd_remap(blockIdx.x, gridDim.x);
   const int seg = lb % nseg;
   lb /= nseg;
-  const int h0 = r0 + (lb % nrow) * NR;
+  const int h0 = (lb % nrow) * NR;
   const int n = lb / nrow;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int d0 = wv * kDChunk;
@@ -1031,7 +1021,7 @@ __global__ __launch_bounds__(64 * (D / kDChunk)) void prob_wta_rows_kernel(
   if (!writes) return;
   for (int r = wv; r < NR; r += NW) {
     const int h = h0 + r;
-    if (h >= r1) break;
+    if (h >= H) break;
     float xl[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) xl[d] = lg[r][d * 64 + lane];
@@ -1297,8 +1287,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV ==
   constexpr int NLD = (NQ + NTH - 1) / NTH;
   __shared__ __attribute__((aligned(16))) float tile[NROW * 2 * SW * 8];
   __shared__ __attribute__((aligned(16))) float wts[28 * 16 * 8];
-  const int rlo = g.r0, rhi = g.r1 < g.Ho ? g.r1 : g.Ho;  // output rows of this launch
-  const int nws = (g.Wo + 15) / 16, nhs = (rhi - rlo + TH - 1) / TH, nds = (g.Do + TD - 1) / TD;
+  const int nws = (g.Wo + 15) / 16, nhs = (g.Ho + TH - 1) / TH, nds = (g.Do + TD - 1) / TD;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int col = lane & 15, kgrp = lane >> 4;
   const int half = kgrp & 1, side = kgrp >> 1;
@@ -1313,7 +1302,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV ==
     TileCoord c;
     c.ow0 = (t % nws) * 16;
     t /= nws;
-    c.oh0 = rlo + (t % nhs) * TH;
+    c.oh0 = (t % nhs) * TH;
     t /= nhs;
     c.od0 = (t % nds) * TD;
     c.n = t / nds;
@@ -1395,7 +1384,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV ==
     for (int r = 0; r < NBW; ++r) {
       const int rr = wv * NBW + r;
       const int od = c.od0 + rr / TH, oh = c.oh0 + rr % TH;
-      if (ow >= g.Wo || od >= g.Do || oh >= rhi) continue;
+      if (ow >= g.Wo || od >= g.Do || oh >= g.Ho) continue;
       float4 o;
       o.x = act(fmaf(acc[r][0], al.x, sh.x), g.lo);
       o.y = act(fmaf(acc[r][1], al.y, sh.y), g.lo);
@@ -1415,9 +1404,7 @@ __global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(NWV ==
 template <int TD, int TH>
 static int launch_conv_s2c8_tile(const float* x, const float* w, const float* al, const float* sh, float* y, int B,
                                  const Geo& g, hipStream_t st) {
-  const int rows = (g.r1 < g.Ho ? g.r1 : g.Ho) - g.r0;
-  if (rows <= 0) return TMVS_OK;
-  const long ntiles = (long)B * ((g.Do + TD - 1) / TD) * ((rows + TH - 1) / TH) * ((g.Wo + 15) / 16);
+  const long ntiles = (long)B * ((g.Do + TD - 1) / TD) * ((g.Ho + TH - 1) / TH) * ((g.Wo + 15) / 16);
   constexpr int NWV = TMVS_S2C8_NWV;
   const int grid = persistent_grid(conv3d_s2c8_tile_kernel<TD, TH, NWV>, ntiles, NWV * 64);
   hipLaunchKernelGGL((conv3d_s2c8_tile_kernel<TD, TH, NWV>), dim3(grid), dim3(NWV * 64), 0, st, x, w, al, sh, y, g,
@@ -1498,8 +1485,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   __shared__ __attribute__((aligned(16))) float wts[27 * 8 * 16];
   __shared__ __attribute__((aligned(16))) float ep[4][32 * 8];
 
-  const int mlo = g.r0, mhi = g.r1 < g.Hi ? g.r1 : g.Hi;  // input rows of this launch
-  const int nws = (g.Wi + 15) / 16, nhs = (mhi - mlo + THI - 1) / THI, nds = (g.Di + TDI - 1) / TDI;
+  const int nws = (g.Wi + 15) / 16, nhs = (g.Hi + THI - 1) / THI, nds = (g.Di + TDI - 1) / TDI;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int col = lane & 15, kgrp = lane >> 4;
   // XCD-contiguous tile ranges: workgroup b runs on XCD b % 8 (round-robin dispatch)
@@ -1515,7 +1501,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     TileCoord c;
     c.mw0 = (t % nws) * 16;
     t /= nws;
-    c.mh0 = mlo + (t % nhs) * THI;
+    c.mh0 = (t % nhs) * THI;
     t /= nhs;
     c.md0 = (t % nds) * TDI;
     c.n = t / nds;
@@ -1581,7 +1567,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     for (int r = 0; r < NBW; ++r) {
       const int rr = wv * NBW + r;
       const int md = c.md0 + rr / THI, mh = c.mh0 + rr % THI;
-      ok[r] = md < g.Di && mh < mhi && ow < 2 * g.Wi;
+      ok[r] = md < g.Di && mh < g.Hi && ow < 2 * g.Wi;
       oo[r] = (out_n + ((size_t)(2 * md) * g.Ho + 2 * mh) * g.Wo + ow) * 8 + (lane & 1) * 4;
 #pragma unroll
       for (int pdh = 0; pdh < 4; ++pdh)
@@ -1653,9 +1639,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 template <int TDI, int THI>
 static int launch_deconv_c8(const float* x, const float* w, const float* al, const float* sh, const float* skip,
                             float* y, int B, const Geo& g, hipStream_t st) {
-  const int rows = (g.r1 < g.Hi ? g.r1 : g.Hi) - g.r0;
-  if (rows <= 0) return TMVS_OK;
-  const long ntiles = (long)B * ((g.Di + TDI - 1) / TDI) * ((rows + THI - 1) / THI) * ((g.Wi + 15) / 16);
+  const long ntiles = (long)B * ((g.Di + TDI - 1) / TDI) * ((g.Hi + THI - 1) / THI) * ((g.Wi + 15) / 16);
   const long grid = persistent_grid(deconv3d_c8_kernel<TDI, THI>, ntiles);
   hipLaunchKernelGGL((deconv3d_c8_kernel<TDI, THI>), dim3((unsigned)grid), dim3(256), 0, st, x, w, al, sh, skip, y, g,
                      (int)ntiles);
@@ -1675,12 +1659,9 @@ static int launch_deconv(const float* x, const float* w, const float* al, const 
 }
 
 static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, const float* wpk, const float* al,
-                         const float* sh, int cout, int stride, float* y, hipStream_t st, float lo = 0.f, int r0 = 0,
-                         int r1 = 0x7fffffff) {
+                         const float* sh, int cout, int stride, float* y, hipStream_t st, float lo = 0.f) {
   Geo g;
   g.lo = lo;
-  g.r0 = r0;  // output rows (honoured by the 8 -> 16 stride-2 kernel, the only one launched row-chunked)
-  g.r1 = r1;
   g.Di = d;
   g.Hi = h;
   g.Wi = w;
@@ -1770,12 +1751,9 @@ static int conv_dispatch(const float* x, int B, int cin, int d, int h, int w, co
 }
 
 static int deconv_dispatch(const float* x, int B, int cin, int d, int h, int w, const float* wpk, const float* al,
-                           const float* sh, int cout, const float* skip, float* y, hipStream_t st, float lo = 0.f,
-                           int r0 = 0, int r1 = 0x7fffffff) {
+                           const float* sh, int cout, const float* skip, float* y, hipStream_t st, float lo = 0.f) {
   Geo g;
   g.lo = lo;
-  g.r0 = r0;  // input rows (honoured by the 16 -> 8 kernel, the only one launched row-chunked)
-  g.r1 = r1;
   g.Di = d;
   g.Hi = h;
   g.Wi = w;
@@ -1868,7 +1846,7 @@ extern "C" int tmvs_conv3d_mfma(const float* x, int batch, int cin, int d, int h
   if (!transposed && stride == 1 && cin == 1 && cout == 8) {  // conv0's VALU kernel, raw epilogue
     if ((long long)d * h * w * 32 >= (1LL << 31)) return TMVS_ERR_SHAPE;
     const dim3 grid((unsigned)(((w + kProbCols - 1) / kProbCols) * ((h + 3) / 4) * batch * ((d + kDChunk - 1) / kDChunk)));
-    hipLaunchKernelGGL(conv0_kernel, grid, dim3(256), 0, st, x, y, d, h, w, wpk, al, sh, lo, 0, h);
+    hipLaunchKernelGGL(conv0_kernel, grid, dim3(256), 0, st, x, y, d, h, w, wpk, al, sh, lo);
     TMVS_CHECK_LAUNCH();
     return TMVS_OK;
   }
@@ -1900,12 +1878,9 @@ extern "C" size_t tmvs_costregnet_workspace(int batch, int depth, int height, in
 
 // CostRegNet up to conv11 + skip (models/module.py:447-455); *x11_out = the 8-channel
 // full-resolution NDHWC volume the prob conv reads, *c0_out = conv0's (dead once x11 exists).
-// chunks > 1: conv0 and conv1 run as `chunks` row-range pairs (conv0 rows [k H/K, (k+1) H/K), then the conv1
-// output rows those feed), so conv1 reads each conv0 chunk right after it was written, while it is still in the
-// 256-MB Infinity Cache; no_conv11: stop after conv9 (*x11_out = x9) for the caller's row-chunked conv11 / prob
 static int costregnet_trunk(const float* x, int batch, int depth, int height, int width, const TmvsCostRegWeights* w,
                             void* workspace, size_t workspace_bytes, hipStream_t st, float** x11_out,
-                            float** c0_out, int chunks = 1, bool no_conv11 = false, float** x11_buf = nullptr) {
+                            float** c0_out) {
   if (!x || !w || !workspace || batch <= 0) return TMVS_ERR_ARG;
   if (depth % 8 || height % 8 || width % 8) return TMVS_ERR_SHAPE;
   if (w->base_ch != 8) return TMVS_ERR_SHAPE;
@@ -1940,16 +1915,11 @@ static int costregnet_trunk(const float* x, int batch, int depth, int height, in
   const int D2 = D1 / 2, H2 = H1 / 2, W2 = W1 / 2;
   const int D3 = D2 / 2, H3 = H2 / 2, W3 = W2 / 2;
   int rc;
-  for (int k = 0; k < chunks; ++k) {
-    const int r0 = k * H0 / chunks, r1 = (k + 1) * H0 / chunks;
-    const dim3 g0x((unsigned)(((W0 + kProbCols - 1) / kProbCols) * ((r1 - r0 + 3) / 4) * batch * ((D0 + kDChunk - 1) / kDChunk)));
-    hipLaunchKernelGGL(conv0_kernel, g0x, dim3(256), 0, st, x, c0, D0, H0, W0, w->w[0], w->alpha[0], w->shift[0],
-                       0.f, r0, r1);
-    TMVS_CHECK_LAUNCH();
-    if ((rc = conv_dispatch(c0, batch, c, D0, H0, W0, w->w[1], w->alpha[1], w->shift[1], 2 * c, 2, c1, st, 0.f,
-                            chunks > 1 ? r0 / 2 : 0, chunks > 1 ? r1 / 2 : 0x7fffffff)))
-      return rc;
-  }
+  const dim3 g0x((unsigned)(((W0 + kProbCols - 1) / kProbCols) * ((H0 + 3) / 4) * batch * ((D0 + kDChunk - 1) / kDChunk)));
+  hipLaunchKernelGGL(conv0_kernel, g0x, dim3(256), 0, st, x, c0, D0, H0, W0, w->w[0], w->alpha[0], w->shift[0],
+                     0.f);
+  TMVS_CHECK_LAUNCH();
+  if ((rc = conv_dispatch(c0, batch, c, D0, H0, W0, w->w[1], w->alpha[1], w->shift[1], 2 * c, 2, c1, st))) return rc;
   if ((rc = conv_dispatch(c1, batch, 2 * c, D1, H1, W1, w->w[2], w->alpha[2], w->shift[2], 2 * c, 1, c2, st)))
     return rc;
   if ((rc = conv_dispatch(c2, batch, 2 * c, D1, H1, W1, w->w[3], w->alpha[3], w->shift[3], 4 * c, 2, c3, st)))
@@ -1964,12 +1934,6 @@ static int costregnet_trunk(const float* x, int batch, int depth, int height, in
     return rc;
   if ((rc = deconv_dispatch(x7, batch, 4 * c, D2, H2, W2, w->w[8], w->alpha[8], w->shift[8], 2 * c, c2, x9, st)))
     return rc;
-  if (no_conv11) {
-    *x11_out = x9;
-    *c0_out = c0;
-    *x11_buf = x11;
-    return TMVS_OK;
-  }
   if ((rc = deconv_dispatch(x9, batch, 2 * c, D1, H1, W1, w->w[9], w->alpha[9], w->shift[9], c, c0, x11, st)))
     return rc;
   *x11_out = x11;
@@ -2000,47 +1964,6 @@ extern "C" int tmvs_costregnet_wta(const float* x, const float* hyp, int batch, 
   hipStream_t st = (hipStream_t)stream;
   float *x11, *c0;
   int rc;
-  // Infinity-Cache chunking (TMVS_MALL_CHUNKS = K): when the 8-channel full-resolution volume is large (DTU
-  // stages 2/3: 255 MB, the size of the 256-MB Infinity Cache) its producer / consumer pairs run as K row
-  // ranges each -- conv0 -> conv1, and conv11 -> prob + softmax / WTA -- so each consumer reads a chunk written
-  // just before. Every output is computed once by the same kernel code: bitwise the unchunked form.
-  const int K = TMVS_MALL_CHUNKS;
-  const bool chunked = K > 1 && depth <= 32 && height % (2 * K) == 0 &&
-                       (long long)batch * depth * height * width * 32 >= (long long)TMVS_MALL_MIN_MB << 20;
-  if (chunked) {
-    float* x11buf;
-    if ((rc = costregnet_trunk(x, batch, depth, height, width, w, workspace, workspace_bytes, st, &x11, &c0, K, true,
-                               &x11buf)))
-      return rc;
-    const float* x9 = x11;
-    const int H1 = height / 2;
-    constexpr int NR = TMVS_PROB_WTA_ROWS;
-    for (int k = 0; k < K; ++k) {
-      // conv11 input rows: chunk k must provide x11 rows up to (k+1) H/K (the prob conv's halo row), i.e. input
-      // row (k+1) H/(2K); the first chunk starts at 0, each later one after the previous one's last row
-      const int i0 = k == 0 ? 0 : k * H1 / K + 1, i1 = k == K - 1 ? H1 : (k + 1) * H1 / K + 1;
-      if ((rc = deconv_dispatch(x9, batch, 16, depth / 2, H1, width / 2, w->w[9], w->alpha[9], w->shift[9], 8, c0,
-                                x11buf, st, 0.f, i0, i1)))
-        return rc;
-      const int r0 = k * height / K, r1 = (k + 1) * height / K;
-      const dim3 gf((unsigned)(((width + kProbCols - 1) / kProbCols) * ((r1 - r0 + NR - 1) / NR) * batch));
-      const dim3 bf((unsigned)(64 * (depth / kDChunk)));
-#define TMVS_PWC_CASE(DD)                                                                                      \
-  case DD:                                                                                                     \
-    hipLaunchKernelGGL((prob_wta_rows_kernel<DD, NR>), gf, bf, 0, st, x11buf, w->w[10], hyp, height, width,    \
-                       clamp_lo, clamp_hi, prob, depth_out, depth_raw, conf, r0, r1);                           \
-    break;
-      switch (depth) {
-        TMVS_PWC_CASE(8)
-        TMVS_PWC_CASE(16)
-        TMVS_PWC_CASE(24)
-        TMVS_PWC_CASE(32)
-      }
-#undef TMVS_PWC_CASE
-      TMVS_CHECK_LAUNCH();
-    }
-    return TMVS_OK;
-  }
   if ((rc = costregnet_trunk(x, batch, depth, height, width, w, workspace, workspace_bytes, st, &x11, &c0))) return rc;
   if (depth > 32) {
     // D = 48 (stage 1) fused measured 53.8 us vs 40.1 + 10.3 us split (r07d vs r07b): few columns
@@ -2059,7 +1982,7 @@ extern "C" int tmvs_costregnet_wta(const float* x, const float* hyp, int batch, 
   case DD:                                                                                                    \
     if constexpr (NR > 1)                                                                                     \
       hipLaunchKernelGGL((prob_wta_rows_kernel<DD, NR>), gf, bf, 0, st, x11, w->w[10], hyp, height, width,    \
-                         clamp_lo, clamp_hi, prob, depth_out, depth_raw, conf, 0, height);                    \
+                         clamp_lo, clamp_hi, prob, depth_out, depth_raw, conf);                               \
     else                                                                                                      \
       hipLaunchKernelGGL(prob_wta_kernel<DD>, gf, bf, 0, st, x11, w->w[10], hyp, height, width, clamp_lo,     \
                          clamp_hi, prob, depth_out, depth_raw, conf);                                         \
