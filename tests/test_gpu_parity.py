@@ -319,11 +319,14 @@ def test_fmt_encoder_layer(model):
     _close(to_np(x), g["enc_out"], 2e-6, "EncoderLayer vs golden")
 
 
-def test_fmt_pathway(sd, model):
+# (views, coarse h, w): one partial tile row; ragged tiles over 798 tiles, i.e. runs of 2 tiles per
+# workgroup of the pipelined stage-2 kernel with a short last run
+@pytest.mark.parametrize("nv,h,w", [(2, 12, 20), (3, 109, 147)])
+def test_fmt_pathway(sd, model, nv, h, w):
     torch.manual_seed(3)
-    coarse = torch.randn(2, 32, 12, 20)
-    lat = torch.randn(2, 16, 24, 40)
-    ref = F.conv2d(F.interpolate(F.conv2d(coarse, sd["FMT_with_pathway.dim_reduction_1.weight"]), size=(24, 40),
+    coarse = torch.randn(nv, 32, h, w)
+    lat = torch.randn(nv, 16, 2 * h, 2 * w)
+    ref = F.conv2d(F.interpolate(F.conv2d(coarse, sd["FMT_with_pathway.dim_reduction_1.weight"]), size=(2 * h, 2 * w),
                                  mode="bilinear") + lat, sd["FMT_with_pathway.smooth_1.weight"], padding=1)
     prep = model._prepared(torch.device(DEV))
     out = ops.fmt_pathway(coarse.permute(0, 2, 3, 1).contiguous().to(DEV), lat.to(DEV), prep["red1"], prep["sm1"])
