@@ -400,29 +400,30 @@ def _conv2d_bn_relu(sd, p, x, stride, padding, training=False):
     return F.relu(_bn(y, sd, p + "bn.", training))
 
 
-def _out_head(sd, p, x, first_k, training=False):
+def _out_head(sd, p, x, first_k, training=False, dcn=_dcn):
     """FeatureNet.out{1,2,3} Sequentials, models/module.py:362-395."""
     t = training
     x = _conv2d_bn_relu(sd, p + "0.", x, 1, 0 if first_k == 1 else 1, t)
-    x = F.relu(_bn(_dcn(sd, p + "1.", x), sd, p + "2.", t))
-    x = F.relu(_bn(_dcn(sd, p + "4.", x), sd, p + "5.", t))
-    return _dcn(sd, p + "7.", x)
+    x = F.relu(_bn(dcn(sd, p + "1.", x), sd, p + "2.", t))
+    x = F.relu(_bn(dcn(sd, p + "4.", x), sd, p + "5.", t))
+    return dcn(sd, p + "7.", x)
 
 
-def feature_net(sd, x, p="feature.", training=False):
+def feature_net(sd, x, p="feature.", training=False, dcn=_dcn):
     """FeatureNet.forward, models/module.py:399-422 (training: BatchNorm2d batch statistics of this
-    call's batch -- the reference calls FeatureNet once per view, models/TransMVSNet.py:151-153)."""
+    call's batch -- the reference calls FeatureNet once per view, models/TransMVSNet.py:151-153).
+    dcn: the DCN block's function (a test may wrap _dcn in activation checkpointing: same values)."""
     t = training
     conv0 = _conv2d_bn_relu(sd, p + "conv0.1.", _conv2d_bn_relu(sd, p + "conv0.0.", x, 1, 1, t), 1, 1, t)
     c1 = _conv2d_bn_relu(sd, p + "conv1.0.", conv0, 2, 2, t)
     conv1 = _conv2d_bn_relu(sd, p + "conv1.2.", _conv2d_bn_relu(sd, p + "conv1.1.", c1, 1, 1, t), 1, 1, t)
     c2 = _conv2d_bn_relu(sd, p + "conv2.0.", conv1, 2, 2, t)
     conv2 = _conv2d_bn_relu(sd, p + "conv2.2.", _conv2d_bn_relu(sd, p + "conv2.1.", c2, 1, 1, t), 1, 1, t)
-    out = {"stage1": _out_head(sd, p + "out1.", conv2, 1, t)}
+    out = {"stage1": _out_head(sd, p + "out1.", conv2, 1, t, dcn)}
     intra = F.interpolate(conv2, scale_factor=2.0, mode="nearest") + F.conv2d(conv1, sd[p + "inner1.weight"], sd[p + "inner1.bias"])
-    out["stage2"] = _out_head(sd, p + "out2.", intra, 3, t)
+    out["stage2"] = _out_head(sd, p + "out2.", intra, 3, t, dcn)
     intra = F.interpolate(intra, scale_factor=2.0, mode="nearest") + F.conv2d(conv0, sd[p + "inner2.weight"], sd[p + "inner2.bias"])
-    out["stage3"] = _out_head(sd, p + "out3.", intra, 3, t)
+    out["stage3"] = _out_head(sd, p + "out3.", intra, 3, t, dcn)
     return out
 
 
