@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TMVS_ABI_VERSION 8
+#define TMVS_ABI_VERSION 9
 
 #define TMVS_OK 0
 #define TMVS_ERR_ARG (-1)    /* null pointer / non-positive size / bad enum        */
@@ -186,6 +186,11 @@ size_t tmvs_fmt_kv_workspace(int nv, int s_tokens);
  * (FMT.py:23-32). source [nv][S][32] -> kv [nv][TMVS_KV_NFLOATS]. */
 int tmvs_fmt_kv(const float* source, int nv, int s_tokens, const float* enc_w, void* workspace,
                 size_t workspace_bytes, float* kv, void* stream);
+/* tmvs_fmt_kv with the partial-sum grouping of a group_nv-view launch: each view's kv is bitwise what a
+ * tmvs_fmt_kv over group_nv views (this view among them) gives, for any subset of views (FMT.py:23-32). */
+size_t tmvs_fmt_kv_grouped_workspace(int nv, int group_nv, int s_tokens);
+int tmvs_fmt_kv_grouped(const float* source, int nv, int group_nv, int s_tokens, const float* enc_w, void* workspace,
+                        size_t workspace_bytes, float* kv, void* stream);
 /* The rest of EncoderLayer.forward (FMT.py:96-111, AttentionLayer :56-75, LinearAttention
  * :22-37) per query token, in place on x [nv][L][32]. kv_view_stride = 0 shares one kv
  * (cross layers: the ref view's K/V serve every source view). */
@@ -211,6 +216,15 @@ size_t tmvs_fmt_forward_workspace(int nv, int l_tokens);
 int tmvs_fmt_forward(const float* stage1, long view_stride, const float* pe, int pe_h, int pe_w, int nv, int height,
                      int width, const float* const* enc_w, void* workspace, size_t workspace_bytes, float* tokens,
                      void* stream);
+/* tmvs_fmt_forward with the reference view's chain -- its self layers 0,2,4,6 and the K/V of their outputs
+ * for the cross layers (FMT.py:155-158,173-174) -- on side_stream, concurrent with the source views' 8
+ * layers on stream. Bitwise the tokens of tmvs_fmt_forward. side_stream forks from stream after the
+ * embedding and is joined back into stream before the call returns (one fork level: graph-capturable).
+ * side_stream NULL (or == stream, or nv < 2) runs tmvs_fmt_forward. */
+size_t tmvs_fmt_forward_split_workspace(int nv, int l_tokens);
+int tmvs_fmt_forward_split(const float* stage1, long view_stride, const float* pe, int pe_h, int pe_w, int nv,
+                           int height, int width, const float* const* enc_w, void* workspace, size_t workspace_bytes,
+                           float* tokens, void* stream, void* side_stream);
 
 /* One cascade stage of TransMVSNet.forward for ONE sample (models/TransMVSNet.py:174-221):
  * tmvs_stage_hypotheses -> tmvs_warp_corr -> tmvs_costregnet -> tmvs_softmax_wta.

@@ -20,7 +20,7 @@ import torch
 import torch.nn.functional as F
 
 from oracle import transmvs_ref as oracle
-from transmvsnet_amd import TransMVSNet, ops, synthetic
+from transmvsnet_amd import TransMVSNet, _lib, ops, synthetic
 from tests._util import GOLDEN_ROT_ORDER, depth_parity, golden, golden_rot, golden_state_dict, to_np
 
 pytestmark = pytest.mark.gpu
@@ -317,6 +317,35 @@ def test_fmt_encoder_layer(model):
     kv = ops.fmt_kv(src, enc)
     ops.fmt_apply(x, kv, enc)
     _close(to_np(x), g["enc_out"], 2e-6, "EncoderLayer vs golden")
+
+
+# the two-stream FMT (reference chain on a side stream) against the one-stream orchestration, bit for bit,
+# at a ragged token count and at the DTU stage-1 size whose K/V launches use 8 tiles per wave; and the
+# grouped K/V of view subsets against the batched launch
+@pytest.mark.parametrize("nv,h,w", [(3, 37, 53), (5, 216, 288)])
+def test_fmt_forward_split_bitwise(model, nv, h, w):
+    torch.manual_seed(11)
+    prep = model._prepared(torch.device(DEV))
+    s1 = torch.randn(nv, 32, h, w, device=DEV)
+    pe = model._pe_slice(h, w, torch.device(DEV))
+    ref = ops.fmt_forward(s1, pe, prep["enc"])
+    side = torch.cuda.Stream(torch.device(DEV))
+    for _ in range(2):
+        out = ops.fmt_forward(s1, pe, prep["enc"], side_stream=side)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), "split FMT differs from the one-stream FMT"
+    lib = _lib.load()
+    L = h * w
+    kv_all = ops.fmt_kv(ref, prep["enc"][2])
+    for lo, hi in ((0, 1), (1, nv)):
+        kv = torch.empty(hi - lo, _lib.KV_NFLOATS, device=DEV)
+        nbytes = lib.tmvs_fmt_kv_grouped_workspace(hi - lo, nv, L)
+        ws = torch.empty(nbytes // 4 + 1, device=DEV)
+        _lib.check(lib.tmvs_fmt_kv_grouped(ref[lo:hi].data_ptr(), hi - lo, nv, L, prep["enc"][2].data_ptr(),
+                                           ws.data_ptr(), ws.numel() * 4, kv.data_ptr(),
+                                           torch.cuda.current_stream().cuda_stream), "kv_grouped")
+        torch.cuda.synchronize()
+        assert torch.equal(kv, kv_all[lo:hi]), f"grouped K/V views {lo}..{hi}"
 
 
 # (views, coarse h, w): one partial tile row; ragged tiles over 798 tiles, i.e. runs of 2 tiles per

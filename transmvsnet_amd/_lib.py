@@ -39,6 +39,10 @@ SIGNATURES = {
     "tmvs_fmt_pathway": (I, [P, P, L, P, P, I, I, I, I, I, P, P]),
     "tmvs_fmt_forward_workspace": (S, [I, I]),
     "tmvs_fmt_forward": (I, [P, L, P, I, I, I, I, I, P, P, S, P, P]),
+    "tmvs_fmt_forward_split_workspace": (S, [I, I]),
+    "tmvs_fmt_forward_split": (I, [P, L, P, I, I, I, I, I, P, P, S, P, P, P]),
+    "tmvs_fmt_kv_grouped_workspace": (S, [I, I, I]),
+    "tmvs_fmt_kv_grouped": (I, [P, I, I, I, P, P, S, P, P]),
     "tmvs_depth_stage_workspace": (S, [I, I, I, I]),
     "tmvs_depth_stage": (I, [P, I, P, I, I, P, I, I, I, F, I, I, I, P, P, P, I, I, P, P, S, F, F, P, P, P, P, P, P]),
     "tmvs_deform_conv2d_packed_floats": (S, [I]),
@@ -103,7 +107,7 @@ SIGNATURES = {
     "tmvs_softmax_backward": (I, [P, P, I, I, I, I, P, P]),
 }
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 PW_NPARAMS = 201
 ENC_NPARAMS = 8544
 KV_NFLOATS = 160

@@ -633,22 +633,32 @@ extern "C" int tmvs_fmt_embed(const float* feat, long feat_view_stride, const fl
   return TMVS_OK;
 }
 
-extern "C" size_t tmvs_fmt_kv_workspace(int nv, int s_tokens) {
-  return (size_t)nv * kv_nblk(nv, s_tokens) * kKV * sizeof(float);
+extern "C" size_t tmvs_fmt_kv_grouped_workspace(int nv, int group_nv, int s_tokens) {
+  if (nv <= 0 || group_nv <= 0 || s_tokens <= 0) return 0;
+  return (size_t)nv * kv_nblk(group_nv, s_tokens) * kKV * sizeof(float);
 }
 
-extern "C" int tmvs_fmt_kv(const float* source, int nv, int s_tokens, const float* enc_w, void* workspace,
-                           size_t workspace_bytes, float* kv, void* stream) {
-  if (!source || !enc_w || !workspace || !kv || nv <= 0 || s_tokens <= 0) return TMVS_ERR_ARG;
-  if (workspace_bytes < tmvs_fmt_kv_workspace(nv, s_tokens)) return TMVS_ERR_ARG;
-  const int nblk = kv_nblk(nv, s_tokens);
+extern "C" size_t tmvs_fmt_kv_workspace(int nv, int s_tokens) { return tmvs_fmt_kv_grouped_workspace(nv, nv, s_tokens); }
+
+// The tiling (tiles per wave, hence each view's partial-sum grouping) is the one a launch over group_nv
+// views uses, so a view's K/V is bitwise the same whichever subset of views a launch carries.
+extern "C" int tmvs_fmt_kv_grouped(const float* source, int nv, int group_nv, int s_tokens, const float* enc_w,
+                                   void* workspace, size_t workspace_bytes, float* kv, void* stream) {
+  if (!source || !enc_w || !workspace || !kv || nv <= 0 || group_nv <= 0 || s_tokens <= 0) return TMVS_ERR_ARG;
+  if (workspace_bytes < tmvs_fmt_kv_grouped_workspace(nv, group_nv, s_tokens)) return TMVS_ERR_ARG;
+  const int nblk = kv_nblk(group_nv, s_tokens);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(fmt_kv_partial_kernel, dim3(nblk, nv), dim3(kKvBlock), 0, st, source, s_tokens, enc_w,
-                     (float*)workspace, kv_tiles_per_wave(nv, s_tokens));
+                     (float*)workspace, kv_tiles_per_wave(group_nv, s_tokens));
   TMVS_CHECK_LAUNCH();
   hipLaunchKernelGGL(fmt_kv_combine_kernel, dim3(nv, kKV / 32), dim3(1024), 0, st, (const float*)workspace, nblk, kv);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
+}
+
+extern "C" int tmvs_fmt_kv(const float* source, int nv, int s_tokens, const float* enc_w, void* workspace,
+                           size_t workspace_bytes, float* kv, void* stream) {
+  return tmvs_fmt_kv_grouped(source, nv, nv, s_tokens, enc_w, workspace, workspace_bytes, kv, stream);
 }
 
 extern "C" int tmvs_fmt_apply(float* x, int nv, int l_tokens, const float* kv, long kv_view_stride,

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -243,6 +244,9 @@ class TransMVSNet(nn.Module):
         self.overlap_pathway = True
         # priority of that side stream (torch.cuda.Stream: lower = higher priority; 0 = default)
         self.side_priority = 0
+        # the FMT's reference-view chain on that side stream, concurrent with the source views (bitwise the same)
+        self.split_fmt = os.environ.get("TMVS_SPLIT_FMT", "1") != "0"  # (env: A/B switch)
+        self.fmt_side_priority = int(os.environ.get("TMVS_FMT_SIDE_PRIO", "0"))
         # rounding of homo_warping's rot·(x, y, 1) to reproduce: 'auto' = the host torch's
         # (ops.host_rot_order), or 'fma' / 'plain' to pin it (fixtures made on another machine)
         self.warp_rot_order = "auto"
@@ -413,15 +417,29 @@ class TransMVSNet(nn.Module):
             return outputs, (vws[0] if b == 1 else torch.cat(vws, 0))
         return outputs
 
-    def _fmt(self, s1, prep):
-        """FMT_with_pathway stage-1 part (models/FMT.py:212-226) -> tokens [N, h1*w1, 32]."""
+    def _side_stream(self, dev, slot, role="pathway"):
+        key = (dev, slot, role)  # one side stream per sample stream (B > 1 runs samples concurrently) and role
+        side = self._side.get(key)
+        if side is None:
+            prio = self.side_priority if role == "pathway" else self.fmt_side_priority
+            side = self._side[key] = torch.cuda.Stream(dev, priority=prio)
+        return side
+
+    def _fmt(self, s1, prep, slot=0):
+        """FMT_with_pathway stage-1 part (models/FMT.py:212-226) -> tokens [N, h1*w1, 32].
+
+        With split_fmt the reference view's chain runs on the side stream next to the source views
+        (tmvs_fmt_forward_split, bitwise the same tokens); like the pathway, only from the caller's stream.
+        """
         n, c, h1, w1 = s1.shape
-        return ops.fmt_forward(s1, self._pe_slice(h1, w1, s1.device), prep["enc"])
+        split = self.split_fmt and not self.decomposed and slot == 0
+        side = self._side_stream(s1.device, slot, "fmt") if split else None
+        return ops.fmt_forward(s1, self._pe_slice(h1, w1, s1.device), prep["enc"], side_stream=side)
 
     def _forward_one(self, f, rows, dv, dv0, img_hw, prep, view_shard, slot=0):
         s1, s2, s3 = f["stage1"], f["stage2"], f["stage3"]
         n, _, h1, w1 = s1.shape
-        tokens = self._fmt(s1, prep)
+        tokens = self._fmt(s1, prep, slot)
         st1 = tokens.view(n, h1, w1, 32)
         # the pathway's side stream forks only from the caller's stream (slot 0): a sample on its own stream
         # (slot > 0, B > 1) runs the pathway in line, so no stream forks from an already-forked stream -- a
@@ -438,10 +456,7 @@ class TransMVSNet(nn.Module):
             """Launch the pathway on a side stream once stage 1's cost volume is queued, so it runs
             beside stage 1's CostRegNet (whose 1/16-resolution grids leave most CUs idle)."""
             main = torch.cuda.current_stream(s1.device)
-            key = (s1.device, slot)  # one pathway side stream per sample stream (B > 1 runs samples concurrently)
-            side = self._side.get(key)
-            if side is None:
-                side = self._side[key] = torch.cuda.Stream(s1.device, priority=self.side_priority)
+            side = self._side_stream(s1.device, slot)
             ready = torch.cuda.Event()
             ready.record(main)
             side.wait_event(ready)

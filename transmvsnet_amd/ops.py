@@ -342,18 +342,31 @@ def fmt_pathway(coarse_nhwc, lateral_nchw, w_reduce, w_smooth):
 
 
 # ----------------------------------------------------------------- native orchestration
-def fmt_forward(stage1_nchw, pe, enc_list, tokens=None):
-    """Whole FMT (models/FMT.py:147-177): stage1 [nv,32,H,W] -> tokens [nv,H*W,32]."""
+def fmt_forward(stage1_nchw, pe, enc_list, tokens=None, side_stream=None):
+    """Whole FMT (models/FMT.py:147-177): stage1 [nv,32,H,W] -> tokens [nv,H*W,32].
+
+    side_stream (a torch.cuda.Stream): the reference view's chain runs on it, concurrently with the source
+    views (tmvs_fmt_forward_split; bitwise the same tokens). It forks from and joins back into the current
+    stream inside the call.
+    """
     _dev(stage1_nchw, "stage1")
     nv, c, h, w = stage1_nchw.shape
     tokens = torch.empty(nv, h * w, c, device=stage1_nchw.device) if tokens is None else tokens
-    nbytes = _lib_h().tmvs_fmt_forward_workspace(nv, h * w)
+    split = side_stream is not None and nv > 1
+    lib = _lib_h()
+    nbytes = lib.tmvs_fmt_forward_split_workspace(nv, h * w) if split else lib.tmvs_fmt_forward_workspace(nv, h * w)
     ws = torch.empty(nbytes // 4 + 64, device=stage1_nchw.device)
     ptrs = (ctypes.c_void_p * 8)(*[e.data_ptr() for e in enc_list])
+    args = (_ptr(stage1_nchw), c * h * w, _ptr(pe), pe.shape[1], pe.shape[2], nv, h, w, ptrs, _ptr(ws), ws.numel() * 4,
+            _ptr(tokens), _stream())
     with _Span("tmvs_fmt_forward"):
-        _lib.check(_lib_h().tmvs_fmt_forward(_ptr(stage1_nchw), c * h * w, _ptr(pe), pe.shape[1], pe.shape[2], nv, h, w,
-                                             ptrs, _ptr(ws), ws.numel() * 4, _ptr(tokens), _stream()),
-                   "tmvs_fmt_forward")
+        if split:
+            _lib.check(lib.tmvs_fmt_forward_split(*args, side_stream.cuda_stream), "tmvs_fmt_forward_split")
+            if not torch.cuda.is_current_stream_capturing():  # allocator: ws / tokens are also used on the side stream
+                ws.record_stream(side_stream)
+                tokens.record_stream(side_stream)
+        else:
+            _lib.check(lib.tmvs_fmt_forward(*args), "tmvs_fmt_forward")
     return tokens
 
 
