@@ -47,3 +47,36 @@ def test_batch2_full_size_capture_equals_eager():
             a = seq[f"stage{s}"][k]
             assert torch.equal(a, con[f"stage{s}"][k]), (s, k, "concurrent eager")
             assert torch.equal(a, g_out[f"stage{s}"][k]), (s, k, "graph replay")
+
+
+# The B = 1 step's stream layouts -- one stream (no overlap, one-stream FMT), the FMT's reference chain on a
+# side stream (tmvs_fmt_forward_split), the pathway forked after stage 1's cost volume or right after the FMT,
+# the reference view's pathway on the FMT side stream -- give the same bits, eager and as a replayed graph.
+@pytest.mark.parametrize("layout", ["split", "split_fmtfork", "split_refearly", "split_refearly_fmtfork"])
+def test_stream_layouts_bitwise(layout):
+    H, W, N = 512, 640, 5
+    m = TransMVSNet().eval()
+    m.load_state_dict(synthetic.synthetic_state_dict(synthetic.state_dict_shapes(m), seed=0, sharpen=100.0))
+    m = m.to(DEV)
+    feats = {k: v.to(DEV).contiguous() for k, v in synthetic.stacked_features(N, H, W, seed=4).items()}
+    proj = synthetic.synthetic_cameras(N, H, W, seed=3)
+    dv = synthetic.synthetic_depth_values(1).to(DEV)
+    with torch.no_grad():
+        m.overlap_pathway, m.split_fmt = False, False
+        ref = m.forward_features(feats, proj, dv, (H, W))
+        m.overlap_pathway, m.split_fmt = True, True
+        m.pathway_fork = "fmt" if "fmtfork" in layout else "warp"
+        m.ref_pathway_early = "refearly" in layout
+        eager = m.forward_features(feats, proj, dv, (H, W))
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            g_out = m.forward_features(feats, proj, dv, (H, W))
+        for _ in range(2):
+            graph.replay()
+        torch.cuda.synchronize()
+    for s in (1, 2, 3):
+        for k in KEYS:
+            a = ref[f"stage{s}"][k]
+            assert torch.equal(a, eager[f"stage{s}"][k]), (layout, s, k, "eager")
+            assert torch.equal(a, g_out[f"stage{s}"][k]), (layout, s, k, "graph replay")

@@ -247,6 +247,9 @@ class TransMVSNet(nn.Module):
         # the FMT's reference-view chain on that side stream, concurrent with the source views (bitwise the same)
         self.split_fmt = os.environ.get("TMVS_SPLIT_FMT", "1") != "0"  # (env: A/B switch)
         self.fmt_side_priority = int(os.environ.get("TMVS_FMT_SIDE_PRIO", "0"))
+        # where the pathway forks: "warp" = once stage 1's cost volume is queued, "fmt" = right after the FMT
+        self.pathway_fork = os.environ.get("TMVS_PATHWAY_FORK", "warp")
+        self.ref_pathway_early = os.environ.get("TMVS_REF_PATHWAY", "0") == "1"
         # rounding of homo_warping's rot·(x, y, 1) to reproduce: 'auto' = the host torch's
         # (ops.host_rot_order), or 'fma' / 'plain' to pin it (fixtures made on another machine)
         self.warp_rot_order = "auto"
@@ -447,8 +450,30 @@ class TransMVSNet(nn.Module):
         # hipStreamEndCapture on the box (r20a); the samples themselves still overlap each other
         overlap = self.overlap_pathway and not self.decomposed and slot == 0
         lateral = {}
+        # the reference view's pathway on the FMT's side stream, right after its FMT chain (which ends well before
+        # the source views'): it then overlaps the source views' last FMT layers; the source views' pathway as below
+        ref_early = overlap and self.split_fmt and self.ref_pathway_early and n > 1
+        v0 = 0
+        if ref_early:
+            v0 = 1
+            h2, w2 = s2.shape[-2:]
+            lateral["st2"] = torch.empty(n, h2, w2, s2.shape[1], device=s1.device)
+            lateral["st3"] = torch.empty(n, s3.shape[-2], s3.shape[-1], s3.shape[1], device=s1.device)
+            fside = self._side_stream(s1.device, slot, "fmt")
+            with torch.cuda.stream(fside):  # already ordered after the reference view's FMT chain
+                ops.fmt_pathway(st1[:1], s2[:1], prep["red1"], prep["sm1"], out=lateral["st2"][:1])
+                ops.fmt_pathway(lateral["st2"][:1], s3[:1], prep["red2"], prep["sm2"], out=lateral["st3"][:1])
+            lateral["ref_done"] = torch.cuda.Event()
+            lateral["ref_done"].record(fside)
+            if not torch.cuda.is_current_stream_capturing():
+                for t in (st1, s2, s3, lateral["st2"], lateral["st3"]):
+                    t.record_stream(fside)
 
         def pathway():
+            if v0:
+                ops.fmt_pathway(st1[v0:], s2[v0:], prep["red1"], prep["sm1"], out=lateral["st2"][v0:])
+                ops.fmt_pathway(lateral["st2"][v0:], s3[v0:], prep["red2"], prep["sm2"], out=lateral["st3"][v0:])
+                return
             lateral["st2"] = ops.fmt_pathway(st1, s2, prep["red1"], prep["sm1"])
             lateral["st3"] = ops.fmt_pathway(lateral["st2"], s3, prep["red2"], prep["sm2"])
 
@@ -475,6 +500,8 @@ class TransMVSNet(nn.Module):
 
         if not overlap:
             pathway()
+        elif self.pathway_fork == "fmt":
+            pathway_side()
         outputs = {}
         depth_raw = None
         view_w = None
@@ -482,6 +509,8 @@ class TransMVSNet(nn.Module):
             name = f"stage{s + 1}"
             if s == 1 and overlap:
                 torch.cuda.current_stream(s1.device).wait_event(lateral["done"])
+                if ref_early:
+                    torch.cuda.current_stream(s1.device).wait_event(lateral["ref_done"])
             fs = (st1, lateral.get("st2"), lateral.get("st3"))[s]
             if view_shard is None and not self.decomposed and s > 0:
                 out, depth_raw = ops.depth_stage(dv0, depth_raw, fs, self.ndepths[s], self.depth_interals_ratio[s],
@@ -502,7 +531,7 @@ class TransMVSNet(nn.Module):
                                               vw_shift=s, rot_order=self.warp_rot_order)
                 if s == 0:
                     view_w = vw_new
-                    if overlap:
+                    if overlap and self.pathway_fork != "fmt":
                         pathway_side()
                 prob, depth, depth_raw, conf = ops.costregnet_wta(sim, prep["cr"][s][0], hyp, DEPTH_CLAMP)
                 out = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}

@@ -330,11 +330,16 @@ def fmt_apply(x_tokens, kv, enc_w, shared_kv=False):
     return x_tokens
 
 
-def fmt_pathway(coarse_nhwc, lateral_nchw, w_reduce, w_smooth):
-    """smooth(up2(reduce(coarse)) + lateral) (FMT.py:221-228): coarse [nv,h,w,cc], lateral [nv,cf,2h,2w]."""
+def fmt_pathway(coarse_nhwc, lateral_nchw, w_reduce, w_smooth, out=None):
+    """smooth(up2(reduce(coarse)) + lateral) (FMT.py:221-228): coarse [nv,h,w,cc], lateral [nv,cf,2h,2w].
+
+    out: optional contiguous [nv,2h,2w,cf] destination (e.g. a view slice of a larger batch)."""
     nv, h, w, cc = coarse_nhwc.shape
     cf = lateral_nchw.shape[1]
-    out = torch.empty(nv, 2 * h, 2 * w, cf, device=coarse_nhwc.device)
+    if out is None:
+        out = torch.empty(nv, 2 * h, 2 * w, cf, device=coarse_nhwc.device)
+    elif tuple(out.shape) != (nv, 2 * h, 2 * w, cf) or not out.is_contiguous():
+        raise ValueError(f"fmt_pathway: out must be a contiguous [{nv},{2 * h},{2 * w},{cf}] tensor")
     with _Span("tmvs_fmt_pathway"):
         _lib.check(_lib_h().tmvs_fmt_pathway(_ptr(coarse_nhwc), _ptr(lateral_nchw), cf * 4 * h * w, _ptr(w_reduce),
                                              _ptr(w_smooth), nv, cc, cf, h, w, _ptr(out), _stream()), "tmvs_fmt_pathway")
