@@ -247,9 +247,12 @@ class TransMVSNet(nn.Module):
         # the FMT's reference-view chain on that side stream, concurrent with the source views (bitwise the same)
         self.split_fmt = os.environ.get("TMVS_SPLIT_FMT", "1") != "0"  # (env: A/B switch)
         self.fmt_side_priority = int(os.environ.get("TMVS_FMT_SIDE_PRIO", "0"))
-        # where the pathway forks: "warp" = once stage 1's cost volume is queued, "fmt" = right after the FMT
-        self.pathway_fork = os.environ.get("TMVS_PATHWAY_FORK", "warp")
-        self.ref_pathway_early = os.environ.get("TMVS_REF_PATHWAY", "0") == "1"
+        # where the pathway forks: "fmt" = right after the FMT (measured 298.5 vs 297.8 depth maps/s for "warp" =
+        # once stage 1's cost volume is queued, and 295.0 on the main stream; profiles/r22/stream_layout_ab.txt)
+        self.pathway_fork = os.environ.get("TMVS_PATHWAY_FORK", "fmt")
+        self.one_side_stream = os.environ.get("TMVS_ONE_SIDE", "0") == "1"  # FMT and pathway on one side stream (A/B)
+        # stage 2 waits only for the pathway's stage-2 output, stage 3 for its stage-3 output (A/B)
+        self.pathway_join2 = os.environ.get("TMVS_PW_JOIN2", "0") == "1"
         # rounding of homo_warping's rot·(x, y, 1) to reproduce: 'auto' = the host torch's
         # (ops.host_rot_order), or 'fma' / 'plain' to pin it (fixtures made on another machine)
         self.warp_rot_order = "auto"
@@ -421,6 +424,8 @@ class TransMVSNet(nn.Module):
         return outputs
 
     def _side_stream(self, dev, slot, role="pathway"):
+        if self.one_side_stream:
+            role = "pathway"
         key = (dev, slot, role)  # one side stream per sample stream (B > 1 runs samples concurrently) and role
         side = self._side.get(key)
         if side is None:
@@ -450,43 +455,24 @@ class TransMVSNet(nn.Module):
         # hipStreamEndCapture on the box (r20a); the samples themselves still overlap each other
         overlap = self.overlap_pathway and not self.decomposed and slot == 0
         lateral = {}
-        # the reference view's pathway on the FMT's side stream, right after its FMT chain (which ends well before
-        # the source views'): it then overlaps the source views' last FMT layers; the source views' pathway as below
-        ref_early = overlap and self.split_fmt and self.ref_pathway_early and n > 1
-        v0 = 0
-        if ref_early:
-            v0 = 1
-            h2, w2 = s2.shape[-2:]
-            lateral["st2"] = torch.empty(n, h2, w2, s2.shape[1], device=s1.device)
-            lateral["st3"] = torch.empty(n, s3.shape[-2], s3.shape[-1], s3.shape[1], device=s1.device)
-            fside = self._side_stream(s1.device, slot, "fmt")
-            with torch.cuda.stream(fside):  # already ordered after the reference view's FMT chain
-                ops.fmt_pathway(st1[:1], s2[:1], prep["red1"], prep["sm1"], out=lateral["st2"][:1])
-                ops.fmt_pathway(lateral["st2"][:1], s3[:1], prep["red2"], prep["sm2"], out=lateral["st3"][:1])
-            lateral["ref_done"] = torch.cuda.Event()
-            lateral["ref_done"].record(fside)
-            if not torch.cuda.is_current_stream_capturing():
-                for t in (st1, s2, s3, lateral["st2"], lateral["st3"]):
-                    t.record_stream(fside)
 
-        def pathway():
-            if v0:
-                ops.fmt_pathway(st1[v0:], s2[v0:], prep["red1"], prep["sm1"], out=lateral["st2"][v0:])
-                ops.fmt_pathway(lateral["st2"][v0:], s3[v0:], prep["red2"], prep["sm2"], out=lateral["st3"][v0:])
-                return
+        def pathway(side=None):
             lateral["st2"] = ops.fmt_pathway(st1, s2, prep["red1"], prep["sm1"])
+            if side is not None:  # stage 2 needs only st2: it waits for this event, stage 3 for "done"
+                lateral["done2"] = torch.cuda.Event()
+                lateral["done2"].record(side)
             lateral["st3"] = ops.fmt_pathway(lateral["st2"], s3, prep["red2"], prep["sm2"])
 
         def pathway_side():
-            """Launch the pathway on a side stream once stage 1's cost volume is queued, so it runs
-            beside stage 1's CostRegNet (whose 1/16-resolution grids leave most CUs idle)."""
+            """Launch the pathway on a side stream (right after the FMT, or once stage 1's cost volume is
+            queued: pathway_fork), so it runs beside stage 1 (whose 1/16-resolution grids leave CUs idle)."""
             main = torch.cuda.current_stream(s1.device)
             side = self._side_stream(s1.device, slot)
             ready = torch.cuda.Event()
             ready.record(main)
             side.wait_event(ready)
             with torch.cuda.stream(side):
-                pathway()
+                pathway(side if self.pathway_join2 else None)
             done = torch.cuda.Event()
             done.record(side)
             # allocator bookkeeping: st2/st3 are consumed on the main stream, st1/s2/s3 read on side
@@ -507,10 +493,10 @@ class TransMVSNet(nn.Module):
         view_w = None
         for s in range(self.num_stage):
             name = f"stage{s + 1}"
-            if s == 1 and overlap:
+            if overlap and s == 1:
+                torch.cuda.current_stream(s1.device).wait_event(lateral.get("done2", lateral["done"]))
+            if overlap and s == 2 and "done2" in lateral:
                 torch.cuda.current_stream(s1.device).wait_event(lateral["done"])
-                if ref_early:
-                    torch.cuda.current_stream(s1.device).wait_event(lateral["ref_done"])
             fs = (st1, lateral.get("st2"), lateral.get("st3"))[s]
             if view_shard is None and not self.decomposed and s > 0:
                 out, depth_raw = ops.depth_stage(dv0, depth_raw, fs, self.ndepths[s], self.depth_interals_ratio[s],
