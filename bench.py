@@ -124,7 +124,11 @@ def batch2_timing(model, feats, proj, dv_dev, steps, graphed):
     outputs); eagerly, one B=2 forward_features call (TransMVSNet.batch_streams)."""
     main = torch.cuda.current_stream()
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    split = model.split_fmt
     if graphed:
+        # two requests side by side: each graph's FMT in one stream (its side-stream fork measured slower next to
+        # the other request's graph, profiles/r22/batch2_ab.txt); the B = 1 headline keeps the fork
+        model.split_fmt = False
         graphs = []
         for st in streams:
             st.wait_stream(main)
@@ -137,6 +141,7 @@ def batch2_timing(model, feats, proj, dv_dev, steps, graphed):
                 model.forward_features(feats, proj, dv_dev, (H, W))
             graphs.append(g)
         torch.cuda.synchronize()
+        model.split_fmt = split
 
         def step():
             ev = torch.cuda.Event()

@@ -252,7 +252,8 @@ class TransMVSNet(nn.Module):
         self.pathway_fork = os.environ.get("TMVS_PATHWAY_FORK", "fmt")
         self.one_side_stream = os.environ.get("TMVS_ONE_SIDE", "0") == "1"  # FMT and pathway on one side stream (A/B)
         # stage 2 waits only for the pathway's stage-2 output, stage 3 for its stage-3 output (A/B)
-        self.pathway_join2 = os.environ.get("TMVS_PW_JOIN2", "0") == "1"
+        # (profiles/r22/batch2_ab.txt: 295.9 vs 295.3 depth maps/s in three alternations)
+        self.pathway_join2 = os.environ.get("TMVS_PW_JOIN2", "1") == "1"
         # rounding of homo_warping's rot·(x, y, 1) to reproduce: 'auto' = the host torch's
         # (ops.host_rot_order), or 'fma' / 'plain' to pin it (fixtures made on another machine)
         self.warp_rot_order = "auto"
@@ -396,7 +397,7 @@ class TransMVSNet(nn.Module):
             with torch.cuda.stream(st):
                 o, vw = self._forward_one({k: v[i] for k, v in feats.items()}, {k: r[i:i + 1] for k, r in rows.items()},
                                           dv[i:i + 1], dv[0:1], img_hw, prep, view_shard,
-                                          slot=i if st is not main else 0)
+                                          slot=i if st is not main else 0, solo=not concurrent)
             if st is not main:
                 ev = torch.cuda.Event()
                 ev.record(st)
@@ -433,21 +434,23 @@ class TransMVSNet(nn.Module):
             side = self._side[key] = torch.cuda.Stream(dev, priority=prio)
         return side
 
-    def _fmt(self, s1, prep, slot=0):
+    def _fmt(self, s1, prep, slot=0, solo=True):
         """FMT_with_pathway stage-1 part (models/FMT.py:212-226) -> tokens [N, h1*w1, 32].
 
         With split_fmt the reference view's chain runs on the side stream next to the source views
-        (tmvs_fmt_forward_split, bitwise the same tokens); like the pathway, only from the caller's stream.
+        (tmvs_fmt_forward_split, bitwise the same tokens); like the pathway, only from the caller's stream,
+        and only when no other sample runs concurrently (solo): beside a second sample the extra fork measured
+        slower (B = 2 on two streams 295.7 vs 303.6 depth maps/s, profiles/r22/batch2_ab.txt).
         """
         n, c, h1, w1 = s1.shape
-        split = self.split_fmt and not self.decomposed and slot == 0
+        split = self.split_fmt and not self.decomposed and slot == 0 and solo
         side = self._side_stream(s1.device, slot, "fmt") if split else None
         return ops.fmt_forward(s1, self._pe_slice(h1, w1, s1.device), prep["enc"], side_stream=side)
 
-    def _forward_one(self, f, rows, dv, dv0, img_hw, prep, view_shard, slot=0):
+    def _forward_one(self, f, rows, dv, dv0, img_hw, prep, view_shard, slot=0, solo=True):
         s1, s2, s3 = f["stage1"], f["stage2"], f["stage3"]
         n, _, h1, w1 = s1.shape
-        tokens = self._fmt(s1, prep, slot)
+        tokens = self._fmt(s1, prep, slot, solo)
         st1 = tokens.view(n, h1, w1, 32)
         # the pathway's side stream forks only from the caller's stream (slot 0): a sample on its own stream
         # (slot > 0, B > 1) runs the pathway in line, so no stream forks from an already-forked stream -- a
