@@ -81,25 +81,3 @@ def test_stream_layouts_bitwise(layout):
             a = ref[f"stage{s}"][k]
             assert torch.equal(a, eager[f"stage{s}"][k]), (layout, s, k, "eager")
             assert torch.equal(a, g_out[f"stage{s}"][k]), (layout, s, k, "graph replay")
-
-
-# forward() from images with FeatureNet's stage-2/3 heads on a side stream beside the stage-1 head, the FMT and
-# stage 1: the same bits as the serial forward (eager; forward() is not captured by the bench)
-def test_forward_heads_overlap_bitwise():
-    H, W, N = 512, 640, 5
-    m = TransMVSNet().eval()
-    m.load_state_dict(synthetic.synthetic_state_dict(synthetic.state_dict_shapes(m), seed=0, sharpen=100.0))
-    m = m.to(DEV)
-    imgs = synthetic.synthetic_images(N, H, W, seed=9).to(DEV)
-    proj = synthetic.synthetic_cameras(N, H, W, seed=3)
-    dv = synthetic.synthetic_depth_values(1).to(DEV)
-    with torch.no_grad():
-        m.overlap_heads = False
-        ref = m.forward(imgs, proj, dv)
-        m.overlap_heads = True
-        for _ in range(2):
-            out = m.forward(imgs, proj, dv)
-        torch.cuda.synchronize()
-    for s in (1, 2, 3):
-        for k in KEYS:
-            assert torch.equal(ref[f"stage{s}"][k], out[f"stage{s}"][k]), (s, k)

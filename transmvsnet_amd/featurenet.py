@@ -141,13 +141,9 @@ class FeatureNet(nn.Module):
         self.out2 = _head(4 * b, 4 * b, 2 * b, 3)
         self.out3 = _head(4 * b, 4 * b, b, 3)
 
-    def forward(self, x, heads_stream=None):
+    def forward(self, x):
         """x [B,3,H,W] -> {stage1: [B,32,H/4,W/4], stage2: [B,16,H/2,W/2], stage3: [B,8,H,W]}.
-        Views may be batched on B (eval BatchNorm is per sample).
-
-        heads_stream (a torch.cuda.Stream): the FPN merges and the stage-2/3 heads run on it, forked after the
-        trunk, while the stage-1 head (and whatever the caller queues next) runs on the current stream; the
-        result then carries "ready", an event on heads_stream after which stage2/stage3 are complete."""
+        Views may be batched on B (eval BatchNorm is per sample)."""
         x = x.contiguous()
         if not x.is_cuda:
             raise RuntimeError("FeatureNet runs on the GPU only (HIP kernels); no CPU fallback")
@@ -158,32 +154,12 @@ class FeatureNet(nn.Module):
         conv2 = conv1
         for blk in self.conv2:
             conv2 = blk.forward_native(conv2)
-        def heads():
-            # intra = interpolate(., 2, nearest) + inner(.) as one NHWC kernel (models/module.py:413, 417)
-            intra = ops.fpn_merge(conv2, conv1, *self._inner(self.inner1, conv2.device))
-            out["stage2"] = _run_head(self.out2, None, intra)
-            intra = ops.fpn_merge(intra, conv0, *self._inner(self.inner2, conv2.device))
-            out["stage3"] = _run_head(self.out3, None, intra)
-
-        out = {}
-        if heads_stream is None:
-            out["stage1"] = _run_head(self.out1, conv2)
-            heads()
-            return out
-        main = torch.cuda.current_stream(x.device)
-        fork = torch.cuda.Event()
-        fork.record(main)
-        heads_stream.wait_event(fork)
-        with torch.cuda.stream(heads_stream):
-            heads()
-        out["ready"] = torch.cuda.Event()
-        out["ready"].record(heads_stream)
-        out["stage1"] = _run_head(self.out1, conv2)
-        if not torch.cuda.is_current_stream_capturing():  # allocator: trunk outputs read on heads_stream, outputs on main
-            for t in (conv0, conv1, conv2):
-                t.record_stream(heads_stream)
-            for k in ("stage2", "stage3"):
-                out[k].record_stream(main)
+        out = {"stage1": _run_head(self.out1, conv2)}
+        # intra = interpolate(., 2, nearest) + inner(.) as one NHWC kernel (models/module.py:413, 417)
+        intra = ops.fpn_merge(conv2, conv1, *self._inner(self.inner1, conv2.device))
+        out["stage2"] = _run_head(self.out2, None, intra)
+        intra = ops.fpn_merge(intra, conv0, *self._inner(self.inner2, conv2.device))
+        out["stage3"] = _run_head(self.out3, None, intra)
         return out
 
     def _inner(self, conv, device):

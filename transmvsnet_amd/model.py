@@ -254,8 +254,6 @@ class TransMVSNet(nn.Module):
         # stage 2 waits only for the pathway's stage-2 output, stage 3 for its stage-3 output (A/B)
         # (profiles/r22/batch2_ab.txt: 295.9 vs 295.3 depth maps/s in three alternations)
         self.pathway_join2 = os.environ.get("TMVS_PW_JOIN2", "1") == "1"
-        # forward() from images, B = 1: FeatureNet's stage-2/3 heads on a side stream beside the stage-1 path (A/B)
-        self.overlap_heads = os.environ.get("TMVS_OVERLAP_HEADS", "0") == "1"
         # rounding of homo_warping's rot·(x, y, 1) to reproduce: 'auto' = the host torch's
         # (ops.host_rot_order), or 'fma' / 'plain' to pin it (fixtures made on another machine)
         self.warp_rot_order = "auto"
@@ -333,15 +331,10 @@ class TransMVSNet(nn.Module):
             return forward_train(self, imgs, proj_matrix, depth_values)
         self._check_eval()
         b, n = imgs.shape[:2]
-        # B = 1: the stage-2/3 heads of FeatureNet on a side stream while the stage-1 head, the FMT and stage 1
-        # (which need only stage-1 features) run on the caller's stream; the pathway waits for the heads
-        heads = self._side_stream(imgs.device, 0, "heads") if (self.overlap_heads and b == 1 and not self.decomposed) else None
         with torch.cuda.device(imgs.device):
-            f = self.feature(imgs.reshape(b * n, *imgs.shape[2:]), heads_stream=heads)
-        ready = f.pop("ready", None)
+            f = self.feature(imgs.reshape(b * n, *imgs.shape[2:]))
         feats = {k: v.reshape(b, n, *v.shape[1:]) for k, v in f.items()}
-        return self.forward_features(feats, proj_matrix, depth_values, (imgs.shape[3], imgs.shape[4]),
-                                     _lateral_ready=ready)
+        return self.forward_features(feats, proj_matrix, depth_values, (imgs.shape[3], imgs.shape[4]))
 
     def _check_eval(self):
         if self.training:
@@ -356,7 +349,7 @@ class TransMVSNet(nn.Module):
         return {k: torch.stack([f[k] for f in features], 1).contiguous() for k in ("stage1", "stage2", "stage3")}
 
     def forward_features(self, features, proj_matrix, depth_values, img_hw, return_view_weights=False,
-                         view_shard=None, _lateral_ready=None):
+                         view_shard=None):
         """Hot path after feature extraction (models/TransMVSNet.py:162-226).
 
         features: per-view list of FeatureNet dicts, or {stage: [B,N,C,h,w]} stacked.
@@ -371,10 +364,9 @@ class TransMVSNet(nn.Module):
             raise RuntimeError("TransMVSNet (HIP) needs GPU features; the HIP path has no CPU fallback")
         with torch.cuda.device(dev):  # kernels + current stream of the features' device
             return self._forward_features(feats, proj_matrix, depth_values, img_hw, return_view_weights,
-                                          view_shard, dev, _lateral_ready)
+                                          view_shard, dev)
 
-    def _forward_features(self, feats, proj_matrix, depth_values, img_hw, return_view_weights, view_shard, dev,
-                          _lateral_ready=None):
+    def _forward_features(self, feats, proj_matrix, depth_values, img_hw, return_view_weights, view_shard, dev):
         prep = self._prepared(dev)
         dv = depth_values.to(dev, torch.float32).contiguous()
         rows = {k: ops.proj_rows(proj_matrix[k]) for k in ("stage1", "stage2", "stage3")}
@@ -405,8 +397,7 @@ class TransMVSNet(nn.Module):
             with torch.cuda.stream(st):
                 o, vw = self._forward_one({k: v[i] for k, v in feats.items()}, {k: r[i:i + 1] for k, r in rows.items()},
                                           dv[i:i + 1], dv[0:1], img_hw, prep, view_shard,
-                                          slot=i if st is not main else 0, solo=not concurrent,
-                                          lateral_ready=_lateral_ready)
+                                          slot=i if st is not main else 0, solo=not concurrent)
             if st is not main:
                 ev = torch.cuda.Event()
                 ev.record(st)
@@ -456,7 +447,7 @@ class TransMVSNet(nn.Module):
         side = self._side_stream(s1.device, slot, "fmt") if split else None
         return ops.fmt_forward(s1, self._pe_slice(h1, w1, s1.device), prep["enc"], side_stream=side)
 
-    def _forward_one(self, f, rows, dv, dv0, img_hw, prep, view_shard, slot=0, solo=True, lateral_ready=None):
+    def _forward_one(self, f, rows, dv, dv0, img_hw, prep, view_shard, slot=0, solo=True):
         s1, s2, s3 = f["stage1"], f["stage2"], f["stage3"]
         n, _, h1, w1 = s1.shape
         tokens = self._fmt(s1, prep, slot, solo)
@@ -483,8 +474,6 @@ class TransMVSNet(nn.Module):
             ready = torch.cuda.Event()
             ready.record(main)
             side.wait_event(ready)
-            if lateral_ready is not None:  # stage-2/3 features still being computed on the heads stream
-                side.wait_event(lateral_ready)
             with torch.cuda.stream(side):
                 pathway(side if self.pathway_join2 else None)
             done = torch.cuda.Event()
@@ -499,8 +488,6 @@ class TransMVSNet(nn.Module):
             lateral["done"] = done
 
         if not overlap:
-            if lateral_ready is not None:
-                torch.cuda.current_stream(s1.device).wait_event(lateral_ready)
             pathway()
         elif self.pathway_fork == "fmt":
             pathway_side()
