@@ -466,13 +466,16 @@ class TransMVSNet(nn.Module):
                 lateral["done2"].record(side)
             lateral["st3"] = ops.fmt_pathway(lateral["st2"], s3, prep["red2"], prep["sm2"])
 
-        def pathway_side():
+        def pathway_side(ready=None):
             """Launch the pathway on a side stream (right after the FMT, or once stage 1's cost volume is
-            queued: pathway_fork), so it runs beside stage 1 (whose 1/16-resolution grids leave CUs idle)."""
+            queued: pathway_fork), so it runs beside stage 1 (whose 1/16-resolution grids leave CUs idle).
+            ready: an event recorded on the main stream earlier (the pathway then depends on that point but is
+            enqueued -- created in a captured graph -- later)."""
             main = torch.cuda.current_stream(s1.device)
             side = self._side_stream(s1.device, slot)
-            ready = torch.cuda.Event()
-            ready.record(main)
+            if ready is None:
+                ready = torch.cuda.Event()
+                ready.record(main)
             side.wait_event(ready)
             with torch.cuda.stream(side):
                 pathway(side if self.pathway_join2 else None)
@@ -491,6 +494,9 @@ class TransMVSNet(nn.Module):
             pathway()
         elif self.pathway_fork == "fmt":
             pathway_side()
+        elif self.pathway_fork == "fmt_late":  # depends on the FMT's end, enqueued after stage 1's cost volume
+            lateral["fmt_done"] = torch.cuda.Event()
+            lateral["fmt_done"].record(torch.cuda.current_stream(s1.device))
         outputs = {}
         depth_raw = None
         view_w = None
@@ -521,7 +527,7 @@ class TransMVSNet(nn.Module):
                 if s == 0:
                     view_w = vw_new
                     if overlap and self.pathway_fork != "fmt":
-                        pathway_side()
+                        pathway_side(lateral.get("fmt_done"))
                 prob, depth, depth_raw, conf = ops.costregnet_wta(sim, prep["cr"][s][0], hyp, DEPTH_CLAMP)
                 out = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}
             outputs[name] = out
