@@ -52,8 +52,7 @@ def test_batch2_full_size_capture_equals_eager():
 # The B = 1 step's stream layouts -- one stream (no overlap, one-stream FMT), the FMT's reference chain on a
 # side stream (tmvs_fmt_forward_split), the pathway forked after stage 1's cost volume or right after the FMT,
 # the FMT and the pathway on one side stream -- give the same bits, eager and as a replayed graph.
-@pytest.mark.parametrize("layout", ["split", "split_fmtfork", "split_fmtfork_oneside", "split_fmtfork_join2",
-                                    "split_fmtlatefork_join2"])
+@pytest.mark.parametrize("layout", ["split", "split_fmtfork", "split_fmtfork_oneside", "split_fmtfork_join2"])
 def test_stream_layouts_bitwise(layout):
     H, W, N = 512, 640, 5
     m = TransMVSNet().eval()
@@ -66,7 +65,7 @@ def test_stream_layouts_bitwise(layout):
         m.overlap_pathway, m.split_fmt = False, False
         ref = m.forward_features(feats, proj, dv, (H, W))
         m.overlap_pathway, m.split_fmt = True, True
-        m.pathway_fork = "fmt" if "fmtfork" in layout else "fmt_late" if "fmtlatefork" in layout else "warp"
+        m.pathway_fork = "fmt" if "fmtfork" in layout else "warp"
         m.one_side_stream = "oneside" in layout
         m.pathway_join2 = "join2" in layout
         eager = m.forward_features(feats, proj, dv, (H, W))

@@ -248,7 +248,8 @@ class TransMVSNet(nn.Module):
         self.split_fmt = os.environ.get("TMVS_SPLIT_FMT", "1") != "0"  # (env: A/B switch)
         self.fmt_side_priority = int(os.environ.get("TMVS_FMT_SIDE_PRIO", "0"))
         # where the pathway forks: "fmt" = right after the FMT (measured 298.5 vs 297.8 depth maps/s for "warp" =
-        # once stage 1's cost volume is queued, and 295.0 on the main stream; profiles/r22/stream_layout_ab.txt)
+        # once stage 1's cost volume is queued, and 295.0 on the main stream; profiles/r22/stream_layout_ab.txt,
+        # fork_join2_ab.txt, fork_late_ab.txt)
         self.pathway_fork = os.environ.get("TMVS_PATHWAY_FORK", "fmt")
         self.one_side_stream = os.environ.get("TMVS_ONE_SIDE", "0") == "1"  # FMT and pathway on one side stream (A/B)
         # stage 2 waits only for the pathway's stage-2 output, stage 3 for its stage-3 output (A/B)
@@ -466,16 +467,13 @@ class TransMVSNet(nn.Module):
                 lateral["done2"].record(side)
             lateral["st3"] = ops.fmt_pathway(lateral["st2"], s3, prep["red2"], prep["sm2"])
 
-        def pathway_side(ready=None):
+        def pathway_side():
             """Launch the pathway on a side stream (right after the FMT, or once stage 1's cost volume is
-            queued: pathway_fork), so it runs beside stage 1 (whose 1/16-resolution grids leave CUs idle).
-            ready: an event recorded on the main stream earlier (the pathway then depends on that point but is
-            enqueued -- created in a captured graph -- later)."""
+            queued: pathway_fork), so it runs beside stage 1 (whose 1/16-resolution grids leave CUs idle)."""
             main = torch.cuda.current_stream(s1.device)
             side = self._side_stream(s1.device, slot)
-            if ready is None:
-                ready = torch.cuda.Event()
-                ready.record(main)
+            ready = torch.cuda.Event()
+            ready.record(main)
             side.wait_event(ready)
             with torch.cuda.stream(side):
                 pathway(side if self.pathway_join2 else None)
@@ -494,9 +492,6 @@ class TransMVSNet(nn.Module):
             pathway()
         elif self.pathway_fork == "fmt":
             pathway_side()
-        elif self.pathway_fork == "fmt_late":  # depends on the FMT's end, enqueued after stage 1's cost volume
-            lateral["fmt_done"] = torch.cuda.Event()
-            lateral["fmt_done"].record(torch.cuda.current_stream(s1.device))
         outputs = {}
         depth_raw = None
         view_w = None
@@ -527,7 +522,7 @@ class TransMVSNet(nn.Module):
                 if s == 0:
                     view_w = vw_new
                     if overlap and self.pathway_fork != "fmt":
-                        pathway_side(lateral.get("fmt_done"))
+                        pathway_side()
                 prob, depth, depth_raw, conf = ops.costregnet_wta(sim, prep["cr"][s][0], hyp, DEPTH_CLAMP)
                 out = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}
             outputs[name] = out
