@@ -86,6 +86,17 @@ def test_argument_validation_without_gpu(lib):
     assert lib.tmvs_softmax_wta(None, None, 1, 48, 8, 8, 425.0, 935.0, None, None, None, None, None) == -1
     assert lib.tmvs_costregnet_workspace(1, 48, 216, 288, 8) > 0
     assert lib.tmvs_depth_stage_workspace(48, 216, 288, 8) > lib.tmvs_costregnet_workspace(1, 48, 216, 288, 8)
+    # the grouped K/V: a view subset keeps the tiling of the larger launch, so its slab is the subset's share
+    L = 216 * 288
+    assert lib.tmvs_fmt_kv_grouped_workspace(5, 5, L) == lib.tmvs_fmt_kv_workspace(5, L)
+    assert 5 * lib.tmvs_fmt_kv_grouped_workspace(1, 5, L) == lib.tmvs_fmt_kv_workspace(5, L)
+    assert lib.tmvs_fmt_kv_grouped_workspace(1, 1, L) == lib.tmvs_fmt_kv_workspace(1, L)
+    assert lib.tmvs_fmt_kv_grouped_workspace(0, 5, L) == 0
+    assert lib.tmvs_fmt_kv_grouped(None, 1, 5, L, None, None, 0, None, None) == -1
+    # the split FMT needs both K/V slabs; NULL side stream falls back to (and validates like) tmvs_fmt_forward
+    assert lib.tmvs_fmt_forward_split_workspace(5, L) > lib.tmvs_fmt_forward_workspace(5, L)
+    assert lib.tmvs_fmt_forward_split_workspace(1, L) == lib.tmvs_fmt_forward_workspace(1, L)
+    assert lib.tmvs_fmt_forward_split(None, 0, None, 0, 0, 5, 216, 288, None, None, 0, None, None, None) == -1
 
 
 def test_forward_refuses_cpu_tensors():
