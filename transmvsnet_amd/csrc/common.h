@@ -217,3 +217,8 @@ __device__ __forceinline__ int softmax_first_max(const float (&x)[D], PutProb pu
 }
 
 }  // namespace tmvs
+
+// fmt.hip: tmvs_fmt_apply with an explicit tiling (internal, used by tmvs_fmt_forward_split; the C-ABI entry point
+// sizes the tiling from the kernel's occupancy)
+int tmvs_fmt_apply_tiled(float* x, int nv, int l_tokens, const float* kv, long kv_view_stride, const float* enc_w,
+                         int tiles_per_wave, void* stream);

@@ -661,12 +661,19 @@ extern "C" int tmvs_fmt_kv(const float* source, int nv, int s_tokens, const floa
   return tmvs_fmt_kv_grouped(source, nv, nv, s_tokens, enc_w, workspace, workspace_bytes, kv, stream);
 }
 
-extern "C" int tmvs_fmt_apply(float* x, int nv, int l_tokens, const float* kv, long kv_view_stride,
-                              const float* enc_w, void* stream) {
+// tiles_per_wave > 0 overrides the occupancy-sized tiling (the per-token arithmetic, hence the output, is the same)
+int tmvs_fmt_apply_tiled(float* x, int nv, int l_tokens, const float* kv, long kv_view_stride, const float* enc_w,
+                         int tiles_per_wave, void* stream) {
   if (!x || !kv || !enc_w || nv <= 0 || l_tokens <= 0 || kv_view_stride < 0) return TMVS_ERR_ARG;
-  const int tpw = apply_tiles_per_wave(nv, l_tokens);
+  const int tpw = tiles_per_wave > 0 ? (tiles_per_wave + kApplyNT - 1) / kApplyNT * kApplyNT
+                                     : apply_tiles_per_wave(nv, l_tokens);
   hipLaunchKernelGGL(fmt_apply_kernel, dim3(apply_nblk(l_tokens, tpw), nv), dim3(256), 0, (hipStream_t)stream, x,
                      l_tokens, kv, kv_view_stride, enc_w, tpw);
   TMVS_CHECK_LAUNCH();
   return TMVS_OK;
+}
+
+extern "C" int tmvs_fmt_apply(float* x, int nv, int l_tokens, const float* kv, long kv_view_stride,
+                              const float* enc_w, void* stream) {
+  return tmvs_fmt_apply_tiled(x, nv, l_tokens, kv, kv_view_stride, enc_w, 0, stream);
 }

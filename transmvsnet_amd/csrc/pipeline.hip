@@ -64,6 +64,9 @@ extern "C" size_t tmvs_fmt_forward_split_workspace(int nv, int l_tokens) {
 #ifndef TMVS_FMT_SPLIT_ORDER
 #define TMVS_FMT_SPLIT_ORDER 0
 #endif
+#ifndef TMVS_SPLIT_REF_TPW
+#define TMVS_SPLIT_REF_TPW 0  // tiles per wave of the reference view's applies (0: occupancy-sized, as if alone)
+#endif
 
 namespace {
 // fork / cross-layer / join events of tmvs_fmt_forward_split, created once per host thread and device
@@ -123,7 +126,7 @@ extern "C" int tmvs_fmt_forward_split(const float* stage1, long view_stride, con
     const int i = 2 * j;
     int r;
     if ((r = tmvs_fmt_kv_grouped(tokens, 1, nv, L, enc_w[i], slab_side, sd, kv_ref, ss))) return r;
-    if ((r = tmvs_fmt_apply(tokens, 1, L, kv_ref, TMVS_KV_NFLOATS, enc_w[i], ss))) return r;
+    if ((r = tmvs_fmt_apply_tiled(tokens, 1, L, kv_ref, TMVS_KV_NFLOATS, enc_w[i], TMVS_SPLIT_REF_TPW, ss))) return r;
     if ((r = tmvs_fmt_kv(tokens, 1, L, enc_w[i + 1], slab_side, sd, kv_cross + j * TMVS_KV_NFLOATS, ss))) return r;
     return hipEventRecord(e->ev[1 + j], ss) != hipSuccess ? TMVS_ERR_HIP : TMVS_OK;
   };

@@ -495,12 +495,14 @@ class TransMVSNet(nn.Module):
         outputs = {}
         depth_raw = None
         view_w = None
+        joined = not overlap  # the pathway's side stream joined back (a capture needs it before it ends)
         for s in range(self.num_stage):
             name = f"stage{s + 1}"
-            if overlap and s == 1:
-                torch.cuda.current_stream(s1.device).wait_event(lateral.get("done2", lateral["done"]))
-            if overlap and s == 2 and "done2" in lateral:
+            if overlap and s == 1 and "done2" in lateral:
+                torch.cuda.current_stream(s1.device).wait_event(lateral["done2"])
+            elif overlap and s in (1, 2) and not joined:
                 torch.cuda.current_stream(s1.device).wait_event(lateral["done"])
+                joined = True
             fs = (st1, lateral.get("st2"), lateral.get("st3"))[s]
             if view_shard is None and not self.decomposed and s > 0:
                 out, depth_raw = ops.depth_stage(dv0, depth_raw, fs, self.ndepths[s], self.depth_interals_ratio[s],
@@ -526,4 +528,6 @@ class TransMVSNet(nn.Module):
                 prob, depth, depth_raw, conf = ops.costregnet_wta(sim, prep["cr"][s][0], hyp, DEPTH_CLAMP)
                 out = {"depth": depth, "photo_confidence": conf, "prob_volume": prob, "depth_values": hyp}
             outputs[name] = out
+        if not joined:  # fewer than 3 stages: the side stream still joins back
+            torch.cuda.current_stream(s1.device).wait_event(lateral["done"])
         return outputs, view_w
