@@ -65,7 +65,10 @@ extern "C" size_t tmvs_fmt_forward_split_workspace(int nv, int l_tokens) {
 #define TMVS_FMT_SPLIT_ORDER 0
 #endif
 #ifndef TMVS_SPLIT_REF_TPW
-#define TMVS_SPLIT_REF_TPW 0  // tiles per wave of the reference view's applies (0: occupancy-sized, as if alone)
+// tiles per wave of the reference view's applies (0: occupancy-sized, as if the launch were alone). Beside the
+// source views' launches a 1-view apply of 2 tiles per wave (half the waves) measured 297.8 vs 296.6 depth maps/s
+// (4: 297.4, 8: 293.6; profiles/r22/reftpw_ab.txt); the tokens are the same either way
+#define TMVS_SPLIT_REF_TPW 2
 #endif
 
 namespace {
